@@ -1,0 +1,179 @@
+"""ctypes binding of libdensepoints.so (the C ABI in include/densepoints.h).
+
+The product path is the HIP library: if it is missing, importing this module
+raises -- there is no CPU fallback anywhere in densepoints_amd.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdensepoints.so")
+
+# dp_patch (include/densepoints.h) -- 80 bytes
+PATCH_DTYPE = np.dtype(
+    [
+        ("pos", "<f4", 3),
+        ("normal", "<f4", 3),
+        ("ref", "<u4"),
+        ("seq", "<u4"),
+        ("vis", "<u8", 2),
+        ("cand", "<u8", 2),
+        ("score", "<f4"),
+        ("evals", "<u4"),
+        ("rgb", "u1", 3),
+        ("flags", "u1"),
+        ("parent", "<u4"),
+    ],
+    align=True,
+)
+assert PATCH_DTYPE.itemsize == 80
+
+DP_OK = 0
+DP_E_ARG = -1
+DP_E_HIP = -2
+DP_E_OOM = -3
+DP_E_DEGENERATE = -4
+DP_E_STATE = -5
+DP_E_NODEVICE = -6
+
+MODE_EVAL, MODE_FILTER, MODE_NM, MODE_SEED, MODE_EXPAND = range(5)
+PATCH_ACCEPTED = 1
+PATCH_DEGENERATE = 2
+
+
+class DpOptions(ctypes.Structure):
+    _fields_ = [
+        ("seed_cell_size", ctypes.c_int32),
+        ("expand_cell_size", ctypes.c_int32),
+        ("grid_scale", ctypes.c_int32),
+        ("max_patches_per_cell", ctypes.c_int32),
+        ("min_visible", ctypes.c_int32),
+        ("min_expand_visible", ctypes.c_int32),
+        ("nm_max_evals", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("ncc_threshold", ctypes.c_double),
+        ("visible_angle", ctypes.c_double),
+        ("candidate_angle", ctypes.c_double),
+        ("nm_step", ctypes.c_double * 3),
+        ("nm_eps", ctypes.c_double),
+        ("ncc_denom_min", ctypes.c_double),
+        ("max_pops", ctypes.c_int64),
+    ]
+
+
+class DpImage(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("stride", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("bgr", ctypes.c_void_p),
+    ]
+
+
+class DpDensifyStats(ctypes.Structure):
+    _fields_ = [
+        ("seeds_in", ctypes.c_int64),
+        ("seed_patches", ctypes.c_int64),
+        ("patches", ctypes.c_int64),
+        ("pops", ctypes.c_int64),
+        ("candidates", ctypes.c_int64),
+        ("evals", ctypes.c_int64),
+        ("generations", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("refine_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double),
+    ]
+
+
+class DpSynthConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_views", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("kind", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("spread_deg", ctypes.c_double),
+        ("seed_stride_px", ctypes.c_double),
+        ("depth_noise", ctypes.c_double),
+    ]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_D = ctypes.c_double
+
+# (name, restype, argtypes) of every exported symbol in include/densepoints.h
+# and include/densepoints_probe.h
+SIGNATURES = [
+    ("dp_default_options", None, [_P]),
+    ("dp_abi_version", _I, []),
+    ("dp_ctx_create", _I, [_P, _I, _P]),
+    ("dp_ctx_destroy", _I, [_P]),
+    ("dp_last_error", ctypes.c_char_p, [_P]),
+    ("dp_set_options", _I, [_P, _P]),
+    ("dp_set_views", _I, [_P, _I, _P, _P]),
+    ("dp_set_views_device", _I, [_P, _I, _P, _P, _P, _P, _P]),
+    ("dp_view_geometry", _I, [_P, _P, _P, _P, _P]),
+    ("dp_seeds_to_patches", _I, [_P, _P, _I, _P]),
+    ("dp_eval_batch", _I, [_P, _P, _I, _I, _P]),
+    ("dp_refine_batch", _I, [_P, _P, _I, _I, _I, _P]),
+    ("dp_refine_batch_device", _I, [_P, _P, _I, _I, _I, _P, _P]),
+    ("dp_densify", _I, [_P, _P, _I, _P, _P, _P]),
+    ("dp_last_kernel_ms", _I, [_P, _P]),
+    ("dp_synth_default", None, [_P]),
+    ("dp_synth_cameras", _I, [_P, _P]),
+    ("dp_synth_render_host", _I, [_P, _P, _I, _P]),
+    ("dp_synth_render_device", _I, [_P, _P, _P, _I, _P, _P]),
+    ("dp_synth_seeds", ctypes.c_int64, [_P, _P, _P, ctypes.c_int64]),
+    ("dp_probe_sincos", None, [_D, _P, _P]),
+    ("dp_probe_acos", _D, [_D]),
+    ("dp_probe_texture", _I, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, _I, _P]),
+    ("dp_probe_ncc", _D, [ctypes.c_int32] * 6 + [_D]),
+    ("dp_probe_math_device", _I, [_P, _I, _P]),
+]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"densepoints_amd: HIP library {LIB_PATH} is missing; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class DensePointsError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"densepoints error {code}: {msg}")
+        self.code = code
+
+
+def check(rc: int, ctx=None) -> None:
+    if rc != DP_OK:
+        msg = lib.dp_last_error(ctx).decode() if ctx else ""
+        raise DensePointsError(rc, msg)
+
+
+def ptr(a) -> int | None:
+    if a is None:
+        return None
+    return a.ctypes.data
+
+
+def default_options() -> DpOptions:
+    o = DpOptions()
+    lib.dp_default_options(ctypes.byref(o))
+    return o

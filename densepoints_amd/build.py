@@ -1,0 +1,65 @@
+"""In-tree build of libdensepoints.so (gfx950) -- no JIT cache, no pip install.
+
+hipcc compiles the kernels and the host-side C ABI in one shared object.
+-ffp-contract=off is part of the parity spec: every fp64/f32 expression of the
+arithmetic spec is one IEEE rounding on both the CPU and CDNA4.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "lib", "libdensepoints.so")
+SOURCES = ["dp_capi.hip", "dp_kernels.hip"]
+HEADERS = ["dp_internal.h", "dp_geom.h", "dp_detmath.h", "dp_synth.h"]
+ARCH = os.environ.get("DP_OFFLOAD_ARCH", "gfx950")
+FLAGS = [
+    "-O3",
+    "-std=c++17",
+    f"--offload-arch={ARCH}",
+    "-ffp-contract=off",
+    "-fno-fast-math",
+    "-fPIC",
+    "-shared",
+    "-Wall",
+    "-Wno-unused-value",
+    "-Wno-unused-result",
+]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps += [os.path.join(HERE, "..", "include", h) for h in ("densepoints.h", "densepoints_probe.h")]
+    deps.append(__file__)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    tmp = OUT + ".tmp"
+    cmd = [hipcc(), *FLAGS, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,943 @@
+// dp_capi.hip -- C ABI (include/densepoints.h): contexts, view upload, batch
+// refine launches and the device-side BFS densify driver.
+//
+// The reference's PMVS driver (methods/pmvs/pmvs.cpp:22-43) runs
+//   seeds -> Seed::FilterPatches/OptimizePatches (cell 16) ->
+//   PatchOrganizer::SetSeeds -> Expand::ExpandPatches (FIFO, cell 11).
+// Here the FIFO runs generation-synchronously on the GPU: generation g+1 is
+// every child of the queue slice [head, np) in (parent, direction) order,
+// refined by one fused kernel; organizer claims resolve by minimum sequence
+// number, which equals the single-thread FIFO's insertion order exactly.
+#include "dp_internal.h"
+#include "../../include/densepoints_probe.h"
+#include "dp_synth.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// host-side parallel loop (the product library carries no OpenMP runtime)
+template <typename F> void parallel_for(int64_t n, F f)
+{
+    unsigned hw = std::thread::hardware_concurrency();
+    int64_t nt = hw ? (int64_t)(hw > 32 ? 32 : hw) : 4;
+    if (nt > n)
+        nt = n;
+    if (nt <= 1) {
+        for (int64_t i = 0; i < n; ++i)
+            f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 0; t < nt; ++t)
+        th.emplace_back([=, &f]() {
+            for (int64_t i = t; i < n; i += nt)
+                f(i);
+        });
+    for (auto &x : th)
+        x.join();
+}
+
+template <typename T> struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n)
+    {
+        if (n <= cap)
+            return hipSuccess;
+        if (p)
+            hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = n < 1024 ? 1024 : n + n / 4;
+        hipError_t e = hipMalloc(&p, want * sizeof(T));
+        if (e == hipSuccess)
+            cap = want;
+        return e;
+    }
+    void release()
+    {
+        if (p)
+            hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+} // namespace
+
+struct dp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    dp_options opt{};
+    std::string err;
+    int V = 0;
+    std::vector<dpg::ViewDev> hv;
+    dpg::ViewDev *d_views = nullptr;
+    std::vector<uint32_t *> own_img;
+    uint32_t *d_work = nullptr;
+    unsigned long long *d_evals = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    bool timed = false;
+    int64_t grid_cells = 0;
+    DevBuf<uint32_t> grid;
+    DevBuf<dp_patch> pat, store, cand;
+    DevBuf<uint8_t> ok, acc;
+    DevBuf<uint32_t> prefix;
+    DevBuf<unsigned char> scan_tmp;
+    std::vector<dp_patch> result;
+};
+
+static int fail(dp_ctx *c, int code, const std::string &msg)
+{
+    if (c)
+        c->err = msg;
+    return code;
+}
+
+#define DP_HIP(c, expr)                                                                       \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return fail((c), _e == hipErrorOutOfMemory ? DP_E_OOM : DP_E_HIP,                 \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// geometry (product implementation of View::SetProjectionMatrix)
+// ---------------------------------------------------------------------------
+
+static double det_cols(const double *a, const double *b, const double *c)
+{
+    return (a[0] * (b[1] * c[2] - b[2] * c[1]) - b[0] * (a[1] * c[2] - a[2] * c[1])) +
+           c[0] * (a[1] * b[2] - a[2] * b[1]);
+}
+
+extern "C" int dp_view_geometry(const double P[12], double C[3], double K[9], double E[12],
+                                double xaxis[3])
+{
+    // camera centre: cofactor null vector of P (types.cpp:34-37 uses SVD)
+    double col[4][3];
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 3; ++r)
+            col[c][r] = P[r * 4 + c];
+    const double cx = det_cols(col[1], col[2], col[3]);
+    const double cy = -det_cols(col[0], col[2], col[3]);
+    const double cz = det_cols(col[0], col[1], col[3]);
+    const double cw = -det_cols(col[0], col[1], col[2]);
+    if (cw == 0.0 || !std::isfinite(cw))
+        return DP_E_ARG;
+    const double Cc[3] = {cx / cw, cy / cw, cz / cw};
+    // RQ with positive K diagonal (types.cpp:39-67): bottom-up Gram-Schmidt
+    const double *m0 = P, *m1 = P + 4, *m2 = P + 8;
+    double q2[3], q1[3], q0[3], t[3];
+    const double l2 = std::sqrt(dpg::dot3(m2, m2));
+    for (int i = 0; i < 3; ++i)
+        q2[i] = m2[i] / l2;
+    const double p12 = dpg::dot3(m1, q2);
+    for (int i = 0; i < 3; ++i)
+        t[i] = m1[i] - p12 * q2[i];
+    const double l1 = std::sqrt(dpg::dot3(t, t));
+    for (int i = 0; i < 3; ++i)
+        q1[i] = t[i] / l1;
+    const double p02 = dpg::dot3(m0, q2), p01 = dpg::dot3(m0, q1);
+    for (int i = 0; i < 3; ++i)
+        t[i] = (m0[i] - p02 * q2[i]) - p01 * q1[i];
+    const double l0 = std::sqrt(dpg::dot3(t, t));
+    for (int i = 0; i < 3; ++i)
+        q0[i] = t[i] / l0;
+    if (C)
+        std::memcpy(C, Cc, sizeof(Cc));
+    if (xaxis)
+        std::memcpy(xaxis, q0, sizeof(q0));
+    if (K) {
+        const double k22 = dpg::dot3(m2, q2);
+        const double k[9] = {dpg::dot3(m0, q0) / k22, dpg::dot3(m0, q1) / k22, dpg::dot3(m0, q2) / k22,
+                             0.0, dpg::dot3(m1, q1) / k22, dpg::dot3(m1, q2) / k22,
+                             0.0, 0.0, 1.0};
+        std::memcpy(K, k, sizeof(k));
+    }
+    if (E) {
+        const double *R[3] = {q0, q1, q2};
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c)
+                E[r * 4 + c] = R[r][c];
+            E[r * 4 + 3] = -dpg::dot3(R[r], Cc);
+        }
+    }
+    return DP_OK;
+}
+
+static int view_from_P(const double *P, int W, int H, int gs, dpg::ViewDev &v)
+{
+    std::memset(&v, 0, sizeof(v));
+    std::memcpy(v.P, P, sizeof(v.P));
+    double xa[3];
+    int rc = dp_view_geometry(P, v.C, nullptr, nullptr, xa);
+    if (rc != DP_OK)
+        return rc;
+    const double nx = std::sqrt(dpg::dot3(xa, xa));
+    for (int i = 0; i < 3; ++i)
+        v.xr[i] = xa[i] / nx; // GetXAxis().normalized() (patch.cpp:95)
+    v.W = W;
+    v.H = H;
+    v.pitch = W;
+    v.gw = W / gs; // PatchOrganizer::AllocateViews (patch_organizer.cpp:35-36)
+    v.gh = H / gs;
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// options / context
+// ---------------------------------------------------------------------------
+
+extern "C" void dp_default_options(dp_options *o)
+{
+    std::memset(o, 0, sizeof(*o));
+    o->seed_cell_size = 16;
+    o->expand_cell_size = 11;
+    o->grid_scale = 8;
+    o->max_patches_per_cell = 1;
+    o->min_visible = 3;
+    o->min_expand_visible = 2;
+    o->nm_max_evals = 500;
+    o->ncc_threshold = 0.6;
+    o->visible_angle = 0.78;
+    o->candidate_angle = 1.04;
+    o->nm_step[0] = 0.02;
+    o->nm_step[1] = 0.2;
+    o->nm_step[2] = 0.2;
+    o->nm_eps = 0.0001;
+    o->ncc_denom_min = 0.1;
+    o->max_pops = 10000000;
+}
+
+extern "C" int dp_abi_version(void) { return DP_ABI_VERSION; }
+
+static int check_options(dp_ctx *c, const dp_options &o)
+{
+    if (o.seed_cell_size < 2 || o.seed_cell_size > DP_MAX_CELL || o.expand_cell_size < 2 ||
+        o.expand_cell_size > DP_MAX_CELL)
+        return fail(c, DP_E_ARG, "cell sizes must be in [2, 16]");
+    if (o.grid_scale <= 0)
+        return fail(c, DP_E_ARG, "grid_scale must be > 0");
+    if (o.max_patches_per_cell != 1)
+        return fail(c, DP_E_ARG, "max_patches_per_cell != 1 is not supported");
+    if (o.nm_max_evals < 1)
+        return fail(c, DP_E_ARG, "nm_max_evals must be >= 1");
+    return DP_OK;
+}
+
+extern "C" int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out)
+{
+    if (!out)
+        return DP_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return DP_E_NODEVICE;
+    if (device < 0 || device >= ndev)
+        return DP_E_ARG;
+    dp_ctx *c = new (std::nothrow) dp_ctx();
+    if (!c)
+        return DP_E_OOM;
+    c->device = device;
+    if (opt)
+        c->opt = *opt;
+    else
+        dp_default_options(&c->opt);
+    int rc = check_options(c, c->opt);
+    if (rc != DP_OK) {
+        delete c;
+        return rc;
+    }
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_work, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_evals, sizeof(unsigned long long)) != hipSuccess ||
+        hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess) {
+        dp_ctx_destroy(c);
+        return DP_E_HIP;
+    }
+    *out = c;
+    return DP_OK;
+}
+
+static void free_views(dp_ctx *c)
+{
+    for (uint32_t *p : c->own_img)
+        hipFree(p);
+    c->own_img.clear();
+    if (c->d_views)
+        hipFree(c->d_views);
+    c->d_views = nullptr;
+    c->hv.clear();
+    c->V = 0;
+}
+
+extern "C" int dp_ctx_destroy(dp_ctx *c)
+{
+    if (!c)
+        return DP_OK;
+    hipSetDevice(c->device);
+    if (c->stream)
+        hipStreamSynchronize(c->stream);
+    free_views(c);
+    c->grid.release();
+    c->pat.release();
+    c->store.release();
+    c->cand.release();
+    c->ok.release();
+    c->acc.release();
+    c->prefix.release();
+    c->scan_tmp.release();
+    if (c->d_work)
+        hipFree(c->d_work);
+    if (c->d_evals)
+        hipFree(c->d_evals);
+    if (c->e0)
+        hipEventDestroy(c->e0);
+    if (c->e1)
+        hipEventDestroy(c->e1);
+    if (c->stream)
+        hipStreamDestroy(c->stream);
+    delete c;
+    return DP_OK;
+}
+
+extern "C" const char *dp_last_error(const dp_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int dp_set_options(dp_ctx *c, const dp_options *opt)
+{
+    if (!c || !opt)
+        return DP_E_ARG;
+    int rc = check_options(c, *opt);
+    if (rc != DP_OK)
+        return rc;
+    c->opt = *opt;
+    // grid geometry depends on grid_scale
+    for (auto &v : c->hv) {
+        v.gw = v.W / opt->grid_scale;
+        v.gh = v.H / opt->grid_scale;
+    }
+    if (c->V) {
+        hipSetDevice(c->device);
+        DP_HIP(c, hipMemcpy(c->d_views, c->hv.data(), sizeof(dpg::ViewDev) * c->V, hipMemcpyHostToDevice));
+    }
+    return DP_OK;
+}
+
+static int upload_view_table(dp_ctx *c)
+{
+    int64_t off = 0;
+    for (auto &v : c->hv) {
+        v.grid_off = off;
+        off += (int64_t)v.gw * v.gh;
+    }
+    c->grid_cells = off;
+    DP_HIP(c, hipMalloc(&c->d_views, sizeof(dpg::ViewDev) * c->V));
+    DP_HIP(c, hipMemcpy(c->d_views, c->hv.data(), sizeof(dpg::ViewDev) * c->V, hipMemcpyHostToDevice));
+    return DP_OK;
+}
+
+extern "C" int dp_set_views(dp_ctx *c, int V, const double *P, const dp_image *images)
+{
+    if (!c || V <= 0 || V > DP_MAX_VIEWS || !P || !images)
+        return fail(c, DP_E_ARG, "dp_set_views: bad arguments (1 <= V <= 128)");
+    hipSetDevice(c->device);
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    free_views(c);
+    c->hv.resize(V);
+    std::vector<uint32_t> tmp;
+    for (int v = 0; v < V; ++v) {
+        const dp_image &im = images[v];
+        if (im.width <= 0 || im.height <= 0 || !im.bgr)
+            return fail(c, DP_E_ARG, "dp_set_views: empty image");
+        if (view_from_P(P + 12 * v, im.width, im.height, c->opt.grid_scale, c->hv[v]) != DP_OK)
+            return fail(c, DP_E_ARG, "dp_set_views: singular projection matrix");
+        const size_t stride = im.stride ? (size_t)im.stride : (size_t)im.width * 3;
+        tmp.resize((size_t)im.width * im.height);
+        parallel_for(im.height, [&](int64_t y) {
+            const uint8_t *row = im.bgr + (size_t)y * stride;
+            uint32_t *o = tmp.data() + (size_t)y * im.width;
+            for (int x = 0; x < im.width; ++x)
+                o[x] = (uint32_t)row[3 * x] | ((uint32_t)row[3 * x + 1] << 8) |
+                       ((uint32_t)row[3 * x + 2] << 16) | 0xFF000000u;
+        });
+        uint32_t *d = nullptr;
+        DP_HIP(c, hipMalloc(&d, tmp.size() * sizeof(uint32_t)));
+        c->own_img.push_back(d);
+        DP_HIP(c, hipMemcpy(d, tmp.data(), tmp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        c->hv[v].img = d;
+    }
+    c->V = V;
+    return upload_view_table(c);
+}
+
+extern "C" int dp_set_views_device(dp_ctx *c, int V, const double *P, const int32_t *W, const int32_t *H,
+                                   const int32_t *pitch, const void *const *dev_bgra)
+{
+    if (!c || V <= 0 || V > DP_MAX_VIEWS || !P || !W || !H || !dev_bgra)
+        return fail(c, DP_E_ARG, "dp_set_views_device: bad arguments");
+    hipSetDevice(c->device);
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    free_views(c);
+    c->hv.resize(V);
+    for (int v = 0; v < V; ++v) {
+        if (W[v] <= 0 || H[v] <= 0 || !dev_bgra[v])
+            return fail(c, DP_E_ARG, "dp_set_views_device: empty image");
+        if (view_from_P(P + 12 * v, W[v], H[v], c->opt.grid_scale, c->hv[v]) != DP_OK)
+            return fail(c, DP_E_ARG, "dp_set_views_device: singular projection matrix");
+        c->hv[v].pitch = pitch ? pitch[v] : W[v];
+        c->hv[v].img = (const uint32_t *)dev_bgra[v];
+    }
+    c->V = V;
+    return upload_view_table(c);
+}
+
+// ---------------------------------------------------------------------------
+// seeds (host; O(N*V), negligible next to the refine)
+// ---------------------------------------------------------------------------
+
+static void seed_patch(const std::vector<dpg::ViewDev> &hv, const dp_options &o, const double *X, dp_patch &p)
+{
+    // Seed::CreatePatchesFromPoints (seed.cpp:30-49)
+    const int V = (int)hv.size();
+    auto dist = [&](int v) {
+        const double d[3] = {X[0] - hv[v].C[0], X[1] - hv[v].C[1], X[2] - hv[v].C[2]};
+        return std::sqrt(dpg::dot3(d, d));
+    };
+    double best = dist(0);
+    int ref = 0;
+    for (int v = 1; v < V; ++v) {
+        const double d = dist(v);
+        if (d < best) {
+            best = d;
+            ref = v;
+        }
+    }
+    const double t[3] = {X[0] - hv[ref].C[0], X[1] - hv[ref].C[1], X[2] - hv[ref].C[2]};
+    const double tn = std::sqrt(dpg::dot3(t, t));
+    std::memset(&p, 0, sizeof(p));
+    p.ref = (uint32_t)ref;
+    p.parent = 0xFFFFFFFFu;
+    for (int i = 0; i < 3; ++i) {
+        p.pos[i] = (float)X[i];
+        p.normal[i] = (float)(t[i] / tn);
+    }
+    // InitRelatedImages on the stored f32 pose (patch.cpp:19-49)
+    const double Xs[3] = {p.pos[0], p.pos[1], p.pos[2]};
+    const double ns[3] = {p.normal[0], p.normal[1], p.normal[2]};
+    for (int v = 0; v < V; ++v) {
+        if (v == ref)
+            continue;
+        const int cls = dpg::classify_view(hv[v], Xs, ns, o.visible_angle, o.candidate_angle);
+        if (cls == 1)
+            p.vis[v >> 6] |= 1ull << (v & 63);
+        else if (cls == 2)
+            p.cand[v >> 6] |= 1ull << (v & 63);
+    }
+}
+
+extern "C" int dp_seeds_to_patches(dp_ctx *c, const double *xyz, int n, dp_patch *out)
+{
+    if (!c || n < 0 || (n > 0 && (!xyz || !out)))
+        return fail(c, DP_E_ARG, "dp_seeds_to_patches: bad arguments");
+    if (!c->V)
+        return fail(c, DP_E_STATE, "dp_seeds_to_patches: no views");
+    parallel_for(n, [&](int64_t i) { seed_patch(c->hv, c->opt, xyz + 3 * i, out[i]); });
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// refine
+// ---------------------------------------------------------------------------
+
+static dpk::RefineArgs refine_args(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc)
+{
+    dpk::RefineArgs a{};
+    a.views = c->d_views;
+    a.V = c->V;
+    a.cell = cell;
+    a.mode = mode;
+    a.n = n;
+    a.opt = c->opt;
+    a.patches = d;
+    a.accept = acc;
+    a.work = c->d_work;
+    a.evals = c->d_evals;
+    a.parents = nullptr;
+    a.max_pops = c->opt.max_pops;
+    return a;
+}
+
+static int launch_timed(dp_ctx *c, const dpk::RefineArgs &a, hipStream_t s)
+{
+    DP_HIP(c, hipEventRecord(c->e0, s));
+    DP_HIP(c, dpk::launch_refine(a, s));
+    DP_HIP(c, hipEventRecord(c->e1, s));
+    c->timed = true;
+    return DP_OK;
+}
+
+static int check_refine(dp_ctx *c, int n, int cell, int mode)
+{
+    if (!c)
+        return DP_E_ARG;
+    if (!c->V)
+        return fail(c, DP_E_STATE, "no views set");
+    if (n < 0 || cell < 2 || cell > DP_MAX_CELL || mode < DP_MODE_EVAL || mode > DP_MODE_EXPAND)
+        return fail(c, DP_E_ARG, "refine: bad n/cell/mode");
+    return DP_OK;
+}
+
+extern "C" int dp_refine_batch_device(dp_ctx *c, dp_patch *d_inout, int n, int cell, int mode,
+                                      uint8_t *d_accept, void *stream)
+{
+    int rc = check_refine(c, n, cell, mode);
+    if (rc != DP_OK)
+        return rc;
+    if (n == 0)
+        return DP_OK;
+    hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    dpk::RefineArgs a = refine_args(c, d_inout, n, cell, mode, d_accept);
+    return launch_timed(c, a, s);
+}
+
+extern "C" int dp_refine_batch(dp_ctx *c, dp_patch *inout, int n, int cell, int mode, uint8_t *accept_out)
+{
+    int rc = check_refine(c, n, cell, mode);
+    if (rc != DP_OK)
+        return rc;
+    if (n == 0)
+        return DP_OK;
+    if (!inout)
+        return fail(c, DP_E_ARG, "refine: null patches");
+    for (int i = 0; i < n; ++i) {
+        const dp_patch &p = inout[i];
+        const bool bad_hi = c->V <= 64 ? (p.vis[1] != 0 || (c->V < 64 && (p.vis[0] >> c->V))) : (c->V < 128 && (p.vis[1] >> (c->V - 64)));
+        if (p.ref >= (uint32_t)c->V || bad_hi)
+            return fail(c, DP_E_ARG, "refine: patch " + std::to_string(i) + " names a view outside the scene");
+    }
+    hipSetDevice(c->device);
+    DP_HIP(c, c->pat.reserve(n));
+    DP_HIP(c, c->ok.reserve(n));
+    DP_HIP(c, hipMemcpyAsync(c->pat.p, inout, sizeof(dp_patch) * n, hipMemcpyHostToDevice, c->stream));
+    dpk::RefineArgs a = refine_args(c, c->pat.p, n, cell, mode, c->ok.p);
+    rc = launch_timed(c, a, c->stream);
+    if (rc != DP_OK)
+        return rc;
+    DP_HIP(c, hipMemcpyAsync(inout, c->pat.p, sizeof(dp_patch) * n, hipMemcpyDeviceToHost, c->stream));
+    if (accept_out)
+        DP_HIP(c, hipMemcpyAsync(accept_out, c->ok.p, n, hipMemcpyDeviceToHost, c->stream));
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    return DP_OK;
+}
+
+extern "C" int dp_eval_batch(dp_ctx *c, const dp_patch *in, int n, int cell, float *score_out)
+{
+    int rc = check_refine(c, n, cell, DP_MODE_EVAL);
+    if (rc != DP_OK)
+        return rc;
+    if (n == 0)
+        return DP_OK;
+    if (!in || !score_out)
+        return fail(c, DP_E_ARG, "eval: null arrays");
+    std::vector<dp_patch> tmp(in, in + n);
+    rc = dp_refine_batch(c, tmp.data(), n, cell, DP_MODE_EVAL, nullptr);
+    if (rc != DP_OK)
+        return rc;
+    for (int i = 0; i < n; ++i)
+        score_out[i] = tmp[i].score;
+    return DP_OK;
+}
+
+extern "C" int dp_last_kernel_ms(dp_ctx *c, double *ms)
+{
+    if (!c || !ms)
+        return DP_E_ARG;
+    if (!c->timed)
+        return fail(c, DP_E_STATE, "no kernel timed yet");
+    DP_HIP(c, hipEventSynchronize(c->e1));
+    float f = 0.f;
+    DP_HIP(c, hipEventElapsedTime(&f, c->e0, c->e1));
+    *ms = f;
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// densify: seeds -> organizer -> generation-synchronous BFS
+// ---------------------------------------------------------------------------
+
+struct U8ToU32 {
+    __host__ __device__ uint32_t operator()(uint8_t v) const { return v; }
+};
+
+static int organize(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int32_t n, uint32_t seq0,
+                    int64_t base, int64_t parent0, int is_seed, int64_t *accepted_total)
+{
+    hipStream_t s = c->stream;
+    dpk::ClaimArgs ca{};
+    ca.views = c->d_views;
+    ca.cand = cand;
+    ca.ok = okf;
+    ca.n = n;
+    ca.seq0 = seq0;
+    ca.grid = c->grid.p;
+    ca.grid_scale = (double)c->opt.grid_scale;
+    DP_HIP(c, c->acc.reserve((size_t)n + 1));
+    DP_HIP(c, dpk::launch_claims(ca, s));
+    DP_HIP(c, dpk::launch_resolve(ca, c->acc.p, s));
+    DP_HIP(c, c->prefix.reserve((size_t)n + 1));
+    size_t tmp_bytes = 0;
+    hipcub::TransformInputIterator<uint32_t, U8ToU32, const uint8_t *> it(c->acc.p, U8ToU32());
+    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, it, c->prefix.p, n + 1, s));
+    DP_HIP(c, c->scan_tmp.reserve(tmp_bytes + 16));
+    // acc[n] must read as 0: scan n+1 items with a zeroed tail
+    DP_HIP(c, hipMemsetAsync(c->acc.p + n, 0, 1, s));
+    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp_bytes, it, c->prefix.p, n + 1, s));
+    uint32_t total = 0;
+    DP_HIP(c, hipMemcpyAsync(&total, c->prefix.p + n, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipStreamSynchronize(s));
+    if (base + (int64_t)total > (int64_t)c->store.cap)
+        return fail(c, DP_E_OOM, "patch store overflow");
+    DP_HIP(c, dpk::launch_append(c->d_views, c->V, cand, c->acc.p, c->prefix.p, n, c->store.p, base,
+                                 parent0, is_seed, s));
+    *accepted_total = total;
+    return DP_OK;
+}
+
+extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch **out, int64_t *n_out,
+                          dp_densify_stats *stats)
+{
+    if (!c || n < 0 || (n > 0 && !seeds) || !out || !n_out)
+        return fail(c, DP_E_ARG, "dp_densify: bad arguments");
+    if (!c->V)
+        return fail(c, DP_E_STATE, "dp_densify: no views");
+    auto t_start = std::chrono::steady_clock::now();
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const dp_options &o = c->opt;
+    dp_densify_stats st{};
+    st.seeds_in = n;
+    c->result.clear();
+    *out = nullptr;
+    *n_out = 0;
+
+    // organizer grid: every cell free (owner seq = UINT32_MAX)
+    DP_HIP(c, c->grid.reserve((size_t)c->grid_cells + 1));
+    DP_HIP(c, hipMemsetAsync(c->grid.p, 0xFF, sizeof(uint32_t) * ((size_t)c->grid_cells + 1), s));
+    // each accepted patch owns >= 2 cells exclusively: np <= cells / 2
+    const int64_t store_cap = c->grid_cells / 2 + 16;
+    DP_HIP(c, c->store.reserve((size_t)store_cap));
+    DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
+
+    double refine_ms = 0.0;
+    int64_t np = 0;
+    if (n > 0) {
+        std::vector<dp_patch> sp(n);
+        int rc = dp_seeds_to_patches(c, seeds, n, sp.data());
+        if (rc != DP_OK)
+            return rc;
+        DP_HIP(c, c->cand.reserve(n));
+        DP_HIP(c, c->ok.reserve(n));
+        DP_HIP(c, hipMemcpyAsync(c->cand.p, sp.data(), sizeof(dp_patch) * n, hipMemcpyHostToDevice, s));
+        // seed.cpp:110-144: FilterPatches then OptimizePatches at the seed cell size
+        dpk::RefineArgs a = refine_args(c, c->cand.p, n, o.seed_cell_size, DP_MODE_SEED, c->ok.p);
+        rc = launch_timed(c, a, s);
+        if (rc != DP_OK)
+            return rc;
+        double ms = 0.0;
+        if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
+            return rc;
+        refine_ms += ms;
+        // PatchOrganizer::SetSeeds: TryInsert in seed order (seq = seed index)
+        rc = organize(c, c->cand.p, c->ok.p, n, 0u, 0, 0, 1, &np);
+        if (rc != DP_OK)
+            return rc;
+    }
+    st.seed_patches = np;
+    const uint32_t seq_base = (uint32_t)n;
+    int64_t head = 0;
+    int gens = 0;
+    while (head < np && head < o.max_pops) {
+        const int64_t F = np - head;
+        const int64_t nc64 = 4 * F;
+        if (nc64 > INT32_MAX)
+            return fail(c, DP_E_OOM, "generation too large");
+        const int32_t nc = (int32_t)nc64;
+        if ((uint64_t)seq_base + 4ull * (uint64_t)np > 0xFFFFFFF0ull)
+            return fail(c, DP_E_OOM, "sequence space exhausted");
+        DP_HIP(c, hipStreamSynchronize(s)); // previous append may still read cand
+        DP_HIP(c, c->cand.reserve(nc));
+        DP_HIP(c, c->ok.reserve(nc));
+        dpk::RefineArgs a = refine_args(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_EXPAND, c->ok.p);
+        a.parents = c->store.p;
+        a.parent0 = head;
+        int rc = launch_timed(c, a, s);
+        if (rc != DP_OK)
+            return rc;
+        double ms = 0.0;
+        if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
+            return rc;
+        refine_ms += ms;
+        const int64_t expandable = std::min<int64_t>(np, o.max_pops) - head;
+        st.candidates += 4 * expandable;
+        int64_t acc = 0;
+        rc = organize(c, c->cand.p, c->ok.p, nc, seq_base + 4u * (uint32_t)head, np, head, 0, &acc);
+        if (rc != DP_OK)
+            return rc;
+        head = np;
+        np += acc;
+        ++gens;
+    }
+    st.pops = std::min<int64_t>(np, o.max_pops);
+    c->result.resize((size_t)np);
+    if (np)
+        DP_HIP(c, hipMemcpyAsync(c->result.data(), c->store.p, sizeof(dp_patch) * np, hipMemcpyDeviceToHost, s));
+    unsigned long long ev = 0;
+    DP_HIP(c, hipMemcpyAsync(&ev, c->d_evals, sizeof(ev), hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipStreamSynchronize(s));
+    st.patches = np;
+    st.evals = (int64_t)ev;
+    st.generations = gens;
+    st.refine_ms = refine_ms;
+    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    if (stats)
+        *stats = st;
+    *out = c->result.empty() ? nullptr : c->result.data();
+    *n_out = np;
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic scenes
+// ---------------------------------------------------------------------------
+
+extern "C" void dp_synth_default(dp_synth_config *cfg)
+{
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->n_views = 8;
+    cfg->width = 640;
+    cfg->height = 480;
+    cfg->kind = 1;
+    cfg->seed = 20261015ull;
+    cfg->spread_deg = 35.0;
+    cfg->seed_stride_px = 32.0;
+    cfg->depth_noise = 0.005;
+}
+
+static const double kSynthDistance = 1.8;
+
+extern "C" int dp_synth_cameras(const dp_synth_config *cfg, double *P)
+{
+    if (!cfg || !P || cfg->n_views <= 0 || cfg->n_views > DP_MAX_VIEWS || cfg->width <= 0 || cfg->height <= 0)
+        return DP_E_ARG;
+    const int V = cfg->n_views;
+    const double spread = cfg->spread_deg * 3.14159265358979323846 / 180.0;
+    const double golden = 2.39996322972865332;
+    const double f = 0.8 * cfg->width, cx = 0.5 * cfg->width, cy = 0.5 * cfg->height;
+    for (int v = 0; v < V; ++v) {
+        const double th = spread * std::sqrt((v + 0.5) / V);
+        const double ph = golden * v;
+        const double C[3] = {kSynthDistance * std::sin(th) * std::cos(ph),
+                             kSynthDistance * std::sin(th) * std::sin(ph), kSynthDistance * std::cos(th)};
+        double z[3] = {-C[0] / kSynthDistance, -C[1] / kSynthDistance, -C[2] / kSynthDistance};
+        const double down[3] = {0.0, -1.0, 0.0};
+        double x[3], y[3];
+        dpg::cross3(down, z, x);
+        const double xn = std::sqrt(dpg::dot3(x, x));
+        for (int i = 0; i < 3; ++i)
+            x[i] /= xn;
+        dpg::cross3(z, x, y);
+        const double *R[3] = {x, y, z};
+        const double K[3][3] = {{f, 0.0, cx}, {0.0, f, cy}, {0.0, 0.0, 1.0}};
+        double Rt[3][4];
+        for (int r = 0; r < 3; ++r) {
+            for (int k = 0; k < 3; ++k)
+                Rt[r][k] = R[r][k];
+            Rt[r][3] = -dpg::dot3(R[r], C);
+        }
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 4; ++k)
+                P[12 * v + 4 * r + k] = (K[r][0] * Rt[0][k] + K[r][1] * Rt[1][k]) + K[r][2] * Rt[2][k];
+    }
+    return DP_OK;
+}
+
+static int render_cam(const dp_synth_config *cfg, const double *P, int v, dps::RenderCam &rc)
+{
+    double C[3], K[9], E[12];
+    if (dp_view_geometry(P + 12 * v, C, K, E, nullptr) != DP_OK)
+        return DP_E_ARG;
+    std::memset(&rc, 0, sizeof(rc));
+    for (int i = 0; i < 3; ++i) {
+        rc.C[i] = C[i];
+        for (int j = 0; j < 3; ++j)
+            rc.Rt[3 * i + j] = E[4 * j + i];
+    }
+    rc.f = K[0];
+    rc.cx = K[2];
+    rc.cy = K[5];
+    rc.W = cfg->width;
+    rc.H = cfg->height;
+    rc.kind = cfg->kind;
+    rc.seed = cfg->seed;
+    rc.px_world = kSynthDistance / (0.8 * cfg->width);
+    return DP_OK;
+}
+
+extern "C" int dp_synth_render_host(const dp_synth_config *cfg, const double *P, int v, uint8_t *bgr)
+{
+    if (!cfg || !P || !bgr || v < 0 || v >= cfg->n_views)
+        return DP_E_ARG;
+    dps::RenderCam rc;
+    if (render_cam(cfg, P, v, rc) != DP_OK)
+        return DP_E_ARG;
+    parallel_for(rc.H, [&](int64_t y) {
+        for (int x = 0; x < rc.W; ++x) {
+            const uint32_t px = dps::render_pixel(rc, x, (int)y);
+            uint8_t *o = bgr + ((size_t)y * rc.W + x) * 3;
+            o[0] = (uint8_t)(px & 255u);
+            o[1] = (uint8_t)((px >> 8) & 255u);
+            o[2] = (uint8_t)((px >> 16) & 255u);
+        }
+    });
+    return DP_OK;
+}
+
+namespace {
+__global__ void render_kernel(dps::RenderCam rc, uint32_t *out)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x < rc.W)
+        out[(size_t)y * rc.W + x] = dps::render_pixel(rc, x, y);
+}
+} // namespace
+
+extern "C" int dp_synth_render_device(dp_ctx *c, const dp_synth_config *cfg, const double *P, int v,
+                                      void *d_bgra, void *stream)
+{
+    if (!c || !cfg || !P || !d_bgra || v < 0 || v >= cfg->n_views)
+        return fail(c, DP_E_ARG, "render: bad arguments");
+    dps::RenderCam rc;
+    if (render_cam(cfg, P, v, rc) != DP_OK)
+        return fail(c, DP_E_ARG, "render: singular camera");
+    hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipLaunchKernelGGL(render_kernel, dim3((rc.W + 255) / 256, rc.H), dim3(256), 0, s, rc, (uint32_t *)d_bgra);
+    DP_HIP(c, hipGetLastError());
+    return DP_OK;
+}
+
+extern "C" int64_t dp_synth_seeds(const dp_synth_config *cfg, const double *P, double *xyz, int64_t cap)
+{
+    if (!cfg || !P)
+        return DP_E_ARG;
+    std::mt19937_64 rng(cfg->seed);
+    const double two53 = 1.0 / 9007199254740992.0;
+    int64_t cnt = 0;
+    const double stride = cfg->seed_stride_px > 0 ? cfg->seed_stride_px : 32.0;
+    for (int v = 0; v < cfg->n_views; ++v) {
+        dps::RenderCam rc;
+        if (render_cam(cfg, P, v, rc) != DP_OK)
+            return DP_E_ARG;
+        for (double y = 0.5 * stride; y < rc.H; y += stride)
+            for (double x = 0.5 * stride; x < rc.W; x += stride) {
+                const double u1 = ((double)(rng() >> 11) + 0.5) * two53;
+                const double u2 = ((double)(rng() >> 11) + 0.5) * two53;
+                const double eps = std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+                double d[3], X[3];
+                dps::ray_dir(rc, x, y, d);
+                if (!dps::intersect(rc, d, X))
+                    continue;
+                const double k = 1.0 + cfg->depth_noise * eps;
+                if (xyz && cnt < cap)
+                    for (int i = 0; i < 3; ++i)
+                        xyz[3 * cnt + i] = rc.C[i] + (X[i] - rc.C[i]) * k;
+                ++cnt;
+            }
+    }
+    return cnt;
+}
+
+// ---------------------------------------------------------------------------
+// probes (densepoints_probe.h)
+// ---------------------------------------------------------------------------
+
+extern "C" void dp_probe_sincos(double x, double *s, double *c) { dpm::sincos(x, *s, *c); }
+extern "C" double dp_probe_acos(double x) { return dpm::acos(x); }
+
+extern "C" int dp_probe_texture(const double P[12], int32_t W, int32_t H, const uint8_t *bgr,
+                                const double corners[12], int cell, int32_t *gray)
+{
+    dpg::ViewDev v;
+    if (view_from_P(P, W, H, 8, v) != DP_OK)
+        return -1;
+    dpg::TexMap tm;
+    if (!dpg::texture_map(v, corners, cell, tm))
+        return 0;
+    auto px = [&](int x, int y) {
+        const uint8_t *p = bgr + ((size_t)(tm.tly + y) * W + (size_t)(tm.tlx + x)) * 3;
+        return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+    };
+    for (int py = 0; py < cell; ++py)
+        for (int pxx = 0; pxx < cell; ++pxx) {
+            const dpg::Tap t = dpg::window_tap(tm, pxx, py);
+            gray[py * cell + pxx] = dpg::blend_gray(px(t.x0, t.y0), px(t.x1, t.y0), px(t.x0, t.y1),
+                                                    px(t.x1, t.y1), t.fx, t.fy);
+        }
+    return 1;
+}
+
+extern "C" double dp_probe_ncc(int32_t N, int32_t Sa, int32_t Saa, int32_t Sb, int32_t Sbb, int32_t Sab,
+                               double denom_min)
+{
+    return dpg::ncc_finish(N, Sa, Saa, Sb, Sbb, Sab, denom_min);
+}
+
+namespace {
+__global__ void probe_math_kernel(const double *x, int n, double *out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    double s, c;
+    dpm::sincos(x[i], s, c);
+    out[4 * i + 0] = s;
+    out[4 * i + 1] = c;
+    out[4 * i + 2] = dpm::acos(x[i]);
+    out[4 * i + 3] = sqrt(fabs(x[i]));
+}
+} // namespace
+
+extern "C" int dp_probe_math_device(const double *x, int n, double *out)
+{
+    if (n <= 0 || !x || !out)
+        return DP_E_ARG;
+    double *dx = nullptr, *dout = nullptr;
+    if (hipMalloc(&dx, sizeof(double) * n) != hipSuccess)
+        return DP_E_HIP;
+    if (hipMalloc(&dout, sizeof(double) * 4 * n) != hipSuccess) {
+        hipFree(dx);
+        return DP_E_HIP;
+    }
+    hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(probe_math_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, dx, n, dout);
+    hipError_t e = hipMemcpy(out, dout, sizeof(double) * 4 * n, hipMemcpyDeviceToHost);
+    hipFree(dx);
+    hipFree(dout);
+    return e == hipSuccess ? DP_OK : DP_E_HIP;
+}

@@ -1,0 +1,263 @@
+// dp_geom.h -- patch geometry, projective window map, fixed-point bilinear
+// sampling and the NCC finish, compiled for BOTH the gfx950 kernels and the
+// host (seed conversion, probes).  This is the product's statement of the
+// arithmetic spec in DESIGN.md ("Arithmetic spec"); every expression is one
+// IEEE rounding in a fixed order (build with -ffp-contract=off).
+//
+// Reference anchors (manlito/densepoints):
+//   View::ProjectPoint / IsPointInside      modules/core/types.cpp:70-84
+//   Patch::GetProjectedXYAxisAndScale       methods/pmvs/patch.cpp:86-104
+//   Patch::ComputePatchToViewHomography     methods/pmvs/patch.cpp:111-164
+//   Optimization::GetProjectedTextures      methods/pmvs/optimization.cpp:14-56
+//   NCCScore / ToFloatMat                   modules/core/error_measurements.cpp:4-60
+//   Optimization::UnparametrizePatch        methods/pmvs/optimization.cpp:78-96
+#pragma once
+
+#include "dp_detmath.h"
+#include <stdint.h>
+
+namespace dpg {
+
+struct ViewDev {
+    double P[12];       // 3x4 row-major projection
+    double C[3];        // camera centre
+    double xr[3];       // GetXAxis().normalized()
+    int32_t W, H;       // loaded image size (IsPointInside bounds)
+    int32_t pitch;      // pixels per row in the BGRA8 plane
+    int32_t gw, gh;     // organizer grid (W/grid_scale, H/grid_scale)
+    int32_t grid_off_hi;
+    int64_t grid_off;   // offset of this view's cells in the grid pool
+    const uint32_t *img; // BGRA8, B in the low byte
+};
+
+DP_HD double dot3(const double *a, const double *b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+
+DP_HD void cross3(const double *a, const double *b, double *o)
+{
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+DP_HD void project(const double *P, double x, double y, double z, double &u, double &v)
+{
+    const double h0 = ((P[0] * x + P[1] * y) + P[2] * z) + P[3];
+    const double h1 = ((P[4] * x + P[5] * y) + P[6] * z) + P[7];
+    const double h2 = ((P[8] * x + P[9] * y) + P[10] * z) + P[11];
+    u = h0 / h2;
+    v = h1 / h2;
+}
+
+DP_HD bool inside(double u, double v, int32_t W, int32_t H)
+{
+    return u > 0.0 && u < (double)W && v > 0.0 && v < (double)H;
+}
+
+// Window corners for one evaluation.  Axes and dx come from the CANDIDATE
+// pose (nn, pp); the corners are centred on the patch's STORED position Xs
+// (patch.cpp:120-123 uses GetPosition()).  Returns false when dx == 0
+// (optimization.cpp:27 LOG(FATAL) -> degenerate flag).
+DP_HD bool window_corners(const ViewDev &rv, const double *Xs, const double *nn, const double *pp,
+                          int cell, double *c12)
+{
+    double y[3];
+    cross3(nn, rv.xr, y);
+    double cu, cv, qu, qv;
+    project(rv.P, pp[0], pp[1], pp[2], cu, cv);
+    project(rv.P, pp[0] + rv.xr[0], pp[1] + rv.xr[1], pp[2] + rv.xr[2], qu, qv);
+    const double du = qu - cu, dv = qv - cv;
+    const double dx = sqrt(du * du + dv * dv);
+    if (dx == 0.0)
+        return false;
+    const double scale = (double)(cell / 2) / dx;
+    for (int i = 0; i < 3; ++i) {
+        const double sx = scale * rv.xr[i];
+        const double sy = scale * y[i];
+        c12[0 + i] = (Xs[i] - sx) - sy;
+        c12[3 + i] = (Xs[i] + sx) - sy;
+        c12[6 + i] = (Xs[i] + sx) + sy;
+        c12[9 + i] = (Xs[i] - sx) + sy;
+    }
+    return true;
+}
+
+// Sampling map of one view: window pixel (x, y) -> ROI coordinates, plus ROI.
+struct TexMap {
+    double m0, m1, m2, m3, m4, m5, m6, m7; // m8 == 1
+    int32_t tlx, tly, w, h;
+};
+
+// Returns false for the reference's empty texture (corner outside the view,
+// empty ROI, or a degenerate quad).
+DP_HD bool texture_map(const ViewDev &v, const double *c12, int cell, TexMap &tm)
+{
+    int tlx = v.W, tly = v.H, brx = 0, bry = 0;
+    float fx[4], fy[4];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 1
+#endif
+    for (int i = 0; i < 4; ++i) {
+        double u, w;
+        project(v.P, c12[3 * i], c12[3 * i + 1], c12[3 * i + 2], u, w);
+        if (!inside(u, w, v.W, v.H))
+            return false;
+        fx[i] = (float)u;
+        fy[i] = (float)w;
+        const int cx = (int)ceil(u), cy = (int)ceil(w);
+        const int lx = (int)floor(u), ly = (int)floor(w);
+        tlx = cx < tlx ? cx : tlx;
+        tly = cy < tly ? cy : tly;
+        brx = lx > brx ? lx : brx;
+        bry = ly > bry ? ly : bry;
+    }
+    const int rw = brx - tlx, rh = bry - tly;
+    if (rw <= 0 || rh <= 0)
+        return false;
+    double x[4], y[4];
+    const float ftx = (float)tlx, fty = (float)tly;
+    for (int i = 0; i < 4; ++i) {
+        x[i] = (double)(fx[i] - ftx);
+        y[i] = (double)(fy[i] - fty);
+    }
+    // square [0,n]^2 -> quad (projective, Heckbert), the inverse of the
+    // reference's findHomography(quad -> square) used by warpPerspective.
+    const double sx = ((x[0] - x[1]) + x[2]) - x[3];
+    const double sy = ((y[0] - y[1]) + y[2]) - y[3];
+    const double ax = x[1] - x[2], bx = x[3] - x[2];
+    const double ay = y[1] - y[2], by = y[3] - y[2];
+    const double det = ax * by - bx * ay;
+    if (det == 0.0)
+        return false;
+    const double g = (sx * by - bx * sy) / det;
+    const double h = (ax * sy - sx * ay) / det;
+    const double n = (double)cell;
+    tm.m0 = ((x[1] - x[0]) + g * x[1]) / n;
+    tm.m1 = ((x[3] - x[0]) + h * x[3]) / n;
+    tm.m2 = x[0];
+    tm.m3 = ((y[1] - y[0]) + g * y[1]) / n;
+    tm.m4 = ((y[3] - y[0]) + h * y[3]) / n;
+    tm.m5 = y[0];
+    tm.m6 = g / n;
+    tm.m7 = h / n;
+    tm.tlx = tlx;
+    tm.tly = tly;
+    tm.w = rw;
+    tm.h = rh;
+    return true;
+}
+
+// warpPerspective(INTER_LINEAR) coordinate of window pixel (px, py):
+// 1/32-px fixed point, round half to even (saturate_cast<int>).
+struct Tap {
+    int32_t x0, x1, y0, y1; // clamped ROI-relative taps (BORDER_REPLICATE)
+    int32_t fx, fy;         // 5-bit fractions
+};
+
+DP_HD Tap window_tap(const TexMap &tm, int px, int py)
+{
+    const double X0 = tm.m1 * (double)py + tm.m2;
+    const double Y0 = tm.m4 * (double)py + tm.m5;
+    const double W0 = tm.m7 * (double)py + 1.0;
+    double W = W0 + tm.m6 * (double)px;
+    W = (W != 0.0) ? 32.0 / W : 0.0;
+    double X = (X0 + tm.m0 * (double)px) * W;
+    double Y = (Y0 + tm.m3 * (double)px) * W;
+    X = X < 2147483647.0 ? X : 2147483647.0;
+    X = X > -2147483648.0 ? X : -2147483648.0;
+    Y = Y < 2147483647.0 ? Y : 2147483647.0;
+    Y = Y > -2147483648.0 ? Y : -2147483648.0;
+    const int32_t ix = (int32_t)rint(X);
+    const int32_t iy = (int32_t)rint(Y);
+    const int32_t sx = ix >> 5, sy = iy >> 5;
+    Tap t;
+    t.fx = ix & 31;
+    t.fy = iy & 31;
+    const int32_t wm = tm.w - 1, hm = tm.h - 1;
+    t.x0 = sx < 0 ? 0 : (sx > wm ? wm : sx);
+    t.x1 = sx + 1 < 0 ? 0 : (sx + 1 > wm ? wm : sx + 1);
+    t.y0 = sy < 0 ? 0 : (sy > hm ? hm : sy);
+    t.y1 = sy + 1 < 0 ? 0 : (sy + 1 > hm ? hm : sy + 1);
+    return t;
+}
+
+// Bilinear blend of four BGRA8 pixels and BGR2GRAY.  OpenCV's 15-bit weights
+// are 32*w' with w' = (32-fy)(32-fx) etc. (the (0,0) entry 32767/0/0/1
+// rounds to p00 exactly like w' = 1024/0/0/0), so
+// (sum 32w'p + 2^14) >> 15 == (sum w'p + 512) >> 10 for u8 inputs.
+DP_HD int32_t blend_gray(uint32_t p00, uint32_t p01, uint32_t p10, uint32_t p11, int32_t fx, int32_t fy)
+{
+    const int32_t w00 = (32 - fy) * (32 - fx), w01 = (32 - fy) * fx;
+    const int32_t w10 = fy * (32 - fx), w11 = fy * fx;
+    int32_t ch[3];
+    for (int k = 0; k < 3; ++k) {
+        const int s = 8 * k;
+        const int32_t a = (int32_t)((p00 >> s) & 255u) * w00 + (int32_t)((p01 >> s) & 255u) * w01 +
+                          (int32_t)((p10 >> s) & 255u) * w10 + (int32_t)((p11 >> s) & 255u) * w11;
+        ch[k] = (a + 512) >> 10;
+    }
+    return (ch[0] * 1868 + ch[1] * 9617 + ch[2] * 4899 + 8192) >> 14;
+}
+
+// NCC from exact integer moments (error_measurements.cpp:36-60 restated).
+DP_HD double ncc_finish(int32_t N, int32_t Sa, int32_t Saa, int32_t Sb, int32_t Sbb, int32_t Sab,
+                        double denom_min)
+{
+    const int64_t n = N;
+    const double dn = (double)n;
+    const double dn2 = (double)(n * n);
+    const double sa = sqrt((double)(n * (int64_t)Saa - (int64_t)Sa * Sa) / dn2);
+    const double sb = sqrt((double)(n * (int64_t)Sbb - (int64_t)Sb * Sb) / dn2);
+    double den = sa * sb;
+    den = (denom_min < den) ? den : denom_min;
+    const double num = (double)(n * (int64_t)Sab - (int64_t)Sa * Sb) / dn;
+    return (num / den) / dn;
+}
+
+// (depth, roll, pitch) -> candidate normal / position (optimization.cpp:78-96)
+DP_HD void unparametrize(const double *C, const double *Xs, const double *ns, double d, double roll,
+                         double pitch, double *nn, double *pp)
+{
+    for (int i = 0; i < 3; ++i)
+        pp[i] = C[i] + (1.0 + d) * (Xs[i] - C[i]);
+    double sa, ca, sb, cb;
+    dpm::sincos(roll, sa, ca);
+    dpm::sincos(pitch, sb, cb);
+    const double r0[3] = {cb, 0.0, -sb};
+    const double r1[3] = {sa * sb, ca, cb * sa};
+    const double r2[3] = {ca * sb, -sa, ca * cb};
+    nn[0] = (r0[0] * ns[0] + r0[1] * ns[1]) + r0[2] * ns[2];
+    nn[1] = (r1[0] * ns[0] + r1[1] * ns[1]) + r1[2] * ns[2];
+    nn[2] = (r2[0] * ns[0] + r2[1] * ns[1]) + r2[2] * ns[2];
+}
+
+// Patch::InitRelatedImages classification of one view (patch.cpp:36-47):
+// 0 = skipped, 1 = visible, 2 = candidate.
+DP_HD int classify_view(const ViewDev &v, const double *X, const double *n, double vis_angle,
+                        double cand_angle)
+{
+    double u, w;
+    project(v.P, X[0], X[1], X[2], u, w);
+    if (!inside(u, w, v.W, v.H))
+        return 0;
+    const double d[3] = {X[0] - v.C[0], X[1] - v.C[1], X[2] - v.C[2]};
+    const double ang = dpm::acos(dot3(n, d) / sqrt(dot3(d, d)));
+    if (ang < vis_angle)
+        return 1;
+    if (ang < cand_angle)
+        return 2;
+    return 0;
+}
+
+// (size_t)(double) as compiled on x86-64: truncation toward zero, values
+// <= -1 wrap to huge (out of bounds); -1 marks out of bounds here.
+DP_HD int64_t grid_coord(double pix, double scale)
+{
+    const double q = pix / scale;
+    if (!(q > -1.0))
+        return -1;
+    if (q >= 9.0e18)
+        return INT64_MAX;
+    return (int64_t)q;
+}
+
+} // namespace dpg

@@ -1,0 +1,52 @@
+// dp_internal.h -- shared between the C-ABI host code and the gfx950 kernels.
+#pragma once
+
+#include "../../include/densepoints.h"
+#include "dp_geom.h"
+#include <hip/hip_runtime.h>
+
+namespace dpk {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+
+// Arguments of the fused refine kernel (one wavefront per patch).
+struct RefineArgs {
+    const dpg::ViewDev *views;
+    int32_t V;
+    int32_t cell;
+    int32_t mode;
+    int32_t n;
+    dp_options opt;
+    dp_patch *patches;       // in/out (EVAL..EXPAND on existing patches)
+    uint8_t *accept;         // optional
+    uint32_t *work;          // dequeue counter (zeroed per launch)
+    unsigned long long *evals; // optional: total objective evaluations
+    // expansion-generation fields (mode DP_MODE_EXPAND with parents != null)
+    const dp_patch *parents; // queue; child c expands parents[parent0 + c/4] direction c%4
+    int64_t parent0;
+    int64_t max_pops;
+};
+
+// organizer / BFS kernels
+struct ClaimArgs {
+    const dpg::ViewDev *views;
+    const dp_patch *cand;    // candidates of this generation, in seq order
+    const uint8_t *ok;       // filter passed
+    int32_t n;
+    uint32_t seq0;           // seq of cand[0]; seq grows by one per candidate
+    uint32_t *grid;          // cell owner = min seq
+    double grid_scale;
+};
+
+hipError_t launch_refine(const RefineArgs &a, hipStream_t s);
+hipError_t launch_claims(const ClaimArgs &a, hipStream_t s);
+hipError_t launch_resolve(const ClaimArgs &a, uint8_t *accepted, hipStream_t s);
+hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand, const uint8_t *accepted,
+                         const uint32_t *prefix, int32_t n, dp_patch *store, int64_t base,
+                         int64_t parent0, int is_seed, hipStream_t s);
+hipError_t launch_render(const dp_synth_config &cfg, const double *P, uint32_t *out, int v,
+                         hipStream_t s);
+
+} // namespace dpk

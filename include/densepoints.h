@@ -1,0 +1,196 @@
+/*
+ * densepoints.h -- C ABI of the MI355X-native PMVS patch-loop engine
+ * (libdensepoints.so, built from densepoints_amd/csrc/).
+ *
+ * Drop-in boundary for the reference's hot path (manlito/densepoints):
+ *   operator seam  methods/pmvs/optimization.h:11-45 (Optimization,
+ *                  virtual Optimize / FilterByErrorMeasurement /
+ *                  GetProjectedTextures), methods/pmvs/optimization_opencv.h:10-14
+ *   scoring op     modules/core/error_measurements.h:11 (NCCScore)
+ *   callers        methods/pmvs/seed.cpp:110-144, expand.cpp:103-143,
+ *                  pmvs.cpp:11-43 (PMVS::AddCamera / Run)
+ * The reference constructs one Optimization per patch on the stack and calls
+ * it from OpenMP workers; this ABI takes BATCHES of patches (one wavefront
+ * per patch on the GPU).  Plain C: POD structs, pointers and sizes only.
+ *
+ * All functions return DP_OK (0) or a negative DP_E_* status; the message of
+ * the last failure on a context is available from dp_last_error().
+ * A context is single-host-thread; use one context per GPU.
+ */
+#ifndef DENSEPOINTS_H
+#define DENSEPOINTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DP_ABI_VERSION 1
+
+/* ---- status codes (replace LOG(FATAL) / cv::Exception) ------- */
+#define DP_OK 0
+#define DP_E_ARG (-1)          /* bad argument / unsupported option value          */
+#define DP_E_HIP (-2)          /* HIP runtime failure (message in dp_last_error)   */
+#define DP_E_OOM (-3)          /* device or host allocation failed                 */
+#define DP_E_DEGENERATE (-4)   /* dx == 0 (optimization.cpp:27 LOG(FATAL))         */
+#define DP_E_STATE (-5)        /* call order violated (e.g. no views set)          */
+#define DP_E_NODEVICE (-6)     /* no HIP device available                          */
+
+#define DP_MAX_VIEWS 128       /* visible/candidate sets are 128-bit masks          */
+#define DP_MAX_CELL 16         /* n x n window, n <= 16 (reference uses 16 and 11)  */
+
+/* ---- options: every hot-path knob, reference defaults --- */
+typedef struct dp_options {
+    int32_t seed_cell_size;       /* 16  matcher.h:25, used at seed.cpp:117,135       */
+    int32_t expand_cell_size;     /* 11  expand.h:12, used at expand.cpp:129          */
+    int32_t grid_scale;           /* 8   patch_organizer.h:43                          */
+    int32_t max_patches_per_cell; /* 1   patch_organizer.h:42 (only 1 is supported)    */
+    int32_t min_visible;          /* 3   optimization.h:17                             */
+    int32_t min_expand_visible;   /* 2   expand.cpp:67                                 */
+    int32_t nm_max_evals;         /* 500 optimization_opencv.cpp:60                    */
+    int32_t reserved0;
+    double ncc_threshold;         /* 0.6  optimization.h:16                            */
+    double visible_angle;         /* 0.78 patch.h:56                                   */
+    double candidate_angle;       /* 1.04 patch.h:57                                   */
+    double nm_step[3];            /* 0.02, 0.2, 0.2 optimization_opencv.cpp:56         */
+    double nm_eps;                /* 1e-4 optimization_opencv.cpp:60                   */
+    double ncc_denom_min;         /* 0.1  error_measurements.cpp:57                    */
+    int64_t max_pops;             /* 1e7  expand.cpp:95                                */
+} dp_options;
+
+/* ---- patch record: pcl::PointXYZRGBNormal + Patch bookkeeping (patch.h:86-100)
+ * Ascending view lists (visible_images_, candidate_images_) are stored as
+ * 128-bit masks, which is lossless because the reference only ever builds
+ * them in ascending order (patch.cpp:37-47) and erases elements in place. */
+typedef struct dp_patch {
+    float pos[3];        /* centre, f32 as stored by Patch::SetPosition          */
+    float normal[3];     /* f32 as stored by Patch::SetNormal                     */
+    uint32_t ref;        /* reference view (Patch::reference_image_)             */
+    uint32_t seq;        /* organizer / queue index (dp_densify output)           */
+    uint64_t vis[2];     /* visible_images_ bitmask                               */
+    uint64_t cand[2];    /* candidate_images_ bitmask                             */
+    float score;         /* mean NCC of the last filter evaluation (extension)    */
+    uint32_t evals;      /* objective evaluations spent on this patch (E)         */
+    uint8_t rgb[3];      /* Patch::ComputeColor (patch.cpp:51-73)                 */
+    uint8_t flags;       /* DP_PATCH_*                                            */
+    uint32_t parent;     /* parent queue index; 0xFFFFFFFF for seed patches       */
+} dp_patch;
+
+#define DP_PATCH_ACCEPTED 1u
+#define DP_PATCH_DEGENERATE 2u
+
+/* ---- refine modes: which reference call sequence runs per patch ---------- */
+#define DP_MODE_EVAL 0    /* one evaluation: scores only, no mutation            */
+#define DP_MODE_FILTER 1  /* Optimization::FilterByErrorMeasurement (opt.cpp:98)*/
+#define DP_MODE_NM 2      /* OptimizationOpenCV::Optimize (opencv.cpp:44-78)     */
+#define DP_MODE_SEED 3    /* Seed::FilterPatches then OptimizePatches            */
+#define DP_MODE_EXPAND 4  /* Optimize -> InitRelatedImages -> Filter (expand.cpp:127-135) */
+
+/* ---- images: BGR8 as cv::imread returns it (types.cpp:9) ----------------- */
+typedef struct dp_image {
+    int32_t width;
+    int32_t height;
+    int32_t stride;      /* bytes per row; 0 = 3*width                            */
+    int32_t reserved;
+    const uint8_t *bgr;  /* host pointer, copied by dp_set_views                 */
+} dp_image;
+
+typedef struct dp_densify_stats {
+    int64_t seeds_in;          /* seed points given                               */
+    int64_t seed_patches;      /* seed patches accepted by the organizer           */
+    int64_t patches;           /* total patches (seed + expanded)                  */
+    int64_t pops;              /* queue pops (expand.cpp:87)                       */
+    int64_t candidates;        /* expansion candidates refined (4 per expanded pop)*/
+    int64_t evals;             /* objective evaluations in all refine kernels      */
+    int32_t generations;       /* BFS generations                                  */
+    int32_t reserved;
+    double refine_ms;          /* device time in the fused refine kernels          */
+    double total_ms;           /* wall time of dp_densify                          */
+} dp_densify_stats;
+
+typedef struct dp_ctx dp_ctx;
+
+/* defaults identical to the reference constructors (list in dp_options) */
+void dp_default_options(dp_options *opt);
+int dp_abi_version(void);
+
+/* Create a context bound to HIP device `device`. */
+int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out);
+int dp_ctx_destroy(dp_ctx *ctx);
+const char *dp_last_error(const dp_ctx *ctx);
+int dp_set_options(dp_ctx *ctx, const dp_options *opt);
+
+/* PMVS::AddCamera (pmvs.cpp:11-20) for all views at once.  P: V x 3x4
+ * row-major fp64; images BGR8 host buffers, uploaded as BGRA8 SoA planes. */
+int dp_set_views(dp_ctx *ctx, int V, const double *P, const dp_image *images);
+
+/* Same, but the views' BGRA8 pixels are already resident on this device
+ * (dev_bgra[v] points to height*pitch_px uint32 pixels, B in the low byte).
+ * No copy: the caller keeps the buffers alive while the context uses them. */
+int dp_set_views_device(dp_ctx *ctx, int V, const double *P, const int32_t *width,
+                        const int32_t *height, const int32_t *pitch_px,
+                        const void *const *dev_bgra);
+
+/* View::SetProjectionMatrix (types.cpp:28-68): camera centre, K (normalised
+ * K(2,2)=1, positive diagonal), [R|t] and the camera x-axis (row 0 of R). */
+int dp_view_geometry(const double P[12], double C[3], double K[9], double E[12],
+                     double xaxis[3]);
+
+/* Seed::CreatePatchesFromPoints (seed.cpp:26-54): ref = nearest camera,
+ * normal = unit ray, InitRelatedImages.  Host arrays. */
+int dp_seeds_to_patches(dp_ctx *ctx, const double *xyz, int n, dp_patch *out);
+
+/* One objective evaluation per patch at its stored pose: score_out[i] = mean
+ * NCC against texture 0 over the visible views (-1 if none). Host arrays. */
+int dp_eval_batch(dp_ctx *ctx, const dp_patch *in, int n, int cell, float *score_out);
+
+/* Fused evaluate + refine + filter over a batch (host arrays).  `mode` is a
+ * DP_MODE_*; accept_out[i] = 1 if patch i survives (may be NULL).
+ * This is the reference's Optimization operator applied to n patches. */
+int dp_refine_batch(dp_ctx *ctx, dp_patch *inout, int n, int cell, int mode,
+                    uint8_t *accept_out);
+
+/* Same with device-resident arrays, asynchronous on `stream` (hipStream_t,
+ * NULL = the context's stream).  Used by bench.py with torch-owned buffers. */
+int dp_refine_batch_device(dp_ctx *ctx, dp_patch *d_inout, int n, int cell, int mode,
+                           uint8_t *d_accept, void *stream);
+
+/* Seeds -> filter+refine (cell 16) -> organizer -> BFS expansion (cell 11):
+ * PMVS::Run minus feature matching (pmvs.cpp:22-43).  The returned patch
+ * array is owned by the context and valid until the next call/destroy. */
+int dp_densify(dp_ctx *ctx, const double *seeds_xyz, int n, const dp_patch **out,
+               int64_t *n_out, dp_densify_stats *stats);
+
+/* Elapsed device milliseconds of the most recent refine kernel launch, timed
+ * with HIP events on the stream the kernel ran on. */
+int dp_last_kernel_ms(dp_ctx *ctx, double *ms);
+
+/* ---- synthetic scenes (build extension: deterministic test/bench input) -- */
+typedef struct dp_synth_config {
+    int32_t n_views;       /* V                                                  */
+    int32_t width, height; /* image size                                         */
+    int32_t kind;          /* 0 = textured plane, 1 = 3x3 tilted-facet heightfield */
+    uint64_t seed;         /* RNG seed (default 20261015)                       */
+    double spread_deg;     /* camera spread around the surface normal (35)      */
+    double seed_stride_px; /* seed grid stride in each nominal ref view (32)    */
+    double depth_noise;    /* relative seed depth noise sigma (0.005)           */
+} dp_synth_config;
+
+void dp_synth_default(dp_synth_config *cfg);
+/* Cameras (V x 12 projection matrices). */
+int dp_synth_cameras(const dp_synth_config *cfg, double *P_out);
+/* Render view v as BGR8 on the host (OpenMP), rows of 3*width bytes. */
+int dp_synth_render_host(const dp_synth_config *cfg, const double *P, int v, uint8_t *bgr_out);
+/* Render view v as BGRA8 into device memory (height*width uint32). */
+int dp_synth_render_device(dp_ctx *ctx, const dp_synth_config *cfg, const double *P, int v,
+                           void *d_bgra, void *stream);
+/* Seed points on the true surface with depth noise; returns count written
+ * (at most cap); xyz_out may be NULL to query the count. */
+int64_t dp_synth_seeds(const dp_synth_config *cfg, const double *P, double *xyz_out, int64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DENSEPOINTS_H */

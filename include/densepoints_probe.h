@@ -1,0 +1,32 @@
+/*
+ * densepoints_probe.h -- diagnostic entry points of libdensepoints.so.
+ *
+ * Host-compiled instances of the SAME arithmetic the gfx950 kernels run
+ * (densepoints_amd/csrc/dp_geom.h, dp_detmath.h), so the CPU test suite can
+ * check the product's spec against the oracle without a GPU, plus a device
+ * probe that runs the math on the GPU for the host==device check.  Not part
+ * of the reference surface.
+ */
+#ifndef DENSEPOINTS_PROBE_H
+#define DENSEPOINTS_PROBE_H
+
+#include "densepoints.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+void dp_probe_sincos(double x, double *s, double *c);
+double dp_probe_acos(double x);
+/* window texture of one view (BGR8 host image): returns 1 + gray[cell*cell], or 0 if empty */
+int dp_probe_texture(const double P[12], int32_t W, int32_t H, const uint8_t *bgr,
+                     const double corners[12], int cell, int32_t *gray);
+double dp_probe_ncc(int32_t N, int32_t Sa, int32_t Saa, int32_t Sb, int32_t Sbb, int32_t Sab,
+                    double denom_min);
+/* device run of sincos/acos/sqrt over n inputs (out: 4*n doubles s,c,acos(x),sqrt|x|) */
+int dp_probe_math_device(const double *x, int n, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

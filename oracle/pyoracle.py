@@ -1,0 +1,203 @@
+"""ctypes wrapper of oracle/build/liboracle.so -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module.  It is the checker, never the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+
+MODE_EVAL, MODE_FILTER, MODE_NM, MODE_SEED, MODE_EXPAND = range(5)
+
+PATCH_DTYPE = np.dtype(
+    [
+        ("pos", "<f4", 3),
+        ("normal", "<f4", 3),
+        ("ref", "<u4"),
+        ("seq", "<u4"),
+        ("vis", "<u8", 2),
+        ("cand", "<u8", 2),
+        ("score", "<f4"),
+        ("evals", "<u4"),
+        ("rgb", "u1", 3),
+        ("flags", "u1"),
+        ("parent", "<u4"),
+    ],
+    align=True,
+)
+
+
+class OrOptions(ctypes.Structure):
+    _fields_ = [
+        ("seed_cell_size", ctypes.c_int32),
+        ("expand_cell_size", ctypes.c_int32),
+        ("grid_scale", ctypes.c_int32),
+        ("max_patches_per_cell", ctypes.c_int32),
+        ("min_visible", ctypes.c_int32),
+        ("min_expand_visible", ctypes.c_int32),
+        ("nm_max_evals", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("ncc_threshold", ctypes.c_double),
+        ("visible_angle", ctypes.c_double),
+        ("candidate_angle", ctypes.c_double),
+        ("nm_step", ctypes.c_double * 3),
+        ("nm_eps", ctypes.c_double),
+        ("ncc_denom_min", ctypes.c_double),
+        ("max_pops", ctypes.c_int64),
+    ]
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def _load():
+    if not os.path.exists(LIB):
+        build()
+    L = ctypes.CDLL(LIB)
+    P = ctypes.c_void_p
+    sig = {
+        "or_default_options": (None, [P]),
+        "or_view_geometry": (ctypes.c_int, [P, P, P, P, P]),
+        "or_ncc_int": (ctypes.c_double, [P, P, ctypes.c_int, ctypes.c_double]),
+        "or_sincos": (None, [ctypes.c_double, P, P]),
+        "or_acos": (ctypes.c_double, [ctypes.c_double]),
+        "or_scene_create": (P, [ctypes.c_int, P, P, P, P, P]),
+        "or_scene_destroy": (None, [P]),
+        "or_scene_view_info": (ctypes.c_int, [P, ctypes.c_int, P, P]),
+        "or_texture": (ctypes.c_int, [P, ctypes.c_int, P, ctypes.c_int, P]),
+        "or_init_related": (ctypes.c_int, [P, P]),
+        "or_scores": (ctypes.c_int, [P, P, P, P, ctypes.c_int, P, P]),
+        "or_objective": (ctypes.c_double, [P, P, P, ctypes.c_int]),
+        "or_refine_batch": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]),
+        "or_seeds_to_patches": (ctypes.c_int, [P, P, ctypes.c_int, P]),
+        "or_expand_children": (ctypes.c_int, [P, P, P, P]),
+        "or_densify": (ctypes.c_int64, [P, P, ctypes.c_int, P, ctypes.c_int64, P, P]),
+        "or_color": (None, [P, P]),
+    }
+    for k, (r, a) in sig.items():
+        f = getattr(L, k)
+        f.restype = r
+        f.argtypes = a
+    return L
+
+
+lib = _load()
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def default_options() -> OrOptions:
+    o = OrOptions()
+    lib.or_default_options(ctypes.byref(o))
+    return o
+
+
+def options_from(opts) -> OrOptions:
+    """Copy a densepoints_amd Options (identical POD layout) or an OrOptions."""
+    if isinstance(opts, OrOptions):
+        return opts
+    o = OrOptions()
+    raw = bytes(opts.to_c())
+    ctypes.memmove(ctypes.byref(o), raw, ctypes.sizeof(o))
+    return o
+
+
+class Scene:
+    """CPU restatement of the reference's view set + patch loop."""
+
+    def __init__(self, P, images, options=None):
+        P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(-1, 12))
+        self.V = len(P)
+        self._imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+        W = np.array([im.shape[1] for im in self._imgs], dtype=np.int32)
+        H = np.array([im.shape[0] for im in self._imgs], dtype=np.int32)
+        ptrs = (ctypes.c_void_p * self.V)(*[im.ctypes.data for im in self._imgs])
+        self.opt = options_from(options) if options is not None else default_options()
+        self._h = lib.or_scene_create(self.V, _p(P), _p(W), _p(H), ptrs, ctypes.byref(self.opt))
+        if not self._h:
+            raise ValueError("or_scene_create failed")
+        self._keep = (P, W, H, ptrs)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.or_scene_destroy(self._h)
+            self._h = None
+
+    def seeds_to_patches(self, xyz):
+        xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 3)
+        out = np.zeros(len(xyz), dtype=PATCH_DTYPE)
+        lib.or_seeds_to_patches(self._h, _p(xyz), len(xyz), _p(out))
+        return out
+
+    def refine(self, patches, cell, mode, nthreads=0):
+        acc = np.zeros(len(patches), dtype=np.uint8)
+        rc = lib.or_refine_batch(self._h, _p(patches), len(patches), cell, mode, _p(acc), nthreads)
+        if rc != 0:
+            raise ValueError("or_refine_batch failed")
+        return acc
+
+    def texture(self, view, corners, cell):
+        c = np.ascontiguousarray(corners, dtype=np.float64).reshape(12)
+        g = np.zeros(cell * cell, dtype=np.int32)
+        ok = lib.or_texture(self._h, view, _p(c), cell, _p(g))
+        return (g.reshape(cell, cell) if ok else None)
+
+    def objective(self, patch, x, cell):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        p = np.ascontiguousarray(np.array([patch], dtype=PATCH_DTYPE))
+        return lib.or_objective(self._h, _p(p), _p(x), cell)
+
+    def expand_children(self, parent):
+        p = np.ascontiguousarray(np.array([parent], dtype=PATCH_DTYPE))
+        out = np.zeros(4, dtype=PATCH_DTYPE)
+        acc = np.zeros(4, dtype=np.uint8)
+        lib.or_expand_children(self._h, _p(p), _p(out), _p(acc))
+        return out, acc
+
+    def densify(self, seeds, cap=None):
+        seeds = np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 3)
+        if cap is None:
+            cap = 2_000_000
+        out = np.zeros(cap, dtype=PATCH_DTYPE)
+        nseed = ctypes.c_int64()
+        pops = ctypes.c_int64()
+        n = lib.or_densify(self._h, _p(seeds), len(seeds), _p(out), cap, ctypes.byref(nseed), ctypes.byref(pops))
+        return out[: min(n, cap)].copy(), {"patches": n, "seed_patches": nseed.value, "pops": pops.value}
+
+
+def ncc_int(a, b, denom_min=0.1):
+    a = np.ascontiguousarray(a, dtype=np.int32).ravel()
+    b = np.ascontiguousarray(b, dtype=np.int32).ravel()
+    return lib.or_ncc_int(_p(a), _p(b), a.size, denom_min)
+
+
+def view_geometry(P):
+    P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(12))
+    C = np.zeros(3)
+    K = np.zeros(9)
+    E = np.zeros(12)
+    x = np.zeros(3)
+    rc = lib.or_view_geometry(_p(P), _p(C), _p(K), _p(E), _p(x))
+    return rc, C, K.reshape(3, 3), E.reshape(3, 4), x
+
+
+def sincos(x):
+    s = ctypes.c_double()
+    c = ctypes.c_double()
+    lib.or_sincos(float(x), ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def acos(x):
+    return lib.or_acos(float(x))
