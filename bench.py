@@ -3,12 +3,14 @@
 filter kernel (BASELINE.json metric) on the 32-view 4K synthetic scene
 (BASELINE config 3, the HBM-roofline run).
 
-One step = one batch of expansion-stage candidates (the reference's hot loop,
-methods/pmvs/expand.cpp:127-135: Nelder-Mead refine at n = 11 on the parent's
-visible set -> InitRelatedImages -> NCC filter) through the HIP kernel, with
-inputs resident in HBM.  Candidates are the synthetic seed points turned into
-patches by Seed::CreatePatchesFromPoints semantics (nearest camera, ray
-normal, 0.5 % depth noise), so every one needs real refinement work.
+One step = one batch of expansion candidates through the HIP kernel -- the
+reference's hot loop, Expand::ExpandPatch (methods/pmvs/expand.cpp:103-143):
+each parent patch spawns 4 children (+-x, +-y at 8 px in its reference view),
+each child is Nelder-Mead refined at n = 11 on the parent's visible set, then
+InitRelatedImages and the NCC filter run -- with inputs resident in HBM.
+Parents are the synthetic seeds after the reference's seed stage
+(Seed::FilterPatches + OptimizePatches at n = 16, run once untimed), so the
+children look exactly like the ones the BFS produces.
 
 Multi-GPU (torchrun, one process per GPU): candidates are sharded by rank
 (weak scaling, per-rank batch fixed); patches are independent, so there is no
@@ -37,7 +39,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="cfg3_32view_4k")
-    ap.add_argument("--batch", type=int, default=65536, help="candidates per step per GPU")
+    ap.add_argument("--batch", type=int, default=65536, help="expansion candidates per step per GPU")
     ap.add_argument("--cell", type=int, default=11)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline wall time")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -66,7 +68,8 @@ def main():
     V, W, H = cfg.n_views, cfg.width, cfg.height
     P = synth.cameras(cfg)
     eng = dp.Engine(dp.Options(), device=local)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real (non-NULL) stream shared by torch and the library
+    torch.cuda.set_stream(stream)
     # render every view straight into HBM as BGRA8 planes (replicated per GPU)
     planes = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(V)]
     for v in range(V):
@@ -76,20 +79,27 @@ def main():
     eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
 
     seeds = synth.seeds(cfg, P)
-    # this rank's shard of candidates (wraps around the seed list)
-    B = args.batch
-    idx = (np.arange(B, dtype=np.int64) + rank * B) % len(seeds)
-    cands = eng.seeds_to_patches(seeds[idx])
-    host_in = torch.from_numpy(cands.view(np.uint8).copy())
-    pristine = host_in.to("cuda")
-    work = torch.empty_like(pristine)
+    # seed stage once (untimed): FilterPatches + OptimizePatches at n = 16
+    seed_p = eng.seeds_to_patches(seeds)
+    d_seed = torch.from_numpy(seed_p.view(np.uint8).copy()).to("cuda")
+    d_ok = torch.empty(len(seed_p), dtype=torch.uint8, device="cuda")
+    eng.refine_device(d_seed.data_ptr(), len(seed_p), 16, N.MODE_SEED, d_ok.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    seed_p = np.frombuffer(d_seed.cpu().numpy().tobytes(), dtype=N.PATCH_DTYPE)
+    parents_all = seed_p[d_ok.cpu().numpy() == 1]
+    # this rank's shard of parents (weak scaling; wraps around the list)
+    B = args.batch - args.batch % 4
+    NP = B // 4
+    idx = (np.arange(NP, dtype=np.int64) + rank * NP) % len(parents_all)
+    parents = np.ascontiguousarray(parents_all[idx])
+    d_parents = torch.from_numpy(parents.view(np.uint8).copy()).to("cuda")
+    work = torch.empty(B * N.PATCH_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
     accept = torch.empty(B, dtype=torch.uint8, device="cuda")
 
     def step(ev=None):
-        work.copy_(pristine, non_blocking=True)
         if ev:
             ev[0].record(stream)
-        eng.refine_device(work.data_ptr(), B, args.cell, N.MODE_EXPAND, accept.data_ptr(), stream.cuda_stream)
+        eng.expand_device(d_parents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
         if ev:
             ev[1].record(stream)
 
@@ -122,7 +132,8 @@ def main():
     out = np.frombuffer(work.cpu().numpy().tobytes(), dtype=N.PATCH_DTYPE)
     acc = accept.cpu().numpy()
     evals = out["evals"].astype(np.float64)
-    nvis = np.array([bin(int(m[0])).count("1") + bin(int(m[1])).count("1") for m in cands["vis"]])
+    pvis = np.array([bin(int(m[0])).count("1") + bin(int(m[1])).count("1") for m in parents["vis"]])
+    nvis = np.repeat(pvis, 4)  # children refine on the parent's visible set
     n1 = args.cell + 1
     # algorithmic bytes: E * sum_v (n+1)^2 * 4 B (BGRA8) + 128 B record in/out
     bytes_alg = float((evals * nvis * n1 * n1 * 4).sum() + 128 * B)
@@ -145,8 +156,9 @@ def main():
         "dtype": "u8 texels, fp64 geometry, int32 moments",
         "data": "synthetic (deterministic 3x3-facet heightfield, rendered on device)",
         "config": {
-            "workload": f"{args.config}: {V} views {W}x{H}, batch {B} expansion candidates/GPU, "
-                        f"n={args.cell}, Nelder-Mead + InitRelatedImages + NCC filter (parity mode)",
+            "workload": f"{args.config}: {V} views {W}x{H}, {B} expansion candidates/GPU/step "
+                        f"({NP} refined seed parents x 4 directions), n={args.cell}, "
+                        f"Nelder-Mead + InitRelatedImages + NCC filter (parity mode)",
             "views": V,
             "width": W,
             "height": H,
@@ -176,7 +188,7 @@ def main():
             result["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
 
     if rank == 0 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, cands, out)
+        result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
@@ -185,10 +197,10 @@ def main():
     eng.close()
 
 
-def cpu_baseline(args, cfg, P, planes, cands, gpu_out):
+def cpu_baseline(args, cfg, P, planes, parents, gpu_out):
     """The oracle (CPU restatement, test infrastructure) on a bounded sample of
-    the same candidates, timed on this host's cores; also a parity spot-check
-    of the GPU results on that sample."""
+    the same parents, timed on this host's cores; also a parity spot-check of
+    the GPU children on that sample."""
     from oracle import pyoracle as orc
 
     imgs = []
@@ -197,23 +209,23 @@ def cpu_baseline(args, cfg, P, planes, cands, gpu_out):
         imgs.append(np.ascontiguousarray(a[:, :, :3]))
     S = orc.Scene(P, imgs)
     threads = args.cpu_threads
-    n = 64
-    t = 0.0
+    n = 16
     while True:
-        sample = cands[:n].copy()
         t0 = time.perf_counter()
-        S.refine(sample, args.cell, orc.MODE_EXPAND, threads)
+        kids, acc = S.expand(parents[:n], threads)
         t = time.perf_counter() - t0
-        if t >= args.cpu_seconds * 0.5 or n >= len(cands):
+        if t >= args.cpu_seconds * 0.5 or n >= len(parents):
             break
-        n = min(len(cands), max(n * 2, int(n * args.cpu_seconds / max(t, 1e-3) * 0.9)))
-    same = sample.tobytes() == gpu_out[:n].tobytes()
+        n = min(len(parents), max(n * 2, int(n * args.cpu_seconds / max(t, 1e-3) * 0.9)))
+    g = gpu_out[: 4 * n]
+    fields = ("pos", "normal", "ref", "vis", "cand", "score", "evals", "flags", "parent")
+    same = all(kids[f].tobytes() == g[f].tobytes() for f in fields)
     return {
-        "value": round(n / t / 1e6, 6),
+        "value": round(4 * n / t / 1e6, 6),
         "unit": "Mpatches/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"first {n} of the GPU batch's candidates, same mode/cell, {t:.1f} s",
+        "sample": f"first {n} parents ({4 * n} candidates) of the GPU batch, same cell, {t:.1f} s",
         "parity_bit_exact_on_sample": bool(same),
     }
 

@@ -123,6 +123,8 @@ SIGNATURES = [
     ("dp_eval_batch", _I, [_P, _P, _I, _I, _P]),
     ("dp_refine_batch", _I, [_P, _P, _I, _I, _I, _P]),
     ("dp_refine_batch_device", _I, [_P, _P, _I, _I, _I, _P, _P]),
+    ("dp_expand_batch", _I, [_P, _P, _I, _P, _P]),
+    ("dp_expand_batch_device", _I, [_P, _P, _I, _P, _P, _P]),
     ("dp_densify", _I, [_P, _P, _I, _P, _P, _P]),
     ("dp_last_kernel_ms", _I, [_P, _P]),
     ("dp_synth_default", None, [_P]),

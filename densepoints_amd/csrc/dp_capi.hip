@@ -545,6 +545,49 @@ extern "C" int dp_refine_batch(dp_ctx *c, dp_patch *inout, int n, int cell, int 
     return DP_OK;
 }
 
+extern "C" int dp_expand_batch_device(dp_ctx *c, const dp_patch *d_parents, int n, dp_patch *d_children,
+                                      uint8_t *d_accept, void *stream)
+{
+    int rc = check_refine(c, n, c ? c->opt.expand_cell_size : 11, DP_MODE_EXPAND);
+    if (rc != DP_OK)
+        return rc;
+    if (n == 0)
+        return DP_OK;
+    if ((int64_t)n * 4 > INT32_MAX || !d_parents || !d_children)
+        return fail(c, DP_E_ARG, "expand: bad arguments");
+    hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    dpk::RefineArgs a = refine_args(c, d_children, 4 * n, c->opt.expand_cell_size, DP_MODE_EXPAND, d_accept);
+    a.parents = d_parents;
+    a.parent0 = 0;
+    a.max_pops = INT64_MAX;
+    return launch_timed(c, a, s);
+}
+
+extern "C" int dp_expand_batch(dp_ctx *c, const dp_patch *parents, int n, dp_patch *children, uint8_t *accept_out)
+{
+    int rc = check_refine(c, n, c ? c->opt.expand_cell_size : 11, DP_MODE_EXPAND);
+    if (rc != DP_OK)
+        return rc;
+    if (n == 0)
+        return DP_OK;
+    if (!parents || !children)
+        return fail(c, DP_E_ARG, "expand: null arrays");
+    hipSetDevice(c->device);
+    DP_HIP(c, c->cand.reserve((size_t)n));
+    DP_HIP(c, c->pat.reserve((size_t)4 * n));
+    DP_HIP(c, c->ok.reserve((size_t)4 * n));
+    DP_HIP(c, hipMemcpyAsync(c->cand.p, parents, sizeof(dp_patch) * n, hipMemcpyHostToDevice, c->stream));
+    rc = dp_expand_batch_device(c, c->cand.p, n, c->pat.p, c->ok.p, c->stream);
+    if (rc != DP_OK)
+        return rc;
+    DP_HIP(c, hipMemcpyAsync(children, c->pat.p, sizeof(dp_patch) * 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (accept_out)
+        DP_HIP(c, hipMemcpyAsync(accept_out, c->ok.p, (size_t)4 * n, hipMemcpyDeviceToHost, c->stream));
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    return DP_OK;
+}
+
 extern "C" int dp_eval_batch(dp_ctx *c, const dp_patch *in, int n, int cell, float *score_out)
 {
     int rc = check_refine(c, n, cell, DP_MODE_EVAL);

@@ -467,7 +467,8 @@ __global__ __launch_bounds__(kBlock) void refine_kernel(RefineArgs a)
         // cannot be validated on the host): such patches are rejected untouched
         const uint64_t vmask0 = a.V >= 64 ? ~0ull : ((1ull << a.V) - 1ull);
         const uint64_t vmask1 = a.V >= 128 ? ~0ull : (a.V <= 64 ? 0ull : ((1ull << (a.V - 64)) - 1ull));
-        if (rec.ref >= (uint32_t)a.V || (rec.vis[0] & ~vmask0) || (rec.vis[1] & ~vmask1))
+        const bool bad = rec.ref >= (uint32_t)a.V || (rec.vis[0] & ~vmask0) || (rec.vis[1] & ~vmask1);
+        if (bad)
             live = false;
 
         PatchState ps;
@@ -477,8 +478,8 @@ __global__ __launch_bounds__(kBlock) void refine_kernel(RefineArgs a)
         }
         ps.vis0 = rec.vis[0];
         ps.vis1 = rec.vis[1];
-        ps.ref = live ? (int)rec.ref : 0;
-        if (!live)
+        ps.ref = bad ? 0 : (int)rec.ref;
+        if (bad)
             ps.vis0 = ps.vis1 = 0;
         decode_vis(L, ps);
 

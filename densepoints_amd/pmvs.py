@@ -221,6 +221,22 @@ class Engine:
                                                ctypes.c_void_p(d_accept) if d_accept else None,
                                                ctypes.c_void_p(stream) if stream else None))
 
+    def expand(self, parents: np.ndarray):
+        """Expand::ExpandPatch over a batch: returns (children[4n], accept[4n])."""
+        parents = np.ascontiguousarray(parents)
+        assert parents.dtype == PATCH_DTYPE
+        kids = empty_patches(4 * len(parents))
+        acc = np.zeros(4 * len(parents), dtype=np.uint8)
+        self._check(lib.dp_expand_batch(self._ctx, ptr(parents), len(parents), ptr(kids), ptr(acc)))
+        return kids, acc
+
+    def expand_device(self, d_parents: int, n: int, d_children: int, d_accept: int | None,
+                      stream: int | None = None):
+        self._check(lib.dp_expand_batch_device(self._ctx, ctypes.c_void_p(d_parents), n,
+                                               ctypes.c_void_p(d_children),
+                                               ctypes.c_void_p(d_accept) if d_accept else None,
+                                               ctypes.c_void_p(stream) if stream else None))
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_double()
         self._check(lib.dp_last_kernel_ms(self._ctx, ctypes.byref(ms)))

@@ -157,6 +157,17 @@ int dp_refine_batch(dp_ctx *ctx, dp_patch *inout, int n, int cell, int mode,
 int dp_refine_batch_device(dp_ctx *ctx, dp_patch *d_inout, int n, int cell, int mode,
                            uint8_t *d_accept, void *stream);
 
+/* Expand::ExpandPatch (expand.cpp:103-143) over a batch of parents: child
+ * 4*i+d is parent i moved by grid_scale/dx pixels along +x,-x,+y,-y (d=0..3)
+ * of the reference view, then Optimize (expand_cell_size, parent's visible
+ * set) -> InitRelatedImages -> FilterByErrorMeasurement.  children and
+ * accept_out hold 4*n entries.  Parents with fewer than min_expand_visible
+ * visible views produce rejected, untouched children (expand.cpp:67). */
+int dp_expand_batch(dp_ctx *ctx, const dp_patch *parents, int n, dp_patch *children,
+                    uint8_t *accept_out);
+int dp_expand_batch_device(dp_ctx *ctx, const dp_patch *d_parents, int n, dp_patch *d_children,
+                           uint8_t *d_accept, void *stream);
+
 /* Seeds -> filter+refine (cell 16) -> organizer -> BFS expansion (cell 11):
  * PMVS::Run minus feature matching (pmvs.cpp:22-43).  The returned patch
  * array is owned by the context and valid until the next call/destroy. */

@@ -865,6 +865,32 @@ int or_expand_children(const or_scene *s, const or_patch *parent, or_patch out[4
     return na;
 }
 
+/* Expand::ExpandPatch over a batch of parents (OpenMP over parents) */
+int or_expand_batch(const or_scene *s, const or_patch *parents, int n, or_patch *children,
+                    uint8_t *acc, int nthreads)
+{
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int i = 0; i < n; ++i) {
+        int vis[OR_MAX_VIEWS];
+        if (decode_mask(parents[i].vis, vis) >= s->opt.min_expand_visible) {
+            or_expand_children(s, &parents[i], children + 4 * i, acc + 4 * i);
+        } else {
+            for (int d = 0; d < 4; ++d) {
+                children[4 * i + d] = parents[i];
+                children[4 * i + d].evals = 0;
+                children[4 * i + d].flags = 0;
+                acc[4 * i + d] = 0;
+            }
+        }
+        for (int d = 0; d < 4; ++d) children[4 * i + d].parent = (uint32_t)i;
+    }
+    (void)nthreads;
+    return 0;
+}
+
 /*
  * PMVS::Run minus seed generation (pmvs.cpp:22-43): seeds -> patches
  * (seed.cpp:26-54), FilterPatches + OptimizePatches at cell 16

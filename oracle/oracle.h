@@ -91,6 +91,8 @@ int or_refine_batch(const or_scene *s, or_patch *p, int n, int cell, int mode,
                     uint8_t *accept, int nthreads);
 int or_seeds_to_patches(const or_scene *s, const double *xyz, int n, or_patch *out);
 int or_expand_children(const or_scene *s, const or_patch *parent, or_patch out[4], uint8_t acc[4]);
+int or_expand_batch(const or_scene *s, const or_patch *parents, int n, or_patch *children,
+                    uint8_t *acc, int nthreads);
 int64_t or_densify(const or_scene *s, const double *seeds, int nseeds, or_patch *out,
                    int64_t cap, int64_t *n_seed_patches, int64_t *pops);
 void or_color(const or_scene *s, or_patch *p);

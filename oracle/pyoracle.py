@@ -80,6 +80,7 @@ def _load():
         "or_refine_batch": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]),
         "or_seeds_to_patches": (ctypes.c_int, [P, P, ctypes.c_int, P]),
         "or_expand_children": (ctypes.c_int, [P, P, P, P]),
+        "or_expand_batch": (ctypes.c_int, [P, P, ctypes.c_int, P, P, ctypes.c_int]),
         "or_densify": (ctypes.c_int64, [P, P, ctypes.c_int, P, ctypes.c_int64, P, P]),
         "or_color": (None, [P, P]),
     }
@@ -164,6 +165,13 @@ class Scene:
         acc = np.zeros(4, dtype=np.uint8)
         lib.or_expand_children(self._h, _p(p), _p(out), _p(acc))
         return out, acc
+
+    def expand(self, parents, nthreads=0):
+        parents = np.ascontiguousarray(parents)
+        kids = np.zeros(4 * len(parents), dtype=PATCH_DTYPE)
+        acc = np.zeros(4 * len(parents), dtype=np.uint8)
+        lib.or_expand_batch(self._h, _p(parents), len(parents), _p(kids), _p(acc), nthreads)
+        return kids, acc
 
     def densify(self, seeds, cap=None):
         seeds = np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 3)

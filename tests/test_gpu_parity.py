@@ -202,3 +202,17 @@ def test_deterministic_repeat(engine):
     engine.refine(a, 11, N.MODE_EXPAND)
     engine.refine(b, 11, N.MODE_EXPAND)
     assert a.tobytes() == b.tobytes()
+
+
+def test_expand_batch_bit_exact(engine, orc):
+    """Expand::ExpandPatch over a batch of refined parents (the bench step)."""
+    sc = scene("hf6")
+    engine.set_views(sc.views)
+    S = orc.Scene(sc.P, sc.imgs)
+    parents = S.seeds_to_patches(sc.seeds[:96])
+    S.refine(parents, 16, orc.MODE_SEED)
+    gk, ga = engine.expand(parents)
+    ok, oa = S.expand(parents)
+    assert np.array_equal(ga, oa)
+    assert_same(gk, ok, FIELDS + ("parent", "seq"))
+    assert ga.sum() > 0
