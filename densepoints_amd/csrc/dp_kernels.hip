@@ -22,15 +22,22 @@ namespace {
 
 constexpr int kMapChunk = 64; // views whose window maps are staged per pass
 
+// Per-wavefront LDS: everything uniform across the wave lives here so that
+// registers only hold short-lived values (the evaluation is fp64-heavy).
 struct WaveLds {
     dpg::TexMap map[kMapChunk];                 // window maps of the current view chunk
     double score[DP_MAX_VIEWS];                 // NCC per scored view
-    double c12[12];                             // window corners (uniform)
+    double c12[12];                             // window corners
+    double X[3], n[3];                          // stored pose (f32 widened)
     double sp[4][3];                            // Nelder-Mead simplex
     double y[4];                                // simplex values
     double cs[3];                               // column sums
+    double pt[3];                               // trial point
+    double ylo, ynhi, ysave;
+    uint64_t vis[2], cand[2];                   // visible / candidate masks
+    int32_t ref, m;                             // reference view, |visible|
     uint16_t anchor[DP_MAX_CELL * DP_MAX_CELL]; // texture 0 (gray)
-    uint8_t vis[DP_MAX_VIEWS];                  // visible list (ascending)
+    uint8_t vlist[DP_MAX_VIEWS];                // visible list (ascending)
 };
 
 __device__ __forceinline__ void wave_sync()
@@ -40,111 +47,123 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int wave_sum(int v)
-{
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
-        v += __shfl_xor(v, o);
-    return v;
-}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-struct PatchState {
-    double X[3];     // stored position (f32 widened)
-    double n[3];     // stored normal
-    uint64_t vis0, vis1;
-    int ref;
-    int m;           // |visible|
-};
-
-__device__ __forceinline__ void decode_vis(WaveLds &L, PatchState &ps)
+// visible mask -> ascending list + count (Patch::GetTrullyVisibleImages)
+__device__ __forceinline__ void decode_vis(WaveLds &L, uint64_t v0, uint64_t v1)
 {
     const int lane = (int)__lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
-    const int c0 = __popcll(ps.vis0);
-    if ((ps.vis0 >> lane) & 1ull)
-        L.vis[__popcll(ps.vis0 & below)] = (uint8_t)lane;
-    if ((ps.vis1 >> lane) & 1ull)
-        L.vis[c0 + __popcll(ps.vis1 & below)] = (uint8_t)(64 + lane);
-    ps.m = c0 + __popcll(ps.vis1);
+    const int c0 = __popcll(v0);
+    if ((v0 >> lane) & 1ull)
+        L.vlist[__popcll(v0 & below)] = (uint8_t)lane;
+    if ((v1 >> lane) & 1ull)
+        L.vlist[c0 + __popcll(v1 & below)] = (uint8_t)(64 + lane);
+    L.vis[0] = v0;
+    L.vis[1] = v1;
+    L.m = c0 + __popcll(v1);
     wave_sync();
 }
 
-// Sum of gray, gray^2 and anchor*gray over texels t = t0, t0+step, ... of one
-// view's window (the map is read from LDS once per view).
-template <bool kAnchor>
-__device__ __forceinline__ void sample_view(const RefineArgs &a, WaveLds &L, int slot, int view, int t0,
-                                            int step, int &S, int &SS, int &SX)
+typedef const __attribute__((address_space(1))) uint32_t *gpix_t;
+typedef const __attribute__((address_space(1))) unsigned long long *gpair_t;
+
+// Full-wavefront integer sum (DPP row_shr / row_bcast), result in every lane
+// via readlane 63 (uniform).
+__device__ __forceinline__ int wave_total(int v)
 {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false); // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false); // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xe, false); // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xc, false); // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// One window texel: 1/32-px coordinate, two 8-byte loads (taps x0,x0+1 of
+// rows y0,y1 -- the right neighbour is always inside the image because the
+// ROI ends at floor(max u) <= W-1), replicate-clamp select, bilinear, gray.
+__device__ __forceinline__ int sample_texel(gpix_t roi, int pitch, const dpg::TexMap &tm, int px, int py)
+{
+    const dpg::Tap t = dpg::window_tap(tm, px, py);
+    const unsigned long long a = *(gpair_t)(roi + t.y0 * pitch + t.x0);
+    const unsigned long long b = *(gpair_t)(roi + t.y1 * pitch + t.x0);
+    const uint32_t a0 = (uint32_t)a, b0 = (uint32_t)b;
+    const bool same = t.x1 == t.x0;
+    const uint32_t a1 = same ? a0 : (uint32_t)(a >> 32);
+    const uint32_t b1 = same ? b0 : (uint32_t)(b >> 32);
+    return dpg::blend_gray(a0, a1, b0, b1, t.fx, t.fy);
+}
+
+// Integer moments of one view's window, all 64 lanes on its texels
+// (t = lane, lane+64, ...): coalesced gathers inside one small window.
+template <bool kAnchor>
+__device__ __forceinline__ void view_moments(const RefineArgs &a, WaveLds &L, int slot, int view, int &S,
+                                             int &SS, int &SX)
+{
+    const int lane = (int)__lane_id();
     const dpg::TexMap tm = L.map[slot];
     const dpg::ViewDev *__restrict__ vw = a.views + view;
     const int pitch = vw->pitch;
-    const uint32_t *__restrict__ roi = vw->img + (size_t)tm.tly * (size_t)pitch + tm.tlx;
+    const gpix_t roi = (gpix_t)vw->img + (size_t)tm.tly * (size_t)pitch + tm.tlx;
     const int cell = a.cell;
     const int N = cell * cell;
-    int py = t0 / cell;
-    int px = t0 - py * cell;
-    const int dy = step / cell, dxs = step - dy * cell;
-#pragma unroll 1
-    for (int t = t0; t < N; t += step) {
-        const dpg::Tap tp = dpg::window_tap(tm, px, py);
-        const uint32_t *r0 = roi + (size_t)tp.y0 * (size_t)pitch;
-        const uint32_t *r1 = roi + (size_t)tp.y1 * (size_t)pitch;
-        const int gv = dpg::blend_gray(r0[tp.x0], r0[tp.x1], r1[tp.x0], r1[tp.x1], tp.fx, tp.fy);
-        S += gv;
-        SS += gv * gv;
+    int s = 0, ss = 0, sx = 0;
+    for (int t = lane; t < N; t += kWave) {
+        const int py = t / cell;
+        const int px = t - py * cell;
+        const int gv = sample_texel(roi, pitch, tm, px, py);
+        s += gv;
+        ss += gv * gv;
         if (kAnchor)
             L.anchor[t] = (uint16_t)gv;
         else
-            SX += (int)L.anchor[t] * gv;
-        px += dxs;
-        py += dy;
-        if (px >= cell) {
-            px -= cell;
-            ++py;
-        }
+            sx += (int)L.anchor[t] * gv;
     }
+    S = wave_total(s);
+    SS = wave_total(ss);
+    SX = kAnchor ? 0 : wave_total(sx);
 }
 
 // One evaluation's NCC scores against texture 0 -> L.score[0..nv-1]
-// (GetProjectedTextures + NCCScore).  Per chunk of up to 64 visible views,
-// lane k builds view k's window map (projective map + ROI) into LDS.  Texture
-// 0 is then sampled by all 64 lanes; the other views are spread as (view
-// slot, texel group) with G lanes per view (G = largest power of two with
-// G * views <= 64), each lane looping over texels t = g, g+G, ..., and the
-// integer moments are reduced over the G lanes with xor shuffles.
-__device__ int wave_scores(const RefineArgs &a, WaveLds &L, const PatchState &ps, const double *nn,
-                           const double *pp, bool &degenerate)
+// (GetProjectedTextures + NCCScore) at candidate pose (nn, pp).  Per chunk of
+// up to 64 visible views, lane k builds view k's window map (projective map +
+// ROI) into LDS; then the views are sampled one after another by the whole
+// wavefront (texture 0 first, kept in LDS), each reduced to exact integer
+// moments with DPP.  Returns the number of scores; sets *degen on dx == 0.
+__device__ int wave_scores(const RefineArgs &a, WaveLds &L, const double *nn, const double *pp, bool &degen)
 {
     const int lane = (int)__lane_id();
-    const int m = ps.m;
+    const int m = uni(L.m);
     const int nv = m - 1;
     const int cell = a.cell;
     const int N = cell * cell;
     {
         double c12[12];
-        degenerate = !dpg::window_corners(a.views[ps.ref], ps.X, nn, pp, cell, c12);
+        const double Xs[3] = {L.X[0], L.X[1], L.X[2]};
+        const bool ok = dpg::window_corners(a.views[uni(L.ref)], Xs, nn, pp, cell, c12);
+        degen = degen || !ok;
+        if (!ok) {
+            for (int k = lane; k < nv; k += kWave)
+                L.score[k] = -1.0;
+            wave_sync();
+            return nv > 0 ? nv : 0;
+        }
         for (int i = 0; i < 12; ++i)
             L.c12[i] = c12[i];
     }
     if (nv <= 0)
         return 0;
-    if (degenerate) {
-        for (int k = lane; k < nv; k += kWave)
-            L.score[k] = -1.0;
-        wave_sync();
-        return nv;
-    }
     wave_sync();
     int Sa = 0, Saa = 0;
     bool va = false;
-#pragma unroll 1
     for (int base = 0; base < m; base += kMapChunk) {
-        // window maps of views base .. base+63
         bool ok = false;
         const int kk = base + lane;
         if (kk < m) {
             dpg::TexMap tm;
-            ok = dpg::texture_map(a.views[L.vis[kk]], L.c12, cell, tm);
+            ok = dpg::texture_map(a.views[L.vlist[kk]], L.c12, cell, tm);
             if (ok)
                 L.map[lane] = tm;
         }
@@ -154,41 +173,21 @@ __device__ int wave_scores(const RefineArgs &a, WaveLds &L, const PatchState &ps
             // texture 0 = lowest-index visible view (optimization_opencv.cpp:24-28)
             va = okmask & 1ull;
             if (va) {
-                int dummy = 0;
-                sample_view<true>(a, L, 0, L.vis[0], lane, kWave, Sa, Saa, dummy);
+                int dummy;
+                view_moments<true>(a, L, 0, uni(L.vlist[0]), Sa, Saa, dummy);
             }
-            Sa = wave_sum(Sa);
-            Saa = wave_sum(Saa);
             wave_sync();
         }
-        // scored views of this chunk: k in [kb, ke)
         const int kb = base == 0 ? 1 : base;
         const int ke = (base + kMapChunk < m) ? base + kMapChunk : m;
-        const int cnt = ke - kb;
-        if (cnt <= 0)
-            continue;
-        int G = kWave;
-        while (G > 1 && G * cnt > kWave)
-            G >>= 1;
-        const int lg = __builtin_ctz(G);
-        const int slots = kWave >> lg;
-        const int j = lane >> lg;
-        const int g = lane & (G - 1);
-#pragma unroll 1
-        for (int s0 = 0; s0 < cnt; s0 += slots) {
-            const int k = kb + s0 + j; // visible index of this lane's view
-            const bool act = k < ke;
-            const bool vb = act && va && ((okmask >> (k - base)) & 1ull);
-            int Sb = 0, Sbb = 0, Sab = 0;
-            if (vb)
-                sample_view<false>(a, L, k - base, L.vis[k], g, G, Sb, Sbb, Sab);
-            for (int o = G >> 1; o >= 1; o >>= 1) {
-                Sb += __shfl_xor(Sb, o);
-                Sbb += __shfl_xor(Sbb, o);
-                Sab += __shfl_xor(Sab, o);
+        for (int k = kb; k < ke; ++k) {
+            double sc = -1.0;
+            if (va && ((okmask >> (k - base)) & 1ull)) {
+                int Sb, Sbb, Sab;
+                view_moments<false>(a, L, k - base, uni(L.vlist[k]), Sb, Sbb, Sab);
+                sc = dpg::ncc_finish(N, Sa, Saa, Sb, Sbb, Sab, a.opt.ncc_denom_min);
             }
-            if (act && g == 0)
-                L.score[k - 1] = vb ? dpg::ncc_finish(N, Sa, Saa, Sb, Sbb, Sab, a.opt.ncc_denom_min) : -1.0;
+            L.score[k - 1] = sc;
         }
         wave_sync();
     }
@@ -196,14 +195,15 @@ __device__ int wave_scores(const RefineArgs &a, WaveLds &L, const PatchState &ps
 }
 
 // functor calc (optimization_opencv.cpp:14-39): mean of (1 - NCC), 2 if none
-__device__ double wave_objective(const RefineArgs &a, WaveLds &L, const PatchState &ps,
-                                 const double *x, bool &degen)
+__device__ double wave_objective(const RefineArgs &a, WaveLds &L, double x0, double x1, double x2, bool &degen)
 {
     double nn[3], pp[3];
-    dpg::unparametrize(a.views[ps.ref].C, ps.X, ps.n, x[0], x[1], x[2], nn, pp);
-    bool dg = false;
-    const int nv = wave_scores(a, L, ps, nn, pp, dg);
-    degen = degen || dg;
+    {
+        const double Xs[3] = {L.X[0], L.X[1], L.X[2]};
+        const double ns[3] = {L.n[0], L.n[1], L.n[2]};
+        dpg::unparametrize(a.views[uni(L.ref)].C, Xs, ns, x0, x1, x2, nn, pp);
+    }
+    const int nv = wave_scores(a, L, nn, pp, degen);
     if (nv == 0)
         return 2.0;
     double sum = 0.0;
@@ -217,12 +217,10 @@ enum NmPhase { kInit = 0, kReflect = 1, kExpand = 2, kContract = 3, kShrink = 4 
 // cv::DownhillSolver::minimize as driven by OptimizationOpenCV::Optimize
 // (optimization_opencv.cpp:44-78; OpenCV 3.4 createInitialSimplex,
 // innerDownhillSimplex, tryNewPoint).  One objective call site; the simplex
-// lives in LDS (uniform across the wave).  Writes back the f32 pose.
-__device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, PatchState &ps, bool &degen)
+// lives in LDS.  Writes back the f32 pose into L.X / L.n.
+__device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, bool &degen)
 {
     const double *step = a.opt.nm_step;
-    const double eps = a.opt.nm_eps;
-    const int nmax = a.opt.nm_max_evals;
     for (int i = 1; i <= 3; ++i) {
         for (int jj = 0; jj < 3; ++jj)
             L.sp[i][jj] = 0.0;
@@ -233,25 +231,24 @@ __device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, PatchState &ps,
 
     int fcount = 4, evals = 0, phase = kInit, vi = 0;
     int ilo = 0, ihi = 0, inhi = 0;
-    double ylo = 0.0, ynhi = 0.0, ysave = 0.0;
-    double pt[3];
     for (;;) {
-        double xq[3];
+        double q0, q1, q2;
         if (phase == kInit || phase == kShrink) {
-            xq[0] = L.sp[vi][0];
-            xq[1] = L.sp[vi][1];
-            xq[2] = L.sp[vi][2];
+            q0 = L.sp[vi][0];
+            q1 = L.sp[vi][1];
+            q2 = L.sp[vi][2];
         } else {
             const double fac = phase == kReflect ? -1.0 : (phase == kExpand ? 2.0 : 0.5);
             const double alpha = (1.0 - fac) / 3.0;
             const double beta = alpha - fac;
-            for (int jj = 0; jj < 3; ++jj)
-                pt[jj] = L.cs[jj] * alpha - L.sp[ihi][jj] * beta;
-            xq[0] = pt[0];
-            xq[1] = pt[1];
-            xq[2] = pt[2];
+            q0 = L.cs[0] * alpha - L.sp[ihi][0] * beta;
+            q1 = L.cs[1] * alpha - L.sp[ihi][1] * beta;
+            q2 = L.cs[2] * alpha - L.sp[ihi][2] * beta;
+            L.pt[0] = q0;
+            L.pt[1] = q1;
+            L.pt[2] = q2;
         }
-        const double f = wave_objective(a, L, ps, xq, degen);
+        const double f = wave_objective(a, L, q0, q1, q2, degen);
         ++evals;
         bool decide = false;
         if (phase == kInit) {
@@ -280,15 +277,15 @@ __device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, PatchState &ps,
             if (f < L.y[ihi]) {
                 L.y[ihi] = f;
                 for (int jj = 0; jj < 3; ++jj)
-                    L.cs[jj] += pt[jj] - L.sp[ihi][jj];
+                    L.cs[jj] += L.pt[jj] - L.sp[ihi][jj];
                 for (int jj = 0; jj < 3; ++jj)
-                    L.sp[ihi][jj] = pt[jj];
+                    L.sp[ihi][jj] = L.pt[jj];
             }
             if (phase == kReflect) {
-                if (f <= ylo) {
+                if (f <= L.ylo) {
                     phase = kExpand;
-                } else if (f >= ynhi) {
-                    ysave = L.y[ihi];
+                } else if (f >= L.ynhi) {
+                    L.ysave = L.y[ihi];
                     phase = kContract;
                 } else {
                     --fcount;
@@ -297,7 +294,7 @@ __device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, PatchState &ps,
             } else if (phase == kExpand) {
                 decide = true;
             } else { // contract
-                if (f >= ysave) {
+                if (f >= L.ysave) {
                     vi = (ilo == 0) ? 1 : 0;
                     for (int jj = 0; jj < 3; ++jj)
                         L.sp[vi][jj] = 0.5 * (L.sp[vi][jj] + L.sp[ilo][jj]);
@@ -349,32 +346,39 @@ __device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, PatchState &ps,
             const double rr = fabs(mx - mn);
             range = (range < rr) ? rr : range;
         }
-        if (range <= eps || err <= eps || fcount >= nmax)
+        if (range <= a.opt.nm_eps || err <= a.opt.nm_eps || fcount >= a.opt.nm_max_evals)
             break;
         fcount += 2;
-        ylo = L.y[ilo];
-        ynhi = L.y[inhi];
+        L.ylo = L.y[ilo];
+        L.ynhi = L.y[inhi];
         phase = kReflect;
     }
-    // best vertex = slot ilo (swapped into row 0 by the reference)
+    // best vertex = slot ilo (swapped into row 0 by the reference), f32 store
     double nn[3], pp[3];
-    dpg::unparametrize(a.views[ps.ref].C, ps.X, ps.n, L.sp[ilo][0], L.sp[ilo][1], L.sp[ilo][2], nn,
-                       pp);
-    for (int i = 0; i < 3; ++i) {
-        ps.n[i] = (double)(float)nn[i];
-        ps.X[i] = (double)(float)pp[i];
+    {
+        const double Xs[3] = {L.X[0], L.X[1], L.X[2]};
+        const double ns[3] = {L.n[0], L.n[1], L.n[2]};
+        dpg::unparametrize(a.views[uni(L.ref)].C, Xs, ns, L.sp[ilo][0], L.sp[ilo][1], L.sp[ilo][2], nn, pp);
     }
+    for (int i = 0; i < 3; ++i) {
+        L.n[i] = (double)(float)nn[i];
+        L.X[i] = (double)(float)pp[i];
+    }
+    wave_sync();
     return evals;
 }
 
 // Optimization::FilterByErrorMeasurement (optimization.cpp:98-132) with the
 // off-by-one erase: score k (texture k+1) < thr removes ORIGINAL index k.
-__device__ bool wave_filter(const RefineArgs &a, WaveLds &L, PatchState &ps, float &score, bool &degen)
+__device__ bool wave_filter(const RefineArgs &a, WaveLds &L, float &score, bool &degen)
 {
     const int lane = (int)__lane_id();
-    bool dg = false;
-    const int nv = wave_scores(a, L, ps, ps.n, ps.X, dg);
-    degen = degen || dg;
+    int nv;
+    {
+        const double nn[3] = {L.n[0], L.n[1], L.n[2]};
+        const double pp[3] = {L.X[0], L.X[1], L.X[2]};
+        nv = wave_scores(a, L, nn, pp, degen);
+    }
     if (nv == 0) {
         score = -1.0f;
         return false;
@@ -383,36 +387,61 @@ __device__ bool wave_filter(const RefineArgs &a, WaveLds &L, PatchState &ps, flo
     for (int k = 0; k < nv; ++k)
         sum = sum + L.score[k];
     score = (float)(sum / (double)nv);
+    const uint64_t v0 = L.vis[0], v1 = L.vis[1];
     const uint64_t below = (1ull << lane) - 1ull;
     const double thr = a.opt.ncc_threshold;
-    const int c0 = __popcll(ps.vis0);
-    const bool in0 = (ps.vis0 >> lane) & 1ull;
-    const int r0 = __popcll(ps.vis0 & below);
+    const int c0 = __popcll(v0);
+    const bool in0 = (v0 >> lane) & 1ull;
+    const int r0 = __popcll(v0 & below);
     const bool drop0 = in0 && r0 < nv && L.score[r0] < thr;
-    const bool in1 = (ps.vis1 >> lane) & 1ull;
-    const int r1 = c0 + __popcll(ps.vis1 & below);
+    const bool in1 = (v1 >> lane) & 1ull;
+    const int r1 = c0 + __popcll(v1 & below);
     const bool drop1 = in1 && r1 < nv && L.score[r1] < thr;
-    ps.vis0 = __ballot(in0 && !drop0);
-    ps.vis1 = __ballot(in1 && !drop1);
-    decode_vis(L, ps);
-    return ps.m >= a.opt.min_visible;
+    const uint64_t n0 = __ballot(in0 && !drop0);
+    const uint64_t n1 = __ballot(in1 && !drop1);
+    wave_sync();
+    decode_vis(L, n0, n1);
+    return uni(L.m) >= a.opt.min_visible;
 }
 
 // Patch::InitRelatedImages (patch.cpp:19-49), one lane per view
-__device__ void wave_init_related(const RefineArgs &a, WaveLds &L, PatchState &ps, uint64_t cand[2])
+__device__ void wave_init_related(const RefineArgs &a, WaveLds &L)
 {
     const int lane = (int)__lane_id();
+    const int ref = uni(L.ref);
+    const double X[3] = {L.X[0], L.X[1], L.X[2]};
+    const double n[3] = {L.n[0], L.n[1], L.n[2]};
     int cls0 = 0, cls1 = 0;
-    if (lane < a.V && lane != ps.ref)
-        cls0 = dpg::classify_view(a.views[lane], ps.X, ps.n, a.opt.visible_angle, a.opt.candidate_angle);
-    if (64 + lane < a.V && 64 + lane != ps.ref)
-        cls1 = dpg::classify_view(a.views[64 + lane], ps.X, ps.n, a.opt.visible_angle,
-                                  a.opt.candidate_angle);
-    ps.vis0 = __ballot(cls0 == 1);
-    ps.vis1 = __ballot(cls1 == 1);
-    cand[0] = __ballot(cls0 == 2);
-    cand[1] = __ballot(cls1 == 2);
-    decode_vis(L, ps);
+    if (lane < a.V && lane != ref)
+        cls0 = dpg::classify_view(a.views[lane], X, n, a.opt.visible_angle, a.opt.candidate_angle);
+    if (64 + lane < a.V && 64 + lane != ref)
+        cls1 = dpg::classify_view(a.views[64 + lane], X, n, a.opt.visible_angle, a.opt.candidate_angle);
+    const uint64_t v0 = __ballot(cls0 == 1), v1 = __ballot(cls1 == 1);
+    const uint64_t c0 = __ballot(cls0 == 2), c1 = __ballot(cls1 == 2);
+    wave_sync();
+    L.cand[0] = c0;
+    L.cand[1] = c1;
+    decode_vis(L, v0, v1);
+}
+
+// Expand::ExpandPatch child position (expand.cpp:107-125)
+__device__ void child_position(const RefineArgs &a, const dp_patch &par, int dir, float *out)
+{
+    const dpg::ViewDev &rv = a.views[par.ref];
+    const double X[3] = {par.pos[0], par.pos[1], par.pos[2]};
+    const double nrm[3] = {par.normal[0], par.normal[1], par.normal[2]};
+    double yax[3];
+    dpg::cross3(nrm, rv.xr, yax);
+    double cu, cv, qu, qv;
+    dpg::project(rv.P, X[0], X[1], X[2], cu, cv);
+    dpg::project(rv.P, X[0] + rv.xr[0], X[1] + rv.xr[1], X[2] + rv.xr[2], qu, qv);
+    const double du = qu - cu, dv = qv - cv;
+    const double dx = sqrt(du * du + dv * dv);
+    const double scale = (double)a.opt.grid_scale / dx;
+    for (int i = 0; i < 3; ++i) {
+        const double d = dir == 0 ? rv.xr[i] : dir == 1 ? -rv.xr[i] : dir == 2 ? yax[i] : -yax[i];
+        out[i] = (float)(X[i] + scale * d);
+    }
 }
 
 template <int kMode>
@@ -426,119 +455,117 @@ __global__ __launch_bounds__(kBlock) void refine_kernel(RefineArgs a)
         uint32_t idx = 0;
         if (lane == 0)
             idx = atomicAdd(a.work, 1u);
-        idx = (uint32_t)__shfl((int)idx, 0);
+        idx = (uint32_t)uni((int)idx);
         if (idx >= (uint32_t)a.n)
             break;
-
-        dp_patch rec;
+        dp_patch *out = a.patches + idx;
         bool live = true;
-        if (a.parents) {
-            // Expand::ExpandPatch (expand.cpp:103-125): child idx of parent idx/4
-            const int64_t qi = a.parent0 + (int64_t)(idx >> 2);
-            const int dir = (int)(idx & 3u);
-            rec = a.parents[qi];
-            const int pm = __popcll(rec.vis[0]) + __popcll(rec.vis[1]);
-            live = qi < a.max_pops && pm >= a.opt.min_expand_visible;
-            if (live) {
-                const dpg::ViewDev &rv = a.views[rec.ref];
-                const double X[3] = {rec.pos[0], rec.pos[1], rec.pos[2]};
-                const double nrm[3] = {rec.normal[0], rec.normal[1], rec.normal[2]};
-                double yax[3];
-                dpg::cross3(nrm, rv.xr, yax);
-                double cu, cv, qu, qv;
-                dpg::project(rv.P, X[0], X[1], X[2], cu, cv);
-                dpg::project(rv.P, X[0] + rv.xr[0], X[1] + rv.xr[1], X[2] + rv.xr[2], qu, qv);
-                const double du = qu - cu, dv = qv - cv;
-                const double dx = sqrt(du * du + dv * dv);
-                const double scale = (double)a.opt.grid_scale / dx;
-                for (int i = 0; i < 3; ++i) {
-                    const double d = dir == 0 ? rv.xr[i] : dir == 1 ? -rv.xr[i] : dir == 2 ? yax[i] : -yax[i];
-                    rec.pos[i] = (float)(X[i] + scale * d);
+        {
+            // load the record (or derive the child from its parent) into LDS
+            const dp_patch *src = out;
+            float cpos[3] = {0.f, 0.f, 0.f};
+            int64_t qi = 0;
+            if (a.parents) {
+                qi = a.parent0 + (int64_t)(idx >> 2);
+                src = a.parents + qi;
+                const int pm = __popcll(src->vis[0]) + __popcll(src->vis[1]);
+                live = qi < a.max_pops && pm >= a.opt.min_expand_visible && src->ref < (uint32_t)a.V;
+                if (live)
+                    child_position(a, *src, (int)(idx & 3u), cpos);
+            }
+            const uint32_t ref = src->ref;
+            const uint64_t v0 = src->vis[0], v1 = src->vis[1];
+            // records naming views outside the scene are rejected untouched
+            const uint64_t m0 = a.V >= 64 ? ~0ull : ((1ull << a.V) - 1ull);
+            const uint64_t m1 = a.V >= 128 ? ~0ull : (a.V <= 64 ? 0ull : ((1ull << (a.V - 64)) - 1ull));
+            const bool bad = ref >= (uint32_t)a.V || (v0 & ~m0) || (v1 & ~m1);
+            if (bad)
+                live = false;
+            if (lane == 0) {
+                if (a.parents) {
+                    *out = *src;
+                    out->evals = 0;
+                    out->flags = 0;
+                    out->parent = (uint32_t)qi;
+                    if (live) {
+                        out->pos[0] = cpos[0];
+                        out->pos[1] = cpos[1];
+                        out->pos[2] = cpos[2];
+                    }
                 }
             }
-            rec.evals = 0;
-            rec.flags = 0;
-            rec.parent = (uint32_t)qi;
-        } else {
-            rec = a.patches[idx];
+            for (int i = 0; i < 3; ++i) {
+                L.X[i] = (a.parents && live) ? (double)cpos[i] : (double)src->pos[i];
+                L.n[i] = (double)src->normal[i];
+            }
+            L.ref = bad ? 0 : (int)ref;
+            L.cand[0] = src->cand[0];
+            L.cand[1] = src->cand[1];
+            decode_vis(L, bad ? 0ull : v0, bad ? 0ull : v1);
         }
-
-        // guard against records naming views outside the scene (device path
-        // cannot be validated on the host): such patches are rejected untouched
-        const uint64_t vmask0 = a.V >= 64 ? ~0ull : ((1ull << a.V) - 1ull);
-        const uint64_t vmask1 = a.V >= 128 ? ~0ull : (a.V <= 64 ? 0ull : ((1ull << (a.V - 64)) - 1ull));
-        const bool bad = rec.ref >= (uint32_t)a.V || (rec.vis[0] & ~vmask0) || (rec.vis[1] & ~vmask1);
-        if (bad)
-            live = false;
-
-        PatchState ps;
-        for (int i = 0; i < 3; ++i) {
-            ps.X[i] = rec.pos[i];
-            ps.n[i] = rec.normal[i];
-        }
-        ps.vis0 = rec.vis[0];
-        ps.vis1 = rec.vis[1];
-        ps.ref = bad ? 0 : (int)rec.ref;
-        if (bad)
-            ps.vis0 = ps.vis1 = 0;
-        decode_vis(L, ps);
 
         bool degen = false, ok = false;
         int evals = 0;
-        float score = rec.score;
-        uint64_t cand[2] = {rec.cand[0], rec.cand[1]};
+        float score = 0.f;
+        bool has_score = false;
         if (live) {
             switch (kMode) {
             case DP_MODE_EVAL: {
-                bool dg = false;
-                const int nv = wave_scores(a, L, ps, ps.n, ps.X, dg);
-                degen = dg;
+                const double nn[3] = {L.n[0], L.n[1], L.n[2]};
+                const double pp[3] = {L.X[0], L.X[1], L.X[2]};
+                const int nv = wave_scores(a, L, nn, pp, degen);
                 double sum = 0.0;
                 for (int k = 0; k < nv; ++k)
                     sum = sum + L.score[k];
                 score = nv ? (float)(sum / (double)nv) : -1.0f;
+                has_score = true;
                 evals = 1;
                 ok = nv > 0;
                 break;
             }
             case DP_MODE_FILTER:
-                ok = wave_filter(a, L, ps, score, degen);
+                ok = wave_filter(a, L, score, degen);
+                has_score = true;
                 evals = 1;
                 break;
             case DP_MODE_NM:
-                evals = wave_nelder_mead(a, L, ps, degen);
+                evals = wave_nelder_mead(a, L, degen);
                 ok = true;
                 break;
             case DP_MODE_SEED:
-                ok = wave_filter(a, L, ps, score, degen);
+                ok = wave_filter(a, L, score, degen);
+                has_score = true;
                 evals = 1;
                 if (ok)
-                    evals += wave_nelder_mead(a, L, ps, degen);
+                    evals += wave_nelder_mead(a, L, degen);
                 break;
             case DP_MODE_EXPAND:
             default:
-                evals = wave_nelder_mead(a, L, ps, degen);
-                wave_init_related(a, L, ps, cand);
-                ok = wave_filter(a, L, ps, score, degen);
+                evals = wave_nelder_mead(a, L, degen);
+                wave_init_related(a, L);
+                ok = wave_filter(a, L, score, degen);
+                has_score = true;
                 evals += 1;
                 break;
             }
         }
         wave_evals += (unsigned long long)evals;
         if (lane == 0) {
-            for (int i = 0; i < 3; ++i) {
-                rec.pos[i] = (float)ps.X[i];
-                rec.normal[i] = (float)ps.n[i];
+            if (live) {
+                for (int i = 0; i < 3; ++i) {
+                    out->pos[i] = (float)L.X[i];
+                    out->normal[i] = (float)L.n[i];
+                }
+                out->vis[0] = L.vis[0];
+                out->vis[1] = L.vis[1];
+                out->cand[0] = L.cand[0];
+                out->cand[1] = L.cand[1];
+                if (has_score)
+                    out->score = score;
+                out->evals += (uint32_t)evals;
             }
-            rec.vis[0] = ps.vis0;
-            rec.vis[1] = ps.vis1;
-            rec.cand[0] = cand[0];
-            rec.cand[1] = cand[1];
-            rec.score = score;
-            rec.evals += (uint32_t)evals;
-            rec.flags = (uint8_t)((rec.flags & ~DP_PATCH_ACCEPTED) |
-                                  (ok ? DP_PATCH_ACCEPTED : 0u) | (degen ? DP_PATCH_DEGENERATE : 0u));
-            a.patches[idx] = rec;
+            out->flags = (uint8_t)((out->flags & ~DP_PATCH_ACCEPTED) | (ok ? DP_PATCH_ACCEPTED : 0u) |
+                                   (degen ? DP_PATCH_DEGENERATE : 0u));
             if (a.accept)
                 a.accept[idx] = ok ? 1 : 0;
         }
