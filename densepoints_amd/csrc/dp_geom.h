@@ -85,6 +85,9 @@ DP_HD bool window_corners(const ViewDev &rv, const double *Xs, const double *nn,
 struct TexMap {
     double m0, m1, m2, m3, m4, m5, m6, m7; // m8 == 1
     int32_t tlx, tly, w, h;
+    int32_t safe; // W > 1e-3 and |X|,|Y| < 2^30 at all window corners: the
+                  // int-range clamps and the W != 0 select never fire
+    int32_t pad;
 };
 
 // Returns false for the reference's empty texture (corner outside the view,
@@ -143,7 +146,32 @@ DP_HD bool texture_map(const ViewDev &v, const double *c12, int cell, TexMap &tm
     tm.tly = tly;
     tm.w = rw;
     tm.h = rh;
+    // W is affine in (x, y) and X/W, Y/W are linear-fractional: with W > 0 on
+    // the window rectangle their extremes are at its corners.
+    bool safe = true;
+    const double e = (double)(cell - 1);
+    for (int c = 0; c < 4; ++c) {
+        const double px = (c & 1) ? e : 0.0, py = (c & 2) ? e : 0.0;
+        const double W = (tm.m7 * py + 1.0) + tm.m6 * px;
+        if (!(W > 1e-3)) {
+            safe = false;
+            continue;
+        }
+        const double q = 32.0 / W;
+        const double X = ((tm.m1 * py + tm.m2) + tm.m0 * px) * q;
+        const double Y = ((tm.m4 * py + tm.m5) + tm.m3 * px) * q;
+        if (!(fabs(X) < 1073741824.0) || !(fabs(Y) < 1073741824.0))
+            safe = false;
+    }
+    tm.safe = safe ? 1 : 0;
+    tm.pad = 0;
     return true;
+}
+
+DP_HD int32_t clampi(int32_t v, int32_t lo, int32_t hi)
+{
+    const int32_t a = v > lo ? v : lo;
+    return a < hi ? a : hi;
 }
 
 // warpPerspective(INTER_LINEAR) coordinate of window pixel (px, py):
@@ -173,10 +201,10 @@ DP_HD Tap window_tap(const TexMap &tm, int px, int py)
     t.fx = ix & 31;
     t.fy = iy & 31;
     const int32_t wm = tm.w - 1, hm = tm.h - 1;
-    t.x0 = sx < 0 ? 0 : (sx > wm ? wm : sx);
-    t.x1 = sx + 1 < 0 ? 0 : (sx + 1 > wm ? wm : sx + 1);
-    t.y0 = sy < 0 ? 0 : (sy > hm ? hm : sy);
-    t.y1 = sy + 1 < 0 ? 0 : (sy + 1 > hm ? hm : sy + 1);
+    t.x0 = clampi(sx, 0, wm);
+    t.x1 = clampi(sx + 1, 0, wm);
+    t.y0 = clampi(sy, 0, hm);
+    t.y1 = clampi(sy + 1, 0, hm);
     return t;
 }
 

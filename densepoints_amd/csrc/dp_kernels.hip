@@ -27,6 +27,9 @@ constexpr int kMapChunk = 64; // views whose window maps are staged per pass
 struct WaveLds {
     dpg::TexMap map[kMapChunk];                 // window maps of the current view chunk
     double score[DP_MAX_VIEWS];                 // NCC per scored view
+    int32_t mom[kMapChunk][3];                  // Sb, Sbb, Sab of the chunk's views
+    double rowt[DP_MAX_CELL][4];                // per window row: X0, Y0, W0 of the current view
+    double colt[DP_MAX_CELL][4];                // per window column: m0*x, m3*x, m6*x
     double c12[12];                             // window corners
     double X[3], n[3];                          // stored pose (f32 widened)
     double sp[4][3];                            // Nelder-Mead simplex
@@ -81,19 +84,70 @@ __device__ __forceinline__ int wave_total(int v)
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-// One window texel: 1/32-px coordinate, two 8-byte loads (taps x0,x0+1 of
-// rows y0,y1 -- the right neighbour is always inside the image because the
-// ROI ends at floor(max u) <= W-1), replicate-clamp select, bilinear, gray.
-__device__ __forceinline__ int sample_texel(gpix_t roi, int pitch, const dpg::TexMap &tm, int px, int py)
+// One window texel of view map `tm` whose row/column terms are in L.rowt /
+// L.colt (same roundings as dpg::window_tap: X0 = m1*y + m2, W0 = m7*y + 1,
+// W = W0 + m6*x, X = (X0 + m0*x) * (32/W)).  Two 8-byte loads fetch taps
+// (x0, x0+1) of rows y0 and y1 -- the right neighbour is always inside the
+// image because the ROI ends at floor(max u) <= W-1 -- and a select applies
+// BORDER_REPLICATE.  kSafe: the map's int-range clamps / W != 0 select never
+// fire on this window (TexMap::safe), so they are skipped.
+template <bool kSafe>
+__device__ __forceinline__ int sample_texel(const WaveLds &L, gpix_t roi, int pitch, int wm, int hm, int px,
+                                            int py)
 {
-    const dpg::Tap t = dpg::window_tap(tm, px, py);
-    const unsigned long long a = *(gpair_t)(roi + t.y0 * pitch + t.x0);
-    const unsigned long long b = *(gpair_t)(roi + t.y1 * pitch + t.x0);
+    const double X0 = L.rowt[py][0], Y0 = L.rowt[py][1], W0 = L.rowt[py][2];
+    const double cX = L.colt[px][0], cY = L.colt[px][1], cW = L.colt[px][2];
+    double W = W0 + cW;
+    if (kSafe) {
+        W = 32.0 / W;
+    } else {
+        W = (W != 0.0) ? 32.0 / W : 0.0;
+    }
+    double X = (X0 + cX) * W;
+    double Y = (Y0 + cY) * W;
+    if (!kSafe) {
+        X = X < 2147483647.0 ? X : 2147483647.0;
+        X = X > -2147483648.0 ? X : -2147483648.0;
+        Y = Y < 2147483647.0 ? Y : 2147483647.0;
+        Y = Y > -2147483648.0 ? Y : -2147483648.0;
+    }
+    const int32_t ix = (int32_t)rint(X);
+    const int32_t iy = (int32_t)rint(Y);
+    const int32_t sx = ix >> 5, sy = iy >> 5;
+    const int32_t x0 = dpg::clampi(sx, 0, wm);
+    const int32_t y0 = dpg::clampi(sy, 0, hm);
+    const int32_t y1 = dpg::clampi(sy + 1, 0, hm);
+    const bool same = (uint32_t)sx >= (uint32_t)wm; // sx < 0 or sx >= w-1: x1 == x0
+    const uint32_t o0 = (uint32_t)(y0 * pitch + x0);
+    const uint32_t o1 = (uint32_t)(y1 * pitch + x0);
+    const unsigned long long a = *(gpair_t)(roi + o0);
+    const unsigned long long b = *(gpair_t)(roi + o1);
     const uint32_t a0 = (uint32_t)a, b0 = (uint32_t)b;
-    const bool same = t.x1 == t.x0;
     const uint32_t a1 = same ? a0 : (uint32_t)(a >> 32);
     const uint32_t b1 = same ? b0 : (uint32_t)(b >> 32);
-    return dpg::blend_gray(a0, a1, b0, b1, t.fx, t.fy);
+    return dpg::blend_gray(a0, a1, b0, b1, ix & 31, iy & 31);
+}
+
+template <bool kAnchor, bool kSafe>
+__device__ __forceinline__ void texel_loop(const RefineArgs &a, WaveLds &L, gpix_t roi, int pitch, int wm, int hm,
+                                           int &s, int &ss, int &sx)
+{
+    const int lane = (int)__lane_id();
+    const int cell = a.cell;
+    const int N = cell * cell;
+    const float inv_cell = 1.0f / (float)cell;
+    for (int t = lane; t < N; t += kWave) {
+        // t / cell exactly: t < 256, cell <= 16, fraction >= 0.5/cell from an integer
+        const int py = (int)(((float)t + 0.5f) * inv_cell);
+        const int px = t - py * cell;
+        const int gv = sample_texel<kSafe>(L, roi, pitch, wm, hm, px, py);
+        s += gv;
+        ss += gv * gv;
+        if (kAnchor)
+            L.anchor[t] = (uint16_t)gv;
+        else
+            sx += (int)L.anchor[t] * gv;
+    }
 }
 
 // Integer moments of one view's window, all 64 lanes on its texels
@@ -103,24 +157,34 @@ __device__ __forceinline__ void view_moments(const RefineArgs &a, WaveLds &L, in
                                              int &SS, int &SX)
 {
     const int lane = (int)__lane_id();
-    const dpg::TexMap tm = L.map[slot];
+    const int cell = a.cell;
+    {
+        // row / column terms of this view's map (lanes 0..15 rows, 16..31 columns)
+        const dpg::TexMap &tm = L.map[slot];
+        if (lane < cell) {
+            const double y = (double)lane;
+            L.rowt[lane][0] = tm.m1 * y + tm.m2;
+            L.rowt[lane][1] = tm.m4 * y + tm.m5;
+            L.rowt[lane][2] = tm.m7 * y + 1.0;
+        } else if (lane >= 16 && lane - 16 < cell) {
+            const double x = (double)(lane - 16);
+            L.colt[lane - 16][0] = tm.m0 * x;
+            L.colt[lane - 16][1] = tm.m3 * x;
+            L.colt[lane - 16][2] = tm.m6 * x;
+        }
+    }
+    const int tlx = uni(L.map[slot].tlx), tly = uni(L.map[slot].tly);
+    const int wm = uni(L.map[slot].w) - 1, hm = uni(L.map[slot].h) - 1;
+    const bool safe = uni(L.map[slot].safe) != 0;
     const dpg::ViewDev *__restrict__ vw = a.views + view;
     const int pitch = vw->pitch;
-    const gpix_t roi = (gpix_t)vw->img + (size_t)tm.tly * (size_t)pitch + tm.tlx;
-    const int cell = a.cell;
-    const int N = cell * cell;
+    const gpix_t roi = (gpix_t)vw->img + ((size_t)tly * (size_t)pitch + (size_t)tlx);
+    wave_sync();
     int s = 0, ss = 0, sx = 0;
-    for (int t = lane; t < N; t += kWave) {
-        const int py = t / cell;
-        const int px = t - py * cell;
-        const int gv = sample_texel(roi, pitch, tm, px, py);
-        s += gv;
-        ss += gv * gv;
-        if (kAnchor)
-            L.anchor[t] = (uint16_t)gv;
-        else
-            sx += (int)L.anchor[t] * gv;
-    }
+    if (safe)
+        texel_loop<kAnchor, true>(a, L, roi, pitch, wm, hm, s, ss, sx);
+    else
+        texel_loop<kAnchor, false>(a, L, roi, pitch, wm, hm, s, ss, sx);
     S = wave_total(s);
     SS = wave_total(ss);
     SX = kAnchor ? 0 : wave_total(sx);
@@ -180,13 +244,26 @@ __device__ int wave_scores(const RefineArgs &a, WaveLds &L, const double *nn, co
         }
         const int kb = base == 0 ? 1 : base;
         const int ke = (base + kMapChunk < m) ? base + kMapChunk : m;
+        const uint64_t valid = va ? okmask : 0ull;
         for (int k = kb; k < ke; ++k) {
-            double sc = -1.0;
-            if (va && ((okmask >> (k - base)) & 1ull)) {
+            if ((valid >> (k - base)) & 1ull) {
                 int Sb, Sbb, Sab;
                 view_moments<false>(a, L, k - base, uni(L.vlist[k]), Sb, Sbb, Sab);
-                sc = dpg::ncc_finish(N, Sa, Saa, Sb, Sbb, Sab, a.opt.ncc_denom_min);
+                if (lane == 0) {
+                    L.mom[k - base][0] = Sb;
+                    L.mom[k - base][1] = Sbb;
+                    L.mom[k - base][2] = Sab;
+                }
             }
+        }
+        wave_sync();
+        // NCC finish, one lane per view of the chunk (error_measurements.cpp:47-59)
+        const int k = base + lane;
+        if (k >= kb && k < ke) {
+            double sc = -1.0;
+            if ((valid >> lane) & 1ull)
+                sc = dpg::ncc_finish(N, Sa, Saa, L.mom[lane][0], L.mom[lane][1], L.mom[lane][2],
+                                     a.opt.ncc_denom_min);
             L.score[k - 1] = sc;
         }
         wave_sync();
