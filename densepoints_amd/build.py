@@ -53,7 +53,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    extra = os.environ.get("DP_EXTRA_FLAGS", "").split()
+    cmd = [hipcc(), *FLAGS, *extra, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

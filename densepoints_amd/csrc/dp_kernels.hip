@@ -20,7 +20,7 @@
 namespace dpk {
 namespace {
 
-constexpr int kMapChunk = 64; // views whose window maps are staged per pass
+constexpr int kMapChunk = 32; // views whose window maps are staged per pass
 
 // Per-wavefront LDS: everything uniform across the wave lives here so that
 // registers only hold short-lived values (the evaluation is fp64-heavy).
@@ -521,8 +521,16 @@ __device__ void child_position(const RefineArgs &a, const dp_patch &par, int dir
     }
 }
 
+// Occupancy target (waves per SIMD).  The kernel is latency-bound on the
+// window gathers; the register allocator spills only in the per-evaluation
+// setup code at this target, never in the texel loops (checked in the ISA).
+#ifndef DP_REFINE_WAVES_PER_EU
+#define DP_REFINE_WAVES_PER_EU 4
+#endif
+#define DP_REFINE_BOUNDS __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DP_REFINE_WAVES_PER_EU)))
+
 template <int kMode>
-__global__ __launch_bounds__(kBlock) void refine_kernel(RefineArgs a)
+__global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
 {
     __shared__ WaveLds lds[kWavesPerBlock];
     WaveLds &L = lds[threadIdx.x / kWave];
