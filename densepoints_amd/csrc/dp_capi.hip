@@ -263,7 +263,7 @@ extern "C" int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out)
         return rc;
     }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->d_work, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_work, dpk::kWorkCounters * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_evals, sizeof(unsigned long long)) != hipSuccess ||
         hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess) {
         dp_ctx_destroy(c);
@@ -920,6 +920,13 @@ extern "C" int64_t dp_synth_seeds(const dp_synth_config *cfg, const double *P, d
 // probes (densepoints_probe.h)
 // ---------------------------------------------------------------------------
 
+extern "C" int dp_debug_stamps(uint64_t *out8)
+{
+    if (!out8)
+        return DP_E_ARG;
+    return dpk::read_stamps((unsigned long long *)out8);
+}
+
 extern "C" void dp_probe_sincos(double x, double *s, double *c) { dpm::sincos(x, *s, *c); }
 extern "C" double dp_probe_acos(double x) { return dpm::acos(x); }
 
@@ -963,6 +970,28 @@ __global__ void probe_math_kernel(const double *x, int n, double *out)
     out[4 * i + 1] = c;
     out[4 * i + 2] = dpm::acos(x[i]);
     out[4 * i + 3] = sqrt(fabs(x[i]));
+    // exact shortcuts of the texel loop vs the plain expressions (0 = equal)
+    const double w = 1e-3 + fabs(x[i]) * 7.0;
+    const double q = 32.0 / w;
+    const double v = x[i] * 3.0e4;
+    const double na = x[i] * 1234.567 + 0.25, nb = x[i] * -0.0071 + 1.5;
+    // each shortcut only inside its documented range
+    int ok = 1;
+    if (w < 1e6)
+        ok = ok && __double_as_longlong(dpk::div32_safe(w)) == __double_as_longlong(q);
+    if (fabs(v) < 2147483647.0)
+        ok = ok && dpk::rint_i32(v) == (int32_t)rint(v);
+    ok = ok && __double_as_longlong(dpk::div_rn(na, nb)) == __double_as_longlong(na / nb);
+    // a sweep of nearby denominators per input (stress the final rounding)
+    for (int k = 1; k <= 16 && ok; ++k) {
+        const double wk = w * (1.0 + k * 1.1102230246251565e-16 * (double)(i % 7 + 1));
+        if (wk < 1e6)
+            ok = __double_as_longlong(dpk::div32_safe(wk)) == __double_as_longlong(32.0 / wk);
+        const double bk = nb + k * 3.3e-5;
+        ok = ok && __double_as_longlong(dpk::div_rn(na, bk)) == __double_as_longlong(na / bk);
+    }
+    if (!ok)
+        out[4 * i + 3] = -1.0;
 }
 } // namespace
 

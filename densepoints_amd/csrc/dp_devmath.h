@@ -1,0 +1,48 @@
+// dp_devmath.h -- device-only exact arithmetic shortcuts used by the texel
+// loop (gfx950).  Both are bit-identical to the plain expressions they replace
+// in the ranges stated; tests/test_gpu_parity.py checks them on the GPU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpk {
+
+// round-half-even of |v| < 2^31 to int32: adding 1.5*2^52 leaves rint(v) in
+// the low mantissa word (the same value rint + cvt produce).
+__device__ __forceinline__ int32_t rint_i32(double v)
+{
+    const double r = v + 6755399441055744.0;
+    return (int32_t)(uint32_t)__double_as_longlong(r);
+}
+
+// Correctly rounded a / b without v_rcp_f64 (a 1/16-rate transcendental on
+// gfx950, measured): the v_rcp_f32 seed (1 ulp of f32) refined by two fp64
+// Newton steps reaches the accuracy of LLVM's f64 division sequence after its
+// two steps, and the same final correction q = fma(fma(-b, q0, a), r, q0)
+// rounds correctly.  Valid when no intermediate overflows/underflows: the
+// guarded form falls back to '/' outside 2^-120 < |b| < 2^120,
+// 2^-900 < |a| < 2^900 (and for a == 0, keeping the sign of zero).
+__device__ __forceinline__ double div_rn_core(double a, double b)
+{
+    double r = (double)__builtin_amdgcn_rcpf((float)b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = a * r;
+    const double rem = __builtin_fma(-b, q, a);
+    return __builtin_fma(rem, r, q);
+}
+
+__device__ __forceinline__ double div_rn(double a, double b)
+{
+    const double ab = fabs(b), aa = fabs(a);
+    if (ab > 7.52316384526264e-37 && ab < 1.329227995784916e+36 && aa > 1.4e-271 && aa < 8.4e270)
+        return div_rn_core(a, b);
+    return a / b;
+}
+
+// 32 / W for 1e-3 < W < 1e6 (TexMap::safe)
+__device__ __forceinline__ double div32_safe(double w) { return div_rn_core(32.0, w); }
+
+} // namespace dpk

@@ -83,12 +83,64 @@ DP_HD bool window_corners(const ViewDev &rv, const double *Xs, const double *nn,
 
 // Sampling map of one view: window pixel (x, y) -> ROI coordinates, plus ROI.
 struct TexMap {
-    double m0, m1, m2, m3, m4, m5, m6, m7; // m8 == 1
+    double m0, m1, m2, m3, m4, m5, m6, m7, m8; // m8 == n (cell)
     int32_t tlx, tly, w, h;
-    int32_t safe; // W > 1e-3 and |X|,|Y| < 2^30 at all window corners: the
+    int32_t safe; // 1e-3 < W < 1e6 and |X|,|Y| < 2^30 at all window corners: the
                   // int-range clamps and the W != 0 select never fire
     int32_t pad;
 };
+
+// Projective map of the window square [0,n]^2 onto the ROI-relative quad
+// (x[i], y[i]) plus the ROI and the `safe` flag; false for a degenerate quad.
+DP_HD bool quad_map(const double *x, const double *y, int tlx, int tly, int rw, int rh, int cell, TexMap &tm)
+{
+    // square [0,n]^2 -> quad (projective, Heckbert), the inverse of the
+    // reference's findHomography(quad -> square) used by warpPerspective.
+    const double sx = ((x[0] - x[1]) + x[2]) - x[3];
+    const double sy = ((y[0] - y[1]) + y[2]) - y[3];
+    const double ax = x[1] - x[2], bx = x[3] - x[2];
+    const double ay = y[1] - y[2], by = y[3] - y[2];
+    const double det = ax * by - bx * ay;
+    if (det == 0.0)
+        return false;
+    const double g = (sx * by - bx * sy) / det;
+    const double h = (ax * sy - sx * ay) / det;
+    // pixel units without divisions: (a x + b y + c n) / (g x + h y + n)
+    const double n = (double)cell;
+    tm.m0 = (x[1] - x[0]) + g * x[1];
+    tm.m1 = (x[3] - x[0]) + h * x[3];
+    tm.m2 = x[0] * n;
+    tm.m3 = (y[1] - y[0]) + g * y[1];
+    tm.m4 = (y[3] - y[0]) + h * y[3];
+    tm.m5 = y[0] * n;
+    tm.m6 = g;
+    tm.m7 = h;
+    tm.m8 = n;
+    tm.tlx = tlx;
+    tm.tly = tly;
+    tm.w = rw;
+    tm.h = rh;
+    // W is affine in (x, y) and X/W, Y/W are linear-fractional: with W > 0 on
+    // the window rectangle their extremes are at its corners.
+    bool safe = true;
+    const double e = (double)(cell - 1);
+    for (int c = 0; c < 4; ++c) {
+        const double px = (c & 1) ? e : 0.0, py = (c & 2) ? e : 0.0;
+        const double W = (tm.m7 * py + tm.m8) + tm.m6 * px;
+        if (!(W > 1e-3) || !(W < 1e6)) {
+            safe = false;
+            continue;
+        }
+        const double q = 32.0 / W;
+        const double X = ((tm.m1 * py + tm.m2) + tm.m0 * px) * q;
+        const double Y = ((tm.m4 * py + tm.m5) + tm.m3 * px) * q;
+        if (!(fabs(X) < 1073741824.0) || !(fabs(Y) < 1073741824.0))
+            safe = false;
+    }
+    tm.safe = safe ? 1 : 0;
+    tm.pad = 0;
+    return true;
+}
 
 // Returns false for the reference's empty texture (corner outside the view,
 // empty ROI, or a degenerate quad).
@@ -122,50 +174,7 @@ DP_HD bool texture_map(const ViewDev &v, const double *c12, int cell, TexMap &tm
         x[i] = (double)(fx[i] - ftx);
         y[i] = (double)(fy[i] - fty);
     }
-    // square [0,n]^2 -> quad (projective, Heckbert), the inverse of the
-    // reference's findHomography(quad -> square) used by warpPerspective.
-    const double sx = ((x[0] - x[1]) + x[2]) - x[3];
-    const double sy = ((y[0] - y[1]) + y[2]) - y[3];
-    const double ax = x[1] - x[2], bx = x[3] - x[2];
-    const double ay = y[1] - y[2], by = y[3] - y[2];
-    const double det = ax * by - bx * ay;
-    if (det == 0.0)
-        return false;
-    const double g = (sx * by - bx * sy) / det;
-    const double h = (ax * sy - sx * ay) / det;
-    const double n = (double)cell;
-    tm.m0 = ((x[1] - x[0]) + g * x[1]) / n;
-    tm.m1 = ((x[3] - x[0]) + h * x[3]) / n;
-    tm.m2 = x[0];
-    tm.m3 = ((y[1] - y[0]) + g * y[1]) / n;
-    tm.m4 = ((y[3] - y[0]) + h * y[3]) / n;
-    tm.m5 = y[0];
-    tm.m6 = g / n;
-    tm.m7 = h / n;
-    tm.tlx = tlx;
-    tm.tly = tly;
-    tm.w = rw;
-    tm.h = rh;
-    // W is affine in (x, y) and X/W, Y/W are linear-fractional: with W > 0 on
-    // the window rectangle their extremes are at its corners.
-    bool safe = true;
-    const double e = (double)(cell - 1);
-    for (int c = 0; c < 4; ++c) {
-        const double px = (c & 1) ? e : 0.0, py = (c & 2) ? e : 0.0;
-        const double W = (tm.m7 * py + 1.0) + tm.m6 * px;
-        if (!(W > 1e-3)) {
-            safe = false;
-            continue;
-        }
-        const double q = 32.0 / W;
-        const double X = ((tm.m1 * py + tm.m2) + tm.m0 * px) * q;
-        const double Y = ((tm.m4 * py + tm.m5) + tm.m3 * px) * q;
-        if (!(fabs(X) < 1073741824.0) || !(fabs(Y) < 1073741824.0))
-            safe = false;
-    }
-    tm.safe = safe ? 1 : 0;
-    tm.pad = 0;
-    return true;
+    return quad_map(x, y, tlx, tly, rw, rh, cell, tm);
 }
 
 DP_HD int32_t clampi(int32_t v, int32_t lo, int32_t hi)
@@ -185,7 +194,7 @@ DP_HD Tap window_tap(const TexMap &tm, int px, int py)
 {
     const double X0 = tm.m1 * (double)py + tm.m2;
     const double Y0 = tm.m4 * (double)py + tm.m5;
-    const double W0 = tm.m7 * (double)py + 1.0;
+    const double W0 = tm.m7 * (double)py + tm.m8;
     double W = W0 + tm.m6 * (double)px;
     W = (W != 0.0) ? 32.0 / W : 0.0;
     double X = (X0 + tm.m0 * (double)px) * W;

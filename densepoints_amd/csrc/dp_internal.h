@@ -3,6 +3,7 @@
 
 #include "../../include/densepoints.h"
 #include "dp_geom.h"
+#include "dp_devmath.h"
 #include <hip/hip_runtime.h>
 
 namespace dpk {
@@ -10,6 +11,9 @@ namespace dpk {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
+// refine work counters: one per XCD range, each on its own 64-B line
+constexpr int kWorkStride = 16;
+constexpr int kWorkCounters = 8 * kWorkStride;
 
 // Arguments of the fused refine kernel (one wavefront per patch).
 struct RefineArgs {
@@ -21,7 +25,7 @@ struct RefineArgs {
     dp_options opt;
     dp_patch *patches;       // in/out (EVAL..EXPAND on existing patches)
     uint8_t *accept;         // optional
-    uint32_t *work;          // dequeue counter (zeroed per launch)
+    uint32_t *work;          // dequeue counters, kWorkCounters (zeroed per launch)
     unsigned long long *evals; // optional: total objective evaluations
     // expansion-generation fields (mode DP_MODE_EXPAND with parents != null)
     const dp_patch *parents; // queue; child c expands parents[parent0 + c/4] direction c%4
@@ -41,6 +45,7 @@ struct ClaimArgs {
 };
 
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s);
+int read_stamps(unsigned long long *out);
 hipError_t launch_claims(const ClaimArgs &a, hipStream_t s);
 hipError_t launch_resolve(const ClaimArgs &a, uint8_t *accepted, hipStream_t s);
 hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand, const uint8_t *accepted,

@@ -28,8 +28,8 @@ struct WaveLds {
     dpg::TexMap map[kMapChunk];                 // window maps of the current view chunk
     double score[DP_MAX_VIEWS];                 // NCC per scored view
     int32_t mom[kMapChunk][3];                  // Sb, Sbb, Sab of the chunk's views
-    double rowt[DP_MAX_CELL][4];                // per window row: X0, Y0, W0 of the current view
-    double colt[DP_MAX_CELL][4];                // per window column: m0*x, m3*x, m6*x
+    double rowt[64][3];                         // per pass: window rows X0, Y0, W0 of slot j at j*(64/G)
+    double colt[64][3];                         // per pass: window columns m0*x, m3*x, m6*x (same slots)
     double c12[12];                             // window corners
     double X[3], n[3];                          // stored pose (f32 widened)
     double sp[4][3];                            // Nelder-Mead simplex
@@ -41,7 +41,26 @@ struct WaveLds {
     int32_t ref, m;                             // reference view, |visible|
     uint16_t anchor[DP_MAX_CELL * DP_MAX_CELL]; // texture 0 (gray)
     uint8_t vlist[DP_MAX_VIEWS];                // visible list (ascending)
+#ifdef DP_STAMPS
+    unsigned long long stamp[8];                // diagnostic build only: cycles per phase
+#endif
 };
+
+#ifdef DP_STAMPS
+// Diagnostic build (-DDP_STAMPS): s_memtime deltas per phase, summed per wave
+// in LDS and flushed to g_stamps.  Shares only; never a timed build.
+__device__ unsigned long long g_stamps[8];
+#define STAMP_BEGIN unsigned long long _st = __builtin_amdgcn_s_memtime()
+#define STAMP(L, cat)                                                    \
+    do {                                                                 \
+        const unsigned long long _n = __builtin_amdgcn_s_memtime();      \
+        (L).stamp[cat] += _n - _st;                                      \
+        _st = _n;                                                        \
+    } while (0)
+#else
+#define STAMP_BEGIN
+#define STAMP(L, cat)
+#endif
 
 __device__ __forceinline__ void wave_sync()
 {
@@ -52,10 +71,21 @@ __device__ __forceinline__ void wave_sync()
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Lane id through an opaque (volatile) mbcnt: values derived from it are
+// recomputed where they are used instead of being hoisted to kernel scope,
+// where dozens of per-lane LDS addresses would stay live in VGPRs across the
+// whole Nelder-Mead loop.
+__device__ __forceinline__ int lane_id()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 // visible mask -> ascending list + count (Patch::GetTrullyVisibleImages)
 __device__ __forceinline__ void decode_vis(WaveLds &L, uint64_t v0, uint64_t v1)
 {
-    const int lane = (int)__lane_id();
+    const int lane = lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
     const int c0 = __popcll(v0);
     if ((v0 >> lane) & 1ull)
@@ -84,22 +114,28 @@ __device__ __forceinline__ int wave_total(int v)
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-// One window texel of view map `tm` whose row/column terms are in L.rowt /
-// L.colt (same roundings as dpg::window_tap: X0 = m1*y + m2, W0 = m7*y + 1,
-// W = W0 + m6*x, X = (X0 + m0*x) * (32/W)).  Two 8-byte loads fetch taps
-// (x0, x0+1) of rows y0 and y1 -- the right neighbour is always inside the
-// image because the ROI ends at floor(max u) <= W-1 -- and a select applies
-// BORDER_REPLICATE.  kSafe: the map's int-range clamps / W != 0 select never
-// fire on this window (TexMap::safe), so they are skipped.
+// Window coordinate of texel (px, py) of the view in table slot j, whose
+// row/column terms are in L.rowt[j] / L.colt[j] (same roundings as
+// dpg::window_tap: X0 = m1*y + m2, W0 = m7*y + m8, W = W0 + m6*x,
+// X = (X0 + m0*x) * (32/W)).  kSafe: the map's int-range clamps / W != 0
+// select never fire on this window (TexMap::safe), so they are skipped.
 template <bool kSafe>
-__device__ __forceinline__ int sample_texel(const WaveLds &L, gpix_t roi, int pitch, int wm, int hm, int px,
-                                            int py)
+__device__ __forceinline__ void texel_coord(const WaveLds &L, int rb, int px, int py, int32_t &ix, int32_t &iy)
 {
-    const double X0 = L.rowt[py][0], Y0 = L.rowt[py][1], W0 = L.rowt[py][2];
-    const double cX = L.colt[px][0], cY = L.colt[px][1], cW = L.colt[px][2];
+    const double X0 = L.rowt[rb + py][0], Y0 = L.rowt[rb + py][1], W0 = L.rowt[rb + py][2];
+    const double cX = L.colt[rb + px][0], cY = L.colt[rb + px][1], cW = L.colt[rb + px][2];
     double W = W0 + cW;
     if (kSafe) {
-        W = 32.0 / W;
+#ifdef DP_DIAG_NODIV
+        W = 32.0 * W; // diagnostic build: timing only, wrong results
+#elif defined(DP_DIAG_RCP0)
+        W = 32.0 * __builtin_amdgcn_rcp(W); // diagnostic: rcp only
+#elif defined(DP_DIAG_RCP1)
+        { const double r = __builtin_amdgcn_rcp(W); const double e = __builtin_fma(-W, r, 1.0);
+          W = 32.0 * __builtin_fma(r, e, r); } // diagnostic: rcp + 1 Newton
+#else
+        W = div32_safe(W);
+#endif
     } else {
         W = (W != 0.0) ? 32.0 / W : 0.0;
     }
@@ -111,83 +147,280 @@ __device__ __forceinline__ int sample_texel(const WaveLds &L, gpix_t roi, int pi
         Y = Y < 2147483647.0 ? Y : 2147483647.0;
         Y = Y > -2147483648.0 ? Y : -2147483648.0;
     }
-    const int32_t ix = (int32_t)rint(X);
-    const int32_t iy = (int32_t)rint(Y);
+    ix = rint_i32(X);
+    iy = rint_i32(Y);
+}
+
+// Taps (x0, x0+1) of rows y0, y1 by two 8-byte loads -- the right neighbour
+// is always inside the image because the ROI ends at floor(max u) <= W-1 --
+// then BORDER_REPLICATE select, bilinear and BGR2GRAY.
+struct TexelLoad {
+    unsigned long long a, b;
+    uint32_t f; // fx | fy << 5 | same << 10
+};
+
+__device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm, int hm, int32_t ix, int32_t iy)
+{
     const int32_t sx = ix >> 5, sy = iy >> 5;
     const int32_t x0 = dpg::clampi(sx, 0, wm);
     const int32_t y0 = dpg::clampi(sy, 0, hm);
     const int32_t y1 = dpg::clampi(sy + 1, 0, hm);
-    const bool same = (uint32_t)sx >= (uint32_t)wm; // sx < 0 or sx >= w-1: x1 == x0
-    const uint32_t o0 = (uint32_t)(y0 * pitch + x0);
-    const uint32_t o1 = (uint32_t)(y1 * pitch + x0);
-    const unsigned long long a = *(gpair_t)(roi + o0);
-    const unsigned long long b = *(gpair_t)(roi + o1);
-    const uint32_t a0 = (uint32_t)a, b0 = (uint32_t)b;
-    const uint32_t a1 = same ? a0 : (uint32_t)(a >> 32);
-    const uint32_t b1 = same ? b0 : (uint32_t)(b >> 32);
-    return dpg::blend_gray(a0, a1, b0, b1, ix & 31, iy & 31);
+    TexelLoad t;
+    const uint32_t same = (uint32_t)sx >= (uint32_t)wm; // sx < 0 or sx >= w-1: x1 == x0
+#ifdef DP_DIAG_HOTIMG
+    // diagnostic build: every gather hits one 1 KiB block (timing only)
+    t.a = *(gpair_t)(roi + ((uint32_t)(y0 * 16 + x0) & 127u));
+    t.b = *(gpair_t)(roi + ((uint32_t)(y1 * 16 + x0) & 127u));
+#else
+    t.a = *(gpair_t)(roi + (uint32_t)(y0 * pitch + x0));
+    t.b = *(gpair_t)(roi + (uint32_t)(y1 * pitch + x0));
+#endif
+    t.f = (uint32_t)(ix & 31) | ((uint32_t)(iy & 31) << 5) | (same << 10);
+    return t;
 }
 
-template <bool kAnchor, bool kSafe>
-__device__ __forceinline__ void texel_loop(const RefineArgs &a, WaveLds &L, gpix_t roi, int pitch, int wm, int hm,
-                                           int &s, int &ss, int &sx)
+__device__ __forceinline__ int texel_gray(const TexelLoad &t)
 {
-    const int lane = (int)__lane_id();
+    const bool same = (t.f >> 10) & 1u;
+    const uint32_t a0 = (uint32_t)t.a, b0 = (uint32_t)t.b;
+    const uint32_t a1 = same ? a0 : (uint32_t)(t.a >> 32);
+    const uint32_t b1 = same ? b0 : (uint32_t)(t.b >> 32);
+    return dpg::blend_gray(a0, a1, b0, b1, (int)(t.f & 31u), (int)((t.f >> 5) & 31u));
+}
+
+// row / column terms of map `tm` into the table rows from rb; entry e in
+// [0, 32): e < 16 -> row e, else column e - 16
+__device__ __forceinline__ void fill_tables(WaveLds &L, int rb, const dpg::TexMap &tm, int e, int cell)
+{
+    if (e < 16) {
+        if (e < cell) {
+            const double y = (double)e;
+            L.rowt[rb + e][0] = tm.m1 * y + tm.m2;
+            L.rowt[rb + e][1] = tm.m4 * y + tm.m5;
+            L.rowt[rb + e][2] = tm.m7 * y + tm.m8;
+        }
+    } else if (e - 16 < cell) {
+        const double x = (double)(e - 16);
+        L.colt[rb + e - 16][0] = tm.m0 * x;
+        L.colt[rb + e - 16][1] = tm.m3 * x;
+        L.colt[rb + e - 16][2] = tm.m6 * x;
+    }
+}
+
+// slot list of a pass: byte j = chunk slot of pass slot j, 0xff = none
+__device__ __forceinline__ int pick8(int j, uint64_t q)
+{
+    return (int)(int8_t)(uint8_t)(q >> (8 * j));
+}
+
+// Sum over each group of LP = 64/G lanes (DPP); the total of group j lands in
+// lane LP*(j+1)-1.
+template <int G>
+__device__ __forceinline__ int group_total(int v)
+{
+    constexpr int LP = kWave / G;
+    static_assert(LP >= 8, "groups of at least 8 lanes");
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false); // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false); // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xe, false); // row_shr:4
+    if (LP >= 16)
+        v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xc, false); // row_shr:8
+    if (LP >= 32)
+        v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    if (LP == 64)
+        v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return v;
+}
+
+#ifndef DP_TEX_PER_LANE
+#define DP_TEX_PER_LANE 4
+#endif
+// texels per lane per view pass: a pass of G views needs N <= 64 * K / G
+constexpr int kTexPerLane = DP_TEX_PER_LANE;
+
+// widest view pass (views per wavefront pass) whose texels fit kTexPerLane per
+// lane; the refine kernels are instantiated per width
+__host__ __device__ constexpr int pass_width(int cell)
+{
+    return cell * cell <= 8 * kTexPerLane    ? 8
+           : cell * cell <= 16 * kTexPerLane ? 4
+           : cell * cell <= 32 * kTexPerLane ? 2
+           : cell * cell <= 64 * kTexPerLane ? 1
+                                             : 0;
+}
+
+// One pass over G views: lanes LP*j .. LP*j+LP-1 own pass slot j and texels
+// t = g, g+LP, ... (at most kTexPerLane).  Safe windows (the common case):
+// all gathers of a lane are issued before any is consumed -- one memory round
+// trip per pass.  kAnchor: slot 0 is texture 0, whose gray values go to LDS
+// before the other slots form their cross moments.
+template <int G, bool kAnchor>
+__device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &L, int j, bool act, gpix_t roi,
+                                                  int pitch, int wm, int hm, int &s, int &ss, int &sx)
+{
+    constexpr int LP = kWave / G;
+    const int g = lane_id() & (LP - 1);
     const int cell = a.cell;
     const int N = cell * cell;
     const float inv_cell = 1.0f / (float)cell;
-    for (int t = lane; t < N; t += kWave) {
+    TexelLoad tl[kTexPerLane];
+#pragma unroll
+    for (int i = 0; i < kTexPerLane; ++i) {
+        int t = g + LP * i;
+        t = t < N ? t : N - 1; // dead texels re-load a live address
         // t / cell exactly: t < 256, cell <= 16, fraction >= 0.5/cell from an integer
         const int py = (int)(((float)t + 0.5f) * inv_cell);
         const int px = t - py * cell;
-        const int gv = sample_texel<kSafe>(L, roi, pitch, wm, hm, px, py);
-        s += gv;
-        ss += gv * gv;
-        if (kAnchor)
-            L.anchor[t] = (uint16_t)gv;
-        else
-            sx += (int)L.anchor[t] * gv;
+        int32_t ix, iy;
+        texel_coord<true>(L, j * (64 / G), px, py, ix, iy);
+        tl[i] = texel_fetch(roi, pitch, wm, hm, ix, iy);
+    }
+    if (kAnchor) {
+        if (j == 0) {
+#pragma unroll
+            for (int i = 0; i < kTexPerLane; ++i) {
+                const int t = g + LP * i;
+                if (t < N) {
+                    const int gv = texel_gray(tl[i]);
+                    L.anchor[t] = (uint16_t)gv;
+                    s += gv;
+                    ss += gv * gv;
+                }
+            }
+        }
+        wave_sync();
+    }
+    if (act && !(kAnchor && j == 0)) {
+#pragma unroll
+        for (int i = 0; i < kTexPerLane; ++i) {
+            const int t = g + LP * i;
+            if (t < N) {
+                const int gv = texel_gray(tl[i]);
+                s += gv;
+                ss += gv * gv;
+                sx += (int)L.anchor[t] * gv;
+            }
+        }
     }
 }
 
-// Integer moments of one view's window, all 64 lanes on its texels
-// (t = lane, lane+64, ...): coalesced gathers inside one small window.
-template <bool kAnchor>
-__device__ __forceinline__ void view_moments(const RefineArgs &a, WaveLds &L, int slot, int view, int &S,
-                                             int &SS, int &SX)
+struct Moments {
+    int s, ss, sx;
+};
+
+// Same pass for windows whose map may hit the int-range clamps or W == 0
+// (TexMap::safe false, rare): one texel at a time, kept out of line so that
+// it does not add to the register pressure of the safe path.  Plain scalar
+// arguments only: a reference to the kernel arguments would force a private
+// copy of them.
+template <int G, bool kAnchor>
+__device__ __attribute__((noinline)) Moments group_sample_clamped(WaveLds &L, int cell, int j, bool act, gpix_t roi,
+                                                                  int pitch, int wm, int hm)
 {
-    const int lane = (int)__lane_id();
-    const int cell = a.cell;
-    {
-        // row / column terms of this view's map (lanes 0..15 rows, 16..31 columns)
-        const dpg::TexMap &tm = L.map[slot];
-        if (lane < cell) {
-            const double y = (double)lane;
-            L.rowt[lane][0] = tm.m1 * y + tm.m2;
-            L.rowt[lane][1] = tm.m4 * y + tm.m5;
-            L.rowt[lane][2] = tm.m7 * y + 1.0;
-        } else if (lane >= 16 && lane - 16 < cell) {
-            const double x = (double)(lane - 16);
-            L.colt[lane - 16][0] = tm.m0 * x;
-            L.colt[lane - 16][1] = tm.m3 * x;
-            L.colt[lane - 16][2] = tm.m6 * x;
+    constexpr int LP = kWave / G;
+    const int g = lane_id() & (LP - 1);
+    const int N = cell * cell;
+    const float inv_cell = 1.0f / (float)cell;
+    Moments m = {0, 0, 0};
+    for (int phase = 0; phase < (kAnchor ? 2 : 1); ++phase) {
+        const bool mine = kAnchor ? ((j == 0) == (phase == 0)) && act : act;
+        if (mine) {
+            for (int t = g; t < N; t += LP) {
+                const int py = (int)(((float)t + 0.5f) * inv_cell);
+                const int px = t - py * cell;
+                int32_t ix, iy;
+                texel_coord<false>(L, j * (64 / G), px, py, ix, iy);
+                const int gv = texel_gray(texel_fetch(roi, pitch, wm, hm, ix, iy));
+                m.s += gv;
+                m.ss += gv * gv;
+                if (kAnchor && j == 0)
+                    L.anchor[t] = (uint16_t)gv;
+                else
+                    m.sx += (int)L.anchor[t] * gv;
+            }
         }
+        if (kAnchor)
+            wave_sync();
     }
-    const int tlx = uni(L.map[slot].tlx), tly = uni(L.map[slot].tly);
-    const int wm = uni(L.map[slot].w) - 1, hm = uni(L.map[slot].h) - 1;
-    const bool safe = uni(L.map[slot].safe) != 0;
-    const dpg::ViewDev *__restrict__ vw = a.views + view;
+    return m;
+}
+
+// Integer moments of up to G views (chunk slots in q; with kAnchor, pass slot
+// 0 is texture 0 and its Sa, Saa are returned in sa/saa) into L.mom[slot].
+template <int G, bool kAnchor>
+__device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, int base, uint64_t q, int &sa, int &saa)
+{
+    constexpr int LP = kWave / G;
+    const int lane = lane_id();
+    const int cell = a.cell;
+    // row/column tables: G slots x 32 entries
+    for (int e = lane; e < 32 * G; e += kWave) {
+        const int je = e >> 5;
+        const int ke = pick8(je, q);
+        if (ke >= 0)
+            fill_tables(L, je * (64 / G), L.map[ke], e & 31, cell);
+    }
+    const int j = lane / LP;
+    const int slot = pick8(j, q);
+    const bool act = slot >= 0;
+    const int sl = act ? slot : pick8(0, q);
+    const int tlx = L.map[sl].tlx, tly = L.map[sl].tly;
+    const int wm = L.map[sl].w - 1, hm = L.map[sl].h - 1;
+    const bool all_safe = __ballot(act && !L.map[sl].safe) == 0ull;
+    const dpg::ViewDev *__restrict__ vw = a.views + L.vlist[base + sl];
     const int pitch = vw->pitch;
     const gpix_t roi = (gpix_t)vw->img + ((size_t)tly * (size_t)pitch + (size_t)tlx);
     wave_sync();
     int s = 0, ss = 0, sx = 0;
-    if (safe)
-        texel_loop<kAnchor, true>(a, L, roi, pitch, wm, hm, s, ss, sx);
-    else
-        texel_loop<kAnchor, false>(a, L, roi, pitch, wm, hm, s, ss, sx);
-    S = wave_total(s);
-    SS = wave_total(ss);
-    SX = kAnchor ? 0 : wave_total(sx);
+    if (all_safe)
+        group_sample_safe<G, kAnchor>(a, L, j, act, roi, pitch, wm, hm, s, ss, sx);
+    else {
+        const Moments mm = group_sample_clamped<G, kAnchor>(L, a.cell, j, act, roi, pitch, wm, hm);
+        s = mm.s;
+        ss = mm.ss;
+        sx = mm.sx;
+    }
+    s = group_total<G>(s);
+    ss = group_total<G>(ss);
+    sx = group_total<G>(sx);
+    if (kAnchor) {
+        sa = __builtin_amdgcn_readlane(s, LP - 1);
+        saa = __builtin_amdgcn_readlane(ss, LP - 1);
+    }
+    if ((lane & (LP - 1)) == LP - 1 && act && !(kAnchor && j == 0)) {
+        L.mom[slot][0] = s;
+        L.mom[slot][1] = ss;
+        L.mom[slot][2] = sx;
+    }
+    wave_sync();
+}
+
+// all valid views of chunk bits `todo`, G at a time (texture 0 first if kAnchor)
+template <int G>
+__device__ __forceinline__ void views_all(const RefineArgs &a, WaveLds &L, int base, uint64_t todo, bool anchor, int &sa, int &saa)
+{
+    bool first = anchor;
+    while (todo || first) {
+        uint64_t q = ~0ull;
+        int i = 0;
+        if (first) {
+            q &= ~0xffull; // pass slot 0 = chunk slot 0 (texture 0)
+            i = 1;
+        }
+#pragma unroll
+        for (int s = 0; s < G; ++s) {
+            if (s >= i && todo) {
+                const uint64_t b = (uint64_t)__builtin_ctzll(todo);
+                todo &= todo - 1;
+                q = (q & ~(0xffull << (8 * s))) | (b << (8 * s));
+            }
+        }
+        if (first)
+            views_pass<G, true>(a, L, base, q, sa, saa);
+        else
+            views_pass<G, false>(a, L, base, q, sa, saa);
+        first = false;
+    }
 }
 
 // One evaluation's NCC scores against texture 0 -> L.score[0..nv-1]
@@ -196,9 +429,11 @@ __device__ __forceinline__ void view_moments(const RefineArgs &a, WaveLds &L, in
 // ROI) into LDS; then the views are sampled one after another by the whole
 // wavefront (texture 0 first, kept in LDS), each reduced to exact integer
 // moments with DPP.  Returns the number of scores; sets *degen on dx == 0.
-__device__ int wave_scores(const RefineArgs &a, WaveLds &L, const double *nn, const double *pp, bool &degen)
+template <int G>
+__device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, const double *nn, const double *pp, bool &degen)
 {
-    const int lane = (int)__lane_id();
+    const int lane = lane_id();
+    STAMP_BEGIN;
     const int m = uni(L.m);
     const int nv = m - 1;
     const int cell = a.cell;
@@ -223,9 +458,10 @@ __device__ int wave_scores(const RefineArgs &a, WaveLds &L, const double *nn, co
     int Sa = 0, Saa = 0;
     bool va = false;
     for (int base = 0; base < m; base += kMapChunk) {
+        // window maps of this chunk: lane k builds view base+k's map
         bool ok = false;
         const int kk = base + lane;
-        if (kk < m) {
+        if (lane < kMapChunk && kk < m) {
             dpg::TexMap tm;
             ok = dpg::texture_map(a.views[L.vlist[kk]], L.c12, cell, tm);
             if (ok)
@@ -233,30 +469,21 @@ __device__ int wave_scores(const RefineArgs &a, WaveLds &L, const double *nn, co
         }
         const uint64_t okmask = __ballot(ok);
         wave_sync();
-        if (base == 0) {
-            // texture 0 = lowest-index visible view (optimization_opencv.cpp:24-28)
+        STAMP(L, 0);
+        // texture 0 = lowest-index visible view (optimization_opencv.cpp:24-28)
+        if (base == 0)
             va = okmask & 1ull;
-            if (va) {
-                int dummy;
-                view_moments<true>(a, L, 0, uni(L.vlist[0]), Sa, Saa, dummy);
-            }
-            wave_sync();
-        }
         const int kb = base == 0 ? 1 : base;
         const int ke = (base + kMapChunk < m) ? base + kMapChunk : m;
         const uint64_t valid = va ? okmask : 0ull;
-        for (int k = kb; k < ke; ++k) {
-            if ((valid >> (k - base)) & 1ull) {
-                int Sb, Sbb, Sab;
-                view_moments<false>(a, L, k - base, uni(L.vlist[k]), Sb, Sbb, Sab);
-                if (lane == 0) {
-                    L.mom[k - base][0] = Sb;
-                    L.mom[k - base][1] = Sbb;
-                    L.mom[k - base][2] = Sab;
-                }
-            }
-        }
+        // scored views of this chunk (invalid ones skipped), G per pass
+        const uint64_t todo = valid & (((ke - base) >= 64 ? ~0ull : ((1ull << (ke - base)) - 1ull)) &
+                                       ~((1ull << (kb - base)) - 1ull));
+        const bool anc = base == 0 && va;
+        views_all<G>(a, L, base, todo, anc, Sa, Saa);
+        STAMP(L, 1);
         wave_sync();
+        STAMP(L, 2);
         // NCC finish, one lane per view of the chunk (error_measurements.cpp:47-59)
         const int k = base + lane;
         if (k >= kb && k < ke) {
@@ -267,12 +494,14 @@ __device__ int wave_scores(const RefineArgs &a, WaveLds &L, const double *nn, co
             L.score[k - 1] = sc;
         }
         wave_sync();
+        STAMP(L, 3);
     }
     return nv;
 }
 
 // functor calc (optimization_opencv.cpp:14-39): mean of (1 - NCC), 2 if none
-__device__ double wave_objective(const RefineArgs &a, WaveLds &L, double x0, double x1, double x2, bool &degen)
+template <int G>
+__device__ __forceinline__ double wave_objective(const RefineArgs &a, WaveLds &L, double x0, double x1, double x2, bool &degen)
 {
     double nn[3], pp[3];
     {
@@ -280,7 +509,7 @@ __device__ double wave_objective(const RefineArgs &a, WaveLds &L, double x0, dou
         const double ns[3] = {L.n[0], L.n[1], L.n[2]};
         dpg::unparametrize(a.views[uni(L.ref)].C, Xs, ns, x0, x1, x2, nn, pp);
     }
-    const int nv = wave_scores(a, L, nn, pp, degen);
+    const int nv = wave_scores<G>(a, L, nn, pp, degen);
     if (nv == 0)
         return 2.0;
     double sum = 0.0;
@@ -295,7 +524,8 @@ enum NmPhase { kInit = 0, kReflect = 1, kExpand = 2, kContract = 3, kShrink = 4 
 // (optimization_opencv.cpp:44-78; OpenCV 3.4 createInitialSimplex,
 // innerDownhillSimplex, tryNewPoint).  One objective call site; the simplex
 // lives in LDS.  Writes back the f32 pose into L.X / L.n.
-__device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, bool &degen)
+template <int G>
+__device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, bool &degen)
 {
     const double *step = a.opt.nm_step;
     for (int i = 1; i <= 3; ++i) {
@@ -325,7 +555,7 @@ __device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, bool &degen)
             L.pt[1] = q1;
             L.pt[2] = q2;
         }
-        const double f = wave_objective(a, L, q0, q1, q2, degen);
+        const double f = wave_objective<G>(a, L, q0, q1, q2, degen);
         ++evals;
         bool decide = false;
         if (phase == kInit) {
@@ -447,14 +677,15 @@ __device__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, bool &degen)
 
 // Optimization::FilterByErrorMeasurement (optimization.cpp:98-132) with the
 // off-by-one erase: score k (texture k+1) < thr removes ORIGINAL index k.
-__device__ bool wave_filter(const RefineArgs &a, WaveLds &L, float &score, bool &degen)
+template <int G>
+__device__ __forceinline__ bool wave_filter(const RefineArgs &a, WaveLds &L, float &score, bool &degen)
 {
-    const int lane = (int)__lane_id();
+    const int lane = lane_id();
     int nv;
     {
         const double nn[3] = {L.n[0], L.n[1], L.n[2]};
         const double pp[3] = {L.X[0], L.X[1], L.X[2]};
-        nv = wave_scores(a, L, nn, pp, degen);
+        nv = wave_scores<G>(a, L, nn, pp, degen);
     }
     if (nv == 0) {
         score = -1.0f;
@@ -484,7 +715,7 @@ __device__ bool wave_filter(const RefineArgs &a, WaveLds &L, float &score, bool 
 // Patch::InitRelatedImages (patch.cpp:19-49), one lane per view
 __device__ void wave_init_related(const RefineArgs &a, WaveLds &L)
 {
-    const int lane = (int)__lane_id();
+    const int lane = lane_id();
     const int ref = uni(L.ref);
     const double X[3] = {L.X[0], L.X[1], L.X[2]};
     const double n[3] = {L.n[0], L.n[1], L.n[2]};
@@ -525,26 +756,80 @@ __device__ void child_position(const RefineArgs &a, const dp_patch &par, int dir
 // window gathers; the register allocator spills only in the per-evaluation
 // setup code at this target, never in the texel loops (checked in the ISA).
 #ifndef DP_REFINE_WAVES_PER_EU
-#define DP_REFINE_WAVES_PER_EU 4
+#define DP_REFINE_WAVES_PER_EU 3
 #endif
+#ifdef DP_REFINE_MAX_VGPR
+#define DP_REFINE_BOUNDS                                                                                       \
+    __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DP_REFINE_WAVES_PER_EU)))                   \
+        __attribute__((amdgpu_num_vgpr(DP_REFINE_MAX_VGPR)))
+#else
 #define DP_REFINE_BOUNDS __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DP_REFINE_WAVES_PER_EU)))
+#endif
 
-template <int kMode>
+#ifndef DP_XCD_RANGES
+#define DP_XCD_RANGES 0
+#endif
+#if DP_XCD_RANGES
+constexpr int kXcds = 8;
+#else
+constexpr int kXcds = 1;
+#endif
+
+__device__ __forceinline__ uint32_t xcc_id()
+{
+#if DP_XCD_RANGES
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x;
+#else
+    return 0;
+#endif
+}
+
+__device__ __forceinline__ uint32_t range_lo(int n, int x)
+{
+    return (uint32_t)(((uint64_t)n * (uint64_t)x) / (uint64_t)kXcds);
+}
+
+template <int kMode, int G>
 __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
 {
     __shared__ WaveLds lds[kWavesPerBlock];
-    WaveLds &L = lds[threadIdx.x / kWave];
-    const int lane = (int)__lane_id();
+    WaveLds &L = lds[uni((int)(threadIdx.x / kWave))];
+    const int lane = lane_id();
     unsigned long long wave_evals = 0;
+#ifdef DP_STAMPS
+    for (int c = 0; c < 8; ++c)
+        L.stamp[c] = 0;
+#endif
+    // XCD-local work ranges: the batch is cut into kXcds contiguous ranges and
+    // the waves of XCD x dequeue from range x first (consecutive candidates are
+    // spatial neighbours, so their windows share the XCD's L2 across the
+    // evaluations of a patch), then help the other ranges in order.
+    int cur = (int)(xcc_id() & (kXcds - 1));
+    int left = kXcds;
     for (;;) {
-        uint32_t idx = 0;
-        if (lane == 0)
-            idx = atomicAdd(a.work, 1u);
+        uint32_t idx = (uint32_t)a.n;
+        if (lane == 0) {
+            while (left > 0) {
+                const uint32_t lo = range_lo(a.n, cur), hi = range_lo(a.n, cur + 1);
+                const uint32_t t = lo + atomicAdd(a.work + kWorkStride * cur, 1u);
+                if (t < hi) {
+                    idx = t;
+                    break;
+                }
+                cur = (cur + 1) & (kXcds - 1);
+                --left;
+            }
+        }
         idx = (uint32_t)uni((int)idx);
         if (idx >= (uint32_t)a.n)
             break;
         dp_patch *out = a.patches + idx;
         bool live = true;
+#ifdef DP_STAMPS
+        const unsigned long long _t_patch = __builtin_amdgcn_s_memtime();
+#endif
         {
             // load the record (or derive the child from its parent) into LDS
             const dp_patch *src = out;
@@ -598,7 +883,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
             case DP_MODE_EVAL: {
                 const double nn[3] = {L.n[0], L.n[1], L.n[2]};
                 const double pp[3] = {L.X[0], L.X[1], L.X[2]};
-                const int nv = wave_scores(a, L, nn, pp, degen);
+                const int nv = wave_scores<G>(a, L, nn, pp, degen);
                 double sum = 0.0;
                 for (int k = 0; k < nv; ++k)
                     sum = sum + L.score[k];
@@ -609,32 +894,36 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
                 break;
             }
             case DP_MODE_FILTER:
-                ok = wave_filter(a, L, score, degen);
+                ok = wave_filter<G>(a, L, score, degen);
                 has_score = true;
                 evals = 1;
                 break;
             case DP_MODE_NM:
-                evals = wave_nelder_mead(a, L, degen);
+                evals = wave_nelder_mead<G>(a, L, degen);
                 ok = true;
                 break;
             case DP_MODE_SEED:
-                ok = wave_filter(a, L, score, degen);
+                ok = wave_filter<G>(a, L, score, degen);
                 has_score = true;
                 evals = 1;
                 if (ok)
-                    evals += wave_nelder_mead(a, L, degen);
+                    evals += wave_nelder_mead<G>(a, L, degen);
                 break;
             case DP_MODE_EXPAND:
             default:
-                evals = wave_nelder_mead(a, L, degen);
+                evals = wave_nelder_mead<G>(a, L, degen);
                 wave_init_related(a, L);
-                ok = wave_filter(a, L, score, degen);
+                ok = wave_filter<G>(a, L, score, degen);
                 has_score = true;
                 evals += 1;
                 break;
             }
         }
         wave_evals += (unsigned long long)evals;
+#ifdef DP_STAMPS
+        L.stamp[7] += __builtin_amdgcn_s_memtime() - _t_patch;
+        L.stamp[6] += 1;
+#endif
         if (lane == 0) {
             if (live) {
                 for (int i = 0; i < 3; ++i) {
@@ -657,6 +946,11 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
     }
     if (a.evals && lane == 0 && wave_evals)
         atomicAdd(a.evals, wave_evals);
+#ifdef DP_STAMPS
+    if (lane == 0)
+        for (int c = 0; c < 8; ++c)
+            atomicAdd(&g_stamps[c], L.stamp[c]);
+#endif
 }
 
 // ---- organizer --------------------------------------------------------------
@@ -761,6 +1055,20 @@ __global__ void append_kernel(const dpg::ViewDev *views, int V, const dp_patch *
 
 } // namespace
 
+int read_stamps(unsigned long long *out)
+{
+#ifdef DP_STAMPS
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -2;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+    return 0;
+#else
+    (void)out;
+    return -5;
+#endif
+}
+
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s)
 {
     if (a.n <= 0)
@@ -772,25 +1080,27 @@ hipError_t launch_refine(const RefineArgs &a, hipStream_t s)
     const int64_t want = ((int64_t)a.n + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t cap = (int64_t)cus * 8;
     const int grid = (int)(want < cap ? want : cap);
-    hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
+    hipError_t e = hipMemsetAsync(a.work, 0, kWorkCounters * sizeof(uint32_t), s);
     if (e != hipSuccess)
         return e;
-    switch (a.mode) {
-    case DP_MODE_EVAL:
-        hipLaunchKernelGGL(refine_kernel<DP_MODE_EVAL>, dim3(grid), dim3(kBlock), 0, s, a);
+    const int g = pass_width(a.cell);
+    if (g <= 0)
+        return hipErrorInvalidValue;
+    switch (a.mode * 16 + g) {
+#define DP_LAUNCH_REFINE(M, GG)                                                                               \
+    case M * 16 + GG:                                                                                          \
+        hipLaunchKernelGGL((refine_kernel<M, GG>), dim3(grid), dim3(kBlock), 0, s, a);                         \
         break;
-    case DP_MODE_FILTER:
-        hipLaunchKernelGGL(refine_kernel<DP_MODE_FILTER>, dim3(grid), dim3(kBlock), 0, s, a);
-        break;
-    case DP_MODE_NM:
-        hipLaunchKernelGGL(refine_kernel<DP_MODE_NM>, dim3(grid), dim3(kBlock), 0, s, a);
-        break;
-    case DP_MODE_SEED:
-        hipLaunchKernelGGL(refine_kernel<DP_MODE_SEED>, dim3(grid), dim3(kBlock), 0, s, a);
-        break;
+#define DP_LAUNCH_REFINE_G(M) DP_LAUNCH_REFINE(M, 8) DP_LAUNCH_REFINE(M, 4) DP_LAUNCH_REFINE(M, 2) DP_LAUNCH_REFINE(M, 1)
+        DP_LAUNCH_REFINE_G(DP_MODE_EVAL)
+        DP_LAUNCH_REFINE_G(DP_MODE_FILTER)
+        DP_LAUNCH_REFINE_G(DP_MODE_NM)
+        DP_LAUNCH_REFINE_G(DP_MODE_SEED)
+        DP_LAUNCH_REFINE_G(DP_MODE_EXPAND)
+#undef DP_LAUNCH_REFINE_G
+#undef DP_LAUNCH_REFINE
     default:
-        hipLaunchKernelGGL(refine_kernel<DP_MODE_EXPAND>, dim3(grid), dim3(kBlock), 0, s, a);
-        break;
+        return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

@@ -25,6 +25,10 @@ double dp_probe_ncc(int32_t N, int32_t Sa, int32_t Saa, int32_t Sb, int32_t Sbb,
                     double denom_min);
 /* device run of sincos/acos/sqrt over n inputs (out: 4*n doubles s,c,acos(x),sqrt|x|) */
 int dp_probe_math_device(const double *x, int n, double *out);
+/* diagnostic builds (-DDP_STAMPS) only: per-phase s_memtime cycle sums of the
+ * refine kernel since the last call (0 maps, 1 texture 0, 2 other views,
+ * 3 NCC finish, 6 patches, 7 whole patch); DP_E_STATE otherwise */
+int dp_debug_stamps(uint64_t *out8);
 
 #ifdef __cplusplus
 }

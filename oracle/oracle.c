@@ -296,14 +296,16 @@ int or_texture(const or_scene *s, int view, const double corners[12], int cell, 
         return 0; /* degenerate quad: findHomography yields no map */
     double g = (sx * dy2 - dx2 * sy) / del;
     double h = (dx1 * sy - sx * dy1) / del;
+    /* pixel units without divisions: with u = x/n the unit-square map
+     * (a u + b v + c)/(g u + h v + 1) equals (a x + b y + c n)/(g x + h y + n) */
     double a = (x[1] - x[0]) + g * x[1];
     double b = (x[3] - x[0]) + h * x[3];
     double d = (y[1] - y[0]) + g * y[1];
     double e = (y[3] - y[0]) + h * y[3];
     double dn = (double)cell;
-    double M0 = a / dn, M1 = b / dn, M2 = x[0];
-    double M3 = d / dn, M4 = e / dn, M5 = y[0];
-    double M6 = g / dn, M7 = h / dn, M8 = 1.0;
+    double M0 = a, M1 = b, M2 = x[0] * dn;
+    double M3 = d, M4 = e, M5 = y[0] * dn;
+    double M6 = g, M7 = h, M8 = dn;
 
     const uint8_t *img = v->bgr;
     const int stride = v->W * 3;
