@@ -187,7 +187,8 @@ def main():
     if N.lib.dp_debug_stamps(N.ptr(st)) == 0:  # -DDP_STAMPS diagnostic builds only
         tot = float(st[7]) or 1.0
         result["stamps_share"] = {k: round(float(st[i]) / tot, 4) for i, k in
-                                  enumerate(["maps", "texture0", "views", "ncc_finish"])}
+                                  enumerate(["corners_maps", "view_passes", "sync", "ncc_finish"])}
+        result["stamps_share"]["rest_nm_geometry"] = round(1.0 - sum(result["stamps_share"].values()), 4)
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             result["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")

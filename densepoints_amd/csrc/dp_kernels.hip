@@ -25,11 +25,12 @@ constexpr int kMapChunk = 32; // views whose window maps are staged per pass
 // Per-wavefront LDS: everything uniform across the wave lives here so that
 // registers only hold short-lived values (the evaluation is fp64-heavy).
 struct WaveLds {
+    // first: the texel loop addresses these with ds_read2 immediate offsets
+    double rowt[64][3];                         // per pass: window rows X0, Y0, W0 of slot j at j*(64/G)
+    double colt[64][3];                         // per pass: window columns m0*x, m3*x, m6*x (same slots)
     dpg::TexMap map[kMapChunk];                 // window maps of the current view chunk
     double score[DP_MAX_VIEWS];                 // NCC per scored view
     int32_t mom[kMapChunk][3];                  // Sb, Sbb, Sab of the chunk's views
-    double rowt[64][3];                         // per pass: window rows X0, Y0, W0 of slot j at j*(64/G)
-    double colt[64][3];                         // per pass: window columns m0*x, m3*x, m6*x (same slots)
     double c12[12];                             // window corners
     double X[3], n[3];                          // stored pose (f32 widened)
     double sp[4][3];                            // Nelder-Mead simplex
@@ -159,33 +160,61 @@ struct TexelLoad {
     uint32_t f; // fx | fy << 5 | same << 10
 };
 
+__device__ __forceinline__ int32_t med3_i32(int32_t v, int32_t lo, int32_t hi)
+{
+    int32_t r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(lo), "v"(hi));
+    return r;
+}
+
 __device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm, int hm, int32_t ix, int32_t iy)
 {
     const int32_t sx = ix >> 5, sy = iy >> 5;
-    const int32_t x0 = dpg::clampi(sx, 0, wm);
-    const int32_t y0 = dpg::clampi(sy, 0, hm);
-    const int32_t y1 = dpg::clampi(sy + 1, 0, hm);
+    const int32_t x0 = med3_i32(sx, 0, wm);
+    const int32_t y0 = med3_i32(sy, 0, hm);
+    const int32_t y1 = med3_i32(sy + 1, 0, hm);
     TexelLoad t;
     const uint32_t same = (uint32_t)sx >= (uint32_t)wm; // sx < 0 or sx >= w-1: x1 == x0
+    // pixel offsets inside one image plane: pitch < 2^24, y < 2^24
+    const uint32_t o0 = __umul24((uint32_t)y0, (uint32_t)pitch) + (uint32_t)x0;
+    const uint32_t o1 = __umul24((uint32_t)y1, (uint32_t)pitch) + (uint32_t)x0;
 #ifdef DP_DIAG_HOTIMG
     // diagnostic build: every gather hits one 1 KiB block (timing only)
     t.a = *(gpair_t)(roi + ((uint32_t)(y0 * 16 + x0) & 127u));
     t.b = *(gpair_t)(roi + ((uint32_t)(y1 * 16 + x0) & 127u));
+    (void)o0;
+    (void)o1;
 #else
-    t.a = *(gpair_t)(roi + (uint32_t)(y0 * pitch + x0));
-    t.b = *(gpair_t)(roi + (uint32_t)(y1 * pitch + x0));
+    t.a = *(gpair_t)(roi + o0);
+    t.b = *(gpair_t)(roi + o1);
 #endif
     t.f = (uint32_t)(ix & 31) | ((uint32_t)(iy & 31) << 5) | (same << 10);
     return t;
 }
 
+// dpg::blend_gray on the texel's two tap pairs, per channel as two u16 dot
+// products: row r contributes [c(r,x0), c(r,x1)] . [(32-fx)(32-fy_r), fx(32-fy_r)]
+// (same integers, same single rounding: (sum w'p + 512) >> 10)
 __device__ __forceinline__ int texel_gray(const TexelLoad &t)
 {
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const uint32_t fx = t.f & 31u, fy = (t.f >> 5) & 31u;
     const bool same = (t.f >> 10) & 1u;
     const uint32_t a0 = (uint32_t)t.a, b0 = (uint32_t)t.b;
     const uint32_t a1 = same ? a0 : (uint32_t)(t.a >> 32);
     const uint32_t b1 = same ? b0 : (uint32_t)(t.b >> 32);
-    return dpg::blend_gray(a0, a1, b0, b1, (int)(t.f & 31u), (int)((t.f >> 5) & 31u));
+    const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
+    const us2 w0 = __builtin_bit_cast(us2, wx * (32u - fy));
+    const us2 w1 = __builtin_bit_cast(us2, wx * fy);
+    uint32_t ch[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t sel = 0x0c000c00u | (uint32_t)k | ((uint32_t)(4 + k) << 16);
+        const us2 p0 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(a1, a0, sel));
+        const us2 p1 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(b1, b0, sel));
+        ch[k] = __builtin_amdgcn_udot2(p0, w0, __builtin_amdgcn_udot2(p1, w1, 512u, false), false) >> 10;
+    }
+    return (int)((ch[0] * 1868u + ch[1] * 9617u + ch[2] * 4899u + 8192u) >> 14);
 }
 
 // row / column terms of map `tm` into the table rows from rb; entry e in
@@ -249,40 +278,73 @@ __host__ __device__ constexpr int pass_width(int cell)
                                              : 0;
 }
 
+// Per-lane texel descriptors of a pass (fixed per launch: depend on the lane,
+// G and the cell only), computed once per wave so the texel loop does no
+// index arithmetic: bits 0-10 byte offset of the texel's row in L.rowt,
+// 11-21 of its column in L.colt, 22-29 texel index t, 30 live (t < N).
+struct TexDesc {
+    uint32_t d[kTexPerLane];
+};
+
+template <int G>
+__device__ __forceinline__ TexDesc make_texdesc(int cell)
+{
+    constexpr int LP = kWave / G;
+    const int lane = lane_id();
+    const int j = lane / LP, g = lane & (LP - 1);
+    const int N = cell * cell;
+    TexDesc td;
+#pragma unroll
+    for (int i = 0; i < kTexPerLane; ++i) {
+        const int tl = g + LP * i;
+        const int t = tl < N ? tl : N - 1; // dead texels re-load a live address
+        const int py = t / cell, px = t - py * cell;
+        const uint32_t ro = (uint32_t)(j * (64 / G) + py) * (uint32_t)sizeof(double[3]);
+        const uint32_t co = (uint32_t)(j * (64 / G) + px) * (uint32_t)sizeof(double[3]);
+        td.d[i] = ro | (co << 11) | ((uint32_t)t << 22) | ((tl < N ? 1u : 0u) << 30);
+    }
+    return td;
+}
+
+__device__ __forceinline__ int td_t(uint32_t d) { return (int)((d >> 22) & 255u); }
+__device__ __forceinline__ bool td_live(uint32_t d) { return (d >> 30) & 1u; }
+
+// texel_coord<true> addressed by a descriptor
+__device__ __forceinline__ void texel_coord_d(const WaveLds &L, uint32_t d, int32_t &ix, int32_t &iy)
+{
+    const double *R = (const double *)((const char *)&L.rowt[0][0] + (d & 2047u));
+    const double *C = (const double *)((const char *)&L.colt[0][0] + ((d >> 11) & 2047u));
+    const double W = div32_safe(R[2] + C[2]);
+    ix = rint_i32((R[0] + C[0]) * W);
+    iy = rint_i32((R[1] + C[1]) * W);
+}
+
 // One pass over G views: lanes LP*j .. LP*j+LP-1 own pass slot j and texels
 // t = g, g+LP, ... (at most kTexPerLane).  Safe windows (the common case):
 // all gathers of a lane are issued before any is consumed -- one memory round
 // trip per pass.  kAnchor: slot 0 is texture 0, whose gray values go to LDS
 // before the other slots form their cross moments.
 template <int G, bool kAnchor>
-__device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &L, int j, bool act, gpix_t roi,
-                                                  int pitch, int wm, int hm, int &s, int &ss, int &sx)
+__device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &L, const TexDesc &td, int j, bool act,
+                                                  gpix_t roi, int pitch, int wm, int hm, int &s, int &ss, int &sx)
 {
-    constexpr int LP = kWave / G;
-    const int g = lane_id() & (LP - 1);
-    const int cell = a.cell;
-    const int N = cell * cell;
-    const float inv_cell = 1.0f / (float)cell;
     TexelLoad tl[kTexPerLane];
 #pragma unroll
     for (int i = 0; i < kTexPerLane; ++i) {
-        int t = g + LP * i;
-        t = t < N ? t : N - 1; // dead texels re-load a live address
-        // t / cell exactly: t < 256, cell <= 16, fraction >= 0.5/cell from an integer
-        const int py = (int)(((float)t + 0.5f) * inv_cell);
-        const int px = t - py * cell;
         int32_t ix, iy;
-        texel_coord<true>(L, j * (64 / G), px, py, ix, iy);
+        texel_coord_d(L, td.d[i], ix, iy);
         tl[i] = texel_fetch(roi, pitch, wm, hm, ix, iy);
+        // one texel's fp64 coordinate math at a time: only the issued loads
+        // stay live across the pass
+        __builtin_amdgcn_sched_barrier(0);
     }
     if (kAnchor) {
         if (j == 0) {
 #pragma unroll
             for (int i = 0; i < kTexPerLane; ++i) {
-                const int t = g + LP * i;
-                if (t < N) {
+                if (td_live(td.d[i])) {
                     const int gv = texel_gray(tl[i]);
-                    L.anchor[t] = (uint16_t)gv;
+                    L.anchor[td_t(td.d[i])] = (uint16_t)gv;
                     s += gv;
                     ss += gv * gv;
                 }
@@ -293,12 +355,11 @@ __device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &
     if (act && !(kAnchor && j == 0)) {
 #pragma unroll
         for (int i = 0; i < kTexPerLane; ++i) {
-            const int t = g + LP * i;
-            if (t < N) {
+            if (td_live(td.d[i])) {
                 const int gv = texel_gray(tl[i]);
                 s += gv;
                 ss += gv * gv;
-                sx += (int)L.anchor[t] * gv;
+                sx += (int)L.anchor[td_t(td.d[i])] * gv;
             }
         }
     }
@@ -348,7 +409,7 @@ __device__ __attribute__((noinline)) Moments group_sample_clamped(WaveLds &L, in
 // Integer moments of up to G views (chunk slots in q; with kAnchor, pass slot
 // 0 is texture 0 and its Sa, Saa are returned in sa/saa) into L.mom[slot].
 template <int G, bool kAnchor>
-__device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, int base, uint64_t q, int &sa, int &saa)
+__device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, const TexDesc &td, int base, uint64_t q, int &sa, int &saa)
 {
     constexpr int LP = kWave / G;
     const int lane = lane_id();
@@ -373,7 +434,7 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, int 
     wave_sync();
     int s = 0, ss = 0, sx = 0;
     if (all_safe)
-        group_sample_safe<G, kAnchor>(a, L, j, act, roi, pitch, wm, hm, s, ss, sx);
+        group_sample_safe<G, kAnchor>(a, L, td, j, act, roi, pitch, wm, hm, s, ss, sx);
     else {
         const Moments mm = group_sample_clamped<G, kAnchor>(L, a.cell, j, act, roi, pitch, wm, hm);
         s = mm.s;
@@ -397,7 +458,7 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, int 
 
 // all valid views of chunk bits `todo`, G at a time (texture 0 first if kAnchor)
 template <int G>
-__device__ __forceinline__ void views_all(const RefineArgs &a, WaveLds &L, int base, uint64_t todo, bool anchor, int &sa, int &saa)
+__device__ __forceinline__ void views_all(const RefineArgs &a, WaveLds &L, const TexDesc &td, int base, uint64_t todo, bool anchor, int &sa, int &saa)
 {
     bool first = anchor;
     while (todo || first) {
@@ -416,9 +477,9 @@ __device__ __forceinline__ void views_all(const RefineArgs &a, WaveLds &L, int b
             }
         }
         if (first)
-            views_pass<G, true>(a, L, base, q, sa, saa);
+            views_pass<G, true>(a, L, td, base, q, sa, saa);
         else
-            views_pass<G, false>(a, L, base, q, sa, saa);
+            views_pass<G, false>(a, L, td, base, q, sa, saa);
         first = false;
     }
 }
@@ -430,7 +491,7 @@ __device__ __forceinline__ void views_all(const RefineArgs &a, WaveLds &L, int b
 // wavefront (texture 0 first, kept in LDS), each reduced to exact integer
 // moments with DPP.  Returns the number of scores; sets *degen on dx == 0.
 template <int G>
-__device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, const double *nn, const double *pp, bool &degen)
+__device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, const TexDesc &td, const double *nn, const double *pp, bool &degen)
 {
     const int lane = lane_id();
     STAMP_BEGIN;
@@ -480,7 +541,7 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
         const uint64_t todo = valid & (((ke - base) >= 64 ? ~0ull : ((1ull << (ke - base)) - 1ull)) &
                                        ~((1ull << (kb - base)) - 1ull));
         const bool anc = base == 0 && va;
-        views_all<G>(a, L, base, todo, anc, Sa, Saa);
+        views_all<G>(a, L, td, base, todo, anc, Sa, Saa);
         STAMP(L, 1);
         wave_sync();
         STAMP(L, 2);
@@ -501,7 +562,7 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
 
 // functor calc (optimization_opencv.cpp:14-39): mean of (1 - NCC), 2 if none
 template <int G>
-__device__ __forceinline__ double wave_objective(const RefineArgs &a, WaveLds &L, double x0, double x1, double x2, bool &degen)
+__device__ __forceinline__ double wave_objective(const RefineArgs &a, WaveLds &L, const TexDesc &td, double x0, double x1, double x2, bool &degen)
 {
     double nn[3], pp[3];
     {
@@ -509,7 +570,7 @@ __device__ __forceinline__ double wave_objective(const RefineArgs &a, WaveLds &L
         const double ns[3] = {L.n[0], L.n[1], L.n[2]};
         dpg::unparametrize(a.views[uni(L.ref)].C, Xs, ns, x0, x1, x2, nn, pp);
     }
-    const int nv = wave_scores<G>(a, L, nn, pp, degen);
+    const int nv = wave_scores<G>(a, L, td, nn, pp, degen);
     if (nv == 0)
         return 2.0;
     double sum = 0.0;
@@ -525,7 +586,7 @@ enum NmPhase { kInit = 0, kReflect = 1, kExpand = 2, kContract = 3, kShrink = 4 
 // innerDownhillSimplex, tryNewPoint).  One objective call site; the simplex
 // lives in LDS.  Writes back the f32 pose into L.X / L.n.
 template <int G>
-__device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, bool &degen)
+__device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, const TexDesc &td, bool &degen)
 {
     const double *step = a.opt.nm_step;
     for (int i = 1; i <= 3; ++i) {
@@ -555,7 +616,7 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
             L.pt[1] = q1;
             L.pt[2] = q2;
         }
-        const double f = wave_objective<G>(a, L, q0, q1, q2, degen);
+        const double f = wave_objective<G>(a, L, td, q0, q1, q2, degen);
         ++evals;
         bool decide = false;
         if (phase == kInit) {
@@ -678,14 +739,14 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
 // Optimization::FilterByErrorMeasurement (optimization.cpp:98-132) with the
 // off-by-one erase: score k (texture k+1) < thr removes ORIGINAL index k.
 template <int G>
-__device__ __forceinline__ bool wave_filter(const RefineArgs &a, WaveLds &L, float &score, bool &degen)
+__device__ __forceinline__ bool wave_filter(const RefineArgs &a, WaveLds &L, const TexDesc &td, float &score, bool &degen)
 {
     const int lane = lane_id();
     int nv;
     {
         const double nn[3] = {L.n[0], L.n[1], L.n[2]};
         const double pp[3] = {L.X[0], L.X[1], L.X[2]};
-        nv = wave_scores<G>(a, L, nn, pp, degen);
+        nv = wave_scores<G>(a, L, td, nn, pp, degen);
     }
     if (nv == 0) {
         score = -1.0f;
@@ -756,7 +817,7 @@ __device__ void child_position(const RefineArgs &a, const dp_patch &par, int dir
 // window gathers; the register allocator spills only in the per-evaluation
 // setup code at this target, never in the texel loops (checked in the ISA).
 #ifndef DP_REFINE_WAVES_PER_EU
-#define DP_REFINE_WAVES_PER_EU 3
+#define DP_REFINE_WAVES_PER_EU 4
 #endif
 #ifdef DP_REFINE_MAX_VGPR
 #define DP_REFINE_BOUNDS                                                                                       \
@@ -802,6 +863,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
     for (int c = 0; c < 8; ++c)
         L.stamp[c] = 0;
 #endif
+    const TexDesc td = make_texdesc<G>(a.cell);
     // XCD-local work ranges: the batch is cut into kXcds contiguous ranges and
     // the waves of XCD x dequeue from range x first (consecutive candidates are
     // spatial neighbours, so their windows share the XCD's L2 across the
@@ -883,7 +945,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
             case DP_MODE_EVAL: {
                 const double nn[3] = {L.n[0], L.n[1], L.n[2]};
                 const double pp[3] = {L.X[0], L.X[1], L.X[2]};
-                const int nv = wave_scores<G>(a, L, nn, pp, degen);
+                const int nv = wave_scores<G>(a, L, td, nn, pp, degen);
                 double sum = 0.0;
                 for (int k = 0; k < nv; ++k)
                     sum = sum + L.score[k];
@@ -894,26 +956,26 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
                 break;
             }
             case DP_MODE_FILTER:
-                ok = wave_filter<G>(a, L, score, degen);
+                ok = wave_filter<G>(a, L, td, score, degen);
                 has_score = true;
                 evals = 1;
                 break;
             case DP_MODE_NM:
-                evals = wave_nelder_mead<G>(a, L, degen);
+                evals = wave_nelder_mead<G>(a, L, td, degen);
                 ok = true;
                 break;
             case DP_MODE_SEED:
-                ok = wave_filter<G>(a, L, score, degen);
+                ok = wave_filter<G>(a, L, td, score, degen);
                 has_score = true;
                 evals = 1;
                 if (ok)
-                    evals += wave_nelder_mead<G>(a, L, degen);
+                    evals += wave_nelder_mead<G>(a, L, td, degen);
                 break;
             case DP_MODE_EXPAND:
             default:
-                evals = wave_nelder_mead<G>(a, L, degen);
+                evals = wave_nelder_mead<G>(a, L, td, degen);
                 wave_init_related(a, L);
-                ok = wave_filter<G>(a, L, score, degen);
+                ok = wave_filter<G>(a, L, td, score, degen);
                 has_score = true;
                 evals += 1;
                 break;
