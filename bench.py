@@ -50,19 +50,15 @@ def parse():
 
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
     import densepoints_amd as dp
     from densepoints_amd import _native as N
+    from densepoints_amd import dist as D
     from densepoints_amd import synth
+
+    rank, world, local = D.env()
+    torch.cuda.set_device(local)
+    # RCCL over xGMI ("nccl" on ROCm): barrier + max-over-ranks time only
+    dist = D.init("nccl", torch.device("cuda", local))
 
     cfg = synth.named(args.config)
     V, W, H = cfg.n_views, cfg.width, cfg.height
@@ -90,7 +86,7 @@ def main():
     # this rank's shard of parents (weak scaling; wraps around the list)
     B = args.batch - args.batch % 4
     NP = B // 4
-    idx = (np.arange(NP, dtype=np.int64) + rank * NP) % len(parents_all)
+    idx = D.weak_shard(len(parents_all), NP, rank)
     parents = np.ascontiguousarray(parents_all[idx])
     d_parents = torch.from_numpy(parents.view(np.uint8).copy()).to("cuda")
     work = torch.empty(B * N.PATCH_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
@@ -124,10 +120,7 @@ def main():
     step_ms = [a.elapsed_time(b) for a, b in kern_ms]
     launch_ms = float(np.mean(step_ms))
     lib_last_ms = eng.last_kernel_ms()  # the library's own events around the last launch
-    if dist:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, dist, torch.device("cuda", local))
 
     out = np.frombuffer(work.cpu().numpy().tobytes(), dtype=N.PATCH_DTYPE)
     acc = accept.cpu().numpy()

@@ -1,0 +1,96 @@
+"""Multi-GPU plumbing for the patch loop: one process per GPU, torch.distributed
+over RCCL (backend "nccl") on MI355X, gloo for CPU tests.
+
+The refine/expand step has no data-path collective. Candidates are independent
+(SURVEY 8e), so each rank refines its own shard. The only exchanges are
+  * the barrier and max-over-ranks step time (bench.py), and
+  * an all-gather of patch records, used when the accepted patches of all ranks
+    are needed in one place (the 1-GPU result in order, or the per-generation
+    exchange of a sharded densify).
+Shards are contiguous ranges of the candidate sequence, so concatenating the
+gathered shards in rank order restores the 1-GPU order bit for bit.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ._native import PATCH_DTYPE
+
+
+def env() -> tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment (1 process = 1 GPU)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: str, device: torch.device | None = None):
+    """Initialise the default process group when WORLD_SIZE > 1; returns the
+    torch.distributed module, or None for a single process. MASTER_ADDR
+    defaults to 127.0.0.1 (the container hostname may not resolve)."""
+    rank, world, _ = env()
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if not dist.is_initialized():
+        kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return dist
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous, balanced [lo, hi) slice of n candidates for `rank` (sizes
+    differ by at most one; every index in exactly one shard)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    q, r = divmod(int(n), world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def weak_shard(n_total: int, per_rank: int, rank: int) -> np.ndarray:
+    """Indices of a fixed-size per-rank shard for weak scaling (bench.py): rank
+    r takes per_rank consecutive items starting at r*per_rank, wrapping around
+    the list, so every rank does the same amount of work at any world size."""
+    if n_total <= 0:
+        raise ValueError("empty candidate list")
+    return (np.arange(per_rank, dtype=np.int64) + rank * per_rank) % n_total
+
+
+def allgather_patches(local: np.ndarray, dist, device: torch.device | None = None) -> np.ndarray:
+    """All-gather variable-length dp_patch arrays; returns the concatenation in
+    rank order on every rank. Records travel as padded uint8 tensors (one
+    count all-gather, one payload all-gather), on `device` for RCCL or on the
+    CPU for gloo."""
+    local = np.ascontiguousarray(local, dtype=PATCH_DTYPE)
+    if dist is None:
+        return local.copy()
+    world = dist.get_world_size()
+    dev = device if device is not None else torch.device("cpu")
+    cnt = torch.tensor([len(local)], dtype=torch.int64, device=dev)
+    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    counts = [int(c.item()) for c in counts]
+    cap = max(counts) * PATCH_DTYPE.itemsize
+    buf = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
+    if len(local):
+        buf[: len(local) * PATCH_DTYPE.itemsize] = torch.from_numpy(local.view(np.uint8).copy()).to(dev)
+    parts = [torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    out = [np.frombuffer(p.cpu().numpy()[: c * PATCH_DTYPE.itemsize].tobytes(), dtype=PATCH_DTYPE)
+           for p, c in zip(parts, counts)]
+    return np.concatenate(out) if out else np.empty(0, dtype=PATCH_DTYPE)
+
+
+def max_over_ranks(x: float, dist, device: torch.device | None = None) -> float:
+    """Maximum of a per-rank scalar (the step time) over all ranks."""
+    if dist is None:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device if device is not None else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

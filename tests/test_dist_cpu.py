@@ -1,0 +1,93 @@
+"""Multi-process path on CPU (gloo, world_size 2): candidates are sharded by
+contiguous rank ranges, each rank refines its shard, and the all-gathered
+shards equal the single-process result bit for bit (the
+candidate loop shards with no data-path collective).  The per-rank refine
+here is the oracle (CPU test infrastructure); the GPU runs the same sharding
+in bench.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from densepoints_amd import dist as D
+from densepoints_amd import synth
+
+
+def test_shard_range_partitions_exactly():
+    for n in (0, 1, 7, 64, 1000, 65537):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                lo, hi = D.shard_range(n, r, world)
+                assert 0 <= lo <= hi <= n
+                assert hi - lo in ((n // world), (n // world) + 1)
+                seen.extend(range(lo, hi))
+            assert seen == list(range(n))
+
+
+def test_weak_shard_fixed_size_and_wraps():
+    for world in (1, 2, 4, 8):
+        for r in range(world):
+            idx = D.weak_shard(100, 64, r)
+            assert len(idx) == 64
+            assert idx[0] == (64 * r) % 100
+            assert np.all(np.diff(idx) % 100 == 1)
+    with pytest.raises(ValueError):
+        D.weak_shard(0, 4, 0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _scene():
+    cfg = synth.config(4, 320, 240, 1)
+    P, imgs, seeds = synth.scene_host(cfg)
+    return P, imgs, seeds
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from oracle import pyoracle
+
+    dist = D.init("gloo")
+    P, imgs, seeds = _scene()
+    S = pyoracle.Scene(P, imgs)
+    parents = S.seeds_to_patches(seeds)[:48]
+    lo, hi = D.shard_range(len(parents), rank, world)
+    kids, acc = S.expand(parents[lo:hi], 2)
+    kids = kids.copy()
+    kids["flags"] = np.where(acc != 0, kids["flags"] | 0x80, kids["flags"])  # carry accept in the record
+    # children of shard [lo, hi) are candidates [4 lo, 4 hi): parent indices are shard-local
+    kids["parent"] = np.where(kids["parent"] != 0xFFFFFFFF, kids["parent"] + lo, kids["parent"])
+    all_kids = D.allgather_patches(kids, dist)
+    t = D.max_over_ranks(float(rank + 1), dist)
+    if rank == 0:
+        np.save(out_path, all_kids.view(np.uint8), allow_pickle=False)
+        with open(out_path + ".max", "w") as f:
+            f.write(repr(t))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_expand_equals_single_process(tmp_path, orc):
+    world = 2
+    out = str(tmp_path / "kids.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    from densepoints_amd._native import PATCH_DTYPE
+
+    got = np.frombuffer(np.load(out, allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
+    P, imgs, seeds = _scene()
+    S = orc.Scene(P, imgs)
+    parents = S.seeds_to_patches(seeds)[:48]
+    kids, acc = S.expand(parents, 2)
+    kids = kids.copy()
+    kids["flags"] = np.where(acc != 0, kids["flags"] | 0x80, kids["flags"])
+    assert len(got) == 4 * len(parents)
+    assert got.tobytes() == kids.tobytes()
+    assert float(open(out + ".max").read()) == 2.0
