@@ -29,6 +29,8 @@ struct WaveLds {
     double rowt[64][3];                         // per pass: window rows X0, Y0, W0 of slot j at j*(64/G)
     double colt[64][3];                         // per pass: window columns m0*x, m3*x, m6*x (same slots)
     dpg::TexMap map[kMapChunk];                 // window maps of the current view chunk
+    uint64_t roi[kMapChunk];                    // global address of each map's ROI origin
+    int32_t pitch[kMapChunk];                   // its image row pitch (pixels)
     double score[DP_MAX_VIEWS];                 // NCC per scored view
     int32_t mom[kMapChunk][3];                  // Sb, Sbb, Sab of the chunk's views
     double c12[12];                             // window corners
@@ -217,23 +219,21 @@ __device__ __forceinline__ int texel_gray(const TexelLoad &t)
     return (int)((ch[0] * 1868u + ch[1] * 9617u + ch[2] * 4899u + 8192u) >> 14);
 }
 
-// row / column terms of map `tm` into the table rows from rb; entry e in
-// [0, 32): e < 16 -> row e, else column e - 16
-__device__ __forceinline__ void fill_tables(WaveLds &L, int rb, const dpg::TexMap &tm, int e, int cell)
+// row r and column r terms of map `tm` into the table rows from rb (one lane
+// per r: all nine coefficients are read before anything is written)
+__device__ __forceinline__ void fill_tables(WaveLds &L, int rb, const dpg::TexMap &tm, int r)
 {
-    if (e < 16) {
-        if (e < cell) {
-            const double y = (double)e;
-            L.rowt[rb + e][0] = tm.m1 * y + tm.m2;
-            L.rowt[rb + e][1] = tm.m4 * y + tm.m5;
-            L.rowt[rb + e][2] = tm.m7 * y + tm.m8;
-        }
-    } else if (e - 16 < cell) {
-        const double x = (double)(e - 16);
-        L.colt[rb + e - 16][0] = tm.m0 * x;
-        L.colt[rb + e - 16][1] = tm.m3 * x;
-        L.colt[rb + e - 16][2] = tm.m6 * x;
-    }
+    const double m0 = tm.m0, m1 = tm.m1, m2 = tm.m2, m3 = tm.m3, m4 = tm.m4, m5 = tm.m5;
+    const double m6 = tm.m6, m7 = tm.m7, m8 = tm.m8;
+    const double v = (double)r;
+    const double r0 = m1 * v + m2, r1 = m4 * v + m5, r2 = m7 * v + m8;
+    const double c0 = m0 * v, c1 = m3 * v, c2 = m6 * v;
+    L.rowt[rb + r][0] = r0;
+    L.rowt[rb + r][1] = r1;
+    L.rowt[rb + r][2] = r2;
+    L.colt[rb + r][0] = c0;
+    L.colt[rb + r][1] = c1;
+    L.colt[rb + r][2] = c2;
 }
 
 // slot list of a pass: byte j = chunk slot of pass slot j, 0xff = none
@@ -414,23 +414,21 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
     constexpr int LP = kWave / G;
     const int lane = lane_id();
     const int cell = a.cell;
-    // row/column tables: G slots x 32 entries
-    for (int e = lane; e < 32 * G; e += kWave) {
-        const int je = e >> 5;
+    // row/column tables: G slots x 16 lanes, lane r of a slot fills row r and column r
+    for (int e = lane; e < 16 * G; e += kWave) {
+        const int je = e >> 4, r = e & 15;
         const int ke = pick8(je, q);
-        if (ke >= 0)
-            fill_tables(L, je * (64 / G), L.map[ke], e & 31, cell);
+        if (ke >= 0 && r < cell)
+            fill_tables(L, je * (64 / G), L.map[ke], r);
     }
     const int j = lane / LP;
     const int slot = pick8(j, q);
     const bool act = slot >= 0;
     const int sl = act ? slot : pick8(0, q);
-    const int tlx = L.map[sl].tlx, tly = L.map[sl].tly;
     const int wm = L.map[sl].w - 1, hm = L.map[sl].h - 1;
     const bool all_safe = __ballot(act && !L.map[sl].safe) == 0ull;
-    const dpg::ViewDev *__restrict__ vw = a.views + L.vlist[base + sl];
-    const int pitch = vw->pitch;
-    const gpix_t roi = (gpix_t)vw->img + ((size_t)tly * (size_t)pitch + (size_t)tlx);
+    const int pitch = L.pitch[sl];
+    const gpix_t roi = (gpix_t)L.roi[sl];
     wave_sync();
     int s = 0, ss = 0, sx = 0;
     if (all_safe)
@@ -524,9 +522,13 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
         const int kk = base + lane;
         if (lane < kMapChunk && kk < m) {
             dpg::TexMap tm;
-            ok = dpg::texture_map(a.views[L.vlist[kk]], L.c12, cell, tm);
-            if (ok)
+            const dpg::ViewDev &vw = a.views[L.vlist[kk]];
+            ok = dpg::texture_map(vw, L.c12, cell, tm);
+            if (ok) {
                 L.map[lane] = tm;
+                L.roi[lane] = (uint64_t)(uintptr_t)(vw.img + ((size_t)tm.tly * (size_t)vw.pitch + (size_t)tm.tlx));
+                L.pitch[lane] = vw.pitch;
+            }
         }
         const uint64_t okmask = __ballot(ok);
         wave_sync();
