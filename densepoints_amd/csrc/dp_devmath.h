@@ -42,6 +42,27 @@ __device__ __forceinline__ double div_rn(double a, double b)
     return a / b;
 }
 
+// a0 / b and a1 / b, correctly rounded, sharing the refined reciprocal of b
+// (same guards as div_rn; any operand outside them -> both by '/')
+__device__ __forceinline__ void div_pair_rn(double a0, double a1, double b, double &q0, double &q1)
+{
+    const double ab = fabs(b), a0a = fabs(a0), a1a = fabs(a1);
+    if (ab > 7.52316384526264e-37 && ab < 1.329227995784916e+36 && a0a > 1.4e-271 && a0a < 8.4e270 &&
+        a1a > 1.4e-271 && a1a < 8.4e270) {
+        double r = (double)__builtin_amdgcn_rcpf((float)b);
+        double e = __builtin_fma(-b, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        e = __builtin_fma(-b, r, 1.0);
+        r = __builtin_fma(r, e, r);
+        const double p0 = a0 * r, p1 = a1 * r;
+        q0 = __builtin_fma(__builtin_fma(-b, p0, a0), r, p0);
+        q1 = __builtin_fma(__builtin_fma(-b, p1, a1), r, p1);
+    } else {
+        q0 = a0 / b;
+        q1 = a1 / b;
+    }
+}
+
 // 32 / W for 1e-3 < W < 1e6 (TexMap::safe)
 __device__ __forceinline__ double div32_safe(double w) { return div_rn_core(32.0, w); }
 

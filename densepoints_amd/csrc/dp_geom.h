@@ -14,6 +14,7 @@
 #pragma once
 
 #include "dp_detmath.h"
+#include "dp_devmath.h"
 #include <stdint.h>
 
 namespace dpg {
@@ -39,13 +40,24 @@ DP_HD void cross3(const double *a, const double *b, double *o)
     o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+// q0 = a0 / b, q1 = a1 / b, IEEE-correct on both sides (the device shares one
+// refined reciprocal: dp_devmath.h div_pair_rn)
+DP_HD void div2(double a0, double a1, double b, double &q0, double &q1)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    dpk::div_pair_rn(a0, a1, b, q0, q1);
+#else
+    q0 = a0 / b;
+    q1 = a1 / b;
+#endif
+}
+
 DP_HD void project(const double *P, double x, double y, double z, double &u, double &v)
 {
     const double h0 = ((P[0] * x + P[1] * y) + P[2] * z) + P[3];
     const double h1 = ((P[4] * x + P[5] * y) + P[6] * z) + P[7];
     const double h2 = ((P[8] * x + P[9] * y) + P[10] * z) + P[11];
-    u = h0 / h2;
-    v = h1 / h2;
+    div2(h0, h1, h2, u, v);
 }
 
 DP_HD bool inside(double u, double v, int32_t W, int32_t H)
@@ -103,8 +115,8 @@ DP_HD bool quad_map(const double *x, const double *y, int tlx, int tly, int rw, 
     const double det = ax * by - bx * ay;
     if (det == 0.0)
         return false;
-    const double g = (sx * by - bx * sy) / det;
-    const double h = (ax * sy - sx * ay) / det;
+    double g, h;
+    div2(sx * by - bx * sy, ax * sy - sx * ay, det, g, h);
     // pixel units without divisions: (a x + b y + c n) / (g x + h y + n)
     const double n = (double)cell;
     tm.m0 = (x[1] - x[0]) + g * x[1];
@@ -121,20 +133,18 @@ DP_HD bool quad_map(const double *x, const double *y, int tlx, int tly, int rw, 
     tm.w = rw;
     tm.h = rh;
     // W is affine in (x, y) and X/W, Y/W are linear-fractional: with W > 0 on
-    // the window rectangle their extremes are at its corners.
+    // the window rectangle their extremes are at its corners.  |X| = |Xn|*32/W
+    // < 2^29 (a factor 2 below the 2^30 the kernel needs), tested without a
+    // division.
     bool safe = true;
     const double e = (double)(cell - 1);
     for (int c = 0; c < 4; ++c) {
         const double px = (c & 1) ? e : 0.0, py = (c & 2) ? e : 0.0;
         const double W = (tm.m7 * py + tm.m8) + tm.m6 * px;
-        if (!(W > 1e-3) || !(W < 1e6)) {
-            safe = false;
-            continue;
-        }
-        const double q = 32.0 / W;
-        const double X = ((tm.m1 * py + tm.m2) + tm.m0 * px) * q;
-        const double Y = ((tm.m4 * py + tm.m5) + tm.m3 * px) * q;
-        if (!(fabs(X) < 1073741824.0) || !(fabs(Y) < 1073741824.0))
+        const double Xn = (tm.m1 * py + tm.m2) + tm.m0 * px;
+        const double Yn = (tm.m4 * py + tm.m5) + tm.m3 * px;
+        const double lim = 536870912.0 * W;
+        if (!(W > 1e-3) || !(W < 1e6) || !(fabs(Xn) * 32.0 < lim) || !(fabs(Yn) * 32.0 < lim))
             safe = false;
     }
     tm.safe = safe ? 1 : 0;

@@ -20,7 +20,10 @@
 namespace dpk {
 namespace {
 
-constexpr int kMapChunk = 32; // views whose window maps are staged per pass
+#ifndef DP_MAP_CHUNK
+#define DP_MAP_CHUNK 32
+#endif
+constexpr int kMapChunk = DP_MAP_CHUNK; // views whose window maps are built per chunk
 
 // Per-wavefront LDS: everything uniform across the wave lives here so that
 // registers only hold short-lived values (the evaluation is fp64-heavy).
@@ -338,30 +341,35 @@ __device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &
         // stay live across the pass
         __builtin_amdgcn_sched_barrier(0);
     }
-    if (kAnchor) {
-        if (j == 0) {
+    // one consume phase for all lanes (no divergence): in the anchor pass the
+    // texture-0 gray of texel t comes from lane (0, g) of the same texel
+    // through the LDS crossbar (ds_bpermute), and slot 0 stores it for the
+    // later passes.
+    constexpr int LP = kWave / G;
+    const int src = (lane_id() & (LP - 1)) << 2;
 #pragma unroll
-            for (int i = 0; i < kTexPerLane; ++i) {
-                if (td_live(td.d[i])) {
-                    const int gv = texel_gray(tl[i]);
-                    L.anchor[td_t(td.d[i])] = (uint16_t)gv;
-                    s += gv;
-                    ss += gv * gv;
-                }
-            }
-        }
-        wave_sync();
-    }
-    if (act && !(kAnchor && j == 0)) {
+    for (int i = 0; i < kTexPerLane; ++i) {
+        const uint32_t d = td.d[i];
+        const int t = td_t(d);
+        int gv = texel_gray(tl[i]);
+#if defined(DP_DIAG_PAD_I32)
+        // diagnostic build: DP_DIAG_PAD_I32 extra int VALU per texel (timing only)
 #pragma unroll
-        for (int i = 0; i < kTexPerLane; ++i) {
-            if (td_live(td.d[i])) {
-                const int gv = texel_gray(tl[i]);
-                s += gv;
-                ss += gv * gv;
-                sx += (int)L.anchor[td_t(td.d[i])] * gv;
-            }
+        for (int k = 0; k < DP_DIAG_PAD_I32; ++k)
+            asm volatile("v_add_u32 %0, %0, 0" : "+v"(gv));
+#endif
+        int av;
+        if (kAnchor) {
+            av = (G == 1) ? gv : __builtin_amdgcn_ds_bpermute(src, gv);
+            if (j == 0 && td_live(d))
+                L.anchor[t] = (uint16_t)gv;
+        } else {
+            av = (int)L.anchor[t];
         }
+        const int g = (act && td_live(d)) ? gv : 0;
+        s += g;
+        ss += g * g;
+        sx += av * g;
     }
 }
 
