@@ -182,9 +182,12 @@ def main():
         result["stamps_share"] = {k: round(float(st[i]) / tot, 4) for i, k in
                                   enumerate(["corners_maps", "view_passes", "sync", "ncc_finish"])}
         result["stamps_share"]["rest_nm_geometry"] = round(1.0 - sum(result["stamps_share"].values()), 4)
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            result["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+    tj = args.traffic_json or latest_traffic_json()
+    if tj and os.path.exists(tj):
+        with open(tj) as f:
+            t = json.load(f)
+        result["roofline"]["traffic"] = t.get("hbm_bytes_per_launch")
+        result["roofline"]["traffic_source"] = os.path.relpath(tj, ROOT)
 
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out)
@@ -194,6 +197,15 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     eng.close()
+
+
+def latest_traffic_json():
+    """profiles/<latest round>/refine_traffic.json: rocprofv3 PMC HBM bytes per
+    launch of the expansion kernel, collected by tools/gpu_profile.sh"""
+    import glob
+
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "refine_traffic.json")))
+    return found[-1] if found else None
 
 
 def cpu_baseline(args, cfg, P, planes, parents, gpu_out):

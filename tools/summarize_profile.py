@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 CSV output (kernel stats + PMC passes) per kernel.
 
-usage: summarize_profile.py <prof_dir> [out.json]
+usage: summarize_profile.py <prof_dir> [out.json] [refine_traffic.json]
 HBM bytes per launch follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and
 WRITE_SIZE are KiB; gfx950 FETCH_SIZE reads 1/2 of the bytes of wide coalesced
 streams, so the corrected read bytes are 2*FETCH_SIZE*1024 (the correction is
@@ -49,6 +49,18 @@ def main():
     js = json.dumps(out, indent=1)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(js)
+    # traffic of the bench's dominant kernel (the expansion refine kernel) per launch
+    if len(sys.argv) > 3:
+        cand = {k: e for k, e in out["kernels"].items() if k.startswith("dpk::refine_kernel<4") and
+                "hbm_bytes_per_launch" in e}
+        if cand:
+            k, e = max(cand.items(), key=lambda kv: kv[1].get("stats", {}).get("total_ns", 0.0))
+            open(sys.argv[3], "w").write(json.dumps({
+                "kernel": k, "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
+                "hbm_bytes_per_launch_raw": e["hbm_bytes_per_launch_raw"],
+                "avg_ns": e.get("stats", {}).get("avg_ns"),
+                "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM/rocprofv3), "
+                          "separate --pmc passes"}, indent=1))
     print(js)
 
 
