@@ -17,6 +17,7 @@ def _build_all():
     spec.loader.exec_module(mod)
     mod.build()
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "programs", "densify")], check=True)
 
 
 def pytest_configure(config):

@@ -1,0 +1,146 @@
+"""programs/densify (the C++ CLI over the C ABI): scene JSON, image decoding,
+seeds and settings on the CPU; the full run (dp_densify -> PLY) on the GPU,
+byte-compared with the oracle's densify written in PrintCloud format."""
+import json
+import os
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+from densepoints_amd import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "programs", "densify", "densify")
+
+
+def fnv(bgr: np.ndarray) -> str:
+    h = 1469598103934665603
+    for b in np.ascontiguousarray(bgr, dtype=np.uint8).ravel().tobytes():
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return f"{h:016x}"
+
+
+def run(*args, check=True):
+    r = subprocess.run([CLI, *args], capture_output=True, text=True, timeout=600)
+    if check and r.returncode != 0:
+        raise AssertionError(f"densify {args} -> {r.returncode}: {r.stderr}")
+    return r
+
+
+@pytest.fixture(scope="module")
+def scene_dir(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("scene"))
+    out = json.loads(run("--synthetic", "4,160,120,1", "--write-scene", d).stdout)
+    assert out["views"] == 4
+    return d
+
+
+def test_synthetic_scene_roundtrip(scene_dir):
+    cfg = synth.config(4, 160, 120, 1)
+    P = synth.cameras(cfg)
+    with open(os.path.join(scene_dir, "scene.json")) as f:
+        sc = json.load(f)
+    assert sc["imagesPath"] == scene_dir and len(sc["views"]) == 4
+    for v, view in enumerate(sc["views"]):
+        assert np.array_equal(np.array(view["projectionMatrix"]), P[v])  # %.17g round trip is exact
+    seeds = np.loadtxt(os.path.join(scene_dir, "seeds.xyz")).reshape(-1, 3)
+    assert np.array_equal(seeds, synth.seeds(cfg, P))
+    chk = json.loads(run("-i", os.path.join(scene_dir, "scene.json"), "--seeds",
+                         os.path.join(scene_dir, "seeds.xyz"), "--check-only").stdout)
+    assert chk["views"] == 4 and chk["width"] == 160 and chk["height"] == 120
+    assert chk["seeds"] == len(seeds)
+    assert chk["image_fnv"] == [fnv(synth.render_host(cfg, P, v)) for v in range(4)]
+
+
+def _png(path, px: np.ndarray, ctype: int):
+    """Minimal PNG encoder exercising every filter type (row y uses filter y % 5)."""
+    h, w = px.shape[:2]
+    ch = {0: 1, 2: 3, 6: 4}[ctype]
+    a = px.reshape(h, w * ch).astype(np.int32)
+    raw = bytearray()
+    for y in range(h):
+        f = y % 5
+        row = a[y]
+        up = a[y - 1] if y else np.zeros_like(row)
+        left = np.concatenate([np.zeros(ch, np.int32), row[:-ch]])
+        ul = np.concatenate([np.zeros(ch, np.int32), up[:-ch]])
+        if f == 0:
+            out = row
+        elif f == 1:
+            out = row - left
+        elif f == 2:
+            out = row - up
+        elif f == 3:
+            out = row - (left + up) // 2
+        else:
+            p = left + up - ul
+            pa, pb, pc = np.abs(p - left), np.abs(p - up), np.abs(p - ul)
+            pred = np.where((pa <= pb) & (pa <= pc), left, np.where(pb <= pc, up, ul))
+            out = row - pred
+        raw.append(f)
+        raw += (out & 255).astype(np.uint8).tobytes()
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n")
+        f.write(chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, ctype, 0, 0, 0)))
+        f.write(chunk(b"IDAT", zlib.compress(bytes(raw), 6)))
+        f.write(chunk(b"IEND", b""))
+
+
+def test_png_decoding_all_filters_and_colour_types(tmp_path):
+    rng = np.random.default_rng(3)
+    rgb = rng.integers(0, 256, (37, 53, 3), dtype=np.uint8)
+    rgba = np.concatenate([rgb, rng.integers(0, 256, (37, 53, 1), dtype=np.uint8)], axis=2)
+    gray = rng.integers(0, 256, (37, 53), dtype=np.uint8)
+    _png(tmp_path / "rgb.png", rgb, 2)
+    _png(tmp_path / "rgba.png", rgba, 6)
+    _png(tmp_path / "gray.png", gray, 0)
+    P = [[1.0, 0.0, 0.0, 0.0], [0.0, 1.0, 0.0, 0.0], [0.0, 0.0, 1.0, 1.0]]
+    scene = {"imagesPath": str(tmp_path),
+             "views": [{"filename": n, "projectionMatrix": P} for n in ("rgb.png", "rgba.png", "gray.png")]}
+    (tmp_path / "scene.json").write_text(json.dumps(scene))
+    (tmp_path / "seeds.xyz").write_text("# x y z\n0 0 1\n0.5 0.25 2\n")
+    chk = json.loads(run("-i", str(tmp_path / "scene.json"), "--seeds", str(tmp_path / "seeds.xyz"),
+                         "--check-only").stdout)
+    bgr = rgb[:, :, ::-1]  # cv::imread order; alpha dropped; gray replicated
+    assert chk["seeds"] == 2
+    assert chk["image_fnv"] == [fnv(bgr), fnv(bgr), fnv(np.repeat(gray[:, :, None], 3, axis=2))]
+
+
+def test_bad_inputs_fail_loudly(tmp_path, scene_dir):
+    (tmp_path / "s.json").write_text('{"expand_cell_size": 11, "no_such_option": 1}')
+    r = run("-i", os.path.join(scene_dir, "scene.json"), "--seeds", os.path.join(scene_dir, "seeds.xyz"),
+            "-s", str(tmp_path / "s.json"), "--check-only", check=False)
+    assert r.returncode == 1 and "no_such_option" in r.stderr
+    (tmp_path / "ok.json").write_text('{"expand_cell_size": 11, "nm_step": [0.02, 0.2, 0.2]}')
+    run("-i", os.path.join(scene_dir, "scene.json"), "--seeds", os.path.join(scene_dir, "seeds.xyz"),
+        "-s", str(tmp_path / "ok.json"), "--check-only")
+    (tmp_path / "bad.json").write_text('{"imagesPath": "x", "views": [ {"filename": 3} ]}')
+    r = run("-i", str(tmp_path / "bad.json"), "--seeds", os.path.join(scene_dir, "seeds.xyz"), "--check-only",
+            check=False)
+    assert r.returncode == 1
+    assert run(check=False).returncode == 2  # no arguments: usage
+
+
+@pytest.mark.gpu
+def test_cli_densify_ply_equals_oracle(scene_dir, tmp_path, orc):
+    from densepoints_amd.pmvs import write_ply
+
+    out = tmp_path / "points.ply"
+    res = json.loads(run("-i", os.path.join(scene_dir, "scene.json"), "--seeds",
+                         os.path.join(scene_dir, "seeds.xyz"), "-o", str(out)).stdout)
+    cfg = synth.config(4, 160, 120, 1)
+    P = synth.cameras(cfg)
+    imgs = [synth.render_host(cfg, P, v) for v in range(4)]
+    S = orc.Scene(P, imgs)
+    op, ost = S.densify(synth.seeds(cfg, P))
+    assert res["patches"] == ost["patches"] > 0
+    ref = tmp_path / "oracle.ply"
+    write_ply(str(ref), op)
+    assert out.read_bytes() == ref.read_bytes()
