@@ -90,6 +90,17 @@ class DpDensifyStats(ctypes.Structure):
     ]
 
 
+class DpGeneration(ctypes.Structure):
+    _fields_ = [
+        ("items", ctypes.c_int64),
+        ("head", ctypes.c_int64),
+        ("per_item", ctypes.c_int32),
+        ("cell", ctypes.c_int32),
+        ("seq0", ctypes.c_uint32),
+        ("index", ctypes.c_int32),
+    ]
+
+
 class DpSynthConfig(ctypes.Structure):
     _fields_ = [
         ("n_views", ctypes.c_int32),
@@ -126,6 +137,10 @@ SIGNATURES = [
     ("dp_expand_batch", _I, [_P, _P, _I, _P, _P]),
     ("dp_expand_batch_device", _I, [_P, _P, _I, _P, _P, _P]),
     ("dp_densify", _I, [_P, _P, _I, _P, _P, _P]),
+    ("dp_densify_begin", _I, [_P, _P, _I, _P]),
+    ("dp_densify_refine", _I, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
+    ("dp_densify_commit", _I, [_P, _P, _P, _P, ctypes.c_int64]),
+    ("dp_densify_result", _I, [_P, _P, _P, _P]),
     ("dp_last_kernel_ms", _I, [_P, _P]),
     ("dp_synth_default", None, [_P]),
     ("dp_synth_cameras", _I, [_P, _P]),

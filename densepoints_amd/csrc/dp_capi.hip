@@ -97,6 +97,13 @@ struct dp_ctx {
     DevBuf<uint32_t> prefix;
     DevBuf<unsigned char> scan_tmp;
     std::vector<dp_patch> result;
+    // generation-at-a-time densify (dp_densify_begin/refine/commit/result)
+    DevBuf<dp_patch> seedp;  // seed patches of generation 0
+    int64_t g_np = 0;        // patches in the replicated store
+    int64_t g_nseeds = 0;
+    int64_t g_expected = -1; // generation index the next commit must carry
+    dp_densify_stats g_st{};
+    std::chrono::steady_clock::time_point g_t0;
 };
 
 static int fail(dp_ctx *c, int code, const std::string &msg)
@@ -757,6 +764,170 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
     st.generations = gens;
     st.refine_ms = refine_ms;
     st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    if (stats)
+        *stats = st;
+    *out = c->result.empty() ? nullptr : c->result.data();
+    *n_out = np;
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// densify one generation at a time (multi-GPU sharding).  Same
+// sequence numbering, organizer and pop cap as dp_densify.
+// ---------------------------------------------------------------------------
+
+// next expansion generation after the store grew to g_np (dp_densify's loop head)
+static void next_generation(dp_ctx *c, dp_generation *g, int64_t head)
+{
+    const int64_t np = c->g_np;
+    g->index += 1;
+    g->head = head;
+    g->per_item = 4;
+    g->cell = c->opt.expand_cell_size;
+    g->items = (head < np && head < c->opt.max_pops) ? np - head : 0;
+    g->seq0 = (uint32_t)c->g_nseeds + 4u * (uint32_t)head;
+}
+
+extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_generation *gen)
+{
+    if (!c || n < 0 || (n > 0 && !seeds) || !gen)
+        return fail(c, DP_E_ARG, "dp_densify_begin: bad arguments");
+    if (!c->V)
+        return fail(c, DP_E_STATE, "dp_densify_begin: no views");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    c->g_t0 = std::chrono::steady_clock::now();
+    c->g_st = dp_densify_stats{};
+    c->g_st.seeds_in = n;
+    c->g_np = 0;
+    c->g_nseeds = n;
+    c->result.clear();
+    DP_HIP(c, c->grid.reserve((size_t)c->grid_cells + 1));
+    DP_HIP(c, hipMemsetAsync(c->grid.p, 0xFF, sizeof(uint32_t) * ((size_t)c->grid_cells + 1), s));
+    DP_HIP(c, c->store.reserve((size_t)(c->grid_cells / 2 + 16)));
+    DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
+    if (n > 0) {
+        std::vector<dp_patch> sp(n);
+        int rc = dp_seeds_to_patches(c, seeds, n, sp.data());
+        if (rc != DP_OK)
+            return rc;
+        DP_HIP(c, c->seedp.reserve(n));
+        DP_HIP(c, hipMemcpyAsync(c->seedp.p, sp.data(), sizeof(dp_patch) * n, hipMemcpyHostToDevice, s));
+    }
+    DP_HIP(c, hipStreamSynchronize(s));
+    *gen = dp_generation{};
+    gen->items = n;
+    gen->per_item = 1;
+    gen->cell = c->opt.seed_cell_size;
+    gen->index = 0;
+    c->g_expected = 0;
+    return DP_OK;
+}
+
+extern "C" int dp_densify_refine(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi, dp_patch *cand_out,
+                                 uint8_t *accept_out)
+{
+    if (!c || !gen || lo < 0 || hi < lo || hi > gen->items)
+        return fail(c, DP_E_ARG, "dp_densify_refine: bad item range");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_refine: generation out of sequence");
+    const int64_t nc64 = (hi - lo) * gen->per_item;
+    if (nc64 == 0)
+        return DP_OK;
+    if (!cand_out || !accept_out)
+        return fail(c, DP_E_ARG, "dp_densify_refine: null output arrays");
+    if (nc64 > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_refine: shard too large");
+    const int32_t nc = (int32_t)nc64;
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    DP_HIP(c, c->cand.reserve(nc));
+    DP_HIP(c, c->ok.reserve(nc));
+    dpk::RefineArgs a{};
+    if (gen->index == 0) {
+        // seed.cpp:110-144 on this shard of the seed patches
+        DP_HIP(c, hipMemcpyAsync(c->cand.p, c->seedp.p + lo, sizeof(dp_patch) * nc, hipMemcpyDeviceToDevice, s));
+        a = refine_args(c, c->cand.p, nc, gen->cell, DP_MODE_SEED, c->ok.p);
+    } else {
+        // Expand::ExpandPatch of parents head+lo .. head+hi-1 (queue order)
+        a = refine_args(c, c->cand.p, nc, gen->cell, DP_MODE_EXPAND, c->ok.p);
+        a.parents = c->store.p;
+        a.parent0 = gen->head + lo;
+    }
+    int rc = launch_timed(c, a, s);
+    if (rc != DP_OK)
+        return rc;
+    double ms = 0.0;
+    if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
+        return rc;
+    c->g_st.refine_ms += ms;
+    DP_HIP(c, hipMemcpyAsync(cand_out, c->cand.p, sizeof(dp_patch) * nc, hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipMemcpyAsync(accept_out, c->ok.p, (size_t)nc, hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipStreamSynchronize(s));
+    return DP_OK;
+}
+
+extern "C" int dp_densify_commit(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
+                                 int64_t n_cand)
+{
+    if (!c || !gen || n_cand != gen->items * gen->per_item || (n_cand > 0 && (!cand || !accept)))
+        return fail(c, DP_E_ARG, "dp_densify_commit: need all candidates of the generation");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_commit: generation out of sequence");
+    if (n_cand > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_commit: generation too large");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const int32_t nc = (int32_t)n_cand;
+    int64_t acc = 0;
+    if (nc > 0) {
+        if ((uint64_t)gen->seq0 + (uint64_t)nc > 0xFFFFFFF0ull)
+            return fail(c, DP_E_OOM, "sequence space exhausted");
+        DP_HIP(c, c->cand.reserve(nc));
+        DP_HIP(c, c->ok.reserve(nc));
+        DP_HIP(c, hipMemcpyAsync(c->cand.p, cand, sizeof(dp_patch) * nc, hipMemcpyHostToDevice, s));
+        DP_HIP(c, hipMemcpyAsync(c->ok.p, accept, (size_t)nc, hipMemcpyHostToDevice, s));
+        const int is_seed = gen->index == 0;
+        int rc = organize(c, c->cand.p, c->ok.p, nc, gen->seq0, c->g_np, is_seed ? 0 : gen->head, is_seed, &acc);
+        if (rc != DP_OK)
+            return rc;
+        DP_HIP(c, hipStreamSynchronize(s));
+    }
+    int64_t head;
+    if (gen->index == 0) {
+        c->g_st.seed_patches = acc;
+        head = 0;
+    } else {
+        c->g_st.candidates += 4 * (std::min<int64_t>(c->g_np, c->opt.max_pops) - gen->head);
+        c->g_st.generations += 1;
+        head = c->g_np;
+    }
+    c->g_np += acc;
+    next_generation(c, gen, head);
+    c->g_expected = gen->index;
+    return DP_OK;
+}
+
+extern "C" int dp_densify_result(dp_ctx *c, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats)
+{
+    if (!c || !out || !n_out)
+        return fail(c, DP_E_ARG, "dp_densify_result: bad arguments");
+    if (c->g_expected < 0)
+        return fail(c, DP_E_STATE, "dp_densify_result: no generation run");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const int64_t np = c->g_np;
+    c->result.resize((size_t)np);
+    if (np)
+        DP_HIP(c, hipMemcpyAsync(c->result.data(), c->store.p, sizeof(dp_patch) * np, hipMemcpyDeviceToHost, s));
+    unsigned long long ev = 0;
+    DP_HIP(c, hipMemcpyAsync(&ev, c->d_evals, sizeof(ev), hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipStreamSynchronize(s));
+    dp_densify_stats st = c->g_st;
+    st.patches = np;
+    st.pops = std::min<int64_t>(np, c->opt.max_pops);
+    st.evals = (int64_t)ev;
+    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->g_t0).count();
     if (stats)
         *stats = st;
     *out = c->result.empty() ? nullptr : c->result.data();

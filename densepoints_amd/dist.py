@@ -67,24 +67,61 @@ def allgather_patches(local: np.ndarray, dist, device: torch.device | None = Non
     rank order on every rank. Records travel as padded uint8 tensors (one
     count all-gather, one payload all-gather), on `device` for RCCL or on the
     CPU for gloo."""
-    local = np.ascontiguousarray(local, dtype=PATCH_DTYPE)
+    return allgather_array(np.ascontiguousarray(local, dtype=PATCH_DTYPE), dist, device)
+
+
+def allgather_array(local: np.ndarray, dist, device: torch.device | None = None) -> np.ndarray:
+    """All-gather of a variable-length 1-D array of any fixed-size dtype (rank order)."""
+    local = np.ascontiguousarray(local)
     if dist is None:
         return local.copy()
+    dt = local.dtype
     world = dist.get_world_size()
     dev = device if device is not None else torch.device("cpu")
     cnt = torch.tensor([len(local)], dtype=torch.int64, device=dev)
     counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(counts, cnt)
-    counts = [int(c.item()) for c in counts]
-    cap = max(counts) * PATCH_DTYPE.itemsize
-    buf = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
+    counts = [int(x.item()) for x in counts]
+    cap = max(max(counts) * dt.itemsize, 1)
+    buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
     if len(local):
-        buf[: len(local) * PATCH_DTYPE.itemsize] = torch.from_numpy(local.view(np.uint8).copy()).to(dev)
-    parts = [torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev) for _ in range(world)]
+        buf[: len(local) * dt.itemsize] = torch.from_numpy(local.view(np.uint8).copy()).to(dev)
+    parts = [torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
     dist.all_gather(parts, buf)
-    out = [np.frombuffer(p.cpu().numpy()[: c * PATCH_DTYPE.itemsize].tobytes(), dtype=PATCH_DTYPE)
-           for p, c in zip(parts, counts)]
-    return np.concatenate(out) if out else np.empty(0, dtype=PATCH_DTYPE)
+    out = [np.frombuffer(p.cpu().numpy()[: n * dt.itemsize].tobytes(), dtype=dt) for p, n in zip(parts, counts)]
+    return np.concatenate(out) if out else np.empty(0, dtype=dt)
+
+
+def densify_sharded(eng, seeds_xyz, dist, device: torch.device | None = None):
+    """dp_densify with every generation sharded across ranks.
+
+    Each rank refines its contiguous range of the generation's items
+    (dp_densify_refine), the candidates and accept flags are all-gathered in
+    rank order (= sequence order), and every rank commits the whole
+    generation to its replicated organizer (dp_densify_commit).  The result
+    equals the 1-GPU dp_densify bit for bit.  `eng` is a densepoints_amd
+    Engine (or any object with the same four densify_* methods).  Returns
+    (patches, stats); stats["evals"] and ["refine_ms"] are summed/maxed over
+    ranks."""
+    rank = dist.get_rank() if dist is not None else 0
+    world = dist.get_world_size() if dist is not None else 1
+    gen = eng.densify_begin(seeds_xyz)
+    while gen.items > 0:
+        lo, hi = shard_range(gen.items, rank, world)
+        cand, acc = eng.densify_refine(gen, lo, hi)
+        all_cand = allgather_array(cand, dist, device)
+        all_acc = allgather_array(acc, dist, device)
+        gen = eng.densify_commit(gen, all_cand, all_acc)
+    patches, stats = eng.densify_result()
+    if dist is not None:
+        dev = device if device is not None else "cpu"
+        ev = torch.tensor([float(stats["evals"])], dtype=torch.float64, device=dev)
+        ms = torch.tensor([float(stats["refine_ms"])], dtype=torch.float64, device=dev)
+        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        stats["evals"] = int(ev.item())
+        stats["refine_ms"] = float(ms.item())
+    return patches, stats
 
 
 def max_over_ranks(x: float, dist, device: torch.device | None = None) -> float:

@@ -269,6 +269,39 @@ class Engine:
         return res, stats
 
 
+    # ---- one generation at a time (multi-GPU sharding; dist.densify_sharded) ----
+    def densify_begin(self, seeds_xyz: np.ndarray) -> N.DpGeneration:
+        seeds = np.ascontiguousarray(seeds_xyz, dtype=np.float64).reshape(-1, 3)
+        g = N.DpGeneration()
+        self._check(lib.dp_densify_begin(self._ctx, ptr(seeds), len(seeds), ctypes.byref(g)))
+        return g
+
+    def densify_refine(self, gen: N.DpGeneration, lo: int, hi: int):
+        """Refine items [lo, hi) of the generation: (candidates, accept) host arrays."""
+        n = (hi - lo) * gen.per_item
+        cand = empty_patches(n)
+        acc = np.zeros(n, dtype=np.uint8)
+        self._check(lib.dp_densify_refine(self._ctx, ctypes.byref(gen), lo, hi, ptr(cand), ptr(acc)))
+        return cand, acc
+
+    def densify_commit(self, gen: N.DpGeneration, cand: np.ndarray, acc: np.ndarray) -> N.DpGeneration:
+        cand = np.ascontiguousarray(cand, dtype=PATCH_DTYPE)
+        acc = np.ascontiguousarray(acc, dtype=np.uint8)
+        self._check(lib.dp_densify_commit(self._ctx, ctypes.byref(gen), ptr(cand), ptr(acc), len(cand)))
+        return gen
+
+    def densify_result(self):
+        out = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        st = N.DpDensifyStats()
+        self._check(lib.dp_densify_result(self._ctx, ctypes.byref(out), ctypes.byref(n), ctypes.byref(st)))
+        res = empty_patches(n.value)
+        if n.value:
+            ctypes.memmove(res.ctypes.data, out.value, n.value * PATCH_DTYPE.itemsize)
+        stats = {name: getattr(st, name) for name, _ in N.DpDensifyStats._fields_ if name != "reserved"}
+        return res, stats
+
+
 class PMVS:
     """PMVS::PMVS (methods/pmvs/pmvs.h:14-35): AddCamera, Run, GetPointCloud.
 

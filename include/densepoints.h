@@ -174,6 +174,43 @@ int dp_expand_batch_device(dp_ctx *ctx, const dp_patch *d_parents, int n, dp_pat
 int dp_densify(dp_ctx *ctx, const double *seeds_xyz, int n, const dp_patch **out,
                int64_t *n_out, dp_densify_stats *stats);
 
+/* ---- the same BFS one generation at a time, for sharding it across GPUs ----
+ * (SURVEY 8e).  Every rank (one context per GPU) keeps a replicated organizer
+ * grid and patch store.  Per generation each rank refines its own contiguous
+ * range of the generation's work items; the caller all-gathers the candidate
+ * records and accept flags in item order (a rank-order concatenation of
+ * contiguous shards); every rank then commits the full generation.  Claims
+ * are deterministic (owner = lowest sequence number), so every rank's store
+ * equals dp_densify's bit for bit.
+ *   dp_densify_begin(ctx, seeds, n, &g)
+ *   while (g.items > 0) {
+ *     dp_densify_refine(ctx, &g, lo, hi, my_cands, my_accept);   (hi-lo)*g.per_item
+ *     <all-gather>
+ *     dp_densify_commit(ctx, &g, all_cands, all_accept, g.items*g.per_item);
+ *   }
+ *   dp_densify_result(ctx, &out, &n_out, &stats);   evals/refine_ms: this rank's share
+ */
+typedef struct dp_generation {
+    int64_t items;    /* work items: seed points (generation 0) or parents; 0 = finished */
+    int64_t head;     /* queue index of the first parent (expansion generations)          */
+    int32_t per_item; /* candidates per item: 1 (seed generation) or 4 (ExpandPatch)      */
+    int32_t cell;     /* refine window size of this generation                            */
+    uint32_t seq0;    /* sequence number of candidate 0                                   */
+    int32_t index;    /* 0 = seed generation, then 1, 2, ...                              */
+} dp_generation;
+
+int dp_densify_begin(dp_ctx *ctx, const double *seeds_xyz, int n, dp_generation *gen);
+/* Refine items [item_lo, item_hi) of the generation (host output arrays of
+ * (item_hi - item_lo) * per_item entries; the seed generation runs
+ * DP_MODE_SEED, expansion generations Expand::ExpandPatch as dp_expand_batch). */
+int dp_densify_refine(dp_ctx *ctx, const dp_generation *gen, int64_t item_lo, int64_t item_hi,
+                      dp_patch *cand_out, uint8_t *accept_out);
+/* Organizer step over ALL candidates of the generation (host arrays in item
+ * order, n_cand = items * per_item); advances *gen to the next generation. */
+int dp_densify_commit(dp_ctx *ctx, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
+                      int64_t n_cand);
+int dp_densify_result(dp_ctx *ctx, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats);
+
 /* Elapsed device milliseconds of the most recent refine kernel launch, timed
  * with HIP events on the stream the kernel ran on. */
 int dp_last_kernel_ms(dp_ctx *ctx, double *ms);

@@ -964,6 +964,46 @@ int64_t or_densify(const or_scene *s, const double *seeds, int nseeds, or_patch 
     return np;
 }
 
+/* The organizer as a stand-alone object (test infrastructure for the
+ * generation-at-a-time densify): PatchOrganizer::TryInsert
+ * (patch_organizer.cpp:42-65) + ComputeColor (patch.cpp:51-73) applied to one
+ * candidate; writes the stored record (seq, parent, accepted flag, colour)
+ * and returns 1 when the candidate is inserted. */
+struct or_org {
+    const or_scene *s;
+    grid_t g[OR_MAX_VIEWS];
+};
+
+or_org *or_org_create(const or_scene *s)
+{
+    or_org *o = (or_org *)calloc(1, sizeof(or_org));
+    o->s = s;
+    for (int v = 0; v < s->V; ++v) {
+        o->g[v].gw = s->v[v].W / s->opt.grid_scale;
+        o->g[v].gh = s->v[v].H / s->opt.grid_scale;
+        o->g[v].cnt = (uint8_t *)calloc((size_t)o->g[v].gw * o->g[v].gh + 1, 1);
+    }
+    return o;
+}
+
+void or_org_destroy(or_org *o)
+{
+    if (!o) return;
+    for (int v = 0; v < o->s->V; ++v) free(o->g[v].cnt);
+    free(o);
+}
+
+int or_org_insert(or_org *o, const or_patch *p, uint32_t seq, uint32_t parent, or_patch *out)
+{
+    if (!try_insert(o->s, o->g, p)) return 0;
+    *out = *p;
+    out->seq = seq;
+    out->parent = parent;
+    out->flags |= OR_FLAG_ACCEPTED;
+    or_color(o->s, out);
+    return 1;
+}
+
 /* exported probes of the fixed transcendental algorithm (tests compare them
  * with glibc and with the product's independent implementation) */
 void or_sincos(double x, double *s, double *c) { ordm_sincos(x, s, c); }

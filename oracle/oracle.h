@@ -95,6 +95,11 @@ int or_expand_batch(const or_scene *s, const or_patch *parents, int n, or_patch 
                     uint8_t *acc, int nthreads);
 int64_t or_densify(const or_scene *s, const double *seeds, int nseeds, or_patch *out,
                    int64_t cap, int64_t *n_seed_patches, int64_t *pops);
+/* organizer object (generation-at-a-time densify tests) */
+typedef struct or_org or_org;
+or_org *or_org_create(const or_scene *s);
+void or_org_destroy(or_org *o);
+int or_org_insert(or_org *o, const or_patch *p, uint32_t seq, uint32_t parent, or_patch *out);
 void or_color(const or_scene *s, or_patch *p);
 
 #ifdef __cplusplus

@@ -83,6 +83,9 @@ def _load():
         "or_expand_batch": (ctypes.c_int, [P, P, ctypes.c_int, P, P, ctypes.c_int]),
         "or_densify": (ctypes.c_int64, [P, P, ctypes.c_int, P, ctypes.c_int64, P, P]),
         "or_color": (None, [P, P]),
+        "or_org_create": (P, [P]),
+        "or_org_destroy": (None, [P]),
+        "or_org_insert": (ctypes.c_int, [P, P, ctypes.c_uint32, ctypes.c_uint32, P]),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)
@@ -182,6 +185,71 @@ class Scene:
         pops = ctypes.c_int64()
         n = lib.or_densify(self._h, _p(seeds), len(seeds), _p(out), cap, ctypes.byref(nseed), ctypes.byref(pops))
         return out[: min(n, cap)].copy(), {"patches": n, "seed_patches": nseed.value, "pops": pops.value}
+
+
+class _Gen:
+    """Mirror of dp_generation (include/densepoints.h)."""
+
+    def __init__(self, items, head, per_item, cell, seq0, index):
+        self.items, self.head, self.per_item, self.cell, self.seq0, self.index = (
+            items, head, per_item, cell, seq0, index)
+
+
+class GenerationEngine:
+    """The generation-at-a-time densify protocol of the C ABI
+    (dp_densify_begin/refine/commit/result) restated on the oracle: test
+    infrastructure for the multi-rank driver (densepoints_amd.dist.densify_sharded)
+    on the CPU.  Same sequence numbering, pop cap and organizer order as
+    or_densify (which it must reproduce)."""
+
+    def __init__(self, scene: "Scene", threads: int = 2):
+        self.S = scene
+        self.threads = threads
+        self.org = None
+
+    def __del__(self):
+        if self.org:
+            lib.or_org_destroy(self.org)
+
+    def densify_begin(self, seeds):
+        if self.org:
+            lib.or_org_destroy(self.org)
+        self.org = lib.or_org_create(self.S._h)
+        seeds = np.ascontiguousarray(seeds, dtype=np.float64).reshape(-1, 3)
+        self.sp = self.S.seeds_to_patches(seeds)
+        self.nseeds = len(seeds)
+        self.store = []
+        return _Gen(len(seeds), 0, 1, self.S.opt.seed_cell_size, 0, 0)
+
+    def densify_refine(self, g, lo, hi):
+        if g.index == 0:
+            r = self.sp[lo:hi].copy()
+            acc = self.S.refine(r, g.cell, 3, self.threads)  # MODE_SEED
+            return r, acc
+        parents = np.array(self.store[g.head + lo: g.head + hi], dtype=PATCH_DTYPE)
+        kids, acc = self.S.expand(parents, self.threads)
+        q = g.head + lo + np.repeat(np.arange(hi - lo), 4)
+        kids["parent"] = q.astype(np.uint32)
+        acc[q >= self.S.opt.max_pops] = 0  # past the pop cap (expand.cpp:95)
+        return kids, acc
+
+    def densify_commit(self, g, cand, acc):
+        out = np.zeros(1, dtype=PATCH_DTYPE)
+        for i in range(len(cand)):
+            if not acc[i]:
+                continue
+            par = 0xFFFFFFFF if g.index == 0 else g.head + i // 4
+            c1 = np.ascontiguousarray(cand[i:i + 1])
+            if lib.or_org_insert(self.org, _p(c1), len(self.store), par, _p(out)):
+                self.store.append(out[0].copy())
+        head = 0 if g.index == 0 else g.head + g.items  # the store size before this generation
+        np_ = len(self.store)
+        items = np_ - head if (head < np_ and head < self.S.opt.max_pops) else 0
+        return _Gen(items, head, 4, self.S.opt.expand_cell_size, self.nseeds + 4 * head, g.index + 1)
+
+    def densify_result(self):
+        res = np.array(self.store, dtype=PATCH_DTYPE) if self.store else np.zeros(0, dtype=PATCH_DTYPE)
+        return res, {"patches": len(res), "evals": 0, "refine_ms": 0.0}
 
 
 def ncc_int(a, b, denom_min=0.1):

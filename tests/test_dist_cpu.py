@@ -91,3 +91,45 @@ def test_gloo_world2_sharded_expand_equals_single_process(tmp_path, orc):
     assert len(got) == 4 * len(parents)
     assert got.tobytes() == kids.tobytes()
     assert float(open(out + ".max").read()) == 2.0
+
+
+def _hf6():
+    # 6-view tilted-facet scene, 320x240 (the GPU suite's "hf6")
+    return synth.scene_host(synth.config(6, 320, 240, 1))
+
+
+def _dens_worker(rank, world, port, out_path, max_pops):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import densepoints_amd as dp
+    from oracle import pyoracle
+
+    dist = D.init("gloo")
+    P, imgs, seeds = _hf6()
+    S = pyoracle.Scene(P, imgs, dp.Options(max_pops=max_pops) if max_pops else None)
+    patches, st = D.densify_sharded(pyoracle.GenerationEngine(S), seeds, dist)
+    if rank == 0:
+        np.save(out_path, patches.view(np.uint8), allow_pickle=False)
+    else:  # every rank holds the same replicated store
+        np.save(out_path + f".r{rank}.npy", patches.view(np.uint8), allow_pickle=False)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("max_pops", [0, 23])
+def test_gloo_world2_sharded_densify_equals_single_process(tmp_path, orc, max_pops):
+    """every generation sharded over 2 ranks, candidates all-gathered,
+    replicated deterministic claims -> the 1-process densify, bit for bit."""
+    import densepoints_amd as dp
+    from densepoints_amd._native import PATCH_DTYPE
+
+    out = str(tmp_path / "dense.npy")
+    mp.spawn(_dens_worker, args=(2, _free_port(), out, max_pops), nprocs=2, join=True)
+    got = np.frombuffer(np.load(out, allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
+    got1 = np.frombuffer(np.load(out + ".r1.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
+    P, imgs, seeds = _hf6()
+    S = orc.Scene(P, imgs, dp.Options(max_pops=max_pops) if max_pops else None)
+    ref, st = S.densify(seeds)
+    assert len(ref) > 50
+    assert got.tobytes() == ref.tobytes()
+    assert got1.tobytes() == ref.tobytes()
