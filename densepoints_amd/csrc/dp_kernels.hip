@@ -490,6 +490,70 @@ __device__ __forceinline__ void views_all(const RefineArgs &a, WaveLds &L, const
     }
 }
 
+// DPP within lane quads: xor 1, xor 2 and broadcast of quad lane i
+__device__ __forceinline__ int quad_xor1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false); }
+__device__ __forceinline__ int quad_xor2(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false); }
+template <int I>
+__device__ __forceinline__ float quad_bcast(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), I * 0x55, 0xf, 0xf, false));
+}
+
+// Window maps of up to 16 views (chunk slots round0 .. round0+15) with four
+// lanes per view: lane 4k+i projects window corner i into view slot
+// round0+k; the ROI min/max and the four f32 corners are combined across the
+// lane quad by DPP; lane 4k then runs dpg::quad_map.  Same arithmetic as
+// dpg::texture_map (its corner loop, one corner per lane).  Returns the
+// chunk-slot bits of the views with a valid map.
+__device__ __forceinline__ uint64_t build_maps_quad(const RefineArgs &a, WaveLds &L, int base, int m, int round0,
+                                                    int cell)
+{
+    const int lane = lane_id();
+    const int k = lane >> 2, ci = lane & 3;
+    const int slot = round0 + k;
+    const int kk = base + slot;
+    const bool act = slot < kMapChunk && kk < m;
+    const dpg::ViewDev &vw = a.views[L.vlist[act ? kk : base]];
+    double u, w;
+    dpg::project(vw.P, L.c12[3 * ci], L.c12[3 * ci + 1], L.c12[3 * ci + 2], u, w);
+    const bool ins = act && dpg::inside(u, w, vw.W, vw.H);
+    const uint64_t insm = __ballot(ins);
+    const bool all_in = ((insm >> (lane & ~3)) & 0xFull) == 0xFull;
+    // texture_map: tl = min(W|H, ceil of the corners), br = max(0, floor of the corners)
+    int cx = (int)ceil(u), cy = (int)ceil(w), lx = (int)floor(u), ly = (int)floor(w);
+    cx = min(cx, quad_xor1(cx));
+    cx = min(cx, quad_xor2(cx));
+    cy = min(cy, quad_xor1(cy));
+    cy = min(cy, quad_xor2(cy));
+    lx = max(lx, quad_xor1(lx));
+    lx = max(lx, quad_xor2(lx));
+    ly = max(ly, quad_xor1(ly));
+    ly = max(ly, quad_xor2(ly));
+    const int tlx = min(vw.W, cx), tly = min(vw.H, cy), brx = max(0, lx), bry = max(0, ly);
+    const float fx = (float)u, fy = (float)w;
+    const float fx0 = quad_bcast<0>(fx), fx1 = quad_bcast<1>(fx), fx2 = quad_bcast<2>(fx), fx3 = quad_bcast<3>(fx);
+    const float fy0 = quad_bcast<0>(fy), fy1 = quad_bcast<1>(fy), fy2 = quad_bcast<2>(fy), fy3 = quad_bcast<3>(fy);
+    bool ok = false;
+    const int rw = brx - tlx, rh = bry - tly;
+    if (ci == 0 && all_in && rw > 0 && rh > 0) {
+        const float ftx = (float)tlx, fty = (float)tly;
+        const double x[4] = {(double)(fx0 - ftx), (double)(fx1 - ftx), (double)(fx2 - ftx), (double)(fx3 - ftx)};
+        const double y[4] = {(double)(fy0 - fty), (double)(fy1 - fty), (double)(fy2 - fty), (double)(fy3 - fty)};
+        dpg::TexMap tm;
+        ok = dpg::quad_map(x, y, tlx, tly, rw, rh, cell, tm);
+        if (ok) {
+            L.map[slot] = tm;
+            L.roi[slot] = (uint64_t)(uintptr_t)(vw.img + ((size_t)tm.tly * (size_t)vw.pitch + (size_t)tm.tlx));
+            L.pitch[slot] = vw.pitch;
+        }
+    }
+    const uint64_t okq = __ballot(ok); // bit 4k <- view slot round0 + k
+    uint64_t bits = 0;
+    for (int q = 0; q < 16; ++q)
+        bits |= ((okq >> (4 * q)) & 1ull) << q;
+    return bits << round0;
+}
+
 // One evaluation's NCC scores against texture 0 -> L.score[0..nv-1]
 // (GetProjectedTextures + NCCScore) at candidate pose (nn, pp).  Per chunk of
 // up to 64 visible views, lane k builds view k's window map (projective map +
@@ -525,20 +589,10 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
     int Sa = 0, Saa = 0;
     bool va = false;
     for (int base = 0; base < m; base += kMapChunk) {
-        // window maps of this chunk: lane k builds view base+k's map
-        bool ok = false;
-        const int kk = base + lane;
-        if (lane < kMapChunk && kk < m) {
-            dpg::TexMap tm;
-            const dpg::ViewDev &vw = a.views[L.vlist[kk]];
-            ok = dpg::texture_map(vw, L.c12, cell, tm);
-            if (ok) {
-                L.map[lane] = tm;
-                L.roi[lane] = (uint64_t)(uintptr_t)(vw.img + ((size_t)tm.tly * (size_t)vw.pitch + (size_t)tm.tlx));
-                L.pitch[lane] = vw.pitch;
-            }
-        }
-        const uint64_t okmask = __ballot(ok);
+        // window maps of this chunk, 16 views per round (4 lanes per view)
+        uint64_t okmask = 0;
+        for (int r0 = 0; r0 < kMapChunk && base + r0 < m; r0 += 16)
+            okmask |= build_maps_quad(a, L, base, m, r0, cell);
         wave_sync();
         STAMP(L, 0);
         // texture 0 = lowest-index visible view (optimization_opencv.cpp:24-28)
