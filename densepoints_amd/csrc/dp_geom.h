@@ -69,14 +69,12 @@ DP_HD bool inside(double u, double v, int32_t W, int32_t H)
 // pose (nn, pp); the corners are centred on the patch's STORED position Xs
 // (patch.cpp:120-123 uses GetPosition()).  Returns false when dx == 0
 // (optimization.cpp:27 LOG(FATAL) -> degenerate flag).
-DP_HD bool window_corners(const ViewDev &rv, const double *Xs, const double *nn, const double *pp,
-                          int cell, double *c12)
+// the part after the two reference-view projections of pp and pp + xr
+DP_HD bool window_corners_sc(const ViewDev &rv, const double *Xs, const double *nn, double cu, double cv,
+                             double qu, double qv, int cell, double *c12)
 {
     double y[3];
     cross3(nn, rv.xr, y);
-    double cu, cv, qu, qv;
-    project(rv.P, pp[0], pp[1], pp[2], cu, cv);
-    project(rv.P, pp[0] + rv.xr[0], pp[1] + rv.xr[1], pp[2] + rv.xr[2], qu, qv);
     const double du = qu - cu, dv = qv - cv;
     const double dx = sqrt(du * du + dv * dv);
     if (dx == 0.0)
@@ -91,6 +89,15 @@ DP_HD bool window_corners(const ViewDev &rv, const double *Xs, const double *nn,
         c12[9 + i] = (Xs[i] - sx) + sy;
     }
     return true;
+}
+
+DP_HD bool window_corners(const ViewDev &rv, const double *Xs, const double *nn, const double *pp,
+                          int cell, double *c12)
+{
+    double cu, cv, qu, qv;
+    project(rv.P, pp[0], pp[1], pp[2], cu, cv);
+    project(rv.P, pp[0] + rv.xr[0], pp[1] + rv.xr[1], pp[2] + rv.xr[2], qu, qv);
+    return window_corners_sc(rv, Xs, nn, cu, cv, qu, qv, cell, c12);
 }
 
 // Sampling map of one view: window pixel (x, y) -> ROI coordinates, plus ROI.
@@ -261,20 +268,27 @@ DP_HD double ncc_finish(int32_t N, int32_t Sa, int32_t Saa, int32_t Sb, int32_t 
 }
 
 // (depth, roll, pitch) -> candidate normal / position (optimization.cpp:78-96)
-DP_HD void unparametrize(const double *C, const double *Xs, const double *ns, double d, double roll,
-                         double pitch, double *nn, double *pp)
+// unparametrize given sin/cos of roll (a) and pitch (b)
+DP_HD void unparametrize_sc(const double *C, const double *Xs, const double *ns, double d, double sa, double ca,
+                            double sb, double cb, double *nn, double *pp)
 {
     for (int i = 0; i < 3; ++i)
         pp[i] = C[i] + (1.0 + d) * (Xs[i] - C[i]);
-    double sa, ca, sb, cb;
-    dpm::sincos(roll, sa, ca);
-    dpm::sincos(pitch, sb, cb);
     const double r0[3] = {cb, 0.0, -sb};
     const double r1[3] = {sa * sb, ca, cb * sa};
     const double r2[3] = {ca * sb, -sa, ca * cb};
     nn[0] = (r0[0] * ns[0] + r0[1] * ns[1]) + r0[2] * ns[2];
     nn[1] = (r1[0] * ns[0] + r1[1] * ns[1]) + r1[2] * ns[2];
     nn[2] = (r2[0] * ns[0] + r2[1] * ns[1]) + r2[2] * ns[2];
+}
+
+DP_HD void unparametrize(const double *C, const double *Xs, const double *ns, double d, double roll,
+                         double pitch, double *nn, double *pp)
+{
+    double sa, ca, sb, cb;
+    dpm::sincos(roll, sa, ca);
+    dpm::sincos(pitch, sb, cb);
+    unparametrize_sc(C, Xs, ns, d, sa, ca, sb, cb, nn, pp);
 }
 
 // Patch::InitRelatedImages classification of one view (patch.cpp:36-47):

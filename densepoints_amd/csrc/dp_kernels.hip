@@ -21,7 +21,7 @@ namespace dpk {
 namespace {
 
 #ifndef DP_MAP_CHUNK
-#define DP_MAP_CHUNK 32
+#define DP_MAP_CHUNK 20
 #endif
 constexpr int kMapChunk = DP_MAP_CHUNK; // views whose window maps are built per chunk
 
@@ -76,6 +76,14 @@ __device__ __forceinline__ void wave_sync()
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
 
 // Lane id through an opaque (volatile) mbcnt: values derived from it are
 // recomputed where they are used instead of being hoisted to kernel scope,
@@ -572,7 +580,14 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
     {
         double c12[12];
         const double Xs[3] = {L.X[0], L.X[1], L.X[2]};
-        const bool ok = dpg::window_corners(a.views[uni(L.ref)], Xs, nn, pp, cell, c12);
+        // the two reference-view projections (pp, pp + x-axis) on lanes 0 / 1
+        const dpg::ViewDev &rv = a.views[uni(L.ref)];
+        const bool l1 = (lane_id() & 1) != 0;
+        double u, w;
+        dpg::project(rv.P, l1 ? pp[0] + rv.xr[0] : pp[0], l1 ? pp[1] + rv.xr[1] : pp[1],
+                     l1 ? pp[2] + rv.xr[2] : pp[2], u, w);
+        const bool ok = dpg::window_corners_sc(rv, Xs, nn, readlane_f64(u, 0), readlane_f64(w, 0),
+                                               readlane_f64(u, 1), readlane_f64(w, 1), cell, c12);
         degen = degen || !ok;
         if (!ok) {
             for (int k = lane; k < nv; k += kWave)
@@ -632,7 +647,13 @@ __device__ __forceinline__ double wave_objective(const RefineArgs &a, WaveLds &L
     {
         const double Xs[3] = {L.X[0], L.X[1], L.X[2]};
         const double ns[3] = {L.n[0], L.n[1], L.n[2]};
-        dpg::unparametrize(a.views[uni(L.ref)].C, Xs, ns, x0, x1, x2, nn, pp);
+        // sin/cos of roll on even lanes and of pitch on odd lanes: one
+        // fdlibm evaluation for both angles, then broadcast
+        double s, co;
+        dpm::sincos((lane_id() & 1) ? x2 : x1, s, co);
+        const double sa = readlane_f64(s, 0), ca = readlane_f64(co, 0);
+        const double sb = readlane_f64(s, 1), cb = readlane_f64(co, 1);
+        dpg::unparametrize_sc(a.views[uni(L.ref)].C, Xs, ns, x0, sa, ca, sb, cb, nn, pp);
     }
     const int nv = wave_scores<G>(a, L, td, nn, pp, degen);
     if (nv == 0)
@@ -881,7 +902,7 @@ __device__ void child_position(const RefineArgs &a, const dp_patch &par, int dir
 // window gathers; the register allocator spills only in the per-evaluation
 // setup code at this target, never in the texel loops (checked in the ISA).
 #ifndef DP_REFINE_WAVES_PER_EU
-#define DP_REFINE_WAVES_PER_EU 4
+#define DP_REFINE_WAVES_PER_EU 5
 #endif
 #ifdef DP_REFINE_MAX_VGPR
 #define DP_REFINE_BOUNDS                                                                                       \
