@@ -77,6 +77,15 @@ __device__ __forceinline__ void wave_sync()
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// wave-uniform copy of a double (lane 0's), so comparisons on it are scalar branches
+__device__ __forceinline__ double uni_f64(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffff));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ double readlane_f64(double v, int l)
 {
     const long long b = __double_as_longlong(v);
@@ -666,6 +675,25 @@ __device__ __forceinline__ double wave_objective(const RefineArgs &a, WaveLds &L
 
 enum NmPhase { kInit = 0, kReflect = 1, kExpand = 2, kContract = 3, kShrink = 4 };
 
+// Nelder-Mead decisions on wave-uniform copies (scalar branches, SGPR state)
+#ifndef DP_NM_UNIFORM
+#define DP_NM_UNIFORM 1
+#endif
+__device__ __forceinline__ double nm_uni(double v)
+{
+#if DP_NM_UNIFORM
+    return uni_f64(v);
+#else
+    return v;
+#endif
+}
+
+// y[i] for a uniform index without a private array
+__device__ __forceinline__ double pick_y(const double *yy, int i)
+{
+    return i == 0 ? yy[0] : (i == 1 ? yy[1] : (i == 2 ? yy[2] : yy[3]));
+}
+
 // cv::DownhillSolver::minimize as driven by OptimizationOpenCV::Optimize
 // (optimization_opencv.cpp:44-78; OpenCV 3.4 createInitialSimplex,
 // innerDownhillSimplex, tryNewPoint).  One objective call site; the simplex
@@ -701,7 +729,7 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
             L.pt[1] = q1;
             L.pt[2] = q2;
         }
-        const double f = wave_objective<G>(a, L, td, q0, q1, q2, degen);
+        const double f = nm_uni(wave_objective<G>(a, L, td, q0, q1, q2, degen));
         ++evals;
         bool decide = false;
         if (phase == kInit) {
@@ -727,7 +755,7 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
             }
         } else {
             // tryNewPoint acceptance
-            if (f < L.y[ihi]) {
+            if (f < nm_uni(L.y[ihi])) {
                 L.y[ihi] = f;
                 for (int jj = 0; jj < 3; ++jj)
                     L.cs[jj] += L.pt[jj] - L.sp[ihi][jj];
@@ -735,9 +763,9 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
                     L.sp[ihi][jj] = L.pt[jj];
             }
             if (phase == kReflect) {
-                if (f <= L.ylo) {
+                if (f <= nm_uni(L.ylo)) {
                     phase = kExpand;
-                } else if (f >= L.ynhi) {
+                } else if (f >= nm_uni(L.ynhi)) {
                     L.ysave = L.y[ihi];
                     phase = kContract;
                 } else {
@@ -747,7 +775,7 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
             } else if (phase == kExpand) {
                 decide = true;
             } else { // contract
-                if (f >= L.ysave) {
+                if (f >= nm_uni(L.ysave)) {
                     vi = (ilo == 0) ? 1 : 0;
                     for (int jj = 0; jj < 3; ++jj)
                         L.sp[vi][jj] = 0.5 * (L.sp[vi][jj] + L.sp[ilo][jj]);
@@ -761,38 +789,42 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
             continue;
         // innerDownhillSimplex: ilo / ihi / inhi scan with the tie fix
         ilo = 0;
-        if (L.y[0] > L.y[1]) {
+        const double y0 = nm_uni(L.y[0]), y1 = nm_uni(L.y[1]), y2 = nm_uni(L.y[2]), y3 = nm_uni(L.y[3]);
+        const double yy[4] = {y0, y1, y2, y3};
+        if (y0 > y1) {
             ihi = 0;
             inhi = 1;
         } else {
             ihi = 1;
             inhi = 0;
         }
+#pragma unroll
         for (int i = 0; i <= 3; ++i) {
-            const double yv = L.y[i];
-            if (yv <= L.y[ilo])
+            const double yv = yy[i];
+            if (yv <= pick_y(yy, ilo))
                 ilo = i;
-            if (yv > L.y[ihi]) {
+            if (yv > pick_y(yy, ihi)) {
                 inhi = ihi;
                 ihi = i;
-            } else if (yv > L.y[inhi] && i != ihi) {
+            } else if (yv > pick_y(yy, inhi) && i != ihi) {
                 inhi = i;
             }
         }
         if (ilo == inhi || ilo == ihi) {
+#pragma unroll
             for (int i = 0; i <= 3; ++i) {
-                if (L.y[i] == L.y[ilo] && i != ihi && i != inhi) {
+                if (yy[i] == pick_y(yy, ilo) && i != ihi && i != inhi) {
                     ilo = i;
                     break;
                 }
             }
         }
-        const double err = fabs(L.y[ihi] - L.y[ilo]);
+        const double err = fabs(pick_y(yy, ihi) - pick_y(yy, ilo));
         double range = 0.0;
         for (int jj = 0; jj < 3; ++jj) {
-            double mn = L.sp[0][jj], mx = L.sp[0][jj];
+            double mn = nm_uni(L.sp[0][jj]), mx = mn;
             for (int i = 1; i <= 3; ++i) {
-                const double v = L.sp[i][jj];
+                const double v = nm_uni(L.sp[i][jj]);
                 mn = (v < mn) ? v : mn;
                 mx = (mx < v) ? v : mx;
             }
