@@ -15,13 +15,14 @@ __device__ __forceinline__ int32_t rint_i32(double v)
     return (int32_t)(uint32_t)__double_as_longlong(r);
 }
 
-// Correctly rounded a / b without v_rcp_f64 (a 1/16-rate transcendental on
-// gfx950, measured): the v_rcp_f32 seed (1 ulp of f32) refined by two fp64
-// Newton steps reaches the accuracy of LLVM's f64 division sequence after its
-// two steps, and the same final correction q = fma(fma(-b, q0, a), r, q0)
-// rounds correctly.  Valid when no intermediate overflows/underflows: the
-// guarded form falls back to '/' outside 2^-120 < |b| < 2^120,
-// 2^-900 < |a| < 2^900 (and for a == 0, keeping the sign of zero).
+// a / b without v_rcp_f64 (a 1/16-rate transcendental on gfx950, measured):
+// the v_rcp_f32 seed (1 ulp of f32) refined by two fp64 Newton steps and the
+// Markstein correction q = fma(fma(-b, q0, a), r, q0).  Equal to IEEE '/'
+// whenever the refined r is RN(1/b); it can be 1 ulp off when b has an
+// all-ones significand or 1/b lies within 2^-92 of a midpoint (~2^-39 of
+// denominators) -- see DESIGN.md "Exactness caveat" for why that never
+// reaches the outputs in practice.  The guarded form falls back to '/'
+// outside 2^-120 < |b| < 2^120, 2^-900 < |a| < 2^900 (and for a == 0).
 __device__ __forceinline__ double div_rn_core(double a, double b)
 {
     double r = (double)__builtin_amdgcn_rcpf((float)b);
