@@ -67,4 +67,17 @@ __device__ __forceinline__ void div_pair_rn(double a0, double a1, double b, doub
 // 32 / W for 1e-3 < W < 1e6 (TexMap::safe)
 __device__ __forceinline__ double div32_safe(double w) { return div_rn_core(32.0, w); }
 
+// 1 / w for 3e-5 < w < 3e4 (the texel loop's W/32): div_rn_core with a = 1,
+// where q0 = a * r = r needs no multiply
+__device__ __forceinline__ double recip_safe(double b)
+{
+    double r = (double)__builtin_amdgcn_rcpf((float)b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double rem = __builtin_fma(-b, r, 1.0);
+    return __builtin_fma(rem, r, r);
+}
+
 } // namespace dpk

@@ -29,8 +29,8 @@ constexpr int kMapChunk = DP_MAP_CHUNK; // views whose window maps are built per
 // registers only hold short-lived values (the evaluation is fp64-heavy).
 struct WaveLds {
     // first: the texel loop addresses these with ds_read2 immediate offsets
-    double rowt[64][3];                         // per pass: window rows X0, Y0, W0 of slot j at j*(64/G)
-    double colt[64][3];                         // per pass: window columns m0*x, m3*x, m6*x (same slots)
+    double rowt[64][3];                         // per pass: window rows X0, Y0, W0/32 of slot j at j*(64/G)
+    double colt[64][3];                         // per pass: window columns m0*x, m3*x, m6*x/32 (same slots)
     dpg::TexMap map[kMapChunk];                 // window maps of the current view chunk
     uint64_t roi[kMapChunk];                    // global address of each map's ROI origin
     int32_t pitch[kMapChunk];                   // its image row pitch (pixels)
@@ -147,21 +147,13 @@ __device__ __forceinline__ void texel_coord(const WaveLds &L, int rb, int px, in
 {
     const double X0 = L.rowt[rb + py][0], Y0 = L.rowt[rb + py][1], W0 = L.rowt[rb + py][2];
     const double cX = L.colt[rb + px][0], cY = L.colt[rb + px][1], cW = L.colt[rb + px][2];
+    // the tables hold W/32: W' = W0' + cW' = fl(W0 + cW)/32 exactly, and
+    // RN(1/W') = RN(32/W)
     double W = W0 + cW;
-    if (kSafe) {
-#ifdef DP_DIAG_NODIV
-        W = 32.0 * W; // diagnostic build: timing only, wrong results
-#elif defined(DP_DIAG_RCP0)
-        W = 32.0 * __builtin_amdgcn_rcp(W); // diagnostic: rcp only
-#elif defined(DP_DIAG_RCP1)
-        { const double r = __builtin_amdgcn_rcp(W); const double e = __builtin_fma(-W, r, 1.0);
-          W = 32.0 * __builtin_fma(r, e, r); } // diagnostic: rcp + 1 Newton
-#else
-        W = div32_safe(W);
-#endif
-    } else {
-        W = (W != 0.0) ? 32.0 / W : 0.0;
-    }
+    if (kSafe)
+        W = recip_safe(W);
+    else
+        W = (W != 0.0) ? 1.0 / W : 0.0;
     double X = (X0 + cX) * W;
     double Y = (Y0 + cY) * W;
     if (!kSafe) {
@@ -179,7 +171,7 @@ __device__ __forceinline__ void texel_coord(const WaveLds &L, int rb, int px, in
 // then BORDER_REPLICATE select, bilinear and BGR2GRAY.
 struct TexelLoad {
     unsigned long long a, b;
-    uint32_t f; // fx | fy << 5 | same << 10
+    uint32_t f; // fx | fy << 5 (fx = 0 where the right tap replicates the left)
 };
 
 __device__ __forceinline__ int32_t med3_i32(int32_t v, int32_t lo, int32_t hi)
@@ -196,7 +188,10 @@ __device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm, 
     const int32_t y0 = med3_i32(sy, 0, hm);
     const int32_t y1 = med3_i32(sy + 1, 0, hm);
     TexelLoad t;
-    const uint32_t same = (uint32_t)sx >= (uint32_t)wm; // sx < 0 or sx >= w-1: x1 == x0
+    // sx < 0 or sx >= w-1: x1 == x0 (BORDER_REPLICATE), i.e. weight 0 on the
+    // right tap -- the same integers as fx = 0; the right tap loaded at x0+1
+    // is still inside the image (x0 + 1 <= tlx + w <= W - 1)
+    const bool same = (uint32_t)sx >= (uint32_t)wm;
     // pixel offsets inside one image plane: pitch < 2^24, y < 2^24
     const uint32_t o0 = __umul24((uint32_t)y0, (uint32_t)pitch) + (uint32_t)x0;
     const uint32_t o1 = __umul24((uint32_t)y1, (uint32_t)pitch) + (uint32_t)x0;
@@ -210,7 +205,7 @@ __device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm, 
     t.a = *(gpair_t)(roi + o0);
     t.b = *(gpair_t)(roi + o1);
 #endif
-    t.f = (uint32_t)(ix & 31) | ((uint32_t)(iy & 31) << 5) | (same << 10);
+    t.f = (same ? 0u : (uint32_t)(ix & 31)) | ((uint32_t)(iy & 31) << 5);
     return t;
 }
 
@@ -220,11 +215,9 @@ __device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm, 
 __device__ __forceinline__ int texel_gray(const TexelLoad &t)
 {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const uint32_t fx = t.f & 31u, fy = (t.f >> 5) & 31u;
-    const bool same = (t.f >> 10) & 1u;
+    const uint32_t fx = t.f & 31u, fy = t.f >> 5;
     const uint32_t a0 = (uint32_t)t.a, b0 = (uint32_t)t.b;
-    const uint32_t a1 = same ? a0 : (uint32_t)(t.a >> 32);
-    const uint32_t b1 = same ? b0 : (uint32_t)(t.b >> 32);
+    const uint32_t a1 = (uint32_t)(t.a >> 32), b1 = (uint32_t)(t.b >> 32);
     const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
     const us2 w0 = __builtin_bit_cast(us2, wx * (32u - fy));
     const us2 w1 = __builtin_bit_cast(us2, wx * fy);
@@ -246,8 +239,9 @@ __device__ __forceinline__ void fill_tables(WaveLds &L, int rb, const dpg::TexMa
     const double m0 = tm.m0, m1 = tm.m1, m2 = tm.m2, m3 = tm.m3, m4 = tm.m4, m5 = tm.m5;
     const double m6 = tm.m6, m7 = tm.m7, m8 = tm.m8;
     const double v = (double)r;
-    const double r0 = m1 * v + m2, r1 = m4 * v + m5, r2 = m7 * v + m8;
-    const double c0 = m0 * v, c1 = m3 * v, c2 = m6 * v;
+    // W terms scaled by 2^-5 (exact): W' = W0' + cW' = W/32, and 32/W = 1/W'
+    const double r0 = m1 * v + m2, r1 = m4 * v + m5, r2 = (m7 * v + m8) * 0.03125;
+    const double c0 = m0 * v, c1 = m3 * v, c2 = (m6 * v) * 0.03125;
     L.rowt[rb + r][0] = r0;
     L.rowt[rb + r][1] = r1;
     L.rowt[rb + r][2] = r2;
@@ -334,7 +328,7 @@ __device__ __forceinline__ void texel_coord_d(const WaveLds &L, uint32_t d, int3
 {
     const double *R = (const double *)((const char *)&L.rowt[0][0] + (d & 2047u));
     const double *C = (const double *)((const char *)&L.colt[0][0] + ((d >> 11) & 2047u));
-    const double W = div32_safe(R[2] + C[2]);
+    const double W = recip_safe(R[2] + C[2]); // tables hold W/32: 1/W' = 32/W
     ix = rint_i32((R[0] + C[0]) * W);
     iy = rint_i32((R[1] + C[1]) * W);
 }
