@@ -516,7 +516,31 @@ __device__ __forceinline__ float quad_bcast(float v)
 // lane quad by DPP; lane 4k then runs dpg::quad_map.  Same arithmetic as
 // dpg::texture_map (its corner loop, one corner per lane).  Returns the
 // chunk-slot bits of the views with a valid map.
-__device__ __forceinline__ uint64_t build_maps_quad(const RefineArgs &a, WaveLds &L, int base, int m, int round0,
+// the view data a map lane needs, loaded ahead of the corner math
+struct MapView {
+    double P[12];
+    int32_t W, H, pitch;
+    const uint32_t *img;
+};
+
+__device__ __forceinline__ MapView load_map_view(const RefineArgs &a, const WaveLds &L, int base, int m, int round0)
+{
+    const int slot = round0 + (lane_id() >> 2);
+    const int kk = base + slot;
+    const bool act = slot < kMapChunk && kk < m;
+    const dpg::ViewDev &vw = a.views[L.vlist[act ? kk : base]];
+    MapView v;
+#pragma unroll
+    for (int i = 0; i < 12; ++i)
+        v.P[i] = vw.P[i];
+    v.W = vw.W;
+    v.H = vw.H;
+    v.pitch = vw.pitch;
+    v.img = vw.img;
+    return v;
+}
+
+__device__ __forceinline__ uint64_t build_maps_quad(const MapView &vw, WaveLds &L, int base, int m, int round0,
                                                     int cell)
 {
     const int lane = lane_id();
@@ -524,7 +548,6 @@ __device__ __forceinline__ uint64_t build_maps_quad(const RefineArgs &a, WaveLds
     const int slot = round0 + k;
     const int kk = base + slot;
     const bool act = slot < kMapChunk && kk < m;
-    const dpg::ViewDev &vw = a.views[L.vlist[act ? kk : base]];
     double u, w;
     dpg::project(vw.P, L.c12[3 * ci], L.c12[3 * ci + 1], L.c12[3 * ci + 2], u, w);
     const bool ins = act && dpg::inside(u, w, vw.W, vw.H);
@@ -580,6 +603,14 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
     const int nv = m - 1;
     const int cell = a.cell;
     const int N = cell * cell;
+    // view data of the first map round: the visible list is fixed during the
+    // refine, so these loads go out before the corner math and overlap it
+#ifndef DP_PRELOAD_VIEWS
+#define DP_PRELOAD_VIEWS 0
+#endif
+#if DP_PRELOAD_VIEWS
+    const MapView mv0 = load_map_view(a, L, 0, m, 0);
+#endif
     {
         double c12[12];
         const double Xs[3] = {L.X[0], L.X[1], L.X[2]};
@@ -610,7 +641,12 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
         // window maps of this chunk, 16 views per round (4 lanes per view)
         uint64_t okmask = 0;
         for (int r0 = 0; r0 < kMapChunk && base + r0 < m; r0 += 16)
-            okmask |= build_maps_quad(a, L, base, m, r0, cell);
+#if DP_PRELOAD_VIEWS
+            okmask |= build_maps_quad((base == 0 && r0 == 0) ? mv0 : load_map_view(a, L, base, m, r0), L, base, m,
+                                      r0, cell);
+#else
+            okmask |= build_maps_quad(load_map_view(a, L, base, m, r0), L, base, m, r0, cell);
+#endif
         wave_sync();
         STAMP(L, 0);
         // texture 0 = lowest-index visible view (optimization_opencv.cpp:24-28)
