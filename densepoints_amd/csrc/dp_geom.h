@@ -143,16 +143,18 @@ DP_HD bool quad_map(const double *x, const double *y, int tlx, int tly, int rw, 
     // the window rectangle their extremes are at its corners.  |X| = |Xn|*32/W
     // < 2^29 (a factor 2 below the 2^30 the kernel needs), tested without a
     // division.
-    bool safe = true;
     const double e = (double)(cell - 1);
+    const double m0e = tm.m0 * e, m1e = tm.m1 * e, m3e = tm.m3 * e, m4e = tm.m4 * e, m6e = tm.m6 * e,
+                 m7e = tm.m7 * e;
+    // corners (0,0), (e,0), (0,e), (e,e): W, Xn, Yn from shared products
+    const double W01 = m7e + tm.m8, X01 = m1e + tm.m2, Y01 = m4e + tm.m5;
+    const double Wc[4] = {tm.m8, tm.m8 + m6e, W01, W01 + m6e};
+    const double Xc[4] = {tm.m2, tm.m2 + m0e, X01, X01 + m0e};
+    const double Yc[4] = {tm.m5, tm.m5 + m3e, Y01, Y01 + m3e};
+    bool safe = true;
     for (int c = 0; c < 4; ++c) {
-        const double px = (c & 1) ? e : 0.0, py = (c & 2) ? e : 0.0;
-        const double W = (tm.m7 * py + tm.m8) + tm.m6 * px;
-        const double Xn = (tm.m1 * py + tm.m2) + tm.m0 * px;
-        const double Yn = (tm.m4 * py + tm.m5) + tm.m3 * px;
-        const double lim = 536870912.0 * W;
-        if (!(W > 1e-3) || !(W < 1e6) || !(fabs(Xn) * 32.0 < lim) || !(fabs(Yn) * 32.0 < lim))
-            safe = false;
+        const double lim = 536870912.0 * Wc[c];
+        safe = safe && (Wc[c] > 1e-3) && (Wc[c] < 1e6) && (fabs(Xc[c]) * 32.0 < lim) && (fabs(Yc[c]) * 32.0 < lim);
     }
     tm.safe = safe ? 1 : 0;
     tm.pad = 0;
