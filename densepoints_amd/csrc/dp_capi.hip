@@ -1153,6 +1153,14 @@ __global__ void probe_math_kernel(const double *x, int n, double *out)
     if (fabs(v) < 2147483647.0)
         ok = ok && dpk::rint_i32(v) == (int32_t)rint(v);
     ok = ok && __double_as_longlong(dpk::div_rn(na, nb)) == __double_as_longlong(na / nb);
+    ok = ok && __double_as_longlong(dpk::recip_safe(w * 0.03125)) == __double_as_longlong(q);
+    // sqrt_rn vs the library sqrt over several magnitudes of each input
+    {
+        const double ax = fabs(x[i]);
+        const double sv[4] = {ax, ax * 1.0e6 + 1.0, ax * 1.0e-6, ax * ax * 14641.0};
+        for (int k = 0; k < 4; ++k)
+            ok = ok && __double_as_longlong(dpk::sqrt_rn(sv[k])) == __double_as_longlong(sqrt(sv[k]));
+    }
     // a sweep of nearby denominators per input (stress the final rounding)
     for (int k = 1; k <= 16 && ok; ++k) {
         const double wk = w * (1.0 + k * 1.1102230246251565e-16 * (double)(i % 7 + 1));
@@ -1160,6 +1168,8 @@ __global__ void probe_math_kernel(const double *x, int n, double *out)
             ok = __double_as_longlong(dpk::div32_safe(wk)) == __double_as_longlong(32.0 / wk);
         const double bk = nb + k * 3.3e-5;
         ok = ok && __double_as_longlong(dpk::div_rn(na, bk)) == __double_as_longlong(na / bk);
+        const double sk = fabs(na) * (1.0 + k * 2.220446049250313e-16);
+        ok = ok && __double_as_longlong(dpk::sqrt_rn(sk)) == __double_as_longlong(sqrt(sk));
     }
     if (!ok)
         out[4 * i + 3] = -1.0;

@@ -80,4 +80,27 @@ __device__ __forceinline__ double recip_safe(double b)
     return __builtin_fma(rem, r, r);
 }
 
+// sqrt(a) without v_rsq_f64/v_sqrt_f64 (slow transcendentals): v_rsq_f32 seed,
+// two Goldschmidt steps (s ~ sqrt a, h ~ 1/(2 sqrt a)) and two exact-residual
+// corrections s += (a - s*s) * h, the refinement LLVM applies after its
+// v_rsq_f64 seed.  Guarded: '1e-290 < a < 1e290' else the library sqrt.  Same
+// exactness caveat as div_rn_core; checked bitwise on the GPU.
+__device__ __forceinline__ double sqrt_rn(double a)
+{
+    if (!(a > 1e-290 && a < 1e290))
+        return sqrt(a);
+    const double y = (double)__builtin_amdgcn_rsqf((float)a);
+    double s = a * y, h = 0.5 * y;
+    double r = __builtin_fma(-s, h, 0.5);
+    s = __builtin_fma(s, r, s);
+    h = __builtin_fma(h, r, h);
+    r = __builtin_fma(-s, h, 0.5);
+    s = __builtin_fma(s, r, s);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-s, s, a);
+    s = __builtin_fma(d, h, s);
+    d = __builtin_fma(-s, s, a);
+    return __builtin_fma(d, h, s);
+}
+
 } // namespace dpk

@@ -40,6 +40,31 @@ DP_HD void cross3(const double *a, const double *b, double *o)
     o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+// a / b and sqrt(a) of the per-evaluation uniform math (NCC finish, window
+// scale).  DP_FAST_DIV=1 routes them through the fp32-seeded dp_devmath.h
+// div_rn / sqrt_rn (no slow f64 transcendental); measured neutral within
+// noise, so the default keeps the library's IEEE sequences.
+#ifndef DP_FAST_DIV
+#define DP_FAST_DIV 0
+#endif
+DP_HD double dvdiv(double a, double b)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && DP_FAST_DIV
+    return dpk::div_rn(a, b);
+#else
+    return a / b;
+#endif
+}
+
+DP_HD double dvsqrt(double a)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && DP_FAST_DIV
+    return dpk::sqrt_rn(a);
+#else
+    return sqrt(a);
+#endif
+}
+
 // q0 = a0 / b, q1 = a1 / b, IEEE-correct on both sides (the device shares one
 // refined reciprocal: dp_devmath.h div_pair_rn)
 DP_HD void div2(double a0, double a1, double b, double &q0, double &q1)
@@ -76,10 +101,10 @@ DP_HD bool window_corners_sc(const ViewDev &rv, const double *Xs, const double *
     double y[3];
     cross3(nn, rv.xr, y);
     const double du = qu - cu, dv = qv - cv;
-    const double dx = sqrt(du * du + dv * dv);
+    const double dx = dvsqrt(du * du + dv * dv);
     if (dx == 0.0)
         return false;
-    const double scale = (double)(cell / 2) / dx;
+    const double scale = dvdiv((double)(cell / 2), dx);
     for (int i = 0; i < 3; ++i) {
         const double sx = scale * rv.xr[i];
         const double sy = scale * y[i];
@@ -261,12 +286,12 @@ DP_HD double ncc_finish(int32_t N, int32_t Sa, int32_t Saa, int32_t Sb, int32_t 
     const int64_t n = N;
     const double dn = (double)n;
     const double dn2 = (double)(n * n);
-    const double sa = sqrt((double)(n * (int64_t)Saa - (int64_t)Sa * Sa) / dn2);
-    const double sb = sqrt((double)(n * (int64_t)Sbb - (int64_t)Sb * Sb) / dn2);
+    const double sa = dvsqrt(dvdiv((double)(n * (int64_t)Saa - (int64_t)Sa * Sa), dn2));
+    const double sb = dvsqrt(dvdiv((double)(n * (int64_t)Sbb - (int64_t)Sb * Sb), dn2));
     double den = sa * sb;
     den = (denom_min < den) ? den : denom_min;
-    const double num = (double)(n * (int64_t)Sab - (int64_t)Sa * Sb) / dn;
-    return (num / den) / dn;
+    const double num = dvdiv((double)(n * (int64_t)Sab - (int64_t)Sa * Sb), dn);
+    return dvdiv(dvdiv(num, den), dn);
 }
 
 // (depth, roll, pitch) -> candidate normal / position (optimization.cpp:78-96)

@@ -700,7 +700,7 @@ __device__ __forceinline__ double wave_objective(const RefineArgs &a, WaveLds &L
     double sum = 0.0;
     for (int k = 0; k < nv; ++k)
         sum = sum + (1.0 - L.score[k]);
-    return sum / (double)nv;
+    return dpg::dvdiv(sum, (double)nv);
 }
 
 enum NmPhase { kInit = 0, kReflect = 1, kExpand = 2, kContract = 3, kShrink = 4 };
@@ -750,7 +750,7 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
             q2 = L.sp[vi][2];
         } else {
             const double fac = phase == kReflect ? -1.0 : (phase == kExpand ? 2.0 : 0.5);
-            const double alpha = (1.0 - fac) / 3.0;
+            const double alpha = dpg::dvdiv(1.0 - fac, 3.0);
             const double beta = alpha - fac;
             q0 = L.cs[0] * alpha - L.sp[ihi][0] * beta;
             q1 = L.cs[1] * alpha - L.sp[ihi][1] * beta;

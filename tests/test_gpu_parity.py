@@ -219,9 +219,11 @@ def test_expand_batch_bit_exact(engine, orc):
 
 
 def test_device_division_shortcuts_are_ieee_exact():
-    """div_rn / div32_safe (fp32-seeded Newton + LLVM's final correction) and
-    the magic-constant rint agree bit-for-bit with '/' and rint on 4M inputs
-    of varied magnitude (each input also sweeps 16 nearby denominators)."""
+    """div_rn / div32_safe / recip_safe (fp32-seeded Newton + the exact-residual
+    correction), sqrt_rn (rsq_f32 seed, Goldschmidt + two corrections) and the
+    magic-constant rint agree bit-for-bit with '/', sqrt and rint on 4M inputs
+    of varied magnitude (each input also sweeps 16 nearby denominators and
+    radicands)."""
     rng = np.random.default_rng(2024)
     x = np.concatenate([rng.uniform(-1, 1, 1_000_000), rng.uniform(-2e3, 2e3, 1_000_000),
                         np.exp(rng.uniform(-30, 30, 1_000_000)) * rng.choice([-1, 1], 1_000_000),
