@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline wall time")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-densify", action="store_true", help="skip the informational end-to-end densify")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes/launch from profiles/")
     return ap.parse_args()
 
@@ -176,6 +177,15 @@ def main():
             "bytes_per_launch_algorithmic": bytes_alg,
         },
     }
+    if rank == 0 and not args.no_densify:
+        # informational: the full PMVS::Run minus matching (dp_densify) on the same scene, untimed by the contract
+        t0 = time.perf_counter()
+        _, dst = eng.densify(seeds)
+        wall = time.perf_counter() - t0
+        result["densify_e2e"] = {"seeds": int(dst["seeds_in"]), "seed_patches": int(dst["seed_patches"]),
+                                 "patches": int(dst["patches"]), "candidates": int(dst["candidates"]),
+                                 "generations": int(dst["generations"]), "evals": int(dst["evals"]),
+                                 "refine_ms": round(dst["refine_ms"], 1), "wall_s": round(wall, 3)}
     st = np.zeros(8, dtype=np.uint64)
     if N.lib.dp_debug_stamps(N.ptr(st)) == 0:  # -DDP_STAMPS diagnostic builds only
         tot = float(st[7]) or 1.0
