@@ -152,6 +152,7 @@ SIGNATURES = [
     ("dp_probe_texture", _I, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, _I, _P]),
     ("dp_probe_ncc", _D, [ctypes.c_int32] * 6 + [_D]),
     ("dp_probe_math_device", _I, [_P, _I, _P]),
+    ("dp_probe_texel_device", _I, [_P, _P, _P, _I, _P]),
     ("dp_debug_stamps", _I, [_P]),
 ]
 

@@ -1176,6 +1176,28 @@ __global__ void probe_math_kernel(const double *x, int n, double *out)
 }
 } // namespace
 
+extern "C" int dp_probe_texel_device(const uint64_t *taps_a, const uint64_t *taps_b, const uint32_t *fxy, int n,
+                                     int32_t *gray)
+{
+    if (n <= 0 || !taps_a || !taps_b || !fxy || !gray)
+        return DP_E_ARG;
+    void *d = nullptr;
+    const size_t nb = (size_t)n;
+    if (hipMalloc(&d, nb * (8 + 8 + 4 + 4)) != hipSuccess)
+        return DP_E_HIP;
+    unsigned long long *da = (unsigned long long *)d, *db = da + nb;
+    uint32_t *df = (uint32_t *)(db + nb);
+    int32_t *dg = (int32_t *)(df + nb);
+    hipMemcpy(da, taps_a, nb * 8, hipMemcpyHostToDevice);
+    hipMemcpy(db, taps_b, nb * 8, hipMemcpyHostToDevice);
+    hipMemcpy(df, fxy, nb * 4, hipMemcpyHostToDevice);
+    hipError_t e = dpk::launch_probe_texel(da, db, df, n, dg);
+    if (e == hipSuccess)
+        e = hipMemcpy(gray, dg, nb * 4, hipMemcpyDeviceToHost);
+    hipFree(d);
+    return e == hipSuccess ? DP_OK : DP_E_HIP;
+}
+
 extern "C" int dp_probe_math_device(const double *x, int n, double *out)
 {
     if (n <= 0 || !x || !out)

@@ -46,6 +46,8 @@ struct ClaimArgs {
 
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s);
 int read_stamps(unsigned long long *out);
+hipError_t launch_probe_texel(const unsigned long long *ta, const unsigned long long *tb, const uint32_t *fxy, int n,
+                              int32_t *gray);
 hipError_t launch_claims(const ClaimArgs &a, hipStream_t s);
 hipError_t launch_resolve(const ClaimArgs &a, uint8_t *accepted, hipStream_t s);
 hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand, const uint8_t *accepted,

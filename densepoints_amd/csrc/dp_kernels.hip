@@ -20,6 +20,10 @@
 namespace dpk {
 namespace {
 
+#ifndef DP_TEX_PER_LANE
+#define DP_TEX_PER_LANE 4
+#endif
+
 #ifndef DP_MAP_CHUNK
 #define DP_MAP_CHUNK 20
 #endif
@@ -45,7 +49,7 @@ struct WaveLds {
     double ylo, ynhi, ysave;
     uint64_t vis[2], cand[2];                   // visible / candidate masks
     int32_t ref, m;                             // reference view, |visible|
-    uint16_t anchor[DP_MAX_CELL * DP_MAX_CELL]; // texture 0 (gray)
+    uint32_t anchor[DP_TEX_PER_LANE * 32];      // texture 0 grays, u16 pairs (anchor_slot)
     uint8_t vlist[DP_MAX_VIEWS];                // visible list (ascending)
 #ifdef DP_STAMPS
     unsigned long long stamp[8];                // diagnostic build only: cycles per phase
@@ -171,7 +175,7 @@ __device__ __forceinline__ void texel_coord(const WaveLds &L, int rb, int px, in
 // then BORDER_REPLICATE select, bilinear and BGR2GRAY.
 struct TexelLoad {
     unsigned long long a, b;
-    uint32_t f; // fx | fy << 5 (fx = 0 where the right tap replicates the left)
+    uint32_t fx, fy; // fractions (fx = 0 where the right tap replicates the left)
 };
 
 __device__ __forceinline__ int32_t med3_i32(int32_t v, int32_t lo, int32_t hi)
@@ -205,32 +209,56 @@ __device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm, 
     t.a = *(gpair_t)(roi + o0);
     t.b = *(gpair_t)(roi + o1);
 #endif
-    t.f = (same ? 0u : (uint32_t)(ix & 31)) | ((uint32_t)(iy & 31) << 5);
+    t.fx = same ? 0u : (uint32_t)(ix & 31);
+    t.fy = (uint32_t)(iy & 31);
     return t;
 }
 
-// dpg::blend_gray on the texel's two tap pairs, per channel as two u16 dot
-// products: row r contributes [c(r,x0), c(r,x1)] . [(32-fx)(32-fy_r), fx(32-fy_r)]
-// (same integers, same single rounding: (sum w'p + 512) >> 10)
-__device__ __forceinline__ int texel_gray(const TexelLoad &t)
+// v_pk_mad_u16 (a.lo * b.lo, a.hi * b.lo) saturated to u16 (clamp)
+__device__ __forceinline__ uint32_t pk_mul_u16_sat(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, %2, 0 op_sel_hi:[1,0,0] clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// v_mad_u32_u16 with op_sel: (a >> 16) * b + c for b < 2^16
+__device__ __forceinline__ uint32_t mad_hi16(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    return r;
+}
+
+// dpg::blend_gray on the texel's two tap pairs, computed 64x scaled so that
+// every rounding lands on a 16-bit boundary: per channel two u16 dot
+// products, row r contributing [c(r,x0), c(r,x1)] . 64*[(32-fx)(32-fy_r),
+// fx(32-fy_r)] + 2^15, whose high half is (sum w'p + 512) >> 10 -- the one
+// weight that overflows u16 (64*1024, fx = fy = 0) saturates to 65535, which
+// still yields p00 exactly; then BGR2GRAY with 4x coefficients (they sum to
+// 2^16) as three v_mad_u32_u16 on those high halves.  Returns the gray value
+// in bits 16..23 (bits 24..31 zero).
+__device__ __forceinline__ uint32_t texel_gray_hi(const TexelLoad &t)
 {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const uint32_t fx = t.f & 31u, fy = t.f >> 5;
     const uint32_t a0 = (uint32_t)t.a, b0 = (uint32_t)t.b;
     const uint32_t a1 = (uint32_t)(t.a >> 32), b1 = (uint32_t)(t.b >> 32);
-    const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
-    const us2 w0 = __builtin_bit_cast(us2, wx * (32u - fy));
-    const us2 w1 = __builtin_bit_cast(us2, wx * fy);
+    const uint32_t wx = 32u + t.fx * 65535u; // (32 - fx) | fx << 16
+    const uint32_t fy64 = t.fy << 6;
+    const us2 w0 = __builtin_bit_cast(us2, pk_mul_u16_sat(wx, 2048u - fy64));
+    const us2 w1 = __builtin_bit_cast(us2, wx * fy64);
     uint32_t ch[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const uint32_t sel = 0x0c000c00u | (uint32_t)k | ((uint32_t)(4 + k) << 16);
         const us2 p0 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(a1, a0, sel));
         const us2 p1 = __builtin_bit_cast(us2, __builtin_amdgcn_perm(b1, b0, sel));
-        ch[k] = __builtin_amdgcn_udot2(p0, w0, __builtin_amdgcn_udot2(p1, w1, 512u, false), false) >> 10;
+        ch[k] = __builtin_amdgcn_udot2(p0, w0, __builtin_amdgcn_udot2(p1, w1, 32768u, false), false);
     }
-    return (int)((ch[0] * 1868u + ch[1] * 9617u + ch[2] * 4899u + 8192u) >> 14);
+    return mad_hi16(ch[0], 7472u, mad_hi16(ch[1], 38468u, mad_hi16(ch[2], 19596u, 32768u)));
 }
+
+__device__ __forceinline__ int texel_gray(const TexelLoad &t) { return (int)(texel_gray_hi(t) >> 16); }
 
 // row r and column r terms of map `tm` into the table rows from rb (one lane
 // per r: all nine coefficients are read before anything is written)
@@ -275,9 +303,6 @@ __device__ __forceinline__ int group_total(int v)
     return v;
 }
 
-#ifndef DP_TEX_PER_LANE
-#define DP_TEX_PER_LANE 4
-#endif
 // texels per lane per view pass: a pass of G views needs N <= 64 * K / G
 constexpr int kTexPerLane = DP_TEX_PER_LANE;
 
@@ -292,42 +317,67 @@ __host__ __device__ constexpr int pass_width(int cell)
                                              : 0;
 }
 
-// Per-lane texel descriptors of a pass (fixed per launch: depend on the lane,
-// G and the cell only), computed once per wave so the texel loop does no
-// index arithmetic: bits 0-10 byte offset of the texel's row in L.rowt,
-// 11-21 of its column in L.colt, 22-29 texel index t, 30 live (t < N).
+static_assert(kTexPerLane % 2 == 0, "texels are packed in u16 pairs");
+
+typedef __attribute__((address_space(3))) const double *lds_f64_t;
+typedef __attribute__((address_space(3))) uint32_t *lds_u32_t;
+typedef __attribute__((address_space(3))) uint16_t *lds_u16_t;
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p)
+{
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char *)p;
+}
+
+// Per-lane texel descriptors of a pass (fixed per launch: depend on the wave's
+// LDS block, the lane, G and the cell only), computed once per wave so the
+// texel loop does no index arithmetic: LDS byte addresses of each texel's row
+// terms (L.rowt) and column terms (L.colt), and per texel pair the v_perm
+// selector that packs the two grays into u16 halves -- a dead texel (t >= N,
+// which re-loads texel N-1's address) gets a zero half, so it drops out of
+// every moment without a mask.
 struct TexDesc {
-    uint32_t d[kTexPerLane];
+    uint32_t ra[kTexPerLane], ca[kTexPerLane];
+    uint32_t sel[kTexPerLane / 2];
 };
 
 template <int G>
-__device__ __forceinline__ TexDesc make_texdesc(int cell)
+__device__ __forceinline__ TexDesc make_texdesc(const WaveLds &L, int cell)
 {
     constexpr int LP = kWave / G;
     const int lane = lane_id();
     const int j = lane / LP, g = lane & (LP - 1);
     const int N = cell * cell;
+    const uint32_t rb = lds_addr(&L.rowt[0][0]), cb = lds_addr(&L.colt[0][0]);
     TexDesc td;
 #pragma unroll
     for (int i = 0; i < kTexPerLane; ++i) {
         const int tl = g + LP * i;
         const int t = tl < N ? tl : N - 1; // dead texels re-load a live address
         const int py = t / cell, px = t - py * cell;
-        const uint32_t ro = (uint32_t)(j * (64 / G) + py) * (uint32_t)sizeof(double[3]);
-        const uint32_t co = (uint32_t)(j * (64 / G) + px) * (uint32_t)sizeof(double[3]);
-        td.d[i] = ro | (co << 11) | ((uint32_t)t << 22) | ((tl < N ? 1u : 0u) << 30);
+        td.ra[i] = rb + (uint32_t)(j * (64 / G) + py) * (uint32_t)sizeof(double[3]);
+        td.ca[i] = cb + (uint32_t)(j * (64 / G) + px) * (uint32_t)sizeof(double[3]);
+        // opaque: keeps the whole address in one VGPR (no per-texel base add)
+        asm volatile("" : "+v"(td.ra[i]), "+v"(td.ca[i]));
+    }
+#pragma unroll
+    for (int p = 0; p < kTexPerLane / 2; ++p) {
+        // gray of texel 2p (bits 16-23 of its sum) -> bits 0-7, of texel 2p+1 -> bits 16-23
+        const bool l0 = g + LP * (2 * p) < N, l1 = g + LP * (2 * p + 1) < N;
+        td.sel[p] = 0x0c000c00u | (l0 ? 0x02u : 0x0cu) | ((l1 ? 0x06u : 0x0cu) << 16);
     }
     return td;
 }
 
-__device__ __forceinline__ int td_t(uint32_t d) { return (int)((d >> 22) & 255u); }
-__device__ __forceinline__ bool td_live(uint32_t d) { return (d >> 30) & 1u; }
+// LDS slot of texel pair p of lane g (LP lanes per view): texture 0's grays
+// are stored as u16 pairs in lane-major order, one ds_read_b32 per pair
+template <int LP>
+__device__ __forceinline__ int anchor_slot(int p, int g) { return p * LP + g; }
 
-// texel_coord<true> addressed by a descriptor
-__device__ __forceinline__ void texel_coord_d(const WaveLds &L, uint32_t d, int32_t &ix, int32_t &iy)
+// texel_coord<true> addressed by the descriptor's LDS addresses
+__device__ __forceinline__ void texel_coord_d(uint32_t ra, uint32_t ca, int32_t &ix, int32_t &iy)
 {
-    const double *R = (const double *)((const char *)&L.rowt[0][0] + (d & 2047u));
-    const double *C = (const double *)((const char *)&L.colt[0][0] + ((d >> 11) & 2047u));
+    const lds_f64_t R = (lds_f64_t)(uintptr_t)ra;
+    const lds_f64_t C = (lds_f64_t)(uintptr_t)ca;
     const double W = recip_safe(R[2] + C[2]); // tables hold W/32: 1/W' = 32/W
     ix = rint_i32((R[0] + C[0]) * W);
     iy = rint_i32((R[1] + C[1]) * W);
@@ -337,51 +387,52 @@ __device__ __forceinline__ void texel_coord_d(const WaveLds &L, uint32_t d, int3
 // t = g, g+LP, ... (at most kTexPerLane).  Safe windows (the common case):
 // all gathers of a lane are issued before any is consumed -- one memory round
 // trip per pass.  kAnchor: slot 0 is texture 0, whose gray values go to LDS
-// before the other slots form their cross moments.
+// before the other slots form their cross moments.  Lanes of an inactive slot
+// (odd view count) sample a valid view too; their group totals are dropped.
 template <int G, bool kAnchor>
-__device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &L, const TexDesc &td, int j, bool act,
+__device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &L, const TexDesc &td, int j,
                                                   gpix_t roi, int pitch, int wm, int hm, int &s, int &ss, int &sx)
 {
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
     TexelLoad tl[kTexPerLane];
 #pragma unroll
     for (int i = 0; i < kTexPerLane; ++i) {
         int32_t ix, iy;
-        texel_coord_d(L, td.d[i], ix, iy);
+        texel_coord_d(td.ra[i], td.ca[i], ix, iy);
         tl[i] = texel_fetch(roi, pitch, wm, hm, ix, iy);
         // one texel's fp64 coordinate math at a time: only the issued loads
         // stay live across the pass
         __builtin_amdgcn_sched_barrier(0);
     }
-    // one consume phase for all lanes (no divergence): in the anchor pass the
-    // texture-0 gray of texel t comes from lane (0, g) of the same texel
-    // through the LDS crossbar (ds_bpermute), and slot 0 stores it for the
-    // later passes.
+    // one consume phase for all lanes (no divergence): grays packed in u16
+    // pairs, moments as u16 dot products.  In the anchor pass the texture-0
+    // pair of lane (0, g) reaches the other slots through the LDS crossbar
+    // (ds_bpermute), and slot 0 stores it for the later passes.
     constexpr int LP = kWave / G;
-    const int src = (lane_id() & (LP - 1)) << 2;
+    const int g = lane_id() & (LP - 1);
+    const us2 ones = {1, 1};
+    uint32_t us = (uint32_t)s, uss = (uint32_t)ss, usx = (uint32_t)sx;
 #pragma unroll
-    for (int i = 0; i < kTexPerLane; ++i) {
-        const uint32_t d = td.d[i];
-        const int t = td_t(d);
-        int gv = texel_gray(tl[i]);
-#if defined(DP_DIAG_PAD_I32)
-        // diagnostic build: DP_DIAG_PAD_I32 extra int VALU per texel (timing only)
-#pragma unroll
-        for (int k = 0; k < DP_DIAG_PAD_I32; ++k)
-            asm volatile("v_add_u32 %0, %0, 0" : "+v"(gv));
-#endif
-        int av;
+    for (int p = 0; p < kTexPerLane / 2; ++p) {
+        const uint32_t r0 = texel_gray_hi(tl[2 * p]);
+        const uint32_t r1 = texel_gray_hi(tl[2 * p + 1]);
+        const uint32_t gg = __builtin_amdgcn_perm(r1, r0, td.sel[p]);
+        uint32_t aa;
         if (kAnchor) {
-            av = (G == 1) ? gv : __builtin_amdgcn_ds_bpermute(src, gv);
-            if (j == 0 && td_live(d))
-                L.anchor[t] = (uint16_t)gv;
+            aa = (G == 1) ? gg : (uint32_t)__builtin_amdgcn_ds_bpermute(g << 2, (int)gg);
+            if (j == 0)
+                L.anchor[anchor_slot<LP>(p, g)] = gg;
         } else {
-            av = (int)L.anchor[t];
+            aa = L.anchor[anchor_slot<LP>(p, g)];
         }
-        const int g = (act && td_live(d)) ? gv : 0;
-        s += g;
-        ss += g * g;
-        sx += av * g;
+        const us2 vg = __builtin_bit_cast(us2, gg);
+        us = __builtin_amdgcn_udot2(vg, ones, us, false);
+        uss = __builtin_amdgcn_udot2(vg, vg, uss, false);
+        usx = __builtin_amdgcn_udot2(vg, __builtin_bit_cast(us2, aa), usx, false);
     }
+    s = (int)us;
+    ss = (int)uss;
+    sx = (int)usx;
 }
 
 struct Moments {
@@ -405,7 +456,7 @@ __device__ __attribute__((noinline)) Moments group_sample_clamped(WaveLds &L, in
     for (int phase = 0; phase < (kAnchor ? 2 : 1); ++phase) {
         const bool mine = kAnchor ? ((j == 0) == (phase == 0)) && act : act;
         if (mine) {
-            for (int t = g; t < N; t += LP) {
+            for (int i = 0, t = g; t < N; ++i, t += LP) {
                 const int py = (int)(((float)t + 0.5f) * inv_cell);
                 const int px = t - py * cell;
                 int32_t ix, iy;
@@ -413,10 +464,12 @@ __device__ __attribute__((noinline)) Moments group_sample_clamped(WaveLds &L, in
                 const int gv = texel_gray(texel_fetch(roi, pitch, wm, hm, ix, iy));
                 m.s += gv;
                 m.ss += gv * gv;
+                // u16 half (i & 1) of anchor pair word anchor_slot(i / 2, g)
+                uint16_t *ah = (uint16_t *)&L.anchor[anchor_slot<LP>(i >> 1, g)] + (i & 1);
                 if (kAnchor && j == 0)
-                    L.anchor[t] = (uint16_t)gv;
+                    *ah = (uint16_t)gv;
                 else
-                    m.sx += (int)L.anchor[t] * gv;
+                    m.sx += (int)*ah * gv;
             }
         }
         if (kAnchor)
@@ -451,7 +504,7 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
     wave_sync();
     int s = 0, ss = 0, sx = 0;
     if (all_safe)
-        group_sample_safe<G, kAnchor>(a, L, td, j, act, roi, pitch, wm, hm, s, ss, sx);
+        group_sample_safe<G, kAnchor>(a, L, td, j, roi, pitch, wm, hm, s, ss, sx);
     else {
         const Moments mm = group_sample_clamped<G, kAnchor>(L, a.cell, j, act, roi, pitch, wm, hm);
         s = mm.s;
@@ -1010,7 +1063,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
     for (int c = 0; c < 8; ++c)
         L.stamp[c] = 0;
 #endif
-    const TexDesc td = make_texdesc<G>(a.cell);
+    const TexDesc td = make_texdesc<G>(L, a.cell);
     // XCD-local work ranges: the batch is cut into kXcds contiguous ranges and
     // the waves of XCD x dequeue from range x first (consecutive candidates are
     // spatial neighbours, so their windows share the XCD's L2 across the
@@ -1262,7 +1315,30 @@ __global__ void append_kernel(const dpg::ViewDev *views, int V, const dp_patch *
     r->rgb[2] = c2;
 }
 
+// probe: the texel loop's bilinear + BGR2GRAY on explicit taps (fxy = fx |
+// fy << 5, fx already 0 where the right tap replicates)
+__global__ void probe_texel_kernel(const unsigned long long *ta, const unsigned long long *tb, const uint32_t *fxy,
+                                   int n, int32_t *gray)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    TexelLoad t;
+    t.a = ta[i];
+    t.b = tb[i];
+    t.fx = fxy[i] & 31u;
+    t.fy = (fxy[i] >> 5) & 31u;
+    gray[i] = texel_gray(t);
+}
+
 } // namespace
+
+hipError_t launch_probe_texel(const unsigned long long *ta, const unsigned long long *tb, const uint32_t *fxy, int n,
+                              int32_t *gray)
+{
+    hipLaunchKernelGGL(probe_texel_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, ta, tb, fxy, n, gray);
+    return hipGetLastError();
+}
 
 int read_stamps(unsigned long long *out)
 {

@@ -25,6 +25,10 @@ double dp_probe_ncc(int32_t N, int32_t Sa, int32_t Saa, int32_t Sb, int32_t Sbb,
                     double denom_min);
 /* device run of sincos/acos/sqrt over n inputs (out: 4*n doubles s,c,acos(x),sqrt|x|) */
 int dp_probe_math_device(const double *x, int n, double *out);
+/* device run of the texel loop's bilinear + BGR2GRAY on n explicit texels:
+ * taps_a/taps_b = BGRA8 pixel pairs (x0, x0+1) of rows y0 / y1, fxy = fx | fy << 5 */
+int dp_probe_texel_device(const uint64_t *taps_a, const uint64_t *taps_b, const uint32_t *fxy, int n,
+                          int32_t *gray);
 /* diagnostic builds (-DDP_STAMPS) only: per-phase s_memtime cycle sums of the
  * refine kernel since the last call (0 maps, 1 texture 0, 2 other views,
  * 3 NCC finish, 6 patches, 7 whole patch); DP_E_STATE otherwise */

@@ -71,6 +71,42 @@ def test_device_math_bitwise_equals_host():
     assert np.array_equal(out[:, 3], np.sqrt(np.abs(x)))  # IEEE-correct sqrt on gfx950
 
 
+def _blend_gray_spec(a, b, fx, fy):
+    """warpPerspective INTER_LINEAR on CV_8UC3 (15-bit table == (sum w'p + 512) >> 10)
+    then BGR2GRAY (1868, 9617, 4899) >> 14 -- DESIGN.md arithmetic spec."""
+    c32 = np.uint64(32)
+    wx0, wx1 = c32 - fx, fx
+    wy0, wy1 = c32 - fy, fy
+    ch = []
+    for k in range(3):
+        lo, hi, m = np.uint64(8 * k), np.uint64(32 + 8 * k), np.uint64(255)
+        p00, p01 = (a >> lo) & m, (a >> hi) & m
+        p10, p11 = (b >> lo) & m, (b >> hi) & m
+        ch.append((wy0 * (wx0 * p00 + wx1 * p01) + wy1 * (wx0 * p10 + wx1 * p11) + np.uint64(512)) >> np.uint64(10))
+    return (ch[0] * np.uint64(1868) + ch[1] * np.uint64(9617) + ch[2] * np.uint64(4899) + np.uint64(8192)) >> np.uint64(14)
+
+
+def test_texel_blend_exhaustive_fractions():
+    """The texel loop's 64x-scaled u16 dot-product blend (incl. the saturated
+    fx = fy = 0 weight) equals the spec on every (fx, fy) with random and
+    extreme pixels."""
+    rng = np.random.default_rng(7)
+    fx, fy = np.meshgrid(np.arange(32, dtype=np.uint64), np.arange(32, dtype=np.uint64))
+    fx, fy = np.tile(fx.ravel(), 300), np.tile(fy.ravel(), 300)
+    n = fx.size
+    a = rng.integers(0, 2**63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    b = rng.integers(0, 2**63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    a[:1024], b[:1024] = np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64(0xFFFFFFFFFFFFFFFF)
+    a[1024:2048], b[1024:2048] = np.uint64(0), np.uint64(0)
+    a[2048:3072], b[2048:3072] = np.uint64(0x00FFFFFF00000000), np.uint64(0x00000000FFFFFFFF)
+    fxy = (fx | (fy << np.uint64(5))).astype(np.uint32)
+    gray = np.zeros(n, np.int32)
+    N.check(N.lib.dp_probe_texel_device(N.ptr(a), N.ptr(b), N.ptr(fxy), n, N.ptr(gray)))
+    want = _blend_gray_spec(a, b, fx, fy).astype(np.int64)
+    bad = np.flatnonzero(gray != want)
+    assert bad.size == 0, f"{bad.size} texels differ, first {bad[:5]}"
+
+
 def test_seed_conversion_equals_oracle(engine, orc):
     sc = scene("hf6")
     engine.set_views(sc.views)
