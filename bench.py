@@ -68,7 +68,8 @@ def main():
     stream = torch.cuda.Stream()  # a real (non-NULL) stream shared by torch and the library
     torch.cuda.set_stream(stream)
     # render every view straight into HBM as BGRA8 planes (replicated per GPU)
-    planes = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(V)]
+    # one pool (V x H x W): every plane within 4 GiB of the first -> narrow 32-bit tap offsets
+    planes = torch.empty((V, H, W), dtype=torch.int32, device="cuda")
     for v in range(V):
         N.check(N.lib.dp_synth_render_device(eng.handle, __import__("ctypes").byref(cfg), N.ptr(P), v,
                                              planes[v].data_ptr(), stream.cuda_stream), eng.handle)

@@ -86,6 +86,8 @@ struct dp_ctx {
     std::vector<dpg::ViewDev> hv;
     dpg::ViewDev *d_views = nullptr;
     std::vector<uint32_t *> own_img;
+    const char *img_base = nullptr; // lowest view plane address
+    bool narrow = false;            // all planes within 4 GiB of img_base (32-bit tap offsets)
     uint32_t *d_work = nullptr;
     unsigned long long *d_evals = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -352,6 +354,23 @@ static int upload_view_table(dp_ctx *c)
         off += (int64_t)v.gw * v.gh;
     }
     c->grid_cells = off;
+    // narrow addressing when every plane ends within 4 GiB of the lowest one
+    // and the 24-bit row multiply holds (pitch * 4 < 2^24, H < 2^24)
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    bool fits = true;
+    for (auto &v : c->hv) {
+        const uintptr_t b = (uintptr_t)v.img;
+        lo = b < lo ? b : lo;
+        const uintptr_t e = b + (uintptr_t)v.pitch * (uintptr_t)v.H * 4u;
+        hi = e > hi ? e : hi;
+        fits = fits && (int64_t)v.pitch * 4 < (1 << 24) && v.H < (1 << 24);
+    }
+    // DP_WIDE_ADDRESSING=1 forces 64-bit tap addresses (tests cover both paths)
+    const char *wide = getenv("DP_WIDE_ADDRESSING");
+    c->narrow = fits && hi - lo <= 0xFFFFFFF0ull && !(wide && wide[0] == '1');
+    c->img_base = (const char *)lo;
+    for (auto &v : c->hv)
+        v.img_off = c->narrow ? (uint32_t)((uintptr_t)v.img - lo) : 0u;
     DP_HIP(c, hipMalloc(&c->d_views, sizeof(dpg::ViewDev) * c->V));
     DP_HIP(c, hipMemcpy(c->d_views, c->hv.data(), sizeof(dpg::ViewDev) * c->V, hipMemcpyHostToDevice));
     return DP_OK;
@@ -365,11 +384,21 @@ extern "C" int dp_set_views(dp_ctx *c, int V, const double *P, const dp_image *i
     DP_HIP(c, hipStreamSynchronize(c->stream));
     free_views(c);
     c->hv.resize(V);
-    std::vector<uint32_t> tmp;
+    // one pool for all planes (narrow addressing whenever it is < 4 GiB)
+    size_t total = 0;
     for (int v = 0; v < V; ++v) {
         const dp_image &im = images[v];
         if (im.width <= 0 || im.height <= 0 || !im.bgr)
             return fail(c, DP_E_ARG, "dp_set_views: empty image");
+        total += (size_t)im.width * (size_t)im.height;
+    }
+    uint32_t *pool = nullptr;
+    DP_HIP(c, hipMalloc(&pool, total * sizeof(uint32_t)));
+    c->own_img.push_back(pool);
+    std::vector<uint32_t> tmp;
+    size_t at = 0;
+    for (int v = 0; v < V; ++v) {
+        const dp_image &im = images[v];
         if (view_from_P(P + 12 * v, im.width, im.height, c->opt.grid_scale, c->hv[v]) != DP_OK)
             return fail(c, DP_E_ARG, "dp_set_views: singular projection matrix");
         const size_t stride = im.stride ? (size_t)im.stride : (size_t)im.width * 3;
@@ -381,9 +410,8 @@ extern "C" int dp_set_views(dp_ctx *c, int V, const double *P, const dp_image *i
                 o[x] = (uint32_t)row[3 * x] | ((uint32_t)row[3 * x + 1] << 8) |
                        ((uint32_t)row[3 * x + 2] << 16) | 0xFF000000u;
         });
-        uint32_t *d = nullptr;
-        DP_HIP(c, hipMalloc(&d, tmp.size() * sizeof(uint32_t)));
-        c->own_img.push_back(d);
+        uint32_t *d = pool + at;
+        at += tmp.size();
         DP_HIP(c, hipMemcpy(d, tmp.data(), tmp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         c->hv[v].img = d;
     }
@@ -485,6 +513,8 @@ static dpk::RefineArgs refine_args(dp_ctx *c, dp_patch *d, int n, int cell, int 
     a.evals = c->d_evals;
     a.parents = nullptr;
     a.max_pops = c->opt.max_pops;
+    a.img_base = c->img_base;
+    a.narrow = c->narrow ? 1 : 0;
     return a;
 }
 

@@ -26,7 +26,7 @@ struct ViewDev {
     int32_t W, H;       // loaded image size (IsPointInside bounds)
     int32_t pitch;      // pixels per row in the BGRA8 plane
     int32_t gw, gh;     // organizer grid (W/grid_scale, H/grid_scale)
-    int32_t grid_off_hi;
+    uint32_t img_off;   // byte offset of the plane from the context's image base (narrow mode)
     int64_t grid_off;   // offset of this view's cells in the grid pool
     const uint32_t *img; // BGRA8, B in the low byte
 };

@@ -31,6 +31,10 @@ struct RefineArgs {
     const dp_patch *parents; // queue; child c expands parents[parent0 + c/4] direction c%4
     int64_t parent0;
     int64_t max_pops;
+    // narrow addressing: every view plane lies within 4 GiB above img_base, so
+    // a window tap is img_base (SGPR) + a 32-bit byte offset (ViewDev::img_off)
+    const char *img_base;
+    int32_t narrow;
 };
 
 // organizer / BFS kernels

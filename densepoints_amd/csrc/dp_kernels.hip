@@ -214,6 +214,30 @@ __device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm, 
     return t;
 }
 
+typedef const __attribute__((address_space(1))) char *gbyte_t;
+
+// texel_fetch with narrow addressing: the taps are base (uniform, SGPR) + a
+// 32-bit byte offset, so each gather is one v_mad_u32_u24 from the shared
+// column offset (global_load saddr form, no 64-bit address arithmetic)
+__device__ __forceinline__ TexelLoad texel_fetch_n(gbyte_t base, uint32_t roi, int pitch4, int wm, int hm, int32_t ix,
+                                                   int32_t iy)
+{
+    const int32_t sx = ix >> 5, sy = iy >> 5;
+    const int32_t x0 = med3_i32(sx, 0, wm);
+    const int32_t y0 = med3_i32(sy, 0, hm);
+    const int32_t y1 = med3_i32(sy + 1, 0, hm);
+    TexelLoad t;
+    const bool same = (uint32_t)sx >= (uint32_t)wm; // as texel_fetch
+    const uint32_t xo = ((uint32_t)x0 << 2) + roi;
+    const uint32_t o0 = __umul24((uint32_t)y0, (uint32_t)pitch4) + xo;
+    const uint32_t o1 = __umul24((uint32_t)y1, (uint32_t)pitch4) + xo;
+    t.a = *(gpair_t)(base + o0);
+    t.b = *(gpair_t)(base + o1);
+    t.fx = same ? 0u : (uint32_t)(ix & 31);
+    t.fy = (uint32_t)(iy & 31);
+    return t;
+}
+
 // v_pk_mad_u16 (a.lo * b.lo, a.hi * b.lo) saturated to u16 (clamp)
 __device__ __forceinline__ uint32_t pk_mul_u16_sat(uint32_t a, uint32_t b)
 {
@@ -389,9 +413,9 @@ __device__ __forceinline__ void texel_coord_d(uint32_t ra, uint32_t ca, int32_t 
 // trip per pass.  kAnchor: slot 0 is texture 0, whose gray values go to LDS
 // before the other slots form their cross moments.  Lanes of an inactive slot
 // (odd view count) sample a valid view too; their group totals are dropped.
-template <int G, bool kAnchor>
+template <int G, bool kAnchor, bool kNarrow>
 __device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &L, const TexDesc &td, int j,
-                                                  gpix_t roi, int pitch, int wm, int hm, int &s, int &ss, int &sx)
+                                                  uint64_t roi, int pitch, int wm, int hm, int &s, int &ss, int &sx)
 {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
     TexelLoad tl[kTexPerLane];
@@ -399,7 +423,10 @@ __device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &
     for (int i = 0; i < kTexPerLane; ++i) {
         int32_t ix, iy;
         texel_coord_d(td.ra[i], td.ca[i], ix, iy);
-        tl[i] = texel_fetch(roi, pitch, wm, hm, ix, iy);
+        if (kNarrow)
+            tl[i] = texel_fetch_n((gbyte_t)a.img_base, (uint32_t)roi, pitch * 4, wm, hm, ix, iy);
+        else
+            tl[i] = texel_fetch((gpix_t)roi, pitch, wm, hm, ix, iy);
         // one texel's fp64 coordinate math at a time: only the issued loads
         // stay live across the pass
         __builtin_amdgcn_sched_barrier(0);
@@ -500,13 +527,17 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
     const int wm = L.map[sl].w - 1, hm = L.map[sl].h - 1;
     const bool all_safe = __ballot(act && !L.map[sl].safe) == 0ull;
     const int pitch = L.pitch[sl];
-    const gpix_t roi = (gpix_t)L.roi[sl];
+    const uint64_t roi = L.roi[sl]; // narrow: byte offset from a.img_base
     wave_sync();
     int s = 0, ss = 0, sx = 0;
-    if (all_safe)
-        group_sample_safe<G, kAnchor>(a, L, td, j, roi, pitch, wm, hm, s, ss, sx);
-    else {
-        const Moments mm = group_sample_clamped<G, kAnchor>(L, a.cell, j, act, roi, pitch, wm, hm);
+    if (all_safe) {
+        if (a.narrow)
+            group_sample_safe<G, kAnchor, true>(a, L, td, j, roi, pitch, wm, hm, s, ss, sx);
+        else
+            group_sample_safe<G, kAnchor, false>(a, L, td, j, roi, pitch, wm, hm, s, ss, sx);
+    } else {
+        const gpix_t roip = a.narrow ? (gpix_t)(a.img_base + (uint32_t)roi) : (gpix_t)roi;
+        const Moments mm = group_sample_clamped<G, kAnchor>(L, a.cell, j, act, roip, pitch, wm, hm);
         s = mm.s;
         ss = mm.ss;
         sx = mm.sx;
@@ -573,6 +604,7 @@ __device__ __forceinline__ float quad_bcast(float v)
 struct MapView {
     double P[12];
     int32_t W, H, pitch;
+    uint32_t img_off;
     const uint32_t *img;
 };
 
@@ -589,12 +621,13 @@ __device__ __forceinline__ MapView load_map_view(const RefineArgs &a, const Wave
     v.W = vw.W;
     v.H = vw.H;
     v.pitch = vw.pitch;
+    v.img_off = vw.img_off;
     v.img = vw.img;
     return v;
 }
 
 __device__ __forceinline__ uint64_t build_maps_quad(const MapView &vw, WaveLds &L, int base, int m, int round0,
-                                                    int cell)
+                                                    int cell, bool narrow)
 {
     const int lane = lane_id();
     const int k = lane >> 2, ci = lane & 3;
@@ -630,7 +663,9 @@ __device__ __forceinline__ uint64_t build_maps_quad(const MapView &vw, WaveLds &
         ok = dpg::quad_map(x, y, tlx, tly, rw, rh, cell, tm);
         if (ok) {
             L.map[slot] = tm;
-            L.roi[slot] = (uint64_t)(uintptr_t)(vw.img + ((size_t)tm.tly * (size_t)vw.pitch + (size_t)tm.tlx));
+            // narrow: byte offset of the ROI origin from img_base (< 4 GiB, host-checked)
+            L.roi[slot] = narrow ? (uint64_t)(vw.img_off + ((uint32_t)tm.tly * (uint32_t)vw.pitch + (uint32_t)tm.tlx) * 4u)
+                                 : (uint64_t)(uintptr_t)(vw.img + ((size_t)tm.tly * (size_t)vw.pitch + (size_t)tm.tlx));
             L.pitch[slot] = vw.pitch;
         }
     }
@@ -696,9 +731,9 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
         for (int r0 = 0; r0 < kMapChunk && base + r0 < m; r0 += 16)
 #if DP_PRELOAD_VIEWS
             okmask |= build_maps_quad((base == 0 && r0 == 0) ? mv0 : load_map_view(a, L, base, m, r0), L, base, m,
-                                      r0, cell);
+                                      r0, cell, a.narrow != 0);
 #else
-            okmask |= build_maps_quad(load_map_view(a, L, base, m, r0), L, base, m, r0, cell);
+            okmask |= build_maps_quad(load_map_view(a, L, base, m, r0), L, base, m, r0, cell, a.narrow != 0);
 #endif
         wave_sync();
         STAMP(L, 0);

@@ -132,6 +132,24 @@ def test_refine_modes_bit_exact(engine, orc, mode, cell):
         assert gp["evals"].mean() > 5  # the optimiser really ran
 
 
+@pytest.mark.parametrize("cell", [16, 11])
+def test_wide_addressing_bit_exact(orc, monkeypatch, cell):
+    """64-bit tap addresses (used when the view planes span more than 4 GiB)
+    give the same bits as the default narrow 32-bit offsets."""
+    monkeypatch.setenv("DP_WIDE_ADDRESSING", "1")
+    sc = scene("hf6")
+    S = orc.Scene(sc.P, sc.imgs)
+    seeds = sc.seeds[:120]
+    op = S.seeds_to_patches(seeds)
+    oa = S.refine(op, cell, N.MODE_SEED)
+    with dp.Engine(device=0) as eng:
+        eng.set_views(sc.views)
+        gp = eng.seeds_to_patches(seeds)
+        ga = eng.refine(gp, cell, N.MODE_SEED)
+    assert np.array_equal(ga, oa)
+    assert_same(gp, op)
+
+
 def test_refine_perturbed_children_bit_exact(engine, orc):
     """Expansion children of refined seeds (the hot loop's real inputs)."""
     sc = scene("hf6")
