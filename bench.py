@@ -75,6 +75,15 @@ def main():
                                              planes[v].data_ptr(), stream.cuda_stream), eng.handle)
     torch.cuda.synchronize()
     eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
+    # image ingest: the config's pyramid (device cv::pyrDown, untimed setup); the
+    # parity patch loop samples level 0 like the reference
+    levels = synth.PYRAMID_LEVELS.get(args.config, 1)
+    torch.cuda.synchronize()
+    tp = time.perf_counter()
+    eng.build_pyramid(levels)
+    pyr_s = time.perf_counter() - tp
+    dims = [eng.level_info(l, 0)[:2] for l in range(levels)]
+    pyr_bytes = sum(4.0 * V * (dims[l][0] * dims[l][1] + dims[l + 1][0] * dims[l + 1][1]) for l in range(levels - 1))
 
     seeds = synth.seeds(cfg, P)
     # seed stage once (untimed): FilterPatches + OptimizePatches at n = 16
@@ -161,6 +170,8 @@ def main():
             "batch_per_gpu": B,
             "parallelism": f"dp{world} (candidate shards, no data-path collective)",
         },
+        "pyramid": {"levels": levels, "dims": dims, "build_ms_wall": round(pyr_s * 1e3, 3),
+                    "bytes_algorithmic": pyr_bytes, "GBps_wall": round(pyr_bytes / max(pyr_s, 1e-9) / 1e9, 1)},
         "E_mean_evals_per_patch": round(float(evals.mean()), 3),
         "mean_visible_views": round(float(nvis.mean()), 3),
         "accept_rate": round(float(acc.mean()), 4),

@@ -129,6 +129,10 @@ SIGNATURES = [
     ("dp_set_options", _I, [_P, _P]),
     ("dp_set_views", _I, [_P, _I, _P, _P]),
     ("dp_set_views_device", _I, [_P, _I, _P, _P, _P, _P, _P]),
+    ("dp_build_pyramid", _I, [_P, _I]),
+    ("dp_set_level", _I, [_P, _I]),
+    ("dp_level_info", _I, [_P, _I, _I, _P, _P, _P]),
+    ("dp_read_level", _I, [_P, _I, _I, _P]),
     ("dp_view_geometry", _I, [_P, _P, _P, _P, _P]),
     ("dp_seeds_to_patches", _I, [_P, _P, _I, _P]),
     ("dp_eval_batch", _I, [_P, _P, _I, _I, _P]),

@@ -87,6 +87,11 @@ struct dp_ctx {
     dpg::ViewDev *d_views = nullptr;
     std::vector<uint32_t *> own_img;
     const char *img_base = nullptr; // lowest view plane address
+    // image pyramid: planes[l][v] (level 0 = the views as set), pools of levels >= 1
+    std::vector<double> P0;                          // V x 12 level-0 projections
+    std::vector<std::vector<dpk::PyrPlane>> planes;
+    std::vector<uint32_t *> pyr_pool;
+    int level = 0;
     bool narrow = false;            // all planes within 4 GiB of img_base (32-bit tap offsets)
     uint32_t *d_work = nullptr;
     unsigned long long *d_evals = nullptr;
@@ -282,8 +287,21 @@ extern "C" int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out)
     return DP_OK;
 }
 
+static void free_pyramid(dp_ctx *c)
+{
+    for (uint32_t *p : c->pyr_pool)
+        hipFree(p);
+    c->pyr_pool.clear();
+    if (c->planes.size() > 1)
+        c->planes.resize(1);
+    c->level = 0;
+}
+
 static void free_views(dp_ctx *c)
 {
+    free_pyramid(c);
+    c->planes.clear();
+    c->P0.clear();
     for (uint32_t *p : c->own_img)
         hipFree(p);
     c->own_img.clear();
@@ -376,6 +394,15 @@ static int upload_view_table(dp_ctx *c)
     return DP_OK;
 }
 
+static void record_level0(dp_ctx *c, const double *P)
+{
+    c->P0.assign(P, P + 12 * (size_t)c->V);
+    c->planes.assign(1, std::vector<dpk::PyrPlane>(c->V));
+    for (int v = 0; v < c->V; ++v)
+        c->planes[0][v] = dpk::PyrPlane{(uint32_t *)c->hv[v].img, c->hv[v].W, c->hv[v].H, c->hv[v].pitch, 0};
+    c->level = 0;
+}
+
 extern "C" int dp_set_views(dp_ctx *c, int V, const double *P, const dp_image *images)
 {
     if (!c || V <= 0 || V > DP_MAX_VIEWS || !P || !images)
@@ -416,6 +443,7 @@ extern "C" int dp_set_views(dp_ctx *c, int V, const double *P, const dp_image *i
         c->hv[v].img = d;
     }
     c->V = V;
+    record_level0(c, P);
     return upload_view_table(c);
 }
 
@@ -437,7 +465,136 @@ extern "C" int dp_set_views_device(dp_ctx *c, int V, const double *P, const int3
         c->hv[v].img = (const uint32_t *)dev_bgra[v];
     }
     c->V = V;
+    record_level0(c, P);
     return upload_view_table(c);
+}
+
+// ---------------------------------------------------------------------------
+// image pyramids
+// ---------------------------------------------------------------------------
+
+extern "C" int dp_build_pyramid(dp_ctx *c, int levels)
+{
+    if (!c || levels < 1 || levels > DP_MAX_LEVELS)
+        return fail(c, DP_E_ARG, "dp_build_pyramid: levels must be in [1, DP_MAX_LEVELS]");
+    if (c->V <= 0 || c->planes.empty())
+        return fail(c, DP_E_STATE, "dp_build_pyramid: no views set");
+    hipSetDevice(c->device);
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->level != 0) {
+        int rc = dp_set_level(c, 0);
+        if (rc != DP_OK)
+            return rc;
+    }
+    free_pyramid(c);
+    const int V = c->V;
+    dpk::PyrPlane *d_tab = nullptr;
+    DP_HIP(c, hipMalloc(&d_tab, sizeof(dpk::PyrPlane) * 2 * V));
+    int rc = DP_OK;
+    for (int l = 1; l < levels && rc == DP_OK; ++l) {
+        const std::vector<dpk::PyrPlane> &src = c->planes[l - 1];
+        std::vector<dpk::PyrPlane> dst(V);
+        size_t total = 0;
+        int mw = 0, mh = 0;
+        for (int v = 0; v < V; ++v) {
+            dst[v].w = (src[v].w + 1) / 2;
+            dst[v].h = (src[v].h + 1) / 2;
+            dst[v].pitch = dst[v].w;
+            total += (size_t)dst[v].w * (size_t)dst[v].h;
+            mw = std::max(mw, dst[v].w);
+            mh = std::max(mh, dst[v].h);
+        }
+        uint32_t *pool = nullptr;
+        if (hipMalloc(&pool, total * sizeof(uint32_t)) != hipSuccess) {
+            rc = fail(c, DP_E_OOM, "dp_build_pyramid: out of device memory");
+            break;
+        }
+        c->pyr_pool.push_back(pool);
+        size_t at = 0;
+        for (int v = 0; v < V; ++v) {
+            dst[v].img = pool + at;
+            at += (size_t)dst[v].w * (size_t)dst[v].h;
+        }
+        hipError_t e = hipMemcpyAsync(d_tab, src.data(), sizeof(dpk::PyrPlane) * V, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d_tab + V, dst.data(), sizeof(dpk::PyrPlane) * V, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess)
+            e = dpk::launch_pyr_down(d_tab, d_tab + V, V, mw, mh, c->stream);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            rc = fail(c, DP_E_HIP, std::string("dp_build_pyramid: ") + hipGetErrorString(e));
+            break;
+        }
+        c->planes.push_back(std::move(dst));
+    }
+    hipFree(d_tab);
+    return rc;
+}
+
+extern "C" int dp_set_level(dp_ctx *c, int level)
+{
+    if (!c)
+        return DP_E_ARG;
+    if (c->V <= 0 || c->planes.empty())
+        return fail(c, DP_E_STATE, "dp_set_level: no views set");
+    if (level < 0 || level >= (int)c->planes.size())
+        return fail(c, DP_E_ARG, "dp_set_level: level not built (dp_build_pyramid)");
+    hipSetDevice(c->device);
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    // the level-L scene: pyrDown^L images, projection rows 0-1 scaled by 2^-L
+    // (exact), camera geometry and grids recomputed from that P
+    const double s = std::ldexp(1.0, -level);
+    std::vector<dpg::ViewDev> hv(c->V);
+    for (int v = 0; v < c->V; ++v) {
+        double P[12];
+        for (int i = 0; i < 12; ++i)
+            P[i] = c->P0[12 * v + i] * (i < 8 ? s : 1.0);
+        const dpk::PyrPlane &pl = c->planes[level][v];
+        if (view_from_P(P, pl.w, pl.h, c->opt.grid_scale, hv[v]) != DP_OK)
+            return fail(c, DP_E_ARG, "dp_set_level: singular projection matrix");
+        hv[v].pitch = pl.pitch;
+        hv[v].img = pl.img;
+    }
+    if (c->d_views)
+        hipFree(c->d_views);
+    c->d_views = nullptr;
+    c->hv = std::move(hv);
+    c->level = level;
+    return upload_view_table(c);
+}
+
+extern "C" int dp_level_info(const dp_ctx *c, int level, int view, int32_t *width, int32_t *height,
+                             const void **d_bgra)
+{
+    if (!c || level < 0 || level >= (int)c->planes.size() || view < 0 || view >= c->V)
+        return DP_E_ARG;
+    const dpk::PyrPlane &pl = c->planes[level][view];
+    if (width)
+        *width = pl.w;
+    if (height)
+        *height = pl.h;
+    if (d_bgra)
+        *d_bgra = pl.img;
+    return DP_OK;
+}
+
+extern "C" int dp_read_level(dp_ctx *c, int level, int view, uint8_t *bgr_out)
+{
+    if (!c || !bgr_out || level < 0 || level >= (int)c->planes.size() || view < 0 || view >= c->V)
+        return fail(c, DP_E_ARG, "dp_read_level: bad level/view");
+    hipSetDevice(c->device);
+    const dpk::PyrPlane &pl = c->planes[level][view];
+    std::vector<uint32_t> tmp((size_t)pl.w * pl.h);
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    DP_HIP(c, hipMemcpy2D(tmp.data(), sizeof(uint32_t) * pl.w, pl.img, sizeof(uint32_t) * pl.pitch,
+                          sizeof(uint32_t) * pl.w, pl.h, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < tmp.size(); ++i) {
+        bgr_out[3 * i] = (uint8_t)(tmp[i] & 255u);
+        bgr_out[3 * i + 1] = (uint8_t)((tmp[i] >> 8) & 255u);
+        bgr_out[3 * i + 2] = (uint8_t)((tmp[i] >> 16) & 255u);
+    }
+    return DP_OK;
 }
 
 // ---------------------------------------------------------------------------

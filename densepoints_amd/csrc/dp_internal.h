@@ -48,7 +48,15 @@ struct ClaimArgs {
     double grid_scale;
 };
 
+// one image plane of a pyramid level (BGRA8, B in the low byte)
+struct PyrPlane {
+    uint32_t *img;
+    int32_t w, h, pitch, pad;
+};
+
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s);
+hipError_t launch_pyr_down(const PyrPlane *d_src, const PyrPlane *d_dst, int V, int max_dw, int max_dh,
+                           hipStream_t s);
 int read_stamps(unsigned long long *out);
 hipError_t launch_probe_texel(const unsigned long long *ta, const unsigned long long *tb, const uint32_t *fxy, int n,
                               int32_t *gray);

@@ -1366,7 +1366,77 @@ __global__ void probe_texel_kernel(const unsigned long long *ta, const unsigned 
     gray[i] = texel_gray(t);
 }
 
+// ---- image pyramid ------------------------------------------------------------
+// cv::pyrDown on BGRA8 planes: dst(x, y) = sum_ij w_i w_j src(2x+j-2, 2y+i-2)
+// with w = [1 4 6 4 1] (total 256), BORDER_REFLECT_101, (s + 128) >> 8 per
+// channel.  One block = 64 x 16 outputs of one view; its 132 x 36 source tile
+// (reflected at the image borders) is staged in LDS once, then each thread
+// forms 4 outputs with SWAR sums: B,R and G,A in the 16-bit halves of two
+// u32 accumulators (column sums <= 16*255, totals <= 256*255 < 2^16, so no
+// carry crosses a half).
+constexpr int kPyrTX = 64, kPyrTY = 16;
+constexpr int kPyrCols = 2 * kPyrTX + 4, kPyrRows = 2 * kPyrTY + 4;
+
+__device__ __forceinline__ int reflect101(int x, int n)
+{
+    x = x < 0 ? -x : x;
+    x = x >= n ? 2 * n - 2 - x : x;
+    return x < 0 ? 0 : (x >= n ? n - 1 : x); // n == 1
+}
+
+__global__ __launch_bounds__(256) void pyr_down_kernel(const PyrPlane *src, const PyrPlane *dst)
+{
+    __shared__ uint32_t tile[kPyrRows][kPyrCols + 1];
+    const PyrPlane s = src[blockIdx.z], d = dst[blockIdx.z];
+    const int ox0 = blockIdx.x * kPyrTX, oy0 = blockIdx.y * kPyrTY;
+    if (ox0 >= d.w || oy0 >= d.h)
+        return; // uniform per block
+    const int sx0 = 2 * ox0 - 2, sy0 = 2 * oy0 - 2;
+    for (int e = threadIdx.x; e < kPyrRows * kPyrCols; e += 256) {
+        const int r = e / kPyrCols, c = e - r * kPyrCols;
+        const int yy = reflect101(sy0 + r, s.h), xx = reflect101(sx0 + c, s.w);
+        tile[r][c] = s.img[(size_t)yy * (size_t)s.pitch + (size_t)xx];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & (kPyrTX - 1), ty = threadIdx.x / kPyrTX;
+    const int ox = ox0 + tx;
+    const uint32_t w[5] = {1u, 4u, 6u, 4u, 1u};
+#pragma unroll
+    for (int k = 0; k < kPyrTY / 4; ++k) {
+        const int r = ty + 4 * k;
+        const int oy = oy0 + r;
+        uint32_t br = 0u, ga = 0u;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            uint32_t cbr = 0u, cga = 0u;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const uint32_t p = tile[2 * r + i][2 * tx + j];
+                cbr += w[i] * (p & 0x00FF00FFu);
+                cga += w[i] * ((p >> 8) & 0x00FF00FFu);
+            }
+            br += w[j] * cbr;
+            ga += w[j] * cga;
+        }
+        if (ox < d.w && oy < d.h) {
+            br = ((br + 0x00800080u) >> 8) & 0x00FF00FFu;
+            ga = ((ga + 0x00800080u) >> 8) & 0x00FF00FFu;
+            d.img[(size_t)oy * (size_t)d.pitch + (size_t)ox] = br | (ga << 8);
+        }
+    }
+}
+
 } // namespace
+
+hipError_t launch_pyr_down(const PyrPlane *d_src, const PyrPlane *d_dst, int V, int max_dw, int max_dh,
+                           hipStream_t s)
+{
+    if (V <= 0 || max_dw <= 0 || max_dh <= 0)
+        return hipSuccess;
+    const dim3 grid((max_dw + kPyrTX - 1) / kPyrTX, (max_dh + kPyrTY - 1) / kPyrTY, V);
+    hipLaunchKernelGGL(pyr_down_kernel, grid, dim3(256), 0, s, d_src, d_dst);
+    return hipGetLastError();
+}
 
 hipError_t launch_probe_texel(const unsigned long long *ta, const unsigned long long *tb, const uint32_t *fxy, int n,
                               int32_t *gray)

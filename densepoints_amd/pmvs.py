@@ -202,6 +202,26 @@ class Engine:
         self._check(lib.dp_set_views_device(self._ctx, V, ptr(P), ptr(w), ptr(h), ptr(pt), arr))
         self._keep = [P, w, h, pt, arr]
 
+    # ---- image pyramid (include/densepoints.h dp_build_pyramid / dp_set_level) ----
+    def build_pyramid(self, levels: int):
+        """Levels 1..levels-1 by cv::pyrDown on the device (level 0 = the views)."""
+        self._check(lib.dp_build_pyramid(self._ctx, int(levels)))
+
+    def set_level(self, level: int):
+        """Run the patch loop on pyramid level `level` (P rows 0-1 scaled by 2^-level)."""
+        self._check(lib.dp_set_level(self._ctx, int(level)))
+
+    def level_info(self, level: int, view: int):
+        w, h, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_void_p()
+        self._check(lib.dp_level_info(self._ctx, level, view, ctypes.byref(w), ctypes.byref(h), ctypes.byref(d)))
+        return w.value, h.value, d.value
+
+    def read_level(self, level: int, view: int) -> np.ndarray:
+        w, h, _ = self.level_info(level, view)
+        out = np.zeros((h, w, 3), dtype=np.uint8)
+        self._check(lib.dp_read_level(self._ctx, level, view, ptr(out)))
+        return out
+
     def seeds_to_patches(self, xyz: np.ndarray) -> np.ndarray:
         xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 3)
         out = empty_patches(len(xyz))

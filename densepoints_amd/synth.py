@@ -23,6 +23,17 @@ CONFIGS = {
 }
 
 
+# image pyramid levels BASELINE.json names per config (level 0 included)
+PYRAMID_LEVELS = {
+    "cfg1_2view_vga": 1,
+    "cfg1_4view_vga": 1,
+    "cfg2_8view_1080p": 3,
+    "cfg3_32view_4k": 4,
+    "cfg4_64view_4k": 4,
+    "cfg5_128view_8k": 4,
+}
+
+
 def config(n_views=8, width=640, height=480, kind=1, seed=20261015, spread_deg=35.0,
            seed_stride_px=32.0, depth_noise=0.005) -> N.DpSynthConfig:
     c = N.DpSynthConfig()

@@ -40,6 +40,7 @@ extern "C" {
 
 #define DP_MAX_VIEWS 128       /* visible/candidate sets are 128-bit masks          */
 #define DP_MAX_CELL 16         /* n x n window, n <= 16 (reference uses 16 and 11)  */
+#define DP_MAX_LEVELS 8        /* image pyramid levels (dp_build_pyramid)           */
 
 /* ---- options: every hot-path knob, reference defaults --- */
 typedef struct dp_options {
@@ -132,6 +133,23 @@ int dp_set_views(dp_ctx *ctx, int V, const double *P, const dp_image *images);
 int dp_set_views_device(dp_ctx *ctx, int V, const double *P, const int32_t *width,
                         const int32_t *height, const int32_t *pitch_px,
                         const void *const *dev_bgra);
+
+/* ---- image pyramids (BASELINE configs "N pyramid levels") --
+ * The reference samples full-resolution images only: methods/pmvs Options::scale
+ * (options.h:10) is stored but never read, and PMVS::AddCamera (pmvs.cpp:11-20)
+ * keeps the cv::imread image.  Level l+1 = cv::pyrDown of level l (5x5 binomial
+ * [1 4 6 4 1]^2/256, BORDER_REFLECT_101, size ((W+1)/2, (H+1)/2), per-channel
+ * (s + 128) >> 8), built on the device from the level-0 planes.
+ * dp_set_level(L) runs every later call on level L: images = level L, projection
+ * rows 0-1 scaled by 2^-L (pyrDown's pixel grid), camera geometry and organizer
+ * grids recomputed from that P -- i.e. the reference algorithm applied to the
+ * level-L scene.  dp_set_views resets to level 0 and drops the pyramid. */
+int dp_build_pyramid(dp_ctx *ctx, int levels);          /* 1 <= levels <= DP_MAX_LEVELS */
+int dp_set_level(dp_ctx *ctx, int level);
+int dp_level_info(const dp_ctx *ctx, int level, int view, int32_t *width, int32_t *height,
+                  const void **d_bgra);
+/* host BGR8 copy (width*height*3 bytes) of one pyramid level of one view */
+int dp_read_level(dp_ctx *ctx, int level, int view, uint8_t *bgr_out);
 
 /* View::SetProjectionMatrix (types.cpp:28-68): camera centre, K (normalised
  * K(2,2)=1, positive diagonal), [R|t] and the camera x-axis (row 0 of R). */

@@ -1008,3 +1008,49 @@ int or_org_insert(or_org *o, const or_patch *p, uint32_t seq, uint32_t parent, o
  * with glibc and with the product's independent implementation) */
 void or_sincos(double x, double *s, double *c) { ordm_sincos(x, s, c); }
 double or_acos(double x) { return ordm_acos(x); }
+
+/* ---- image pyramid (build extension) ---------------------
+ * cv::pyrDown restated as OpenCV 3.4 computes it: an integer row pass
+ * (taps 1 4 6 4 1 around src column 2x) into a buffer row, a column pass over
+ * five buffer rows around src row 2y, then (sum + 128) >> 8.  Borders by
+ * borderInterpolate(BORDER_REFLECT_101). */
+static int or_reflect101(int p, int n)
+{
+    if (n == 1)
+        return 0;
+    while (p < 0 || p >= n)
+        p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
+int or_pyr_down(const uint8_t *bgr, int W, int H, uint8_t *out)
+{
+    if (!bgr || !out || W <= 0 || H <= 0)
+        return -1;
+    const int dw = (W + 1) / 2, dh = (H + 1) / 2;
+    static const int k[5] = {1, 4, 6, 4, 1};
+    int *rows = (int *)malloc(sizeof(int) * 5 * (size_t)dw * 3);
+    if (!rows)
+        return -1;
+    for (int y = 0; y < dh; ++y) {
+        for (int i = 0; i < 5; ++i) {
+            const uint8_t *src = bgr + (size_t)or_reflect101(2 * y + i - 2, H) * (size_t)W * 3;
+            int *r = rows + (size_t)i * dw * 3;
+            for (int x = 0; x < dw; ++x)
+                for (int c = 0; c < 3; ++c) {
+                    int acc = 0;
+                    for (int j = 0; j < 5; ++j)
+                        acc += k[j] * src[(size_t)or_reflect101(2 * x + j - 2, W) * 3 + c];
+                    r[x * 3 + c] = acc;
+                }
+        }
+        for (int x = 0; x < dw * 3; ++x) {
+            int acc = 0;
+            for (int i = 0; i < 5; ++i)
+                acc += k[i] * rows[(size_t)i * dw * 3 + x];
+            out[(size_t)y * dw * 3 + x] = (uint8_t)((acc + 128) >> 8);
+        }
+    }
+    free(rows);
+    return 0;
+}

@@ -101,6 +101,10 @@ or_org *or_org_create(const or_scene *s);
 void or_org_destroy(or_org *o);
 int or_org_insert(or_org *o, const or_patch *p, uint32_t seq, uint32_t parent, or_patch *out);
 void or_color(const or_scene *s, or_patch *p);
+/* cv::pyrDown (OpenCV 3.4 imgproc/pyramids.cpp pyrDown_: 5x5 kernel
+ * [1 4 6 4 1]^T[1 4 6 4 1]/256, BORDER_REFLECT_101, dst ((W+1)/2, (H+1)/2),
+ * CV_DESCALE(sum, 8)) on a BGR8 image; out holds dw*dh*3 bytes. */
+int or_pyr_down(const uint8_t *bgr, int W, int H, uint8_t *out);
 
 #ifdef __cplusplus
 }

@@ -86,6 +86,7 @@ def _load():
         "or_org_create": (P, [P]),
         "or_org_destroy": (None, [P]),
         "or_org_insert": (ctypes.c_int, [P, P, ctypes.c_uint32, ctypes.c_uint32, P]),
+        "or_pyr_down": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, P]),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)
@@ -277,3 +278,23 @@ def sincos(x):
 
 def acos(x):
     return lib.or_acos(float(x))
+
+
+def pyr_down(bgr):
+    """cv::pyrDown of a BGR8 image (or_pyr_down)."""
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    H, W = bgr.shape[:2]
+    out = np.zeros(((H + 1) // 2, (W + 1) // 2, 3), dtype=np.uint8)
+    assert lib.or_pyr_down(_p(bgr), W, H, _p(out)) == 0
+    return out
+
+
+def level_scene(P, images, level):
+    """(P_L, images_L) of the level-L scene: pyrDown^L images and projection
+    rows 0-1 scaled by 2^-L (include/densepoints.h dp_set_level)."""
+    P = np.asarray(P, dtype=np.float64).reshape(-1, 3, 4).copy()
+    imgs = list(images)
+    for _ in range(level):
+        imgs = [pyr_down(im) for im in imgs]
+    P[:, :2, :] *= 2.0 ** -level
+    return P, imgs

@@ -8,7 +8,7 @@
 // libdensepoints.so (include/densepoints.h): dp_set_views + dp_densify.
 //
 //   densify -i scene.json --seeds seeds.xyz [-s settings.json] [-o points.ply]
-//           [--device N] [--max-pops N] [--check-only]
+//           [--device N] [--max-pops N] [--level L] [--check-only]
 //   densify --synthetic V,W,H,KIND --write-scene DIR   (deterministic test scene
 //           written as scene.json + PPM images + seeds.xyz; no GPU needed)
 #include "scene_io.h"
@@ -30,7 +30,7 @@ void usage()
 {
     std::fprintf(stderr,
                  "usage: densify -i scene.json --seeds seeds.xyz [-s settings.json] [-o points.ply]\n"
-                 "               [--device N] [--max-pops N] [--check-only]\n"
+                 "               [--device N] [--max-pops N] [--level L] [--check-only]\n"
                  "       densify --synthetic V,W,H,KIND --write-scene DIR\n");
 }
 
@@ -128,6 +128,7 @@ int main(int argc, char **argv)
     std::string input, settings, output = "points.ply", seeds_path, synth, scene_dir;
     int device = 0;
     long long max_pops = -1;
+    int level = 0;
     bool check_only = false;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -144,6 +145,7 @@ int main(int argc, char **argv)
         else if (a == "--seeds") seeds_path = next();
         else if (a == "--device") device = std::atoi(next().c_str());
         else if (a == "--max-pops") max_pops = std::atoll(next().c_str());
+        else if (a == "--level") level = std::atoi(next().c_str());
         else if (a == "--check-only") check_only = true;
         else if (a == "--synthetic") synth = next();
         else if (a == "--write-scene") scene_dir = next();
@@ -211,6 +213,11 @@ int main(int argc, char **argv)
             }
         };
         check(dp_set_views(ctx, (int)imgs.size(), P.data(), dimg.data()), "dp_set_views");
+        if (level > 0) {
+            // run on pyramid level L (cv::pyrDown^L on the device, P rows 0-1 / 2^L)
+            check(dp_build_pyramid(ctx, level + 1), "dp_build_pyramid");
+            check(dp_set_level(ctx, level), "dp_set_level");
+        }
         const dp_patch *out = nullptr;
         int64_t n_out = 0;
         dp_densify_stats st;

@@ -286,3 +286,40 @@ def test_device_division_shortcuts_are_ieee_exact():
     N.check(N.lib.dp_probe_math_device(N.ptr(x), len(x), N.ptr(out)))
     bad = np.flatnonzero(out[:, 3] == -1.0)
     assert bad.size == 0, f"{bad.size} mismatches, e.g. x={x[bad[:5]]}"
+
+
+@pytest.mark.parametrize("levels", [4])
+def test_pyramid_bit_exact(engine, orc, levels):
+    """dp_build_pyramid (device cv::pyrDown, LDS-tiled SWAR) equals the oracle's
+    pyrDown chain, on the hf6 views and on odd-sized random images."""
+    sc = scene("hf6")
+    rng = np.random.default_rng(3)
+    extra = [rng.integers(0, 256, (61, 97, 3), dtype=np.uint8), rng.integers(0, 256, (130, 67, 3), dtype=np.uint8)]
+    views = sc.views + [dp.View(sc.P[0], im) for im in extra]
+    engine.set_views(views)
+    engine.build_pyramid(levels)
+    for v, vw in enumerate(views):
+        ref = vw.image
+        for lvl in range(1, levels):
+            ref = orc.pyr_down(ref)
+            got = engine.read_level(lvl, v)
+            assert got.shape == ref.shape
+            assert np.array_equal(got, ref), f"view {v} level {lvl}"
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_densify_on_pyramid_level_bit_exact(orc, level):
+    """The patch loop on level L equals the reference algorithm on the level-L
+    scene (pyrDown^L images, P rows 0-1 scaled by 2^-L)."""
+    sc = scene("plane4")
+    PL, imgs = orc.level_scene(sc.P, sc.imgs, level)
+    S = orc.Scene(PL, imgs)
+    op, ost = S.densify(sc.seeds)
+    with dp.Engine(device=0) as eng:
+        eng.set_views(sc.views)
+        eng.build_pyramid(3)
+        eng.set_level(level)
+        gp, gst = eng.densify(sc.seeds)
+    assert gst["patches"] == ost["patches"] and gst["pops"] == ost["pops"]
+    assert len(gp) > 10
+    assert_same(gp, op, FIELDS + ("seq", "parent", "rgb"))

@@ -83,3 +83,33 @@ def test_transcendentals_within_one_ulp(orc):
         assert ulp_diff(orc.acos(x), math.acos(x)) <= 1.0
     assert math.isnan(orc.acos(float("nan")))
     assert math.isnan(orc.acos(1.5))
+
+
+def _pyr_down_numpy(img):
+    """Independent numpy statement of cv::pyrDown (reflect-101 = np.pad 'reflect')."""
+    k = np.array([1, 4, 6, 4, 1], dtype=np.int64)
+    H, W = img.shape[:2]
+    a = np.pad(img.astype(np.int64), ((2, 2), (2, 2), (0, 0)), mode="reflect") if min(H, W) > 2 else None
+    if a is None:
+        pytest.skip("tiny image")
+    rows = sum(k[j] * a[:, j:j + W, :] for j in range(5))
+    full = sum(k[i] * rows[i:i + H, :, :] for i in range(5))
+    return ((full[::2, ::2, :] + 128) >> 8).astype(np.uint8)
+
+
+@pytest.mark.parametrize("shape", [(240, 320), (61, 97), (5, 6), (33, 4)])
+def test_oracle_pyr_down_matches_numpy(orc, shape):
+    rng = np.random.default_rng(shape[0] * 1000 + shape[1])
+    img = rng.integers(0, 256, shape + (3,), dtype=np.uint8)
+    out = orc.pyr_down(img)
+    assert out.shape == ((shape[0] + 1) // 2, (shape[1] + 1) // 2, 3)
+    assert np.array_equal(out, _pyr_down_numpy(img))
+
+
+def test_oracle_pyr_down_constant_and_level_scene(orc):
+    img = np.full((31, 45, 3), 200, dtype=np.uint8)
+    assert (orc.pyr_down(img) == 200).all()
+    P = np.arange(24, dtype=np.float64).reshape(2, 3, 4) + 1.0
+    PL, imgs = orc.level_scene(P, [img, img], 2)
+    assert np.array_equal(PL[:, 2], P[:, 2]) and np.array_equal(PL[:, :2], P[:, :2] / 4.0)
+    assert imgs[0].shape == (8, 12, 3)
