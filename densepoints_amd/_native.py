@@ -101,6 +101,17 @@ class DpGeneration(ctypes.Structure):
     ]
 
 
+class DpFilterOptions(ctypes.Structure):
+    _fields_ = [
+        ("passes", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("min_neighbor_frac", ctypes.c_double),
+    ]
+
+
+FILTER_VISIBILITY, FILTER_NEIGHBORS = 1, 2
+
+
 class DpSynthConfig(ctypes.Structure):
     _fields_ = [
         ("n_views", ctypes.c_int32),
@@ -145,6 +156,9 @@ SIGNATURES = [
     ("dp_densify_refine", _I, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
     ("dp_densify_commit", _I, [_P, _P, _P, _P, ctypes.c_int64]),
     ("dp_densify_result", _I, [_P, _P, _P, _P]),
+    ("dp_default_filter_options", None, [_P]),
+    ("dp_filter_patches", _I, [_P, _P, ctypes.c_int64, _P, _P]),
+    ("dp_filter_patches_device", _I, [_P, _P, ctypes.c_int64, _P, _P, _P]),
     ("dp_last_kernel_ms", _I, [_P, _P]),
     ("dp_synth_default", None, [_P]),
     ("dp_synth_cameras", _I, [_P, _P]),

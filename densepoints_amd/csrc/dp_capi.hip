@@ -103,6 +103,11 @@ struct dp_ctx {
     DevBuf<uint8_t> ok, acc;
     DevBuf<uint32_t> prefix;
     DevBuf<unsigned char> scan_tmp;
+    // patch filter scratch
+    DevBuf<unsigned long long> front;
+    DevBuf<uint8_t> f_alive, f_keep;
+    DevBuf<double> f_rho;
+    DevBuf<dp_patch> f_pat;
     std::vector<dp_patch> result;
     // generation-at-a-time densify (dp_densify_begin/refine/commit/result)
     DevBuf<dp_patch> seedp;  // seed patches of generation 0
@@ -321,6 +326,11 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
         hipStreamSynchronize(c->stream);
     free_views(c);
     c->grid.release();
+    c->front.release();
+    c->f_alive.release();
+    c->f_keep.release();
+    c->f_rho.release();
+    c->f_pat.release();
     c->pat.release();
     c->store.release();
     c->cand.release();
@@ -594,6 +604,85 @@ extern "C" int dp_read_level(dp_ctx *c, int level, int view, uint8_t *bgr_out)
         bgr_out[3 * i + 1] = (uint8_t)((tmp[i] >> 8) & 255u);
         bgr_out[3 * i + 2] = (uint8_t)((tmp[i] >> 16) & 255u);
     }
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// patch filter (spec in include/densepoints.h)
+// ---------------------------------------------------------------------------
+
+extern "C" void dp_default_filter_options(dp_filter_options *fo)
+{
+    if (!fo)
+        return;
+    fo->passes = DP_FILTER_VISIBILITY | DP_FILTER_NEIGHBORS;
+    fo->reserved = 0;
+    fo->min_neighbor_frac = 0.25;
+}
+
+extern "C" int dp_filter_patches_device(dp_ctx *c, const dp_patch *d_patches, int64_t n, const dp_filter_options *fo,
+                                        uint8_t *d_keep, void *stream)
+{
+    if (!c || n < 0 || (n > 0 && (!d_patches || !d_keep)) || n > 0xFFFFFFFFll)
+        return fail(c, DP_E_ARG, "dp_filter_patches: bad arguments");
+    if (c->V <= 0)
+        return fail(c, DP_E_STATE, "dp_filter_patches: no views set");
+    dp_filter_options o;
+    dp_default_filter_options(&o);
+    if (fo)
+        o = *fo;
+    if (n == 0)
+        return DP_OK;
+    hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    DP_HIP(c, c->front.reserve((size_t)c->grid_cells + 1));
+    DP_HIP(c, c->f_alive.reserve((size_t)n));
+    DP_HIP(c, c->f_rho.reserve((size_t)n));
+    dpk::FilterArgs a{};
+    a.views = c->d_views;
+    a.V = c->V;
+    a.patches = d_patches;
+    a.n = n;
+    a.alive = c->f_alive.p;
+    a.front = c->front.p;
+    a.rho = c->f_rho.p;
+    a.grid_scale = (double)c->opt.grid_scale;
+    a.min_neighbor_frac = o.min_neighbor_frac;
+    const size_t fb = sizeof(unsigned long long) * ((size_t)c->grid_cells + 1);
+    DP_HIP(c, hipMemsetAsync(c->f_alive.p, 1, (size_t)n, s));
+    DP_HIP(c, dpk::launch_filter_rho(a, s));
+    if (o.passes & DP_FILTER_VISIBILITY) {
+        DP_HIP(c, hipMemsetAsync(c->front.p, 0xFF, fb, s));
+        DP_HIP(c, dpk::launch_filter_front(a, s));
+        DP_HIP(c, dpk::launch_filter_visibility(a, d_keep, s));
+        DP_HIP(c, hipMemcpyAsync(c->f_alive.p, d_keep, (size_t)n, hipMemcpyDeviceToDevice, s));
+    }
+    if (o.passes & DP_FILTER_NEIGHBORS) {
+        DP_HIP(c, hipMemsetAsync(c->front.p, 0xFF, fb, s));
+        DP_HIP(c, dpk::launch_filter_front(a, s));
+        DP_HIP(c, dpk::launch_filter_neighbors(a, d_keep, s));
+    } else if (!(o.passes & DP_FILTER_VISIBILITY)) {
+        DP_HIP(c, hipMemsetAsync(d_keep, 1, (size_t)n, s));
+    }
+    return DP_OK;
+}
+
+extern "C" int dp_filter_patches(dp_ctx *c, const dp_patch *patches, int64_t n, const dp_filter_options *fo,
+                                 uint8_t *keep_out)
+{
+    if (!c || n < 0 || (n > 0 && (!patches || !keep_out)))
+        return fail(c, DP_E_ARG, "dp_filter_patches: bad arguments");
+    if (n == 0)
+        return DP_OK;
+    hipSetDevice(c->device);
+    DP_HIP(c, c->f_pat.reserve((size_t)n));
+    DP_HIP(c, c->f_keep.reserve((size_t)n));
+    DP_HIP(c, hipMemcpyAsync(c->f_pat.p, patches, sizeof(dp_patch) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    const int rc = dp_filter_patches_device(c, c->f_pat.p, n, fo, c->f_keep.p, c->stream);
+    if (rc != DP_OK)
+        return rc;
+    DP_HIP(c, hipMemcpyAsync(keep_out, c->f_keep.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    DP_HIP(c, hipStreamSynchronize(c->stream));
     return DP_OK;
 }
 

@@ -54,6 +54,25 @@ struct PyrPlane {
     int32_t w, h, pitch, pad;
 };
 
+// PMVS-style filter (dp_filter.hip)
+struct FilterArgs {
+    const dpg::ViewDev *views;
+    int32_t V;
+    int32_t pad;
+    const dp_patch *patches;
+    int64_t n;
+    const uint8_t *alive;          // patches taking part in this pass
+    unsigned long long *front;     // per (view, cell): f32 depth bits << 32 | index, ~0 = empty
+    double *rho;                   // per patch: grid_scale / dx in its reference view
+    double grid_scale;
+    double min_neighbor_frac;
+};
+
+hipError_t launch_filter_rho(const FilterArgs &a, hipStream_t s);
+hipError_t launch_filter_front(const FilterArgs &a, hipStream_t s);
+hipError_t launch_filter_visibility(const FilterArgs &a, uint8_t *keep, hipStream_t s);
+hipError_t launch_filter_neighbors(const FilterArgs &a, uint8_t *keep, hipStream_t s);
+
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s);
 hipError_t launch_pyr_down(const PyrPlane *d_src, const PyrPlane *d_dst, int V, int max_dw, int max_dh,
                            hipStream_t s);

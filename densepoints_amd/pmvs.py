@@ -222,6 +222,17 @@ class Engine:
         self._check(lib.dp_read_level(self._ctx, level, view, ptr(out)))
         return out
 
+    # ---- PMVS-style filter (include/densepoints.h dp_filter_patches) ----
+    def filter_patches(self, patches: np.ndarray, passes: int = 3, min_neighbor_frac: float = 0.25) -> np.ndarray:
+        """Visibility-consistency + neighbourhood filter (PMVS::FilterPatches,
+        pmvs.h:27, which the reference leaves undefined); returns keep flags."""
+        patches = np.ascontiguousarray(patches)
+        assert patches.dtype == PATCH_DTYPE
+        fo = N.DpFilterOptions(passes, 0, min_neighbor_frac)
+        keep = np.zeros(len(patches), dtype=np.uint8)
+        self._check(lib.dp_filter_patches(self._ctx, ptr(patches), len(patches), ctypes.byref(fo), ptr(keep)))
+        return keep
+
     def seeds_to_patches(self, xyz: np.ndarray) -> np.ndarray:
         xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 3)
         out = empty_patches(len(xyz))
@@ -342,10 +353,16 @@ class PMVS:
             return
         self.views.append(view)
 
-    def run(self, seeds_xyz) -> bool:
+    def run(self, seeds_xyz, filter_passes: int = 0) -> bool:
+        """PMVS::Run (pmvs.cpp:22-43) minus matching; filter_passes != 0 then
+        applies FilterPatches (pmvs.h:27; spec in dp_filter_patches)."""
         with Engine(self.options, self.device) as eng:
             eng.set_views(self.views)
             self.patches, self.stats = eng.densify(np.asarray(seeds_xyz, dtype=np.float64))
+            if filter_passes:
+                keep = eng.filter_patches(self.patches, filter_passes)
+                self.stats["filtered_out"] = int(len(keep) - keep.sum())
+                self.patches = self.patches[keep == 1]
         return True
 
     def get_point_cloud(self) -> np.ndarray:

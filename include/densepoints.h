@@ -229,6 +229,37 @@ int dp_densify_commit(dp_ctx *ctx, dp_generation *gen, const dp_patch *cand, con
                       int64_t n_cand);
 int dp_densify_result(dp_ctx *ctx, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats);
 
+/* ---- patch filter ----------------------------------------
+ * PMVS::FilterPatches is declared (methods/pmvs/pmvs.h:27) but never defined
+ * and modules/filtering is empty, so this spec follows PMVS (Furukawa & Ponce,
+ * PAMI 2010, 3.4).  Every decision of a pass reads a snapshot of the previous
+ * pass's survivors (order-independent).  For view v and organizer cell c
+ * (grid_scale px, the TryInsert indexing), front(v, c) is the surviving patch
+ * with v in its visible set whose (f32 depth, index) is smallest there; depth =
+ * third row of P [X;1].  rho(p) = grid_scale / dx(p) (dx as in ExpandPatch);
+ * p, q are neighbours iff |(Xq-Xp).np| + |(Xq-Xp).nq| < 2 rho(p) (fp64).
+ *   DP_FILTER_VISIBILITY: U(p) = { front(v, c_v(p)) : v in V(p) } minus p and
+ *     its neighbours (a multiset over views); p is removed iff
+ *     |V(p)| * score(p) < sum_{q in U(p)} score(q).
+ *   DP_FILTER_NEIGHBORS: over v in V(p) and the 3x3 cells around c_v(p), T =
+ *     front patches other than p, M = those that are neighbours of p; p is
+ *     removed iff T > 0 and M < min_neighbor_frac * T.
+ * keep_out[i] = 1 for survivors.  Multi-GPU: the patch store is replicated on
+ * every rank after the generation all-gathers, so each rank filters locally. */
+#define DP_FILTER_VISIBILITY 1
+#define DP_FILTER_NEIGHBORS 2
+typedef struct dp_filter_options {
+    int32_t passes;            /* DP_FILTER_* bits (default both)                   */
+    int32_t reserved;
+    double min_neighbor_frac;  /* 0.25 (PMVS neighbourhood filter)                  */
+} dp_filter_options;
+
+void dp_default_filter_options(dp_filter_options *fo);
+int dp_filter_patches(dp_ctx *ctx, const dp_patch *patches, int64_t n, const dp_filter_options *fo,
+                      uint8_t *keep_out);
+int dp_filter_patches_device(dp_ctx *ctx, const dp_patch *d_patches, int64_t n, const dp_filter_options *fo,
+                             uint8_t *d_keep, void *stream);
+
 /* Elapsed device milliseconds of the most recent refine kernel launch, timed
  * with HIP events on the stream the kernel ran on. */
 int dp_last_kernel_ms(dp_ctx *ctx, double *ms);

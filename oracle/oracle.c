@@ -1054,3 +1054,167 @@ int or_pyr_down(const uint8_t *bgr, int W, int H, uint8_t *out)
     free(rows);
     return 0;
 }
+
+/* ---- PMVS-style filter (spec: include/densepoints.h) ------
+ * Restated from Furukawa & Ponce (PAMI 2010) 3.4 as the product specifies it:
+ * every decision of a pass reads a snapshot of the survivors of the previous
+ * pass.  front(v, cell) = the visible patch with the smallest (f32 depth,
+ * index) in that organizer cell of view v. */
+typedef struct {
+    int64_t off;
+    int gw, gh;
+} or_fgrid;
+
+static int or_fcell(const or_scene *s, const or_fgrid *g, int vi, const or_patch *p, int64_t *row, int64_t *col)
+{
+    double X[3], u, w;
+    get_pos(p, X);
+    proj(&s->v[vi], X, &u, &w);
+    *row = cell_index(w, (double)s->opt.grid_scale);
+    *col = cell_index(u, (double)s->opt.grid_scale);
+    return *col >= 0 && *col < g[vi].gw && *row >= 0 && *row < g[vi].gh;
+}
+
+static void or_build_front(const or_scene *s, const or_fgrid *g, const or_patch *p, int64_t n,
+                           const uint8_t *alive, uint64_t *front, int64_t cells)
+{
+    for (int64_t c = 0; c < cells; ++c)
+        front[c] = ~0ull;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!alive[i])
+            continue;
+        int vis[OR_MAX_VIEWS];
+        const int m = decode_mask(p[i].vis, vis);
+        double X[3];
+        get_pos(&p[i], X);
+        for (int k = 0; k < m; ++k) {
+            int64_t row, col;
+            if (!or_fcell(s, g, vis[k], &p[i], &row, &col))
+                continue;
+            const double *P = s->v[vis[k]].P;
+            const float d = (float)(((P[8] * X[0] + P[9] * X[1]) + P[10] * X[2]) + P[11]);
+            if (!(d > 0.0f))
+                continue;
+            uint32_t bits;
+            memcpy(&bits, &d, 4);
+            const uint64_t key = ((uint64_t)bits << 32) | (uint32_t)i;
+            uint64_t *f = &front[g[vis[k]].off + row * g[vis[k]].gw + col];
+            if (key < *f)
+                *f = key;
+        }
+    }
+}
+
+/* |(Xq - Xp).np| + |(Xp - Xq).nq| < 2 rho(p), rho(p) = grid_scale / dx(p) */
+static int or_neighbours(const or_patch *a, const or_patch *b, double rho2)
+{
+    double d[3], na[3], nb[3];
+    for (int k = 0; k < 3; ++k) {
+        d[k] = (double)b->pos[k] - (double)a->pos[k];
+        na[k] = a->normal[k];
+        nb[k] = b->normal[k];
+    }
+    const double x = (d[0] * na[0] + d[1] * na[1]) + d[2] * na[2];
+    const double y = (d[0] * nb[0] + d[1] * nb[1]) + d[2] * nb[2];
+    return fabs(x) + fabs(y) < rho2;
+}
+
+static double or_rho(const or_scene *s, const or_patch *p)
+{
+    if (p->ref >= (uint32_t)s->V)
+        return 0.0;
+    const or_view *rv = &s->v[p->ref];
+    double X[3], u0, w0, u1, w1;
+    get_pos(p, X);
+    proj(rv, X, &u0, &w0);
+    const double X1[3] = {X[0] + rv->xr[0], X[1] + rv->xr[1], X[2] + rv->xr[2]};
+    proj(rv, X1, &u1, &w1);
+    const double du = u1 - u0, dw = w1 - w0;
+    const double dx = sqrt(du * du + dw * dw);
+    return dx > 0.0 ? (double)s->opt.grid_scale / dx : 0.0;
+}
+
+int or_filter_patches(const or_scene *s, const or_patch *p, int64_t n, int passes, double min_neighbor_frac,
+                      uint8_t *keep)
+{
+    if (!s || (n > 0 && (!p || !keep)) || n < 0)
+        return -1;
+    or_fgrid g[OR_MAX_VIEWS];
+    int64_t cells = 0;
+    for (int v = 0; v < s->V; ++v) {
+        g[v].gw = s->v[v].W / s->opt.grid_scale;
+        g[v].gh = s->v[v].H / s->opt.grid_scale;
+        g[v].off = cells;
+        cells += (int64_t)g[v].gw * g[v].gh;
+    }
+    uint64_t *front = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(cells + 1));
+    uint8_t *alive = (uint8_t *)calloc((size_t)n + 1, 1);
+    double *rho = (double *)malloc(sizeof(double) * (size_t)(n + 1));
+    if (!front || !alive || !rho) {
+        free(front);
+        free(alive);
+        free(rho);
+        return -1;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        alive[i] = 1;
+        rho[i] = or_rho(s, &p[i]);
+    }
+    if (passes & OR_FILTER_VISIBILITY) {
+        or_build_front(s, g, p, n, alive, front, cells);
+        for (int64_t i = 0; i < n; ++i) {
+            int vis[OR_MAX_VIEWS];
+            const int m = decode_mask(p[i].vis, vis);
+            double occ = 0.0;
+            for (int k = 0; k < m; ++k) {
+                int64_t row, col;
+                if (!or_fcell(s, g, vis[k], &p[i], &row, &col))
+                    continue;
+                const uint64_t key = front[g[vis[k]].off + row * g[vis[k]].gw + col];
+                if (key == ~0ull)
+                    continue;
+                const int64_t q = (int64_t)(uint32_t)key;
+                if (q == i || or_neighbours(&p[i], &p[q], 2.0 * rho[i]))
+                    continue;
+                occ = occ + (double)p[q].score;
+            }
+            keep[i] = ((double)m * (double)p[i].score < occ) ? 0 : 1;
+        }
+        memcpy(alive, keep, (size_t)n);
+    }
+    if (passes & OR_FILTER_NEIGHBORS) {
+        or_build_front(s, g, p, n, alive, front, cells);
+        for (int64_t i = 0; i < n; ++i) {
+            if (!alive[i]) {
+                keep[i] = 0;
+                continue;
+            }
+            int vis[OR_MAX_VIEWS];
+            const int m = decode_mask(p[i].vis, vis);
+            int total = 0, near = 0;
+            for (int k = 0; k < m; ++k) {
+                int64_t row, col;
+                if (!or_fcell(s, g, vis[k], &p[i], &row, &col))
+                    continue;
+                for (int dr = -1; dr <= 1; ++dr)
+                    for (int dc = -1; dc <= 1; ++dc) {
+                        const int64_t r = row + dr, c = col + dc;
+                        if (r < 0 || r >= g[vis[k]].gh || c < 0 || c >= g[vis[k]].gw)
+                            continue;
+                        const uint64_t key = front[g[vis[k]].off + r * g[vis[k]].gw + c];
+                        if (key == ~0ull || (int64_t)(uint32_t)key == i)
+                            continue;
+                        ++total;
+                        near += or_neighbours(&p[i], &p[(uint32_t)key], 2.0 * rho[i]);
+                    }
+            }
+            keep[i] = (total > 0 && (double)near < min_neighbor_frac * (double)total) ? 0 : 1;
+        }
+    } else {
+        memcpy(keep, alive, (size_t)n);
+    }
+    free(front);
+    free(alive);
+    free(rho);
+    return 0;
+}

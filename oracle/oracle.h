@@ -105,6 +105,13 @@ void or_color(const or_scene *s, or_patch *p);
  * [1 4 6 4 1]^T[1 4 6 4 1]/256, BORDER_REFLECT_101, dst ((W+1)/2, (H+1)/2),
  * CV_DESCALE(sum, 8)) on a BGR8 image; out holds dw*dh*3 bytes. */
 int or_pyr_down(const uint8_t *bgr, int W, int H, uint8_t *out);
+/* PMVS-style filter (the spec of include/densepoints.h dp_filter_patches; no
+ * reference implementation exists: pmvs.h:27 is undefined, modules/filtering
+ * is empty).  passes: bit 0 visibility consistency, bit 1 neighbourhood. */
+#define OR_FILTER_VISIBILITY 1
+#define OR_FILTER_NEIGHBORS 2
+int or_filter_patches(const or_scene *s, const or_patch *p, int64_t n, int passes, double min_neighbor_frac,
+                      uint8_t *keep);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,7 @@ def _load():
         "or_org_destroy": (None, [P]),
         "or_org_insert": (ctypes.c_int, [P, P, ctypes.c_uint32, ctypes.c_uint32, P]),
         "or_pyr_down": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, P]),
+        "or_filter_patches": (ctypes.c_int, [P, P, ctypes.c_int64, ctypes.c_int, ctypes.c_double, P]),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)
@@ -186,6 +187,18 @@ class Scene:
         pops = ctypes.c_int64()
         n = lib.or_densify(self._h, _p(seeds), len(seeds), _p(out), cap, ctypes.byref(nseed), ctypes.byref(pops))
         return out[: min(n, cap)].copy(), {"patches": n, "seed_patches": nseed.value, "pops": pops.value}
+
+
+def _scene_filter(self, patches, passes=3, min_neighbor_frac=0.25):
+    """or_filter_patches: keep flags of the PMVS-style filter (dp_filter_patches spec)."""
+    patches = np.ascontiguousarray(patches, dtype=PATCH_DTYPE)
+    keep = np.zeros(len(patches), dtype=np.uint8)
+    if lib.or_filter_patches(self._h, _p(patches), len(patches), passes, min_neighbor_frac, _p(keep)) != 0:
+        raise ValueError("or_filter_patches failed")
+    return keep
+
+
+Scene.filter_patches = _scene_filter
 
 
 class _Gen:

@@ -8,7 +8,7 @@
 // libdensepoints.so (include/densepoints.h): dp_set_views + dp_densify.
 //
 //   densify -i scene.json --seeds seeds.xyz [-s settings.json] [-o points.ply]
-//           [--device N] [--max-pops N] [--level L] [--check-only]
+//           [--device N] [--max-pops N] [--level L] [--filter] [--check-only]
 //   densify --synthetic V,W,H,KIND --write-scene DIR   (deterministic test scene
 //           written as scene.json + PPM images + seeds.xyz; no GPU needed)
 #include "scene_io.h"
@@ -30,7 +30,7 @@ void usage()
 {
     std::fprintf(stderr,
                  "usage: densify -i scene.json --seeds seeds.xyz [-s settings.json] [-o points.ply]\n"
-                 "               [--device N] [--max-pops N] [--level L] [--check-only]\n"
+                 "               [--device N] [--max-pops N] [--level L] [--filter] [--check-only]\n"
                  "       densify --synthetic V,W,H,KIND --write-scene DIR\n");
 }
 
@@ -129,7 +129,7 @@ int main(int argc, char **argv)
     int device = 0;
     long long max_pops = -1;
     int level = 0;
-    bool check_only = false;
+    bool check_only = false, do_filter = false;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> std::string {
@@ -146,6 +146,7 @@ int main(int argc, char **argv)
         else if (a == "--device") device = std::atoi(next().c_str());
         else if (a == "--max-pops") max_pops = std::atoll(next().c_str());
         else if (a == "--level") level = std::atoi(next().c_str());
+        else if (a == "--filter") do_filter = true;
         else if (a == "--check-only") check_only = true;
         else if (a == "--synthetic") synth = next();
         else if (a == "--write-scene") scene_dir = next();
@@ -223,22 +224,34 @@ int main(int argc, char **argv)
         dp_densify_stats st;
         std::memset(&st, 0, sizeof st);
         check(dp_densify(ctx, seeds.data(), (int)(seeds.size() / 3), &out, &n_out, &st), "dp_densify");
-        std::vector<dpio::CloudPoint> cloud((size_t)n_out);
+        // PMVS::FilterPatches (pmvs.h:27, undefined in the reference): dp_filter_patches spec
+        std::vector<uint8_t> keep((size_t)n_out, 1);
+        if (do_filter && n_out > 0) {
+            dp_filter_options fo;
+            dp_default_filter_options(&fo);
+            check(dp_filter_patches(ctx, out, n_out, &fo, keep.data()), "dp_filter_patches");
+        }
+        std::vector<dpio::CloudPoint> cloud;
+        cloud.reserve((size_t)n_out);
         for (int64_t i = 0; i < n_out; ++i) {
+            if (!keep[i])
+                continue;
+            dpio::CloudPoint cp;
             for (int k = 0; k < 3; ++k) {
-                cloud[i].pos[k] = out[i].pos[k];
-                cloud[i].normal[k] = out[i].normal[k];
-                cloud[i].rgb[k] = out[i].rgb[k];
+                cp.pos[k] = out[i].pos[k];
+                cp.normal[k] = out[i].normal[k];
+                cp.rgb[k] = out[i].rgb[k];
             }
+            cloud.push_back(cp);
         }
         dp_ctx_destroy(ctx);
         dpio::write_ply(output, cloud);
         const double wall =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        std::printf("{\"output\": \"%s\", \"patches\": %lld, \"seed_patches\": %lld, \"pops\": %lld, "
+        std::printf("{\"output\": \"%s\", \"patches\": %lld, \"written\": %zu, \"seed_patches\": %lld, \"pops\": %lld, "
                     "\"candidates\": %lld, \"evals\": %lld, \"generations\": %d, \"refine_ms\": %.3f, "
                     "\"densify_ms\": %.3f, \"wall_ms\": %.3f}\n",
-                    output.c_str(), (long long)st.patches, (long long)st.seed_patches, (long long)st.pops,
+                    output.c_str(), (long long)st.patches, cloud.size(), (long long)st.seed_patches, (long long)st.pops,
                     (long long)st.candidates, (long long)st.evals, st.generations, st.refine_ms, st.total_ms, wall);
         return 0;
     } catch (const std::exception &e) {

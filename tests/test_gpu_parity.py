@@ -323,3 +323,22 @@ def test_densify_on_pyramid_level_bit_exact(orc, level):
     assert gst["patches"] == ost["patches"] and gst["pops"] == ost["pops"]
     assert len(gp) > 10
     assert_same(gp, op, FIELDS + ("seq", "parent", "rgb"))
+
+
+@pytest.mark.parametrize("passes", [1, 2, 3])
+def test_filter_bit_exact(orc, passes):
+    """dp_filter_patches (front map by atomicMin, one thread per patch) equals
+    the oracle's or_filter_patches on a densify result, with planted occluders."""
+    from test_filter_cpu import with_occluders
+
+    sc = scene("hf6")
+    S = orc.Scene(sc.P, sc.imgs)
+    op, _ = S.densify(sc.seeds)
+    pat = with_occluders(orc, sc.P.reshape(-1, 3, 4), op, k=40)
+    want = S.filter_patches(pat, passes)
+    with dp.Engine(device=0) as eng:
+        eng.set_views(sc.views)
+        got = eng.filter_patches(pat, passes)
+    assert np.array_equal(got, want)
+    if passes & 1:
+        assert got[:40].sum() < 40
