@@ -198,6 +198,21 @@ def main():
                                  "patches": int(dst["patches"]), "candidates": int(dst["candidates"]),
                                  "generations": int(dst["generations"]), "evals": int(dst["evals"]),
                                  "refine_ms": round(dst["refine_ms"], 1), "wall_s": round(wall, 3)}
+    if world > 1 and not args.no_densify:
+        # informational: the same densify sharded over the ranks --
+        # per generation each rank refines its item range into HBM, the
+        # candidate shards are all-gathered over RCCL (all_gather_into_tensor),
+        # every rank commits the replicated organizer step
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        _, sst = D.densify_sharded_device(eng, seeds, dist, torch.device("cuda", local))
+        torch.cuda.synchronize()
+        wall = D.max_over_ranks(time.perf_counter() - t0, dist, torch.device("cuda", local))
+        result["densify_sharded"] = {"ranks": world, "patches": int(sst["patches"]),
+                                     "generations": int(sst["generations"]), "evals": int(sst["evals"]),
+                                     "refine_ms_max_rank": round(sst["refine_ms"], 1), "wall_s": round(wall, 3),
+                                     "collective": "all_gather_into_tensor (RCCL) of 80-B candidate records"}
     st = np.zeros(8, dtype=np.uint64)
     if N.lib.dp_debug_stamps(N.ptr(st)) == 0:  # -DDP_STAMPS diagnostic builds only
         tot = float(st[7]) or 1.0

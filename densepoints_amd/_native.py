@@ -156,6 +156,8 @@ SIGNATURES = [
     ("dp_densify_refine", _I, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
     ("dp_densify_commit", _I, [_P, _P, _P, _P, ctypes.c_int64]),
     ("dp_densify_result", _I, [_P, _P, _P, _P]),
+    ("dp_densify_refine_device", _I, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P, _P]),
+    ("dp_densify_commit_device", _I, [_P, _P, _P, _P, ctypes.c_int64, _P]),
     ("dp_default_filter_options", None, [_P]),
     ("dp_filter_patches", _I, [_P, _P, ctypes.c_int64, _P, _P]),
     ("dp_filter_patches_device", _I, [_P, _P, ctypes.c_int64, _P, _P, _P]),

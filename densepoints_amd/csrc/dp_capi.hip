@@ -1100,8 +1100,10 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
     return DP_OK;
 }
 
-extern "C" int dp_densify_refine(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi, dp_patch *cand_out,
-                                 uint8_t *accept_out)
+// dp_densify_refine / _device: `dev` = the output arrays are device memory
+// (refined in place, asynchronously on `s`), else host arrays (synchronous).
+static int densify_refine_impl(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi, dp_patch *cand_out,
+                               uint8_t *accept_out, bool dev, hipStream_t s)
 {
     if (!c || !gen || lo < 0 || hi < lo || hi > gen->items)
         return fail(c, DP_E_ARG, "dp_densify_refine: bad item range");
@@ -1116,17 +1118,22 @@ extern "C" int dp_densify_refine(dp_ctx *c, const dp_generation *gen, int64_t lo
         return fail(c, DP_E_OOM, "dp_densify_refine: shard too large");
     const int32_t nc = (int32_t)nc64;
     hipSetDevice(c->device);
-    hipStream_t s = c->stream;
-    DP_HIP(c, c->cand.reserve(nc));
-    DP_HIP(c, c->ok.reserve(nc));
+    dp_patch *work = cand_out;
+    uint8_t *okp = accept_out;
+    if (!dev) {
+        DP_HIP(c, c->cand.reserve(nc));
+        DP_HIP(c, c->ok.reserve(nc));
+        work = c->cand.p;
+        okp = c->ok.p;
+    }
     dpk::RefineArgs a{};
     if (gen->index == 0) {
         // seed.cpp:110-144 on this shard of the seed patches
-        DP_HIP(c, hipMemcpyAsync(c->cand.p, c->seedp.p + lo, sizeof(dp_patch) * nc, hipMemcpyDeviceToDevice, s));
-        a = refine_args(c, c->cand.p, nc, gen->cell, DP_MODE_SEED, c->ok.p);
+        DP_HIP(c, hipMemcpyAsync(work, c->seedp.p + lo, sizeof(dp_patch) * nc, hipMemcpyDeviceToDevice, s));
+        a = refine_args(c, work, nc, gen->cell, DP_MODE_SEED, okp);
     } else {
         // Expand::ExpandPatch of parents head+lo .. head+hi-1 (queue order)
-        a = refine_args(c, c->cand.p, nc, gen->cell, DP_MODE_EXPAND, c->ok.p);
+        a = refine_args(c, work, nc, gen->cell, DP_MODE_EXPAND, okp);
         a.parents = c->store.p;
         a.parent0 = gen->head + lo;
     }
@@ -1137,14 +1144,29 @@ extern "C" int dp_densify_refine(dp_ctx *c, const dp_generation *gen, int64_t lo
     if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
         return rc;
     c->g_st.refine_ms += ms;
-    DP_HIP(c, hipMemcpyAsync(cand_out, c->cand.p, sizeof(dp_patch) * nc, hipMemcpyDeviceToHost, s));
-    DP_HIP(c, hipMemcpyAsync(accept_out, c->ok.p, (size_t)nc, hipMemcpyDeviceToHost, s));
-    DP_HIP(c, hipStreamSynchronize(s));
+    if (!dev) {
+        DP_HIP(c, hipMemcpyAsync(cand_out, work, sizeof(dp_patch) * nc, hipMemcpyDeviceToHost, s));
+        DP_HIP(c, hipMemcpyAsync(accept_out, okp, (size_t)nc, hipMemcpyDeviceToHost, s));
+        DP_HIP(c, hipStreamSynchronize(s));
+    }
     return DP_OK;
 }
 
-extern "C" int dp_densify_commit(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
-                                 int64_t n_cand)
+extern "C" int dp_densify_refine(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi, dp_patch *cand_out,
+                                 uint8_t *accept_out)
+{
+    return densify_refine_impl(c, gen, lo, hi, cand_out, accept_out, false, c ? c->stream : nullptr);
+}
+
+extern "C" int dp_densify_refine_device(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi,
+                                        dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream)
+{
+    return densify_refine_impl(c, gen, lo, hi, d_cand_out, d_accept_out, true,
+                               stream ? (hipStream_t)stream : (c ? c->stream : nullptr));
+}
+
+static int densify_commit_impl(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
+                               int64_t n_cand, bool dev, hipStream_t user)
 {
     if (!c || !gen || n_cand != gen->items * gen->per_item || (n_cand > 0 && (!cand || !accept)))
         return fail(c, DP_E_ARG, "dp_densify_commit: need all candidates of the generation");
@@ -1159,12 +1181,23 @@ extern "C" int dp_densify_commit(dp_ctx *c, dp_generation *gen, const dp_patch *
     if (nc > 0) {
         if ((uint64_t)gen->seq0 + (uint64_t)nc > 0xFFFFFFF0ull)
             return fail(c, DP_E_OOM, "sequence space exhausted");
-        DP_HIP(c, c->cand.reserve(nc));
-        DP_HIP(c, c->ok.reserve(nc));
-        DP_HIP(c, hipMemcpyAsync(c->cand.p, cand, sizeof(dp_patch) * nc, hipMemcpyHostToDevice, s));
-        DP_HIP(c, hipMemcpyAsync(c->ok.p, accept, (size_t)nc, hipMemcpyHostToDevice, s));
+        const dp_patch *cp = cand;
+        const uint8_t *op = accept;
+        if (dev) {
+            // the gathered records are produced on the caller's stream (RCCL,
+            // torch ops); NULL = the legacy default stream, which is synced too
+            if (user != s)
+                DP_HIP(c, hipStreamSynchronize(user));
+        } else {
+            DP_HIP(c, c->cand.reserve(nc));
+            DP_HIP(c, c->ok.reserve(nc));
+            DP_HIP(c, hipMemcpyAsync(c->cand.p, cand, sizeof(dp_patch) * nc, hipMemcpyHostToDevice, s));
+            DP_HIP(c, hipMemcpyAsync(c->ok.p, accept, (size_t)nc, hipMemcpyHostToDevice, s));
+            cp = c->cand.p;
+            op = c->ok.p;
+        }
         const int is_seed = gen->index == 0;
-        int rc = organize(c, c->cand.p, c->ok.p, nc, gen->seq0, c->g_np, is_seed ? 0 : gen->head, is_seed, &acc);
+        int rc = organize(c, cp, op, nc, gen->seq0, c->g_np, is_seed ? 0 : gen->head, is_seed, &acc);
         if (rc != DP_OK)
             return rc;
         DP_HIP(c, hipStreamSynchronize(s));
@@ -1182,6 +1215,18 @@ extern "C" int dp_densify_commit(dp_ctx *c, dp_generation *gen, const dp_patch *
     next_generation(c, gen, head);
     c->g_expected = gen->index;
     return DP_OK;
+}
+
+extern "C" int dp_densify_commit(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
+                                 int64_t n_cand)
+{
+    return densify_commit_impl(c, gen, cand, accept, n_cand, false, nullptr);
+}
+
+extern "C" int dp_densify_commit_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_cand,
+                                        const uint8_t *d_accept, int64_t n_cand, void *stream)
+{
+    return densify_commit_impl(c, gen, d_cand, d_accept, n_cand, true, (hipStream_t)stream);
 }
 
 extern "C" int dp_densify_result(dp_ctx *c, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats)

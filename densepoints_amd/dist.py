@@ -124,6 +124,68 @@ def densify_sharded(eng, seeds_xyz, dist, device: torch.device | None = None):
     return patches, stats
 
 
+def _reduce_stats(stats, dist, device):
+    if dist is None:
+        return stats
+    dev = device if (device is not None and dist.get_backend() == "nccl") else "cpu"
+    ev = torch.tensor([float(stats["evals"])], dtype=torch.float64, device=dev)
+    ms = torch.tensor([float(stats["refine_ms"])], dtype=torch.float64, device=dev)
+    dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+    dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    stats["evals"] = int(ev.item())
+    stats["refine_ms"] = float(ms.item())
+    return stats
+
+
+def densify_sharded_device(eng, seeds_xyz, dist, device: torch.device):
+    """densify_sharded with the candidate records resident in HBM.
+
+    Per generation each rank refines its contiguous item range straight into a
+    device buffer (dp_densify_refine_device), the padded equal-size shards are
+    all-gathered with ONE all_gather_into_tensor per array (RCCL over xGMI on
+    "nccl"; staged through the host on "gloo", which the CPU-side tests use),
+    trimmed back to the true shard sizes and concatenated in rank order on the
+    device, and every rank commits the whole generation from device memory
+    (dp_densify_commit_device).  80 B per candidate cross the links; nothing
+    else moves.  Bit-identical to dp_densify (replicated deterministic claims)."""
+    rank = dist.get_rank() if dist is not None else 0
+    world = dist.get_world_size() if dist is not None else 1
+    rccl = dist is not None and dist.get_backend() == "nccl"
+    rec = PATCH_DTYPE.itemsize
+    stream = torch.cuda.current_stream(device)
+    gen = eng.densify_begin(seeds_xyz)
+    while gen.items > 0:
+        per = gen.per_item
+        ranges = [shard_range(gen.items, r, world) for r in range(world)]
+        sizes = [(hi - lo) * per for lo, hi in ranges]
+        cap = max(max(sizes), 1)
+        buf = torch.empty(cap * rec, dtype=torch.uint8, device=device)
+        acc = torch.zeros(cap, dtype=torch.uint8, device=device)
+        lo, hi = ranges[rank]
+        eng.densify_refine_device(gen, lo, hi, buf.data_ptr(), acc.data_ptr(), stream.cuda_stream)
+        if dist is None:
+            all_c, all_a = buf[: sizes[0] * rec], acc[: sizes[0]]
+        else:
+            if rccl:
+                gb = torch.empty(world * cap * rec, dtype=torch.uint8, device=device)
+                ga = torch.empty(world * cap, dtype=torch.uint8, device=device)
+                dist.all_gather_into_tensor(gb, buf)
+                dist.all_gather_into_tensor(ga, acc)
+            else:
+                gb = torch.empty(world * cap * rec, dtype=torch.uint8)
+                ga = torch.empty(world * cap, dtype=torch.uint8)
+                dist.all_gather_into_tensor(gb, buf.cpu())
+                dist.all_gather_into_tensor(ga, acc.cpu())
+                gb, ga = gb.to(device), ga.to(device)
+            all_c = torch.cat([gb[r * cap * rec: r * cap * rec + sizes[r] * rec] for r in range(world)])
+            all_a = torch.cat([ga[r * cap: r * cap + sizes[r]] for r in range(world)])
+        n = sum(sizes)
+        gen = eng.densify_commit_device(gen, all_c.data_ptr(), all_a.data_ptr(), n, stream.cuda_stream)
+        del buf, acc, all_c, all_a
+    patches, stats = eng.densify_result()
+    return patches, _reduce_stats(stats, dist, device)
+
+
 def max_over_ranks(x: float, dist, device: torch.device | None = None) -> float:
     """Maximum of a per-rank scalar (the step time) over all ranks."""
     if dist is None:

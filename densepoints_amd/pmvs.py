@@ -321,6 +321,20 @@ class Engine:
         self._check(lib.dp_densify_commit(self._ctx, ctypes.byref(gen), ptr(cand), ptr(acc), len(cand)))
         return gen
 
+    def densify_refine_device(self, gen: N.DpGeneration, lo: int, hi: int, d_cand: int, d_accept: int,
+                              stream: int | None = None):
+        """Refine items [lo, hi) into device arrays ((hi-lo)*per_item records / flags)."""
+        self._check(lib.dp_densify_refine_device(self._ctx, ctypes.byref(gen), lo, hi, ctypes.c_void_p(d_cand),
+                                                 ctypes.c_void_p(d_accept),
+                                                 ctypes.c_void_p(stream) if stream else None))
+
+    def densify_commit_device(self, gen: N.DpGeneration, d_cand: int, d_accept: int, n: int,
+                              stream: int | None = None) -> N.DpGeneration:
+        self._check(lib.dp_densify_commit_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_cand),
+                                                 ctypes.c_void_p(d_accept), n,
+                                                 ctypes.c_void_p(stream) if stream else None))
+        return gen
+
     def densify_result(self):
         out = ctypes.c_void_p()
         n = ctypes.c_int64()

@@ -228,6 +228,15 @@ int dp_densify_refine(dp_ctx *ctx, const dp_generation *gen, int64_t item_lo, in
 int dp_densify_commit(dp_ctx *ctx, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
                       int64_t n_cand);
 int dp_densify_result(dp_ctx *ctx, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats);
+/* Device-resident variants (the records never leave HBM; the all-gather runs
+ * over RCCL on device buffers): refine writes (item_hi - item_lo) * per_item
+ * records/flags into device arrays asynchronously on `stream` (NULL = the
+ * context's stream); commit reads the gathered device arrays after waiting
+ * for `stream` (NULL = the default stream). */
+int dp_densify_refine_device(dp_ctx *ctx, const dp_generation *gen, int64_t item_lo, int64_t item_hi,
+                             dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream);
+int dp_densify_commit_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_cand,
+                             const uint8_t *d_accept, int64_t n_cand, void *stream);
 
 /* ---- patch filter ----------------------------------------
  * PMVS::FilterPatches is declared (methods/pmvs/pmvs.h:27) but never defined

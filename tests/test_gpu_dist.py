@@ -76,3 +76,46 @@ def test_two_ranks_sharded_densify_equals_dp_densify(tmp_path):
         assert got.tobytes() == ref.tobytes(), f"rank {r}"
         # each rank refined half of every generation; the summed evaluation count is the 1-GPU one
         assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
+
+
+def _worker_dev(rank, world, port, out_path, backend):
+    import torch
+    import torch.distributed as tdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # torch's HIP runtime initialises the device before libdensepoints' (the
+    # wheel bundles its own libamdhip64; bench.py uses the same order)
+    torch.cuda.set_device(0)
+    group = None
+    if backend:
+        kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+        tdist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        group = tdist
+    P, imgs, seeds = _scene("hf6")
+    with dp.Engine(device=0) as eng:
+        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+        got, st = D.densify_sharded_device(eng, seeds, group, torch.device("cuda", 0))
+    np.save(out_path + f".r{rank}.npy", got.view(np.uint8), allow_pickle=False)
+    with open(out_path + f".r{rank}.evals", "w") as f:
+        f.write(str(st["evals"]))
+    if group:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("backend,world", [(None, 1), ("nccl", 1), ("gloo", 2)])
+def test_device_resident_sharded_densify(tmp_path, backend, world):
+    """dp_densify_refine_device / dp_densify_commit_device with the candidate
+    shards all-gathered on the device (no group; world 1 over RCCL
+    all_gather_into_tensor; two ranks sharing cuda:0 over gloo) equal
+    dp_densify bit for bit."""
+    out = str(tmp_path / "dense")
+    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend), nprocs=world, join=True)
+    P, imgs, seeds = _scene("hf6")
+    with dp.Engine(device=0) as eng:
+        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+        ref, rst = eng.densify(seeds)
+    for r in range(world):
+        got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
+        assert got.tobytes() == ref.tobytes(), f"rank {r}"
+        assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
