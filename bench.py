@@ -57,9 +57,15 @@ def main():
     from densepoints_amd import synth
 
     rank, world, local = D.env()
+    # rehearsal knobs for a 1-GPU box (never set by the driver): DP_BENCH_BACKEND=gloo
+    # and DP_BENCH_ONE_DEVICE=1 run N ranks on cuda:0 over gloo
+    if os.environ.get("DP_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("DP_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     # RCCL over xGMI ("nccl" on ROCm): barrier + max-over-ranks time only
-    dist = D.init("nccl", torch.device("cuda", local))
+    dist = D.init(backend, torch.device("cuda", local))
+    coll_dev = torch.device("cuda", local) if backend == "nccl" else None
 
     cfg = synth.named(args.config)
     V, W, H = cfg.n_views, cfg.width, cfg.height
@@ -131,7 +137,7 @@ def main():
     step_ms = [a.elapsed_time(b) for a, b in kern_ms]
     launch_ms = float(np.mean(step_ms))
     lib_last_ms = eng.last_kernel_ms()  # the library's own events around the last launch
-    elapsed = D.max_over_ranks(elapsed, dist, torch.device("cuda", local))
+    elapsed = D.max_over_ranks(elapsed, dist, coll_dev)
 
     out = np.frombuffer(work.cpu().numpy().tobytes(), dtype=N.PATCH_DTYPE)
     acc = accept.cpu().numpy()
@@ -208,7 +214,7 @@ def main():
         t0 = time.perf_counter()
         _, sst = D.densify_sharded_device(eng, seeds, dist, torch.device("cuda", local))
         torch.cuda.synchronize()
-        wall = D.max_over_ranks(time.perf_counter() - t0, dist, torch.device("cuda", local))
+        wall = D.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
         result["densify_sharded"] = {"ranks": world, "patches": int(sst["patches"]),
                                      "generations": int(sst["generations"]), "evals": int(sst["evals"]),
                                      "refine_ms_max_rank": round(sst["refine_ms"], 1), "wall_s": round(wall, 3),
