@@ -125,6 +125,45 @@ class DpSynthConfig(ctypes.Structure):
     ]
 
 
+class DpMatcherOptions(ctypes.Structure):
+    """dp_matcher_options: Features::MatcherOptions (matcher.h:14-33) + cv::ORB knobs."""
+
+    _fields_ = [
+        ("n_features", ctypes.c_int32),
+        ("n_levels", ctypes.c_int32),
+        ("scale_factor", ctypes.c_double),
+        ("edge_threshold", ctypes.c_int32),
+        ("fast_threshold", ctypes.c_int32),
+        ("cell_size", ctypes.c_int32),
+        ("max_keypoints_per_cell", ctypes.c_int32),
+        ("epipolar_matching", ctypes.c_int32),
+        ("max_epipolar_distance", ctypes.c_float),
+        ("nn_match_ratio", ctypes.c_float),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class DpSeedStats(ctypes.Structure):
+    _fields_ = [
+        ("keypoints_detected", ctypes.c_int64),
+        ("keypoints", ctypes.c_int64),
+        ("pairs", ctypes.c_int64),
+        ("ratio_matches", ctypes.c_int64),
+        ("matches", ctypes.c_int64),
+        ("points", ctypes.c_int64),
+        ("detect_ms", ctypes.c_double),
+        ("describe_ms", ctypes.c_double),
+        ("match_ms", ctypes.c_double),
+        ("triangulate_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double),
+    ]
+
+
+# dp_keypoint: the cv::KeyPoint fields the matcher reads
+KEYPOINT_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("angle", "<f4"), ("octave", "<i4"), ("reserved", "<i4")]
+)
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _D = ctypes.c_double
@@ -162,6 +201,13 @@ SIGNATURES = [
     ("dp_filter_patches", _I, [_P, _P, ctypes.c_int64, _P, _P]),
     ("dp_filter_patches_device", _I, [_P, _P, ctypes.c_int64, _P, _P, _P]),
     ("dp_last_kernel_ms", _I, [_P, _P]),
+    ("dp_default_matcher_options", None, [_P]),
+    ("dp_generate_seeds", _I, [_P, _P, _P, _P, _P]),
+    ("dp_seed_keypoints", _I, [_P, _I, _P, _P, _P]),
+    ("dp_seed_matches", _I, [_P, _I, _P, _P, _P, _P]),
+    ("dp_knn_match", _I, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P]),
+    ("dp_fundamental_matrix", _I, [_P, _P, _P]),
+    ("dp_triangulate", _I, [_P, ctypes.c_int64, _P, _P, _P, _P]),
     ("dp_synth_default", None, [_P]),
     ("dp_synth_cameras", _I, [_P, _P]),
     ("dp_synth_render_host", _I, [_P, _P, _I, _P]),

@@ -1,0 +1,124 @@
+// dp_ctx.h -- the context object behind the C ABI, shared by the C-ABI
+// translation units (dp_capi.hip: views, refine, densify; dp_seeds.hip:
+// seed generation).
+#pragma once
+
+#include "dp_internal.h"
+
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+struct dp_seedgen; // seed-generation state (dp_seeds.hip)
+void dp_seedgen_free(dp_seedgen *s);
+
+namespace {
+
+// host-side parallel loop (the product library carries no OpenMP runtime)
+template <typename F> void parallel_for(int64_t n, F f)
+{
+    unsigned hw = std::thread::hardware_concurrency();
+    int64_t nt = hw ? (int64_t)(hw > 32 ? 32 : hw) : 4;
+    if (nt > n)
+        nt = n;
+    if (nt <= 1) {
+        for (int64_t i = 0; i < n; ++i)
+            f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 0; t < nt; ++t)
+        th.emplace_back([=, &f]() {
+            for (int64_t i = t; i < n; i += nt)
+                f(i);
+        });
+    for (auto &x : th)
+        x.join();
+}
+
+template <typename T> struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n)
+    {
+        if (n <= cap)
+            return hipSuccess;
+        if (p)
+            hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = n < 1024 ? 1024 : n + n / 4;
+        hipError_t e = hipMalloc(&p, want * sizeof(T));
+        if (e == hipSuccess)
+            cap = want;
+        return e;
+    }
+    void release()
+    {
+        if (p)
+            hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+} // namespace
+
+struct dp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    dp_options opt{};
+    std::string err;
+    int V = 0;
+    std::vector<dpg::ViewDev> hv;
+    dpg::ViewDev *d_views = nullptr;
+    std::vector<uint32_t *> own_img;
+    const char *img_base = nullptr; // lowest view plane address
+    // image pyramid: planes[l][v] (level 0 = the views as set), pools of levels >= 1
+    std::vector<double> P0;                          // V x 12 level-0 projections
+    std::vector<std::vector<dpk::PyrPlane>> planes;
+    std::vector<uint32_t *> pyr_pool;
+    int level = 0;
+    bool narrow = false;            // all planes within 4 GiB of img_base (32-bit tap offsets)
+    uint32_t *d_work = nullptr;
+    unsigned long long *d_evals = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    bool timed = false;
+    int64_t grid_cells = 0;
+    DevBuf<uint32_t> grid;
+    DevBuf<dp_patch> pat, store, cand;
+    DevBuf<uint8_t> ok, acc;
+    DevBuf<uint32_t> prefix;
+    DevBuf<unsigned char> scan_tmp;
+    // patch filter scratch
+    DevBuf<unsigned long long> front;
+    DevBuf<uint8_t> f_alive, f_keep;
+    DevBuf<double> f_rho;
+    DevBuf<dp_patch> f_pat;
+    std::vector<dp_patch> result;
+    // generation-at-a-time densify (dp_densify_begin/refine/commit/result)
+    DevBuf<dp_patch> seedp;  // seed patches of generation 0
+    int64_t g_np = 0;        // patches in the replicated store
+    int64_t g_nseeds = 0;
+    int64_t g_expected = -1; // generation index the next commit must carry
+    dp_densify_stats g_st{};
+    std::chrono::steady_clock::time_point g_t0;
+    // seed generation (Features::Matcher, dp_seeds.hip)
+    dp_seedgen *seeds = nullptr;
+};
+
+static inline int fail(dp_ctx *c, int code, const std::string &msg)
+{
+    if (c)
+        c->err = msg;
+    return code;
+}
+
+#define DP_HIP(c, expr)                                                                       \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return fail((c), _e == hipErrorOutOfMemory ? DP_E_OOM : DP_E_HIP,                 \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+    } while (0)

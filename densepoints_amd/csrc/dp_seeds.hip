@@ -1,0 +1,402 @@
+// dp_seeds.hip -- seed generation on the device:
+// Features::Matcher::GenerateSeeds, modules/features/matcher.cpp:18-474.
+//
+// Kernels:
+//   knn_kernel      BruteForce-Hamming knnMatch(k=2) on MFMA: Hamming distances
+//                   of 256-bit descriptors as an i8 GEMM (train bits 0/1 x
+//                   query bits +-1), top-2 per query kept in registers
+//   match_kernel    ratio test (matcher.cpp:221) + epipolar filter
+//                   (matcher.cpp:319-372) + the GetAllMatches lookup tables
+//   triang_kernel   GetAllMatches + multi-view DLT per keypoint
+//                   (matcher.cpp:374-450, triangulation.cpp:15-34)
+// ORB detection / description kernels are in dp_orb.hip.
+#include "dp_ctx.h"
+#include "dp_dlt.h"
+#include "dp_seeds.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace dpk {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// kNN (BFMatcher NORM_HAMMING, k = 2)
+//
+// acc = sum_k trainbit_k * (1 - 2 querybit_k) = popcnt(t & ~q) - popcnt(t & q)
+//     = hamming(t, q) - popcnt(q)
+// so within one query column the order of acc is the order of the Hamming
+// distance.  Per element the key (acc + 256) << 22 | train_row (mod 2^32) is
+// kept as a running (smallest, second) pair: m1 = med3(m0, k, m1),
+// m0 = min(m0, k).  Ties go to the lower train row, which is batchDistance's
+// strict-< insertion order (the first of equal distances wins).
+// ---------------------------------------------------------------------------
+
+constexpr int kKnnQB = 2;                 // 32-query blocks per wave
+constexpr int kKnnWaves = 4;              // waves per workgroup
+constexpr int kKnnWQ = 32 * kKnnQB;       // queries per wave
+static_assert(kKnnWQ * kKnnWaves == kKnnQueriesPerBlock, "knn workgroup shape");
+constexpr int kKnnTiles = 4;              // 32-row train tiles per stage
+constexpr int kKnnRows = 32 * kKnnTiles;  // train rows per stage
+
+__device__ __forceinline__ uint32_t spread4(uint32_t nib)
+{
+    // bit j of the nibble -> byte j (0/1)
+    return (nib * 0x00204081u) & 0x01010101u;
+}
+
+__device__ __forceinline__ v4i bits16_01(uint32_t b)
+{
+    v4i r;
+    r[0] = (int)spread4(b & 15u);
+    r[1] = (int)spread4((b >> 4) & 15u);
+    r[2] = (int)spread4((b >> 8) & 15u);
+    r[3] = (int)spread4((b >> 12) & 15u);
+    return r;
+}
+
+// bit 0 -> +1, bit 1 -> -1 (i8)
+__device__ __forceinline__ int pm1(uint32_t d) { return (int)(0x01010101u | ((d << 8) - d)); }
+
+__device__ __forceinline__ v4i bits16_pm1(uint32_t b)
+{
+    v4i r = bits16_01(b);
+    r[0] = pm1((uint32_t)r[0]);
+    r[1] = pm1((uint32_t)r[1]);
+    r[2] = pm1((uint32_t)r[2]);
+    r[3] = pm1((uint32_t)r[3]);
+    return r;
+}
+
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
+{
+    __shared__ v4i tileA[kKnnTiles][8][64]; // A fragments of one stage, 32 KB
+
+    const int2 blk = a.blocks[blockIdx.x];
+    const KnnJob job = a.jobs[blk.x];
+    const int tid = threadIdx.x;
+    const int w = tid >> 6, l = tid & 63;
+    const int col = l & 31, h = l >> 5;
+    const uint32_t *qd = a.desc + (size_t)job.q_off * 8;
+    const uint32_t *td = a.desc + (size_t)job.t_off * 8;
+
+    // query fragments: B[k][col], k = 32 s + 16 h + j for element j
+    v4i bq[kKnnQB][8];
+#pragma unroll
+    for (int b = 0; b < kKnnQB; ++b) {
+        const int q = blk.y + w * kKnnWQ + b * 32 + col;
+        const bool ok = q < job.nq;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const uint32_t d = ok ? qd[(size_t)q * 8 + s] : 0u;
+            bq[b][s] = bits16_pm1(d >> (16 * h));
+        }
+    }
+    uint32_t m0[kKnnQB], m1[kKnnQB];
+#pragma unroll
+    for (int b = 0; b < kKnnQB; ++b)
+        m0[b] = m1[b] = 0xFFFFFFFFu;
+
+    for (int t0 = 0; t0 < job.nt; t0 += kKnnRows) {
+        // stage: thread -> (row, 4 dwords); rows past nt unpack as zeros
+        {
+            const int r = tid >> 1, hh = tid & 1;
+            const int row = t0 + r;
+            uint4 d = make_uint4(0, 0, 0, 0);
+            if (row < job.nt)
+                d = *reinterpret_cast<const uint4 *>(td + (size_t)row * 8 + 4 * hh);
+            const uint32_t dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int s = 4 * hh + i;
+                tileA[r >> 5][s][r & 31] = bits16_01(dv[i] & 0xFFFFu);
+                tileA[r >> 5][s][32 + (r & 31)] = bits16_01(dv[i] >> 16);
+            }
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int ti = 0; ti < kKnnTiles; ++ti) {
+            const int tb = t0 + ti * 32;
+            if (tb >= job.nt)
+                break;
+            v4i af[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                af[s] = tileA[ti][s][l];
+            // key base per accumulator register: rows (r&3) + 8 (r>>2) + 4 h
+            const uint32_t base = (256u << 22) + (uint32_t)(tb + 4 * h);
+            const bool partial = tb + 32 > job.nt;
+#pragma unroll
+            for (int b = 0; b < kKnnQB; ++b) {
+                v16i acc = {};
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[b][s], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint32_t roff = (uint32_t)((r & 3) + 8 * (r >> 2));
+                    uint32_t k = ((uint32_t)acc[r] << 22) + base + roff;
+                    if (partial && tb + 4 * h + (int)roff >= job.nt)
+                        k = 0xFFFFFFFFu;
+                    m1[b] = med3u(m0[b], k, m1[b]);
+                    m0[b] = min(m0[b], k);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // merge the two row halves of each column (lanes l and l ^ 32)
+#pragma unroll
+    for (int b = 0; b < kKnnQB; ++b) {
+        const uint32_t p0 = (uint32_t)__shfl_xor((int)m0[b], 32);
+        const uint32_t p1 = (uint32_t)__shfl_xor((int)m1[b], 32);
+        const uint32_t n0 = min(m0[b], p0);
+        const uint32_t n1 = min(max(m0[b], p0), min(m1[b], p1));
+        const int q = blk.y + w * kKnnWQ + b * 32 + col;
+        if (h == 0 && q < job.nq) {
+            a.keys[2 * ((size_t)job.out_off + q)] = n0;
+            a.keys[2 * ((size_t)job.out_off + q) + 1] = n1;
+        }
+    }
+}
+
+// keys -> (index, distance); distance = (key >> 22) - 256 + popcnt(query)
+__global__ void knn_decode_kernel(const uint32_t *desc, int64_t q_off, int64_t nq, const uint32_t *keys,
+                                  int32_t *idx2, int32_t *dist2)
+{
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq)
+        return;
+    int pq = 0;
+    for (int s = 0; s < 8; ++s)
+        pq += __popc(desc[(size_t)(q_off + q) * 8 + s]);
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t k = keys[2 * q + j];
+        if (k == 0xFFFFFFFFu) {
+            idx2[2 * q + j] = -1;
+            dist2[2 * q + j] = -1;
+        } else {
+            idx2[2 * q + j] = (int32_t)(k & ((1u << 22) - 1));
+            dist2[2 * q + j] = (int32_t)(k >> 22) - 256 + pq;
+        }
+    }
+}
+
+hipError_t launch_knn(const KnnArgs &a, int nblocks, hipStream_t s)
+{
+    if (nblocks <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(knn_kernel, dim3(nblocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// ratio test + epipolar filter + GetAllMatches tables, one thread per query
+// ---------------------------------------------------------------------------
+__global__ void match_kernel(MatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_total)
+        return;
+    // pair of this query: jobs sorted by out_off
+    int lo = 0, hi = a.n_jobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.jobs[mid].out_off <= i)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const KnnJob job = a.jobs[lo];
+    const SeedPair pr = a.pairs[lo];
+    const int64_t q = i - job.out_off;
+    int32_t t = -1;
+    if (job.nt >= 2) { // knnMatch with one train row leaves matches_groups[i][1] undefined
+        const uint32_t k0 = a.keys[2 * i], k1 = a.keys[2 * i + 1];
+        // Hamming distances: (key >> 22) - 256 + popcnt(query)
+        int pq = 0;
+        for (int s = 0; s < 8; ++s)
+            pq += __popc(a.desc[(size_t)(job.q_off + q) * 8 + s]);
+        const int32_t h0 = (int32_t)(k0 >> 22) - 256 + pq, h1 = (int32_t)(k1 >> 22) - 256 + pq;
+        // DMatch::distance is float; nn_match_ratio is a float constant
+        if ((float)h0 < a.ratio * (float)h1) {
+            const int32_t tt = (int32_t)(k0 & ((1u << 22) - 1));
+            atomicAdd(a.n_ratio, 1ull);
+            const dp_keypoint &kl = a.kp[job.q_off + q];
+            const dp_keypoint &kr = a.kp[job.t_off + tt];
+            const float dist = dpt::epipolar_distance(pr.F, kl.x, kl.y, kr.x, kr.y);
+            if (!(dist > a.max_dist))
+                t = tt;
+        }
+    }
+    a.q2t[i] = t;
+    if (t >= 0) {
+        atomicAdd(a.n_match, 1ull);
+        // GetAllMatches (matcher.cpp:401-405): from the train side, the FIRST
+        // match in list order, i.e. the smallest query index
+        atomicMin(&a.t2q[pr.t2q_off + t], (int32_t)q);
+    }
+}
+
+hipError_t launch_match(const MatchArgs &a, hipStream_t s)
+{
+    if (a.n_total <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(match_kernel, dim3((unsigned)((a.n_total + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// DirectEpipolarMatching: one thread per (pair, query) scans the train set
+__global__ void epipolar_match_kernel(MatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_total)
+        return;
+    int lo = 0, hi = a.n_jobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.jobs[mid].out_off <= i)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const KnnJob job = a.jobs[lo];
+    const SeedPair pr = a.pairs[lo];
+    const int32_t q = (int32_t)(i - job.out_off);
+    const dp_keypoint kl = a.kp[job.q_off + q];
+    int32_t first = -1;
+    unsigned long long cnt = 0;
+    for (int32_t t = 0; t < job.nt; ++t) {
+        const dp_keypoint kr = a.kp[job.t_off + t];
+        const float dist = dpt::epipolar_distance(pr.F, kl.x, kl.y, kr.x, kr.y);
+        if (dist <= a.max_dist) {
+            if (first < 0)
+                first = t;
+            ++cnt;
+            atomicMin(&a.t2q[pr.t2q_off + t], q);
+        }
+    }
+    a.q2t[i] = first;
+    if (cnt) {
+        atomicAdd(a.n_ratio, cnt);
+        atomicAdd(a.n_match, cnt);
+    }
+}
+
+hipError_t launch_epipolar_match(const MatchArgs &a, hipStream_t s)
+{
+    if (a.n_total <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(epipolar_match_kernel, dim3((unsigned)((a.n_total + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// TriangulateMatches: one thread per (view, keypoint)
+// ---------------------------------------------------------------------------
+__global__ void triang_kernel(TriangArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_kp)
+        return;
+    int v = 0;
+    while (v + 1 < a.V && a.kp_off[v + 1] <= i)
+        ++v;
+    const int32_t k = (int32_t)(i - a.kp_off[v]);
+    dpt::Dlt d;
+    dpt::dlt_init(d);
+    int m = 0;
+    // the keypoint itself (cv::Point: rounded to int)
+    const dp_keypoint &kp = a.kp[i];
+    dpt::dlt_add_obs(d, a.P + 12 * v, (float)(int)rintf(kp.x), (float)(int)rintf(kp.y));
+    // pairs in list order (matcher.cpp:377-412)
+    for (int p = 0; p < a.n_pairs; ++p) {
+        const SeedPair pr = a.pairs[p];
+        int ov;
+        int32_t ok;
+        if (pr.first == v) {
+            ok = a.q2t[a.jobs[p].out_off + k];
+            ov = pr.second;
+        } else if (pr.second == v) {
+            ok = a.t2q[pr.t2q_off + k];
+            if (ok == kNoMatch)
+                ok = -1;
+            ov = pr.first;
+        } else {
+            continue;
+        }
+        if (ok < 0)
+            continue;
+        const dp_keypoint &o = a.kp[a.kp_off[ov] + ok];
+        dpt::dlt_add_obs(d, a.P + 12 * ov, (float)(int)rintf(o.x), (float)(int)rintf(o.y));
+        ++m;
+    }
+    a.valid[i] = m >= 1;
+    if (m >= 1) {
+        double X[3];
+        dpt::dlt_solve(d, X);
+        a.X[3 * i] = X[0];
+        a.X[3 * i + 1] = X[1];
+        a.X[3 * i + 2] = X[2];
+    }
+}
+
+hipError_t launch_triang(const TriangArgs &a, hipStream_t s)
+{
+    if (a.n_kp <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(triang_kernel, dim3((unsigned)((a.n_kp + 127) / 128)), dim3(128), 0, s, a);
+    return hipGetLastError();
+}
+
+// batched DLT over explicit observation lists (dp_triangulate)
+__global__ void dlt_batch_kernel(int64_t n, const int32_t *off, const double *P, const double *obs, double *X)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    dpt::Dlt d;
+    dpt::dlt_init(d);
+    for (int j = off[i]; j < off[i + 1]; ++j)
+        dpt::dlt_add_obs(d, P + 12 * (size_t)j, (float)obs[2 * j], (float)obs[2 * j + 1]);
+    double x[3];
+    dpt::dlt_solve(d, x);
+    X[3 * i] = x[0];
+    X[3 * i + 1] = x[1];
+    X[3 * i + 2] = x[2];
+}
+
+hipError_t launch_dlt_batch(int64_t n, const int32_t *off, const double *P, const double *obs, double *X,
+                            hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(dlt_batch_kernel, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, n, off, P, obs, X);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn_decode(const uint32_t *desc, int64_t q_off, int64_t nq, const uint32_t *keys, int32_t *idx2,
+                             int32_t *dist2, hipStream_t s)
+{
+    if (nq <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(knn_decode_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, desc, q_off, nq, keys,
+                       idx2, dist2);
+    return hipGetLastError();
+}
+
+} // namespace dpk

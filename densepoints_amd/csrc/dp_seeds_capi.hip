@@ -1,0 +1,693 @@
+// dp_seeds_capi.hip -- C ABI of seed generation (include/densepoints.h,
+// "seed generation"): Features::Matcher::GenerateSeeds
+// (modules/features/matcher.cpp:18-43) on the device, plus the standalone
+// operators (knnMatch, ComputeFundamentalMatrix, DirectLinearTriangulation).
+#include "dp_ctx.h"
+#include "dp_dlt.h"
+#include "dp_orb.h"
+#include "dp_seeds.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+// seed-generation state owned by the context
+struct dp_seedgen {
+    // scratch of the standalone operators
+    DevBuf<uint32_t> desc, keys;
+    DevBuf<int32_t> i2, d2, off;
+    DevBuf<double> P, obs, X;
+    DevBuf<dpk::KnnJob> jobs;
+    DevBuf<int2> blocks;
+    // GenerateSeeds
+    DevBuf<dpk::OrbLevel> lv;
+    DevBuf<dpk::PyrPlane> planes0;
+    DevBuf<uint8_t> gray, score, blur;
+    DevBuf<uint16_t> htmp;
+    DevBuf<int64_t> row_cnt, row_off;
+    DevBuf<dpk::OrbCand> cand, cand2;
+    DevBuf<uint32_t> hist, hkey, hkey_sorted, seg_cnt;
+    DevBuf<int32_t> seg_off32, fthr, umax;
+    DevBuf<int64_t> seg_off;
+    DevBuf<float> hthr;
+    DevBuf<uint8_t> keep_all, flag;
+    DevBuf<dp_keypoint> kp_a, kp_b;
+    DevBuf<int32_t> kv_a, kv_b, idx_a, idx_b, gcols, vw, vh;
+    DevBuf<int64_t> cell_off;
+    DevBuf<uint32_t> cell_cnt, okey, okey_sorted;
+    DevBuf<uint64_t> ckey, ckey_sorted;
+    DevBuf<int8_t> pattern;
+    DevBuf<unsigned char> cub_tmp;
+    DevBuf<int64_t> n_sel;
+    DevBuf<dpk::SeedPair> pairs;
+    DevBuf<int32_t> q2t, t2q;
+    DevBuf<int64_t> kp_off;
+    DevBuf<uint8_t> valid;
+    DevBuf<unsigned long long> counters;
+    std::vector<dpk::SeedPair> h_pairs;
+    std::vector<dpk::KnnJob> h_jobs;
+    std::vector<int64_t> h_kp_off;
+    std::vector<dp_keypoint> h_kp;
+    std::vector<uint8_t> h_desc;
+    std::vector<int32_t> h_q2t;
+    std::vector<double> h_xyz;
+    bool have_stages = false;
+};
+
+void dp_seedgen_free(dp_seedgen *s)
+{
+    if (!s)
+        return;
+    s->desc.release();
+    s->keys.release();
+    s->i2.release();
+    s->d2.release();
+    s->off.release();
+    s->P.release();
+    s->obs.release();
+    s->X.release();
+    s->jobs.release();
+    s->blocks.release();
+    for (auto *b : {&s->gray, &s->score, &s->blur, &s->keep_all, &s->flag})
+        b->release();
+    s->lv.release();
+    s->planes0.release();
+    s->htmp.release();
+    s->row_cnt.release();
+    s->row_off.release();
+    s->cand.release();
+    s->cand2.release();
+    for (auto *b : {&s->hist, &s->hkey, &s->hkey_sorted, &s->seg_cnt, &s->cell_cnt, &s->okey, &s->okey_sorted})
+        b->release();
+    for (auto *b : {&s->seg_off32, &s->fthr, &s->umax, &s->kv_a, &s->kv_b, &s->idx_a, &s->idx_b, &s->gcols, &s->vw,
+                    &s->vh})
+        b->release();
+    s->seg_off.release();
+    s->hthr.release();
+    s->kp_a.release();
+    s->kp_b.release();
+    s->cell_off.release();
+    s->ckey.release();
+    s->ckey_sorted.release();
+    s->pattern.release();
+    s->cub_tmp.release();
+    s->n_sel.release();
+    s->pairs.release();
+    s->q2t.release();
+    s->t2q.release();
+    s->kp_off.release();
+    s->valid.release();
+    s->counters.release();
+    delete s;
+}
+
+static dp_seedgen *seedgen(dp_ctx *c)
+{
+    if (!c->seeds)
+        c->seeds = new (std::nothrow) dp_seedgen();
+    return c->seeds;
+}
+
+extern "C" void dp_default_matcher_options(dp_matcher_options *mo)
+{
+    if (!mo)
+        return;
+    std::memset(mo, 0, sizeof(*mo));
+    mo->n_features = 40000;
+    mo->n_levels = 8;
+    mo->scale_factor = 1.2;
+    mo->edge_threshold = 31;
+    mo->fast_threshold = 20;
+    mo->cell_size = 16;
+    mo->max_keypoints_per_cell = 4;
+    mo->epipolar_matching = 0;
+    mo->max_epipolar_distance = 1.5f;
+    mo->nn_match_ratio = 0.7f;
+}
+
+// ---------------------------------------------------------------------------
+// Geometry::ComputeFundamentalMatrix (fundamental_matrix.cpp:6-34):
+// F = [P' C]_x P' P^+,  P^+ = P^T (P P^T)^-1,  C = cofactor null vector of P
+// (the reference's FullPivLU kernel is the same line, scaled).
+// ---------------------------------------------------------------------------
+static double det3c(const double *a, const double *b, const double *c)
+{
+    return (a[0] * (b[1] * c[2] - b[2] * c[1]) - b[0] * (a[1] * c[2] - a[2] * c[1])) +
+           c[0] * (a[1] * b[2] - a[2] * b[1]);
+}
+
+extern "C" int dp_fundamental_matrix(const double P1[12], const double P2[12], double F[9])
+{
+    if (!P1 || !P2 || !F)
+        return DP_E_ARG;
+    double col[4][3];
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 3; ++r)
+            col[c][r] = P1[r * 4 + c];
+    const double C[4] = {det3c(col[1], col[2], col[3]), -det3c(col[0], col[2], col[3]),
+                         det3c(col[0], col[1], col[3]), -det3c(col[0], col[1], col[2])};
+    double e[3];
+    for (int i = 0; i < 3; ++i)
+        e[i] = ((P2[i * 4] * C[0] + P2[i * 4 + 1] * C[1]) + P2[i * 4 + 2] * C[2]) + P2[i * 4 + 3] * C[3];
+    double M[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            M[i][j] = ((P1[i * 4] * P1[j * 4] + P1[i * 4 + 1] * P1[j * 4 + 1]) + P1[i * 4 + 2] * P1[j * 4 + 2]) +
+                      P1[i * 4 + 3] * P1[j * 4 + 3];
+    double cof[3][3];
+    cof[0][0] = M[1][1] * M[2][2] - M[1][2] * M[2][1];
+    cof[0][1] = -(M[1][0] * M[2][2] - M[1][2] * M[2][0]);
+    cof[0][2] = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+    cof[1][0] = -(M[0][1] * M[2][2] - M[0][2] * M[2][1]);
+    cof[1][1] = M[0][0] * M[2][2] - M[0][2] * M[2][0];
+    cof[1][2] = -(M[0][0] * M[2][1] - M[0][1] * M[2][0]);
+    cof[2][0] = M[0][1] * M[1][2] - M[0][2] * M[1][1];
+    cof[2][1] = -(M[0][0] * M[1][2] - M[0][2] * M[1][0]);
+    cof[2][2] = M[0][0] * M[1][1] - M[0][1] * M[1][0];
+    const double det = (M[0][0] * cof[0][0] + M[0][1] * cof[0][1]) + M[0][2] * cof[0][2];
+    if (det == 0.0 || !std::isfinite(det))
+        return DP_E_ARG;
+    double Mi[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            Mi[i][j] = cof[j][i] / det;
+    double Pp[4][3]; // P^T Mi
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 3; ++j)
+            Pp[k][j] = (P1[k] * Mi[0][j] + P1[4 + k] * Mi[1][j]) + P1[8 + k] * Mi[2][j];
+    const double ex[3][3] = {{0.0, -e[2], e[1]}, {e[2], 0.0, -e[0]}, {-e[1], e[0], 0.0}};
+    double A[3][4];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 4; ++j)
+            A[i][j] = (ex[i][0] * P2[j] + ex[i][1] * P2[4 + j]) + ex[i][2] * P2[8 + j];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            F[i * 3 + j] = ((A[i][0] * Pp[0][j] + A[i][1] * Pp[1][j]) + A[i][2] * Pp[2][j]) + A[i][3] * Pp[3][j];
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// knnMatch on one (query, train) pair
+// ---------------------------------------------------------------------------
+static void knn_blocks(const std::vector<dpk::KnnJob> &jobs, std::vector<int2> &blocks)
+{
+    blocks.clear();
+    for (size_t j = 0; j < jobs.size(); ++j)
+        for (int q = 0; q < jobs[j].nq; q += dpk::kKnnQueriesPerBlock)
+            blocks.push_back(make_int2((int)j, q));
+}
+
+extern "C" int dp_knn_match(dp_ctx *c, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt,
+                            int32_t *idx2, int32_t *dist2)
+{
+    if (!c)
+        return DP_E_ARG;
+    if (nq < 0 || nt < 0 || nt >= (1 << 22) || nq > INT32_MAX || (nq > 0 && (!query || !idx2 || !dist2)) ||
+        (nt > 0 && !train))
+        return fail(c, DP_E_ARG, "dp_knn_match: bad arguments");
+    if (nq == 0)
+        return DP_OK;
+    dp_seedgen *s = seedgen(c);
+    if (!s)
+        return fail(c, DP_E_OOM, "seedgen state");
+    DP_HIP(c, hipSetDevice(c->device));
+    DP_HIP(c, s->desc.reserve((size_t)(nq + nt) * 8));
+    DP_HIP(c, s->keys.reserve((size_t)nq * 2));
+    DP_HIP(c, s->i2.reserve((size_t)nq * 2));
+    DP_HIP(c, s->d2.reserve((size_t)nq * 2));
+    DP_HIP(c, hipMemcpyAsync(s->desc.p, query, (size_t)nq * 32, hipMemcpyHostToDevice, c->stream));
+    if (nt > 0)
+        DP_HIP(c, hipMemcpyAsync(s->desc.p + nq * 8, train, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream));
+    std::vector<dpk::KnnJob> jobs(1);
+    jobs[0].q_off = 0;
+    jobs[0].t_off = nq;
+    jobs[0].out_off = 0;
+    jobs[0].nq = (int32_t)nq;
+    jobs[0].nt = (int32_t)nt;
+    std::vector<int2> blocks;
+    knn_blocks(jobs, blocks);
+    DP_HIP(c, s->jobs.reserve(1));
+    DP_HIP(c, s->blocks.reserve(blocks.size()));
+    DP_HIP(c, hipMemcpyAsync(s->jobs.p, jobs.data(), sizeof(dpk::KnnJob), hipMemcpyHostToDevice, c->stream));
+    DP_HIP(c, hipMemcpyAsync(s->blocks.p, blocks.data(), blocks.size() * sizeof(int2), hipMemcpyHostToDevice,
+                             c->stream));
+    dpk::KnnArgs ka{s->desc.p, s->jobs.p, s->blocks.p, s->keys.p};
+    DP_HIP(c, hipEventRecord(c->e0, c->stream));
+    DP_HIP(c, dpk::launch_knn(ka, (int)blocks.size(), c->stream));
+    DP_HIP(c, hipEventRecord(c->e1, c->stream));
+    c->timed = true;
+    DP_HIP(c, dpk::launch_knn_decode(s->desc.p, 0, nq, s->keys.p, s->i2.p, s->d2.p, c->stream));
+    DP_HIP(c, hipMemcpyAsync(idx2, s->i2.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    DP_HIP(c, hipMemcpyAsync(dist2, s->d2.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// batched DLT
+// ---------------------------------------------------------------------------
+extern "C" int dp_triangulate(dp_ctx *c, int64_t n, const int32_t *offsets, const double *P, const double *obs,
+                              double *X)
+{
+    if (!c)
+        return DP_E_ARG;
+    if (n < 0 || (n > 0 && (!offsets || !P || !obs || !X)))
+        return fail(c, DP_E_ARG, "dp_triangulate: bad arguments");
+    if (n == 0)
+        return DP_OK;
+    if (offsets[0] != 0)
+        return fail(c, DP_E_ARG, "dp_triangulate: offsets[0] must be 0");
+    for (int64_t i = 0; i < n; ++i)
+        if (offsets[i + 1] < offsets[i] + 1)
+            return fail(c, DP_E_ARG, "dp_triangulate: every point needs at least one observation");
+    const int64_t m = offsets[n];
+    dp_seedgen *s = seedgen(c);
+    if (!s)
+        return fail(c, DP_E_OOM, "seedgen state");
+    DP_HIP(c, hipSetDevice(c->device));
+    DP_HIP(c, s->off.reserve((size_t)n + 1));
+    DP_HIP(c, s->P.reserve((size_t)m * 12));
+    DP_HIP(c, s->obs.reserve((size_t)m * 2));
+    DP_HIP(c, s->X.reserve((size_t)n * 3));
+    DP_HIP(c, hipMemcpyAsync(s->off.p, offsets, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    DP_HIP(c, hipMemcpyAsync(s->P.p, P, (size_t)m * 96, hipMemcpyHostToDevice, c->stream));
+    DP_HIP(c, hipMemcpyAsync(s->obs.p, obs, (size_t)m * 16, hipMemcpyHostToDevice, c->stream));
+    DP_HIP(c, dpk::launch_dlt_batch(n, s->off.p, s->P.p, s->obs.p, s->X.p, c->stream));
+    DP_HIP(c, hipMemcpyAsync(X, s->X.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// GenerateSeeds
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Timer {
+    hipEvent_t e = nullptr;
+    Timer() { hipEventCreate(&e); }
+    ~Timer() { hipEventDestroy(e); }
+};
+
+double ev_ms(hipEvent_t a, hipEvent_t b)
+{
+    float ms = 0.0f;
+    hipEventElapsedTime(&ms, a, b);
+    return (double)ms;
+}
+
+} // namespace
+
+// hipcub helpers on the context stream, temp storage in s->cub_tmp
+#define DP_CUB(c, s, call_with_tmp)                                                                \
+    do {                                                                                           \
+        size_t _bytes = 0;                                                                         \
+        void *_tmp = nullptr;                                                                      \
+        DP_HIP(c, (call_with_tmp));                                                                \
+        DP_HIP(c, (s)->cub_tmp.reserve(_bytes + 16));                                              \
+        _tmp = (s)->cub_tmp.p;                                                                     \
+        DP_HIP(c, (call_with_tmp));                                                                \
+    } while (0)
+
+static int check_matcher_options(dp_ctx *c, const dp_matcher_options &m)
+{
+    if (m.n_features < 0 || m.n_levels < 1 || m.n_levels > dpk::kOrbMaxLevels || !(m.scale_factor > 1.0) ||
+        m.edge_threshold < 19 || m.fast_threshold < 0 || m.fast_threshold > 254 || m.cell_size < 1 ||
+        m.max_keypoints_per_cell < 0 || (m.epipolar_matching != 0 && m.epipolar_matching != 1) ||
+        !(m.nn_match_ratio >= 0.0f) || !(m.max_epipolar_distance >= 0.0f))
+        return fail(c, DP_E_ARG, "dp_matcher_options: value out of range (edge_threshold >= 19, 1 <= n_levels <= 16)");
+    return DP_OK;
+}
+
+extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, const double **xyz_out, int64_t *n_out,
+                                 dp_seed_stats *stats)
+{
+    if (!c)
+        return DP_E_ARG;
+    if (!xyz_out || !n_out)
+        return fail(c, DP_E_ARG, "dp_generate_seeds: null output");
+    *xyz_out = nullptr;
+    *n_out = 0;
+    if (c->V < 1 || c->planes.empty())
+        return fail(c, DP_E_STATE, "dp_generate_seeds: no views set");
+    dp_matcher_options mo;
+    if (mo_in)
+        mo = *mo_in;
+    else
+        dp_default_matcher_options(&mo);
+    int rc = check_matcher_options(c, mo);
+    if (rc != DP_OK)
+        return rc;
+    dp_seedgen *s = seedgen(c);
+    if (!s)
+        return fail(c, DP_E_OOM, "seedgen state");
+    s->have_stages = false;
+    DP_HIP(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const auto t_wall0 = std::chrono::steady_clock::now();
+    const int V = c->V, L = mo.n_levels;
+    dp_seed_stats S{};
+
+    // ---- pyramid geometry (ORB_Impl: layerScale, level sizes, features/level)
+    std::vector<int32_t> nfeat(L);
+    dpk::orb_features_per_level(mo.n_features, mo.scale_factor, L, nfeat.data());
+    std::vector<dpk::OrbLevel> lv((size_t)V * L);
+    int64_t pool = 0, rows = 0;
+    int max_w = 0, max_h = 0;
+    std::vector<int32_t> vw(V), vh(V);
+    for (int v = 0; v < V; ++v) {
+        vw[v] = c->hv[v].W;
+        vh[v] = c->hv[v].H;
+        for (int l = 0; l < L; ++l) {
+            const float sc = (float)std::pow(mo.scale_factor, (double)l);
+            dpk::OrbLevel &o = lv[(size_t)v * L + l];
+            o.scale = sc;
+            o.w = l == 0 ? vw[v] : (int)std::lrint((float)vw[v] / sc);
+            o.h = l == 0 ? vh[v] : (int)std::lrint((float)vh[v] / sc);
+            if (o.w < 4 || o.h < 4)
+                return fail(c, DP_E_ARG, "dp_generate_seeds: pyramid level smaller than 4 px (reduce n_levels)");
+            o.off = pool;
+            o.row0 = rows;
+            o.nfeat = nfeat[l];
+            pool += (int64_t)o.w * o.h;
+            rows += o.h;
+            max_w = std::max(max_w, o.w);
+            max_h = std::max(max_h, o.h);
+        }
+    }
+    DP_HIP(c, s->lv.reserve(lv.size()));
+    DP_HIP(c, hipMemcpyAsync(s->lv.p, lv.data(), lv.size() * sizeof(dpk::OrbLevel), hipMemcpyHostToDevice, st));
+    DP_HIP(c, s->planes0.reserve(V));
+    DP_HIP(c, hipMemcpyAsync(s->planes0.p, c->planes[0].data(), (size_t)V * sizeof(dpk::PyrPlane), hipMemcpyHostToDevice,
+                             st));
+    DP_HIP(c, s->gray.reserve(pool));
+    DP_HIP(c, s->score.reserve(pool));
+    DP_HIP(c, s->blur.reserve(pool));
+    DP_HIP(c, s->htmp.reserve(pool));
+    DP_HIP(c, s->row_cnt.reserve(rows + 1));
+    DP_HIP(c, s->row_off.reserve(rows + 1));
+    dpk::OrbGeom g{s->lv.p, V, L, s->gray.p, s->blur.p, s->htmp.p};
+
+    Timer t0, t1, t2, t3, t4;
+    DP_HIP(c, hipEventRecord(t0.e, st));
+    // ---- DetectKeypoints (matcher.cpp:45-87)
+    DP_HIP(c, dpk::launch_orb_gray(s->planes0.p, g, lv[0].w > 0 ? max_w : 0, max_h, st));
+    for (int l = 1; l < L; ++l)
+        DP_HIP(c, dpk::launch_orb_resize(g, l, max_w, max_h, st));
+    for (int l = 0; l < L; ++l)
+        DP_HIP(c, dpk::launch_orb_fast(g, l, mo.fast_threshold, s->score.p, max_w, max_h, st));
+    DP_HIP(c, hipMemsetAsync(s->row_cnt.p, 0, (size_t)(rows + 1) * sizeof(int64_t), st));
+    // row counts as int32 into the low half of an int64 buffer would alias: count into idx_a
+    DP_HIP(c, s->idx_a.reserve(rows + 1));
+    DP_HIP(c, hipMemsetAsync(s->idx_a.p, 0, (size_t)(rows + 1) * sizeof(int32_t), st));
+    for (int l = 0; l < L; ++l)
+        DP_HIP(c, dpk::launch_orb_nms(g, l, s->score.p, mo.edge_threshold, nullptr, s->idx_a.p, nullptr, max_h, st));
+    DP_CUB(c, s, hipcub::DeviceScan::ExclusiveSum(_tmp, _bytes, s->idx_a.p, s->row_off.p, (int)(rows + 1), st));
+    int64_t n_cand = 0;
+    DP_HIP(c, hipMemcpyAsync(&n_cand, s->row_off.p + rows, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    DP_HIP(c, s->cand.reserve(n_cand + 1));
+    DP_HIP(c, s->cand2.reserve(n_cand + 1));
+    DP_HIP(c, s->flag.reserve(n_cand + 1));
+    DP_HIP(c, s->n_sel.reserve(1));
+    for (int l = 0; l < L; ++l)
+        DP_HIP(c, dpk::launch_orb_nms(g, l, s->score.p, mo.edge_threshold, s->row_off.p, nullptr, s->cand.p, max_h, st));
+    // retainBest(2 n_l) by FAST score
+    const int nseg = V * L;
+    DP_HIP(c, s->hist.reserve((size_t)nseg * 256));
+    DP_HIP(c, hipMemsetAsync(s->hist.p, 0, (size_t)nseg * 256 * 4, st));
+    DP_HIP(c, s->fthr.reserve(nseg));
+    DP_HIP(c, dpk::launch_orb_hist(s->cand.p, n_cand, s->hist.p, st));
+    DP_HIP(c, dpk::launch_orb_fast_thresh(g, s->hist.p, s->fthr.p, st));
+    DP_HIP(c, dpk::launch_orb_flag_fast(s->cand.p, n_cand, s->fthr.p, s->flag.p, st));
+    DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, s->cand.p, s->flag.p, s->cand2.p, s->n_sel.p,
+                                                (int)n_cand, st));
+    int64_t n2 = 0;
+    DP_HIP(c, hipMemcpyAsync(&n2, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    // Harris responses, retainBest(n_l)
+    DP_HIP(c, s->hkey.reserve(n2 + 1));
+    DP_HIP(c, s->hkey_sorted.reserve(n2 + 1));
+    DP_HIP(c, s->seg_cnt.reserve(nseg + 1));
+    DP_HIP(c, s->seg_off.reserve(nseg + 1));
+    DP_HIP(c, s->seg_off32.reserve(nseg + 1));
+    DP_HIP(c, s->hthr.reserve(nseg));
+    DP_HIP(c, s->keep_all.reserve(nseg));
+    DP_HIP(c, hipMemsetAsync(s->seg_cnt.p, 0, (size_t)(nseg + 1) * 4, st));
+    DP_HIP(c, dpk::launch_orb_harris(g, s->cand2.p, n2, s->hkey.p, s->seg_cnt.p, st));
+    DP_CUB(c, s, hipcub::DeviceScan::ExclusiveSum(_tmp, _bytes, s->seg_cnt.p, s->seg_off32.p, nseg + 1, st));
+    DP_CUB(c, s, hipcub::DeviceScan::ExclusiveSum(_tmp, _bytes, s->seg_cnt.p, s->seg_off.p, nseg + 1, st));
+    if (n2 > 0)
+        DP_CUB(c, s, hipcub::DeviceSegmentedRadixSort::SortKeys(_tmp, _bytes, s->hkey.p, s->hkey_sorted.p, (int)n2, nseg,
+                                                                 s->seg_off32.p, s->seg_off32.p + 1, 0, 32, st));
+    DP_HIP(c, dpk::launch_orb_harris_thresh(g, s->hkey_sorted.p, s->seg_off.p, s->hthr.p, s->keep_all.p, st));
+    DP_HIP(c, dpk::launch_orb_flag_harris(s->cand2.p, n2, s->hthr.p, s->keep_all.p, s->flag.p, st));
+    DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, s->cand2.p, s->flag.p, s->cand.p, s->n_sel.p, (int)n2,
+                                                st));
+    int64_t n3 = 0;
+    DP_HIP(c, hipMemcpyAsync(&n3, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    // angles, level-0 coordinates
+    std::vector<int32_t> umax(dpk::kOrbHalfPatch + 2);
+    dpk::orb_umax(umax.data());
+    DP_HIP(c, s->umax.reserve(umax.size()));
+    DP_HIP(c, hipMemcpyAsync(s->umax.p, umax.data(), umax.size() * 4, hipMemcpyHostToDevice, st));
+    DP_HIP(c, s->kp_a.reserve(n3 + 1));
+    DP_HIP(c, s->kp_b.reserve(n3 + 1));
+    DP_HIP(c, s->kv_a.reserve(n3 + 1));
+    DP_HIP(c, s->kv_b.reserve(n3 + 1));
+    DP_HIP(c, dpk::launch_orb_angle(g, s->cand.p, n3, s->umax.p, s->kp_a.p, s->kv_a.p, st));
+    S.keypoints_detected = n3;
+
+    // ---- FilterKeypoints (matcher.cpp:89-153)
+    std::vector<int32_t> gcols(V);
+    std::vector<int64_t> cell_off(V + 1, 0);
+    for (int v = 0; v < V; ++v) {
+        gcols[v] = (vw[v] + mo.cell_size - 1) / mo.cell_size;
+        const int64_t grows = (vh[v] + mo.cell_size - 1) / mo.cell_size;
+        if ((int64_t)gcols[v] * grows >= (1ll << 24))
+            return fail(c, DP_E_ARG, "dp_generate_seeds: more than 2^24 keypoint cells per view");
+        cell_off[v + 1] = cell_off[v] + (int64_t)gcols[v] * grows;
+    }
+    DP_HIP(c, s->gcols.reserve(V));
+    DP_HIP(c, s->cell_off.reserve(V + 1));
+    DP_HIP(c, s->cell_cnt.reserve(cell_off[V] + 1));
+    DP_HIP(c, hipMemcpyAsync(s->gcols.p, gcols.data(), V * 4, hipMemcpyHostToDevice, st));
+    DP_HIP(c, hipMemcpyAsync(s->cell_off.p, cell_off.data(), (V + 1) * 8, hipMemcpyHostToDevice, st));
+    DP_HIP(c, hipMemsetAsync(s->cell_cnt.p, 0, (size_t)(cell_off[V] + 1) * 4, st));
+    DP_HIP(c, s->ckey.reserve(n3 + 1));
+    DP_HIP(c, s->ckey_sorted.reserve(n3 + 1));
+    DP_HIP(c, s->idx_a.reserve(n3 + 1));
+    DP_HIP(c, s->idx_b.reserve(n3 + 1));
+    DP_HIP(c, s->flag.reserve(n3 + 1));
+    DP_HIP(c, dpk::launch_cell_count(s->kp_a.p, s->kv_a.p, n3, s->gcols.p, s->cell_off.p, mo.cell_size, s->cell_cnt.p,
+                                     st));
+    DP_HIP(c, dpk::launch_cell_key(s->kp_a.p, s->kv_a.p, n3, s->gcols.p, s->cell_off.p, mo.cell_size,
+                                   mo.max_keypoints_per_cell, s->cell_cnt.p, s->ckey.p, s->idx_a.p, st));
+    if (n3 > 0)
+        DP_CUB(c, s, hipcub::DeviceRadixSort::SortPairs(_tmp, _bytes, s->ckey.p, s->ckey_sorted.p, s->idx_a.p,
+                                                         s->idx_b.p, (int)n3, 0, 64, st));
+    DP_HIP(c, dpk::launch_cell_keep(s->ckey_sorted.p, n3, mo.max_keypoints_per_cell, s->flag.p, st));
+    DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, s->idx_b.p, s->flag.p, s->idx_a.p, s->n_sel.p, (int)n3,
+                                                st));
+    int64_t n4 = 0;
+    DP_HIP(c, hipMemcpyAsync(&n4, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    DP_HIP(c, dpk::launch_gather_kp(s->kp_a.p, s->kv_a.p, s->idx_a.p, n4, s->kp_b.p, s->kv_b.p, st));
+
+    // ---- ComputeDescriptors (matcher.cpp:155-183): runByImageBorder, stable by octave
+    DP_HIP(c, s->vw.reserve(V));
+    DP_HIP(c, s->vh.reserve(V));
+    DP_HIP(c, hipMemcpyAsync(s->vw.p, vw.data(), V * 4, hipMemcpyHostToDevice, st));
+    DP_HIP(c, hipMemcpyAsync(s->vh.p, vh.data(), V * 4, hipMemcpyHostToDevice, st));
+    DP_HIP(c, s->okey.reserve(n4 + 1));
+    DP_HIP(c, s->okey_sorted.reserve(n4 + 1));
+    DP_HIP(c, dpk::launch_desc_prep(s->kp_b.p, s->kv_b.p, s->vw.p, s->vh.p, n4, mo.edge_threshold, s->flag.p,
+                                    s->okey.p, st));
+    {
+        hipcub::CountingInputIterator<int32_t> iota(0);
+        DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, iota, s->flag.p, s->idx_a.p, s->n_sel.p, (int)n4, st));
+    }
+    int64_t n5 = 0;
+    DP_HIP(c, hipMemcpyAsync(&n5, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    DP_HIP(c, dpk::launch_gather_kp(s->kp_b.p, s->kv_b.p, s->idx_a.p, n5, s->kp_a.p, s->kv_a.p, st));
+    DP_HIP(c, dpk::launch_desc_prep(s->kp_a.p, s->kv_a.p, s->vw.p, s->vh.p, n5, mo.edge_threshold, s->flag.p,
+                                    s->okey.p, st));
+    DP_HIP(c, dpk::launch_iota(s->idx_a.p, n5, st));
+    if (n5 > 0)
+        DP_CUB(c, s, hipcub::DeviceRadixSort::SortPairs(_tmp, _bytes, s->okey.p, s->okey_sorted.p, s->idx_a.p,
+                                                         s->idx_b.p, (int)n5, 0, 16, st));
+    DP_HIP(c, dpk::launch_gather_kp(s->kp_a.p, s->kv_a.p, s->idx_b.p, n5, s->kp_b.p, s->kv_b.p, st));
+    S.keypoints = n5;
+    // per-view counts (host)
+    s->h_kp.resize(n5);
+    std::vector<int32_t> h_kv(n5);
+    DP_HIP(c, hipMemcpyAsync(s->h_kp.data(), s->kp_b.p, n5 * sizeof(dp_keypoint), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipMemcpyAsync(h_kv.data(), s->kv_b.p, n5 * 4, hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipEventRecord(t1.e, st));
+    // descriptors
+    for (int l = 0; l < L; ++l)
+        DP_HIP(c, dpk::launch_orb_blur(g, l, max_w, max_h, st));
+    std::vector<int8_t> pat(4 * dpk::kOrbPatternPairs);
+    dpk::orb_pattern(pat.data());
+    DP_HIP(c, s->pattern.reserve(pat.size()));
+    DP_HIP(c, hipMemcpyAsync(s->pattern.p, pat.data(), pat.size(), hipMemcpyHostToDevice, st));
+    DP_HIP(c, s->desc.reserve((size_t)(n5 + 1) * 8));
+    DP_HIP(c, dpk::launch_orb_desc(g, s->kp_b.p, s->kv_b.p, n5, s->pattern.p, s->desc.p, st));
+    DP_HIP(c, hipEventRecord(t2.e, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    s->h_kp_off.assign(V + 1, 0);
+    for (int64_t i = 0; i < n5; ++i)
+        s->h_kp_off[h_kv[i] + 1]++;
+    for (int v = 0; v < V; ++v)
+        s->h_kp_off[v + 1] += s->h_kp_off[v];
+    for (int v = 0; v < V; ++v)
+        if (s->h_kp_off[v + 1] - s->h_kp_off[v] >= (1 << 22))
+            return fail(c, DP_E_ARG, "dp_generate_seeds: more than 2^22 keypoints in one view");
+
+    // ---- DefaultPairsList + MatchKeypoints + FilterMatches
+    s->h_pairs.clear();
+    s->h_jobs.clear();
+    int64_t q_total = 0, t2q_total = 0;
+    for (int i = 0; i < V; ++i)
+        for (int j = i + 1; j < V; ++j) {
+            dpk::SeedPair pr{};
+            if (dp_fundamental_matrix(c->P0.data() + 12 * i, c->P0.data() + 12 * j, pr.F) != DP_OK)
+                return fail(c, DP_E_ARG, "dp_generate_seeds: degenerate projection matrix");
+            pr.first = i;
+            pr.second = j;
+            pr.t2q_off = t2q_total;
+            dpk::KnnJob jb{};
+            jb.q_off = s->h_kp_off[i];
+            jb.t_off = s->h_kp_off[j];
+            jb.out_off = q_total;
+            jb.nq = (int32_t)(s->h_kp_off[i + 1] - s->h_kp_off[i]);
+            jb.nt = (int32_t)(s->h_kp_off[j + 1] - s->h_kp_off[j]);
+            q_total += jb.nq;
+            t2q_total += jb.nt;
+            s->h_pairs.push_back(pr);
+            s->h_jobs.push_back(jb);
+        }
+    const int np = (int)s->h_pairs.size();
+    S.pairs = np;
+    DP_HIP(c, s->pairs.reserve(np + 1));
+    DP_HIP(c, s->jobs.reserve(np + 1));
+    DP_HIP(c, s->q2t.reserve(q_total + 1));
+    DP_HIP(c, s->t2q.reserve(t2q_total + 1));
+    DP_HIP(c, s->keys.reserve((size_t)2 * (q_total + 1)));
+    DP_HIP(c, s->counters.reserve(2));
+    if (np > 0) {
+        DP_HIP(c, hipMemcpyAsync(s->pairs.p, s->h_pairs.data(), np * sizeof(dpk::SeedPair), hipMemcpyHostToDevice, st));
+        DP_HIP(c, hipMemcpyAsync(s->jobs.p, s->h_jobs.data(), np * sizeof(dpk::KnnJob), hipMemcpyHostToDevice, st));
+    }
+    static_assert(dpk::kNoMatch == 0x7F7F7F7F, "t2q sentinel is the 0x7F byte fill");
+    DP_HIP(c, hipMemsetAsync(s->t2q.p, 0x7F, (size_t)(t2q_total + 1) * 4, st)); // kNoMatch > any index
+    DP_HIP(c, hipMemsetAsync(s->counters.p, 0, 2 * sizeof(unsigned long long), st));
+    dpk::MatchArgs ma{s->jobs.p, s->pairs.p, np, q_total, s->keys.p, s->desc.p, s->kp_b.p,
+                      mo.nn_match_ratio, mo.max_epipolar_distance, s->q2t.p, s->t2q.p, s->counters.p,
+                      s->counters.p + 1};
+    if (mo.epipolar_matching) {
+        DP_HIP(c, dpk::launch_epipolar_match(ma, st));
+    } else {
+        std::vector<int2> blocks;
+        knn_blocks(s->h_jobs, blocks);
+        DP_HIP(c, s->blocks.reserve(blocks.size() + 1));
+        if (!blocks.empty())
+            DP_HIP(c, hipMemcpyAsync(s->blocks.p, blocks.data(), blocks.size() * sizeof(int2), hipMemcpyHostToDevice,
+                                     st));
+        dpk::KnnArgs ka{s->desc.p, s->jobs.p, s->blocks.p, s->keys.p};
+        DP_HIP(c, dpk::launch_knn(ka, (int)blocks.size(), st));
+        DP_HIP(c, dpk::launch_match(ma, st));
+    }
+    DP_HIP(c, hipEventRecord(t3.e, st));
+
+    // ---- TriangulateMatches (matcher.cpp:415-450)
+    DP_HIP(c, s->kp_off.reserve(V + 1));
+    DP_HIP(c, hipMemcpyAsync(s->kp_off.p, s->h_kp_off.data(), (V + 1) * 8, hipMemcpyHostToDevice, st));
+    DP_HIP(c, s->P.reserve((size_t)V * 12));
+    DP_HIP(c, hipMemcpyAsync(s->P.p, c->P0.data(), (size_t)V * 96, hipMemcpyHostToDevice, st));
+    DP_HIP(c, s->X.reserve((size_t)3 * (n5 + 1)));
+    DP_HIP(c, s->obs.reserve((size_t)3 * (n5 + 1)));
+    DP_HIP(c, s->valid.reserve(n5 + 1));
+    dpk::TriangArgs ta{V, np, n5, s->kp_off.p, s->kp_b.p, s->P.p, s->jobs.p, s->pairs.p, s->q2t.p, s->t2q.p,
+                       s->X.p, s->valid.p};
+    DP_HIP(c, dpk::launch_triang(ta, st));
+    {
+        struct P3 {
+            double x, y, z;
+        };
+        DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, reinterpret_cast<P3 *>(s->X.p), s->valid.p,
+                                                    reinterpret_cast<P3 *>(s->obs.p), s->n_sel.p, (int)n5, st));
+    }
+    DP_HIP(c, hipEventRecord(t4.e, st));
+    int64_t n6 = 0;
+    unsigned long long cnt[2] = {0, 0};
+    DP_HIP(c, hipMemcpyAsync(&n6, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipMemcpyAsync(cnt, s->counters.p, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    s->h_xyz.resize((size_t)3 * n6);
+    s->h_desc.resize((size_t)32 * n5);
+    s->h_q2t.resize(q_total);
+    DP_HIP(c, hipMemcpyAsync(s->h_xyz.data(), s->obs.p, (size_t)n6 * 24, hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipMemcpyAsync(s->h_desc.data(), s->desc.p, (size_t)n5 * 32, hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipMemcpyAsync(s->h_q2t.data(), s->q2t.p, (size_t)q_total * 4, hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    S.ratio_matches = (int64_t)cnt[0];
+    S.matches = (int64_t)cnt[1];
+    S.points = n6;
+    S.detect_ms = ev_ms(t0.e, t1.e);
+    S.describe_ms = ev_ms(t1.e, t2.e);
+    S.match_ms = ev_ms(t2.e, t3.e);
+    S.triangulate_ms = ev_ms(t3.e, t4.e);
+    S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wall0).count();
+    s->have_stages = true;
+    if (stats)
+        *stats = S;
+    *xyz_out = s->h_xyz.data();
+    *n_out = n6;
+    return DP_OK;
+}
+
+extern "C" int dp_seed_keypoints(dp_ctx *c, int view, const dp_keypoint **kp, const uint8_t **desc32, int64_t *n)
+{
+    if (!c)
+        return DP_E_ARG;
+    dp_seedgen *s = c->seeds;
+    if (!s || !s->have_stages)
+        return fail(c, DP_E_STATE, "dp_seed_keypoints: no dp_generate_seeds result");
+    if (view < 0 || view >= (int)s->h_kp_off.size() - 1 || !n)
+        return fail(c, DP_E_ARG, "dp_seed_keypoints: bad view");
+    const int64_t a = s->h_kp_off[view], b = s->h_kp_off[view + 1];
+    if (kp)
+        *kp = s->h_kp.data() + a;
+    if (desc32)
+        *desc32 = s->h_desc.data() + 32 * a;
+    *n = b - a;
+    return DP_OK;
+}
+
+extern "C" int dp_seed_matches(dp_ctx *c, int pair, int32_t *first, int32_t *second, const int32_t **q2t, int64_t *nq)
+{
+    if (!c)
+        return DP_E_ARG;
+    dp_seedgen *s = c->seeds;
+    if (!s || !s->have_stages)
+        return fail(c, DP_E_STATE, "dp_seed_matches: no dp_generate_seeds result");
+    if (pair < 0 || pair >= (int)s->h_pairs.size())
+        return fail(c, DP_E_ARG, "dp_seed_matches: bad pair");
+    if (first)
+        *first = s->h_pairs[pair].first;
+    if (second)
+        *second = s->h_pairs[pair].second;
+    if (q2t)
+        *q2t = s->h_q2t.data() + s->h_jobs[pair].out_off;
+    if (nq)
+        *nq = s->h_jobs[pair].nq;
+    return DP_OK;
+}

@@ -367,12 +367,23 @@ class PMVS:
             return
         self.views.append(view)
 
-    def run(self, seeds_xyz, filter_passes: int = 0) -> bool:
-        """PMVS::Run (pmvs.cpp:22-43) minus matching; filter_passes != 0 then
-        applies FilterPatches (pmvs.h:27; spec in dp_filter_patches)."""
+    def run(self, seeds_xyz=None, filter_passes: int = 0, matcher_options=None) -> bool:
+        """PMVS::Run (pmvs.cpp:22-43).  With seeds_xyz None the seeds come from
+        Matcher::GenerateSeeds on the device (PMVS::InsertSeeds, pmvs.cpp:29-34);
+        filter_passes != 0 then applies FilterPatches (pmvs.h:27; spec in
+        dp_filter_patches)."""
+        from .matcher import Matcher
+
         with Engine(self.options, self.device) as eng:
             eng.set_views(self.views)
+            seed_stats = None
+            if seeds_xyz is None:
+                m = Matcher(eng, matcher_options)
+                seeds_xyz = m.generate_seeds()
+                seed_stats = m.stats
             self.patches, self.stats = eng.densify(np.asarray(seeds_xyz, dtype=np.float64))
+            if seed_stats is not None:
+                self.stats["seed_generation"] = seed_stats
             if filter_passes:
                 keep = eng.filter_patches(self.patches, filter_passes)
                 self.stats["filtered_out"] = int(len(keep) - keep.sum())

@@ -269,6 +269,82 @@ int dp_filter_patches(dp_ctx *ctx, const dp_patch *patches, int64_t n, const dp_
 int dp_filter_patches_device(dp_ctx *ctx, const dp_patch *d_patches, int64_t n, const dp_filter_options *fo,
                              uint8_t *d_keep, void *stream);
 
+/* ---- seed generation: Features::Matcher::GenerateSeeds ---
+ * modules/features/matcher.cpp:18-43 with the default MatcherOptions
+ * (matcher.h:21-32: ORB detector, kNN matcher, no direct epipolar matching,
+ * 1.5 px epipolar distance, 16 px cells, 4 keypoints per cell).  Stages:
+ *   DetectKeypoints   matcher.cpp:45-87   ORB::create(40000)->detect
+ *   FilterKeypoints   matcher.cpp:89-153  per-cell best responses
+ *   ComputeDescriptors matcher.cpp:155-183 ORB::create()->compute (rBRIEF)
+ *   DefaultPairsList  matcher.cpp:185-204 (0,1),(0,2),..,(1,2),.. lexicographic
+ *   MatchKeypoints    matcher.cpp:206-265 BruteForce-Hamming knnMatch k=2,
+ *                                         d0 < 0.7f * d1
+ *   FilterMatches     matcher.cpp:319-372 epipolar distance <= 1.5f, F from
+ *                                         geometry/fundamental_matrix.cpp:6-53
+ *   TriangulateMatches matcher.cpp:374-450 DLT, geometry/triangulation.cpp:15-34
+ * OpenCV's ORB is restated, not reproduced bit-for-bit (OpenCV is absent from
+ * the image; DESIGN.md "Seed generation" lists the restated semantics and the
+ * points that are parity-unpinned, e.g. the rBRIEF sampling pattern).  The
+ * reference's unspecified orders (nth_element, omp critical push_back) are
+ * fixed here: keypoints in (level, y, x) order, per-cell picks by (response
+ * desc, index), seed points in (view, keypoint) order. */
+typedef struct dp_matcher_options {
+    int32_t n_features;             /* 40000 ORB::create(40000) matcher.cpp:62        */
+    int32_t n_levels;               /* 8     cv::ORB default                          */
+    double scale_factor;            /* 1.2   cv::ORB default                          */
+    int32_t edge_threshold;         /* 31    cv::ORB default (border excluded)        */
+    int32_t fast_threshold;         /* 20    cv::ORB default                          */
+    int32_t cell_size;              /* 16    MatcherOptions::cell_size matcher.h:25   */
+    int32_t max_keypoints_per_cell; /* 4     matcher.h:26                             */
+    int32_t epipolar_matching;      /* 0     matcher.h:23 (1: DirectEpipolarMatching) */
+    float max_epipolar_distance;    /* 1.5f  matcher.h:24                             */
+    float nn_match_ratio;           /* 0.7f  matcher.cpp:217                          */
+    int32_t reserved;
+} dp_matcher_options;
+
+/* the cv::KeyPoint fields the matcher reads (pt, response, angle, octave) */
+typedef struct dp_keypoint {
+    float x, y;        /* level-0 pixels                                        */
+    float response;    /* Harris response (ORB HARRIS_SCORE)                    */
+    float angle;       /* degrees, intensity-centroid orientation              */
+    int32_t octave;    /* pyramid level                                        */
+    int32_t reserved;
+} dp_keypoint;
+
+typedef struct dp_seed_stats {
+    int64_t keypoints_detected;  /* after detect, all views                         */
+    int64_t keypoints;           /* after FilterKeypoints                           */
+    int64_t pairs;               /* view pairs                                      */
+    int64_t ratio_matches;       /* kNN ratio-test survivors, all pairs             */
+    int64_t matches;             /* after the epipolar filter                       */
+    int64_t points;              /* triangulated seed points                        */
+    double detect_ms, describe_ms, match_ms, triangulate_ms, total_ms;
+} dp_seed_stats;
+
+void dp_default_matcher_options(dp_matcher_options *mo);
+/* GenerateSeeds over the context's level-0 views.  *xyz_out (n x 3 doubles)
+ * is context-owned, valid until the next dp_generate_seeds or destroy. */
+int dp_generate_seeds(dp_ctx *ctx, const dp_matcher_options *mo, const double **xyz_out, int64_t *n_out,
+                      dp_seed_stats *stats);
+/* Stage results of the last dp_generate_seeds (context-owned, host copies). */
+int dp_seed_keypoints(dp_ctx *ctx, int view, const dp_keypoint **kp, const uint8_t **desc32, int64_t *n);
+int dp_seed_matches(dp_ctx *ctx, int pair, int32_t *first, int32_t *second, const int32_t **query_to_train,
+                    int64_t *nq);
+
+/* Standalone operators of the path.
+ * BFMatcher(NORM_HAMMING).knnMatch(query, train, k=2) on 32-byte descriptors:
+ * idx2/dist2 (nq x 2) hold the two nearest train rows by (distance, index);
+ * -1 / -1 where train has fewer rows.  nt < 2^22. */
+int dp_knn_match(dp_ctx *ctx, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt,
+                 int32_t *idx2, int32_t *dist2);
+/* Geometry::ComputeFundamentalMatrix (fundamental_matrix.cpp:6-34), F 3x3 row-major. */
+int dp_fundamental_matrix(const double P1[12], const double P2[12], double F[9]);
+/* Geometry::DirectLinearTriangulation (triangulation.cpp:15-34), batched: point
+ * i uses observations offsets[i] .. offsets[i+1]-1 (P: 12 doubles, obs: x, y
+ * cast to float as the reference does). */
+int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const double *P, const double *obs,
+                   double *X);
+
 /* Elapsed device milliseconds of the most recent refine kernel launch, timed
  * with HIP events on the stream the kernel ran on. */
 int dp_last_kernel_ms(dp_ctx *ctx, double *ms);

@@ -88,6 +88,19 @@ def _load():
         "or_org_insert": (ctypes.c_int, [P, P, ctypes.c_uint32, ctypes.c_uint32, P]),
         "or_pyr_down": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, P]),
         "or_filter_patches": (ctypes.c_int, [P, P, ctypes.c_int64, ctypes.c_int, ctypes.c_double, P]),
+        # seed generation (or_seeds.c)
+        "or_orb_pattern": (None, [P]),
+        "or_features_per_level": (None, [ctypes.c_int, ctypes.c_double, ctypes.c_int, P]),
+        "or_knn_match": (ctypes.c_int, [P, ctypes.c_int64, P, ctypes.c_int64, P, P]),
+        "or_fundamental_matrix": (ctypes.c_int, [P, P, P]),
+        "or_epipolar_distance": (ctypes.c_float, [P, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+        "or_triangulate": (None, [ctypes.c_int64, P, P, P, P]),
+        "or_seeds_run": (P, [ctypes.c_int, P, P, P, P, P]),
+        "or_seeds_free": (None, [P]),
+        "or_seeds_counts": (None, [P, P]),
+        "or_seeds_view": (ctypes.c_int64, [P, ctypes.c_int, P, P]),
+        "or_seeds_pair": (ctypes.c_int64, [P, ctypes.c_int, P, P]),
+        "or_seeds_points": (None, [P, P]),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)
@@ -311,3 +324,121 @@ def level_scene(P, images, level):
         imgs = [pyr_down(im) for im in imgs]
     P[:, :2, :] *= 2.0 ** -level
     return P, imgs
+
+
+# ---------------------------------------------------------------------------
+# seed generation (or_seeds.c): Matcher::GenerateSeeds restated
+# ---------------------------------------------------------------------------
+class OrMatcherOptions(ctypes.Structure):
+    _fields_ = [
+        ("n_features", ctypes.c_int32),
+        ("n_levels", ctypes.c_int32),
+        ("scale_factor", ctypes.c_double),
+        ("edge_threshold", ctypes.c_int32),
+        ("fast_threshold", ctypes.c_int32),
+        ("cell_size", ctypes.c_int32),
+        ("max_keypoints_per_cell", ctypes.c_int32),
+        ("epipolar_matching", ctypes.c_int32),
+        ("max_epipolar_distance", ctypes.c_float),
+        ("nn_match_ratio", ctypes.c_float),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+KEYPOINT_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("angle", "<f4"), ("octave", "<i4"), ("reserved", "<i4")]
+)
+
+
+def matcher_options(**kw) -> OrMatcherOptions:
+    o = OrMatcherOptions(n_features=40000, n_levels=8, scale_factor=1.2, edge_threshold=31, fast_threshold=20,
+                         cell_size=16, max_keypoints_per_cell=4, epipolar_matching=0, max_epipolar_distance=1.5,
+                         nn_match_ratio=0.7)
+    for k, v in kw.items():
+        setattr(o, k, int(v) if isinstance(v, bool) else v)
+    return o
+
+
+def orb_pattern() -> np.ndarray:
+    a = np.zeros(1024, dtype=np.int8)
+    lib.or_orb_pattern(_p(a))
+    return a.reshape(512, 2)
+
+
+def features_per_level(n, sf, L) -> np.ndarray:
+    a = np.zeros(L, dtype=np.int32)
+    lib.or_features_per_level(n, sf, L, _p(a))
+    return a
+
+
+def knn_match(q: np.ndarray, t: np.ndarray):
+    q = np.ascontiguousarray(q, dtype=np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(t, dtype=np.uint8).reshape(-1, 32)
+    idx = np.zeros((len(q), 2), dtype=np.int32)
+    dist = np.zeros((len(q), 2), dtype=np.int32)
+    lib.or_knn_match(_p(q), len(q), _p(t), len(t), _p(idx), _p(dist))
+    return idx, dist
+
+
+def fundamental_matrix(P1, P2) -> np.ndarray:
+    a = np.ascontiguousarray(P1, dtype=np.float64).reshape(12)
+    b = np.ascontiguousarray(P2, dtype=np.float64).reshape(12)
+    F = np.zeros(9)
+    lib.or_fundamental_matrix(_p(a), _p(b), _p(F))
+    return F.reshape(3, 3)
+
+
+def epipolar_distance(F, x1, y1, x2, y2) -> float:
+    f = np.ascontiguousarray(F, dtype=np.float64).reshape(9)
+    return lib.or_epipolar_distance(_p(f), x1, y1, x2, y2)
+
+
+def triangulate(projections: list, observations: list) -> np.ndarray:
+    off = np.zeros(len(projections) + 1, dtype=np.int32)
+    off[1:] = np.cumsum([len(p) for p in projections])
+    P = np.ascontiguousarray(np.concatenate([np.asarray(p, dtype=np.float64).reshape(-1, 12) for p in projections]))
+    obs = np.ascontiguousarray(np.concatenate([np.asarray(o, dtype=np.float64).reshape(-1, 2) for o in observations]))
+    X = np.zeros((len(projections), 3))
+    lib.or_triangulate(len(projections), _p(off), _p(P), _p(obs), _p(X))
+    return X
+
+
+def seeds_run(P: np.ndarray, images: list, mo: OrMatcherOptions | None = None) -> dict:
+    """Full GenerateSeeds on BGR8 images (H x W x 3); every stage's output."""
+    mo = mo or matcher_options()
+    V = len(images)
+    P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(V, 12))
+    imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+    W = np.array([im.shape[1] for im in imgs], dtype=np.int32)
+    H = np.array([im.shape[0] for im in imgs], dtype=np.int32)
+    ptrs = (ctypes.c_void_p * V)(*[im.ctypes.data for im in imgs])
+    h = lib.or_seeds_run(V, _p(P), _p(W), _p(H), ptrs, ctypes.byref(mo))
+    if not h:
+        raise ValueError("or_seeds_run: image too small for the pyramid")
+    try:
+        c = np.zeros(7, dtype=np.int64)
+        lib.or_seeds_counts(h, _p(c))
+        out = {"counts": dict(zip(["views", "pairs", "detected", "keypoints", "ratio_matches", "matches", "points"],
+                                  c.tolist())),
+               "keypoints": [], "descriptors": [], "pairs": [], "q2t": []}
+        for v in range(V):
+            n = lib.or_seeds_view(h, v, None, None)
+            kp = np.zeros(n, dtype=KEYPOINT_DTYPE)
+            d = np.zeros((n, 32), dtype=np.uint8)
+            lib.or_seeds_view(h, v, _p(kp), _p(d))
+            out["keypoints"].append(kp)
+            out["descriptors"].append(d)
+        for p in range(int(c[1])):
+            n = lib.or_seeds_pair(h, p, None, None)
+            fs = np.zeros(2, dtype=np.int32)
+            q = np.zeros(n, dtype=np.int32)
+            lib.or_seeds_pair(h, p, _p(fs), _p(q))
+            out["pairs"].append((int(fs[0]), int(fs[1])))
+            out["q2t"].append(q)
+        pts = np.zeros((int(c[6]), 3))
+        if len(pts):
+            lib.or_seeds_points(h, _p(pts))
+        out["points"] = pts
+        return out
+    finally:
+        lib.or_seeds_free(h)

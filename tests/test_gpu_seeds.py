@@ -1,0 +1,177 @@
+"""GPU parity of seed generation (Features::Matcher::GenerateSeeds,
+modules/features/matcher.cpp:18-474): the HIP path through the C ABI against
+the oracle (oracle/or_seeds.c) on the same inputs, bit-exact on every stage --
+keypoints (coordinates, response, angle, octave, order), descriptors, the
+query->train match table of every pair, and the triangulated points."""
+import os
+
+import numpy as np
+import pytest
+
+import densepoints_amd as dp
+from densepoints_amd import matcher as M
+from densepoints_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def engine_with(P, imgs):
+    eng = dp.Engine()
+    eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(imgs))])
+    return eng
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+def compare_run(eng, r, mo_kw, V):
+    m = M.Matcher(eng, M.MatcherOptions(**mo_kw))
+    pts = m.generate_seeds()
+    c = r["counts"]
+    st = m.stats
+    assert (st["keypoints_detected"], st["keypoints"], st["ratio_matches"], st["matches"], st["points"]) == \
+        (c["detected"], c["keypoints"], c["ratio_matches"], c["matches"], c["points"]), (st, c)
+    for v in range(V):
+        kp, d = m.keypoints(v)
+        ok, od = r["keypoints"][v], r["descriptors"][v]
+        assert len(kp) == len(ok), f"view {v}: {len(kp)} vs {len(ok)} keypoints"
+        bad = np.flatnonzero((bits(kp).reshape(len(kp), -1) != bits(ok).reshape(len(ok), -1)).any(axis=1))
+        assert bad.size == 0, f"view {v}: keypoints differ at {bad[:5]}: {kp[bad[:3]]} vs {ok[bad[:3]]}"
+        assert np.array_equal(d, od), f"view {v}: descriptors differ"
+    for p, (a, b) in enumerate(r["pairs"]):
+        fa, fb, q2t = m.matches(p)
+        assert (fa, fb) == (a, b)
+        assert np.array_equal(q2t, r["q2t"][p]), f"pair {p}: match tables differ"
+    assert np.array_equal(bits(pts), bits(r["points"]))
+    return m
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_generate_seeds_matches_oracle(orc, kind):
+    cfg = synth.config(n_views=4, width=640, height=480, kind=kind)
+    P, imgs, _ = synth.scene_host(cfg)
+    kw = dict(n_features=5000, fast_threshold=10)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    with engine_with(P, imgs) as eng:
+        m = compare_run(eng, r, kw, 4)
+        assert m.stats["points"] > 300
+
+
+def test_generate_seeds_reference_defaults(orc):
+    """ORB::create(40000), 8 levels, FAST 20 -- the reference's own settings."""
+    cfg = synth.config(n_views=3, width=960, height=720, kind=1)
+    P, imgs, _ = synth.scene_host(cfg)
+    r = orc.seeds_run(P, imgs, orc.matcher_options())
+    with engine_with(P, imgs) as eng:
+        compare_run(eng, r, {}, 3)
+
+
+def test_generate_seeds_direct_epipolar(orc):
+    """DirectEpipolarMatching (matcher.cpp:267-317, epipolar_matching = true)."""
+    cfg = synth.config(n_views=3, width=320, height=240, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    kw = dict(n_features=600, n_levels=3, fast_threshold=8, epipolar_matching=True)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    with engine_with(P, imgs) as eng:
+        compare_run(eng, r, kw, 3)
+
+
+def test_generate_seeds_golden_fixture():
+    g = np.load(os.path.join(ROOT, "tests", "golden", "seeds_small.npz"))
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("mgs", os.path.join(ROOT, "tests", "golden", "make_golden_seeds.py"))
+    mgs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mgs)
+    with engine_with(g["P"], list(g["images"])) as eng:
+        m = M.Matcher(eng, M.MatcherOptions(**mgs.OPTIONS))
+        pts = m.generate_seeds()
+        kps = np.concatenate([m.keypoints(v)[0] for v in range(3)])
+        desc = np.concatenate([m.keypoints(v)[1] for v in range(3)])
+        q2t = np.concatenate([m.matches(p)[2] for p in range(3)])
+    assert np.array_equal(bits(kps), bits(g["keypoints"]))
+    assert np.array_equal(desc, g["descriptors"])
+    assert np.array_equal(q2t, g["q2t"])
+    assert np.array_equal(bits(pts), bits(g["points"]))
+
+
+def _random_desc(rng, n, pool=None):
+    d = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    if pool is not None and len(pool) and n:
+        k = rng.integers(0, len(pool), size=n // 3)
+        d[: len(k)] = pool[k]
+        # near-duplicates: one flipped bit (distance 1 ties across rows)
+        d[len(k): 2 * len(k)] = pool[k] ^ np.eye(32, dtype=np.uint8)[rng.integers(0, 32, len(k))]
+    return d
+
+
+@pytest.mark.parametrize("nq,nt", [(1, 0), (5, 1), (33, 2), (257, 31), (300, 33), (513, 129), (1000, 4099),
+                                   (4096, 3000)])
+def test_knn_match_matches_oracle(orc, nq, nt):
+    rng = np.random.default_rng(nq * 7919 + nt)
+    t = _random_desc(rng, nt)
+    if nt > 8:
+        t[nt - 1] = t[3]  # equal rows across tiles: the lower index must win
+        t[nt // 2] = t[3]
+    q = _random_desc(rng, nq, pool=t)
+    io, do = orc.knn_match(q, t)
+    with dp.Engine() as eng:
+        ig, dg = M.knn_match(eng, q, t)
+    assert np.array_equal(dg, do)
+    assert np.array_equal(ig, io)
+
+
+def test_knn_match_extreme_distances(orc):
+    # distances 0 and 256 (all bits differ) and all-equal train sets
+    t = np.zeros((70, 32), dtype=np.uint8)
+    t[5:] = 255
+    q = np.concatenate([np.zeros((3, 32), np.uint8), np.full((3, 32), 255, np.uint8)])
+    io, do = orc.knn_match(q, t)
+    with dp.Engine() as eng:
+        ig, dg = M.knn_match(eng, q, t)
+    assert np.array_equal(ig, io) and np.array_equal(dg, do)
+    assert do[0].tolist() == [0, 0] and io[0].tolist() == [0, 1] and io[3].tolist() == [5, 6]
+
+
+def test_triangulate_matches_oracle_and_reference_property(orc):
+    from tests.test_seeds_cpu import project, random_view
+
+    rng = np.random.default_rng(21)
+    Ps, obs, truth = [], [], []
+    for i in range(500):
+        m = 2 + i % 5
+        P = [random_view(rng) for _ in range(m)]
+        X = rng.uniform(0, 10, size=3)
+        Ps.append(P)
+        noise = 0.0 if i % 2 == 0 else 1.5
+        obs.append([project(p, X) + rng.normal(0, noise, size=2) for p in P])
+        truth.append(X)
+    want = orc.triangulate(Ps, obs)
+    with dp.Engine() as eng:
+        got = M.triangulate(eng, Ps, obs)
+    assert np.array_equal(bits(got), bits(want))
+    exact = np.array(truth)[0::2]
+    assert np.all(np.abs(got[0::2] - exact) < 0.01)  # test_triangulation.cpp EXPECT_NEAR 0.01
+
+
+def test_pmvs_run_generates_its_own_seeds(orc):
+    """PMVS::Run (pmvs.cpp:22-27): InsertSeeds (GenerateSeeds) then expansion,
+    equal to the oracle's densify on the oracle's seed points."""
+    cfg = synth.config(n_views=4, width=320, height=240, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    kw = dict(n_features=2000, n_levels=4, fast_threshold=8)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    pm = dp.PMVS()
+    for v in range(4):
+        pm.add_camera(dp.View(P[v], imgs[v]))
+    pm.run(None, matcher_options=M.MatcherOptions(**kw))
+    got = pm.get_point_cloud()
+    assert pm.stats["seed_generation"]["points"] == len(r["points"])
+    S = orc.Scene(P, imgs)
+    want, _ = S.densify(r["points"])
+    assert len(got) == len(want) and len(got) > 0
+    for f in ("pos", "normal", "ref", "vis", "rgb"):
+        assert np.array_equal(bits(got[f]), bits(want[f])), f

@@ -1,0 +1,185 @@
+"""Seed generation on the CPU (no GPU): the oracle's restatement pinned by the
+reference's own tests and by independent numpy statements, plus the parts of
+the product that are host code (dp_fundamental_matrix).
+
+Reference anchors: modules/features/matcher.cpp:18-474,
+modules/geometry/fundamental_matrix.cpp:6-53, triangulation.cpp:15-34,
+tests/core/test_triangulation.cpp:11-52, tests/test_data_generator.cpp:4-55.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from densepoints_amd import matcher as M
+from densepoints_amd import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---- TestScene (tests/test_data_generator.cpp): K fixed, R = Rx Ry Rz with
+# angles uniform(-90, 90) (radians, as Eigen::AngleAxis reads them),
+# t = uniform[0, 10)^3 + (0, 0, -20); points uniform[0, 10)^3
+def _axis_angle(axis, a):
+    c, s = np.cos(a), np.sin(a)
+    if axis == 0:
+        return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+    if axis == 1:
+        return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+
+
+def random_view(rng):
+    K = np.array([[1000.0, 0, 2000], [0, 1000, 1500], [0, 0, 1]])
+    R = np.eye(3)
+    t = np.zeros(3)
+    for ax in range(3):
+        R = R @ _axis_angle(ax, rng.uniform(-90, 90))
+        t[ax] = rng.uniform(0, 10) + (0.0, 0.0, -20.0)[ax]
+    return K @ np.hstack([R, t[:, None]])
+
+
+def project(P, X):
+    h = P @ np.append(X, 1.0)
+    return h[:2] / h[2]
+
+
+def _hamming_matrix(q, t):
+    x = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2)
+    return x.sum(axis=2).astype(np.int64)
+
+
+def _knn_numpy(q, t):
+    """knnMatch(k=2) by definition: the two smallest (distance, train index)."""
+    idx = -np.ones((len(q), 2), dtype=np.int32)
+    dist = -np.ones((len(q), 2), dtype=np.int32)
+    if len(t) == 0:
+        return idx, dist
+    D = _hamming_matrix(q, t)
+    for i in range(len(q)):
+        order = np.lexsort((np.arange(len(t)), D[i]))[:2]
+        idx[i, : len(order)] = order
+        dist[i, : len(order)] = D[i, order]
+    return idx, dist
+
+
+def random_descriptors(rng, n, pool=None):
+    d = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    if pool is not None and n:
+        # plant exact duplicates so distance ties occur
+        k = rng.integers(0, len(pool), size=n // 3)
+        d[: len(k)] = pool[k]
+    return d
+
+
+@pytest.mark.parametrize("nq,nt", [(0, 5), (7, 0), (9, 1), (13, 2), (40, 97), (100, 300)])
+def test_oracle_knn_is_lexicographic_top2(orc, nq, nt):
+    rng = np.random.default_rng(nq * 1000 + nt)
+    t = random_descriptors(rng, nt)
+    q = random_descriptors(rng, nq, pool=t if nt else None)
+    if nt > 3:
+        t[nt // 2] = t[1]  # duplicate train rows: equal distances, lower index wins
+    i_o, d_o = orc.knn_match(q, t)
+    i_n, d_n = _knn_numpy(q, t)
+    assert np.array_equal(i_o, i_n) and np.array_equal(d_o, d_n)
+
+
+def test_reference_triangulation_2view(orc):
+    """tests/core/test_triangulation.cpp:11-28 (EXPECT_NEAR 0.01), seeded."""
+    rng = np.random.default_rng(11)
+    for _ in range(200):
+        P, Pp = random_view(rng), random_view(rng)
+        X = rng.uniform(0, 10, size=3)
+        Xt = orc.triangulate([[P, Pp]], [[project(P, X), project(Pp, X)]])[0]
+        assert np.all(np.abs(Xt - X) < 0.01), (X, Xt)
+
+
+def test_reference_triangulation_multiview(orc):
+    """tests/core/test_triangulation.cpp:30-52 (3 views, EXPECT_NEAR 0.01), seeded."""
+    rng = np.random.default_rng(12)
+    for _ in range(200):
+        Ps = [random_view(rng) for _ in range(3)]
+        X = rng.uniform(0, 10, size=3)
+        Xt = orc.triangulate([Ps], [[project(P, X) for P in Ps]])[0]
+        assert np.all(np.abs(Xt - X) < 0.01), (X, Xt)
+
+
+def test_oracle_dlt_matches_numpy_svd(orc):
+    """The Givens-QR + one-sided Jacobi restatement returns Eigen's
+    JacobiSVD null vector (here: numpy's SVD) on noisy observations."""
+    rng = np.random.default_rng(13)
+    Ps, obs, ref = [], [], []
+    for _ in range(100):
+        m = int(rng.integers(2, 7))
+        P = [random_view(rng) for _ in range(m)]
+        X = rng.uniform(0, 10, size=3)
+        o = [project(p, X) + rng.normal(0, 2.0, size=2) for p in P]
+        A = []
+        for p, (x, y) in zip(P, o):
+            x, y = float(np.float32(x)), float(np.float32(y))
+            A += [x * p[2] - p[0], y * p[2] - p[1]]
+        v = np.linalg.svd(np.array(A))[2][-1]
+        Ps.append(P)
+        obs.append(o)
+        ref.append(v[:3] / v[3])
+    got = orc.triangulate(Ps, obs)
+    np.testing.assert_allclose(got, np.array(ref), rtol=1e-6, atol=1e-7)
+
+
+def test_fundamental_matrix_product_equals_oracle_and_is_epipolar(orc):
+    rng = np.random.default_rng(14)
+    for _ in range(50):
+        P1, P2 = random_view(rng), random_view(rng)
+        F = M.fundamental_matrix(P1, P2)
+        assert np.array_equal(F, orc.fundamental_matrix(P1, P2))  # bit-exact host code
+        X = rng.uniform(0, 10, size=3)
+        x1, x2 = project(P1, X), project(P2, X)
+        r = np.append(x2, 1) @ F @ np.append(x1, 1)
+        assert abs(r) < 1e-6 * np.linalg.norm(F) * np.linalg.norm(np.append(x1, 1)) * np.linalg.norm(np.append(x2, 1))
+        d = orc.epipolar_distance(F, float(x1[0]), float(x1[1]), float(x2[0]), float(x2[1]))
+        # the reference stores the line's y at x = 0 and x = 1 as float
+        # (fundamental_matrix.cpp:44-49) and extrapolates them to x2: the distance
+        # is exact up to that rounding times |x2|
+        l = F @ np.append(x1, 1)
+        ys = max(abs(l[2] / l[1]), abs((l[2] + l[0]) / l[1]), abs(x2[1]), 1.0)
+        assert d < 1e-3 + 4 * float(np.spacing(np.float32(ys))) * (1.0 + abs(x2[0]))
+
+
+def test_orb_constants(orc):
+    pat = orc.orb_pattern()
+    assert pat.shape == (512, 2) and pat.min() >= -13 and pat.max() <= 13
+    assert len({tuple(r) for r in pat.reshape(256, 4)}) > 250  # pairs are distinct tests
+    for n, L in ((40000, 8), (3000, 4), (500, 1)):
+        f = orc.features_per_level(n, 1.2, L)
+        assert f.sum() == n and np.all(np.diff(f[:-1]) <= 0)
+
+
+def test_oracle_seeds_lie_on_the_plane(orc):
+    """End-to-end restatement on the textured plane (z = 0): triangulated
+    seeds land on the surface to a fraction of a pixel."""
+    cfg = synth.config(n_views=4, width=640, height=480, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(n_features=5000, fast_threshold=10))
+    c = r["counts"]
+    assert c["points"] > 500 and c["matches"] <= c["ratio_matches"] and c["keypoints"] <= c["detected"]
+    z = np.abs(r["points"][:, 2])
+    assert np.median(z) < 0.01 and np.percentile(z, 90) < 0.03
+    # FilterKeypoints: at most max_keypoints_per_cell per 16 px cell of each view
+    for kp in r["keypoints"]:
+        cells = (kp["y"].astype(np.int64) // 16) * 1000 + kp["x"].astype(np.int64) // 16
+        assert np.bincount(np.unique(cells, return_inverse=True)[1]).max() <= 4
+        assert np.all(np.diff(kp["octave"]) >= 0)  # compute() buckets by octave
+
+
+def test_golden_seeds_fixture_pins_the_oracle(orc):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "seeds_small.npz"))
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("mgs", os.path.join(ROOT, "tests", "golden", "make_golden_seeds.py"))
+    mgs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mgs)
+    r = orc.seeds_run(g["P"], list(g["images"]), orc.matcher_options(**mgs.OPTIONS))
+    assert np.array_equal(np.concatenate(r["keypoints"]), g["keypoints"])
+    assert np.array_equal(np.concatenate(r["descriptors"]), g["descriptors"])
+    assert np.array_equal(np.concatenate(r["q2t"]), g["q2t"])
+    assert np.array_equal(r["points"], g["points"])

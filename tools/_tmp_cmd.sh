@@ -1,4 +1,5 @@
 set -u
-PASSES="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE
-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM" TAG=r01b bash tools/gpu_counters.sh || exit $?
-VARIANTS="-DDP_STAMPS" BENCH_ARGS="--steps 2 --warmup 1 --no-cpu --no-densify" bash tools/ab_bench.sh
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_seeds.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_seeds.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_seeds.log
+exit $rc
