@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-densify", action="store_true", help="skip the informational end-to-end densify")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes/launch from profiles/")
+    ap.add_argument("--no-seeds", action="store_true", help="skip the informational seed generation")
+    ap.add_argument("--knn-rows", type=int, default=40000, help="descriptors per side of the kNN kernel timing")
     return ap.parse_args()
 
 
@@ -219,6 +221,8 @@ def main():
                                      "generations": int(sst["generations"]), "evals": int(sst["evals"]),
                                      "refine_ms_max_rank": round(sst["refine_ms"], 1), "wall_s": round(wall, 3),
                                      "collective": "all_gather_into_tensor (RCCL) of 80-B candidate records"}
+    if rank == 0 and not args.no_seeds:
+        result["seed_generation"] = seed_generation(eng, args)
     st = np.zeros(8, dtype=np.uint64)
     if N.lib.dp_debug_stamps(N.ptr(st)) == 0:  # -DDP_STAMPS diagnostic builds only
         tot = float(st[7]) or 1.0
@@ -240,6 +244,48 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     eng.close()
+
+
+def seed_generation(eng, args):
+    """Informational (not the headline): Matcher::GenerateSeeds on the bench's
+    views with the reference's settings, and the brute-force Hamming knnMatch
+    kernel at the reference's ORB budget (40000 x 40000 descriptors, one view
+    pair) against the dense i8 MFMA peak.  The oracle's knnMatch on a bounded
+    sample is the CPU baseline of that kernel."""
+    from densepoints_amd import matcher as M
+
+    m = M.Matcher(eng)
+    m.generate_seeds()  # first call allocates
+    t0 = time.perf_counter()
+    m.generate_seeds()
+    wall = time.perf_counter() - t0
+    st = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in m.stats.items()}
+    rng = np.random.default_rng(7)
+    n = args.knn_rows
+    q = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    ms = []
+    for _ in range(3):
+        M.knn_match(eng, q, t)
+        ms.append(eng.last_kernel_ms())  # HIP events around the kernel, on its stream
+    kms = float(np.mean(ms[1:]))
+    ops = 2.0 * 256 * n * n  # i8 MACs of the Hamming GEMM, x2
+    peak = 5000.0  # dense i8 MFMA TOPS: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, Matrix cores)
+    out = {"settings": "reference defaults (ORB 40000 features, 8 levels, FAST 20, 16 px cells x 4, ratio 0.7, "
+                       "1.5 px epipolar)", "wall_s": round(wall, 4), **st,
+           "knn_kernel": {"rows": n, "kernel_ms": round(kms, 4), "Gpairs_per_s": round(n * n / kms / 1e6, 1),
+                          "roofline": {"bound": "mfma", "achieved": round(ops / kms / 1e9, 1), "peak": peak,
+                                       "unit": "TOPS (i8)", "frac": round(ops / kms / 1e9 / peak, 4)}}}
+    if not args.no_cpu:
+        from oracle import pyoracle as orc
+
+        s = 3000
+        t0 = time.perf_counter()
+        orc.knn_match(q[:s], t[:s])
+        ct = time.perf_counter() - t0
+        out["knn_kernel"]["cpu_baseline"] = {"Gpairs_per_s": round(s * s / ct / 1e9, 4), "cores": 1, "kind": "port",
+                                             "sample": f"oracle knnMatch {s} x {s}, {ct:.2f} s"}
+    return out
 
 
 def latest_traffic_json():

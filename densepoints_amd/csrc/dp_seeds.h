@@ -19,12 +19,22 @@ struct KnnJob {
     int32_t nq, nt;
 };
 
+// one workgroup: 256 queries of a job against train rows [t_lo, t_hi)
+struct KnnBlock {
+    int32_t job, q0, t_lo, t_hi, slot, pad;
+};
+
 struct KnnArgs {
     const uint32_t *desc;  // packed descriptors, 32 B each
     const KnnJob *jobs;
-    const int2 *blocks;    // per workgroup: (job, first query)
-    uint32_t *keys;        // 2 per query: (acc + 256) << 22 | train row, ~0 = none
+    const KnnBlock *blocks;
+    uint32_t *keys;        // per slot, 2 per query: (acc + 256) << 22 | train row, ~0 = none
+    int64_t slot_stride;   // elements between slots (train-range splits)
 };
+
+// merge the per-split (smallest, second) keys of every query into slot 0 order
+hipError_t launch_knn_merge(const uint32_t *partial, int nsplit, int64_t slot_stride, int64_t nq, uint32_t *keys,
+                            hipStream_t s);
 
 // a view pair of DefaultPairsList with its fundamental matrix
 struct SeedPair {

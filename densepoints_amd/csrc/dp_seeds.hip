@@ -86,8 +86,9 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
 {
     __shared__ v4i tileA[kKnnTiles][8][64]; // A fragments of one stage, 32 KB
 
-    const int2 blk = a.blocks[blockIdx.x];
-    const KnnJob job = a.jobs[blk.x];
+    const KnnBlock kb = a.blocks[blockIdx.x];
+    const int2 blk = make_int2(kb.job, kb.q0);
+    const KnnJob job = a.jobs[kb.job];
     const int tid = threadIdx.x;
     const int w = tid >> 6, l = tid & 63;
     const int col = l & 31, h = l >> 5;
@@ -111,27 +112,34 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
     for (int b = 0; b < kKnnQB; ++b)
         m0[b] = m1[b] = 0xFFFFFFFFu;
 
-    for (int t0 = 0; t0 < job.nt; t0 += kKnnRows) {
-        // stage: thread -> (row, 4 dwords); rows past nt unpack as zeros
+    // train rows [t_lo, t_end) of this workgroup; stage loads are prefetched
+    // into registers one stage ahead, so the global latency hides behind MFMA
+    const int t_end = min(kb.t_hi, job.nt);
+    const int sr = tid >> 1, shh = tid & 1; // stage slot of this thread: (row, 4 dwords)
+    auto stage_load = [&](int t0) {
+        uint4 d = make_uint4(0, 0, 0, 0);
+        if (t0 + sr < t_end)
+            d = *reinterpret_cast<const uint4 *>(td + (size_t)(t0 + sr) * 8 + 4 * shh);
+        return d;
+    };
+    uint4 dnext = stage_load(kb.t_lo);
+    for (int t0 = kb.t_lo; t0 < t_end; t0 += kKnnRows) {
+        // stage: unpack this thread's 128 bits to 0/1 bytes in A-fragment order
         {
-            const int r = tid >> 1, hh = tid & 1;
-            const int row = t0 + r;
-            uint4 d = make_uint4(0, 0, 0, 0);
-            if (row < job.nt)
-                d = *reinterpret_cast<const uint4 *>(td + (size_t)row * 8 + 4 * hh);
-            const uint32_t dv[4] = {d.x, d.y, d.z, d.w};
+            const uint32_t dv[4] = {dnext.x, dnext.y, dnext.z, dnext.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int s = 4 * hh + i;
-                tileA[r >> 5][s][r & 31] = bits16_01(dv[i] & 0xFFFFu);
-                tileA[r >> 5][s][32 + (r & 31)] = bits16_01(dv[i] >> 16);
+                const int s = 4 * shh + i;
+                tileA[sr >> 5][s][sr & 31] = bits16_01(dv[i] & 0xFFFFu);
+                tileA[sr >> 5][s][32 + (sr & 31)] = bits16_01(dv[i] >> 16);
             }
         }
         __syncthreads();
+        dnext = stage_load(t0 + kKnnRows);
 #pragma unroll 1
         for (int ti = 0; ti < kKnnTiles; ++ti) {
             const int tb = t0 + ti * 32;
-            if (tb >= job.nt)
+            if (tb >= t_end)
                 break;
             v4i af[8];
 #pragma unroll
@@ -139,22 +147,45 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
                 af[s] = tileA[ti][s][l];
             // key base per accumulator register: rows (r&3) + 8 (r>>2) + 4 h
             const uint32_t base = (256u << 22) + (uint32_t)(tb + 4 * h);
-            const bool partial = tb + 32 > job.nt;
+            const bool partial = tb + 32 > t_end;
+            // the blocks' accumulation chains interleaved (independent MFMAs back to back)
+            v16i acc[kKnnQB];
 #pragma unroll
-            for (int b = 0; b < kKnnQB; ++b) {
-                v16i acc = {};
+            for (int b = 0; b < kKnnQB; ++b)
+                acc[b] = v16i{};
 #pragma unroll
-                for (int s = 0; s < 8; ++s)
-                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[b][s], acc, 0, 0, 0);
+            for (int s = 0; s < 8; ++s)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const uint32_t roff = (uint32_t)((r & 3) + 8 * (r >> 2));
-                    uint32_t k = ((uint32_t)acc[r] << 22) + base + roff;
-                    if (partial && tb + 4 * h + (int)roff >= job.nt)
-                        k = 0xFFFFFFFFu;
-                    m1[b] = med3u(m0[b], k, m1[b]);
-                    m0[b] = min(m0[b], k);
-                }
+                for (int b = 0; b < kKnnQB; ++b)
+                    acc[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[b][s], acc[b], 0, 0, 0);
+            // (a wave-uniform skip when no lane's tile minimum beats its second
+            // best was measured slower: with ~2.5k-row train ranges it rarely fires)
+            if (!partial) {
+                // key = (acc << 22) + R[r]: one v_lshl_add_u32 per element, R shared by the blocks
+                uint32_t R[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    R[r] = base + (uint32_t)((r & 3) + 8 * (r >> 2));
+#pragma unroll
+                for (int b = 0; b < kKnnQB; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const uint32_t k = ((uint32_t)acc[b][r] << 22) + R[r];
+                        m1[b] = med3u(m0[b], k, m1[b]);
+                        m0[b] = min(m0[b], k);
+                    }
+            } else {
+#pragma unroll
+                for (int b = 0; b < kKnnQB; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const uint32_t roff = (uint32_t)((r & 3) + 8 * (r >> 2));
+                        uint32_t k = ((uint32_t)acc[b][r] << 22) + base + roff;
+                        if (tb + 4 * h + (int)roff >= t_end)
+                            k = 0xFFFFFFFFu;
+                        m1[b] = med3u(m0[b], k, m1[b]);
+                        m0[b] = min(m0[b], k);
+                    }
             }
         }
         __syncthreads();
@@ -168,10 +199,37 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
         const uint32_t n1 = min(max(m0[b], p0), min(m1[b], p1));
         const int q = blk.y + w * kKnnWQ + b * 32 + col;
         if (h == 0 && q < job.nq) {
-            a.keys[2 * ((size_t)job.out_off + q)] = n0;
-            a.keys[2 * ((size_t)job.out_off + q) + 1] = n1;
+            uint32_t *o = a.keys + (size_t)kb.slot * a.slot_stride + 2 * ((size_t)job.out_off + q);
+            o[0] = n0;
+            o[1] = n1;
         }
     }
+}
+
+__global__ void knn_merge_kernel(const uint32_t *partial, int nsplit, int64_t stride, int64_t nq, uint32_t *keys)
+{
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq)
+        return;
+    uint32_t m0 = 0xFFFFFFFFu, m1 = 0xFFFFFFFFu;
+    for (int s = 0; s < nsplit; ++s) {
+        const uint32_t a0 = partial[s * stride + 2 * q], a1 = partial[s * stride + 2 * q + 1];
+        const uint32_t n1 = min(max(m0, a0), min(m1, a1));
+        m0 = min(m0, a0);
+        m1 = n1;
+    }
+    keys[2 * q] = m0;
+    keys[2 * q + 1] = m1;
+}
+
+hipError_t launch_knn_merge(const uint32_t *partial, int nsplit, int64_t slot_stride, int64_t nq, uint32_t *keys,
+                            hipStream_t s)
+{
+    if (nq <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(knn_merge_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, partial, nsplit,
+                       slot_stride, nq, keys);
+    return hipGetLastError();
 }
 
 // keys -> (index, distance); distance = (key >> 22) - 256 + popcnt(query)

@@ -23,7 +23,8 @@ struct dp_seedgen {
     DevBuf<int32_t> i2, d2, off;
     DevBuf<double> P, obs, X;
     DevBuf<dpk::KnnJob> jobs;
-    DevBuf<int2> blocks;
+    DevBuf<dpk::KnnBlock> blocks;
+    DevBuf<uint32_t> pkeys; // per-split partial top-2 keys
     // GenerateSeeds
     DevBuf<dpk::OrbLevel> lv;
     DevBuf<dpk::PyrPlane> planes0;
@@ -73,6 +74,7 @@ void dp_seedgen_free(dp_seedgen *s)
     s->X.release();
     s->jobs.release();
     s->blocks.release();
+    s->pkeys.release();
     for (auto *b : {&s->gray, &s->score, &s->blur, &s->keep_all, &s->flag})
         b->release();
     s->lv.release();
@@ -194,12 +196,67 @@ extern "C" int dp_fundamental_matrix(const double P1[12], const double P2[12], d
 // ---------------------------------------------------------------------------
 // knnMatch on one (query, train) pair
 // ---------------------------------------------------------------------------
-static void knn_blocks(const std::vector<dpk::KnnJob> &jobs, std::vector<int2> &blocks)
+// Workgroups of a knn launch: 256 queries each; when the query blocks alone
+// cannot fill the chip (one view pair), the train rows are split into nsplit
+// ranges (multiples of the 128-row stage) whose top-2 keys knn_merge_kernel
+// combines.  Every (query block, split) gets a workgroup, so every slot is
+// written.
+static int knn_blocks(const std::vector<dpk::KnnJob> &jobs, std::vector<dpk::KnnBlock> &blocks)
 {
+    int64_t qblocks = 0, max_nt = 0;
+    for (const auto &j : jobs) {
+        qblocks += (j.nq + dpk::kKnnQueriesPerBlock - 1) / dpk::kKnnQueriesPerBlock;
+        max_nt = std::max<int64_t>(max_nt, j.nt);
+    }
+    const int64_t target = 3072; // ~12 workgroups per CU: 3 resident per CU, 4 rounds
+    int nsplit = 1;
+    if (qblocks > 0 && qblocks < target)
+        nsplit = (int)std::min<int64_t>((target + qblocks - 1) / qblocks, std::max<int64_t>(1, max_nt / 1024));
     blocks.clear();
-    for (size_t j = 0; j < jobs.size(); ++j)
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        int64_t chunk = (jobs[j].nt + nsplit - 1) / nsplit;
+        chunk = (chunk + 127) / 128 * 128;
         for (int q = 0; q < jobs[j].nq; q += dpk::kKnnQueriesPerBlock)
-            blocks.push_back(make_int2((int)j, q));
+            for (int sp = 0; sp < nsplit; ++sp) {
+                dpk::KnnBlock b{};
+                b.job = (int)j;
+                b.q0 = q;
+                b.t_lo = (int)std::min<int64_t>(sp * chunk, jobs[j].nt);
+                b.t_hi = (int)std::min<int64_t>((sp + 1) * chunk, jobs[j].nt);
+                b.slot = sp;
+                blocks.push_back(b);
+            }
+    }
+    return nsplit;
+}
+
+// knn over uploaded jobs (device copy in s->jobs); final keys into `keys`
+static int run_knn(dp_ctx *c, dp_seedgen *s, const std::vector<dpk::KnnJob> &jobs, int64_t q_total, uint32_t *keys,
+                   bool timed)
+{
+    std::vector<dpk::KnnBlock> blocks;
+    const int nsplit = knn_blocks(jobs, blocks);
+    DP_HIP(c, s->blocks.reserve(blocks.size() + 1));
+    if (!blocks.empty())
+        DP_HIP(c, hipMemcpyAsync(s->blocks.p, blocks.data(), blocks.size() * sizeof(dpk::KnnBlock),
+                                 hipMemcpyHostToDevice, c->stream));
+    uint32_t *out = keys;
+    const int64_t stride = 2 * q_total;
+    if (nsplit > 1) {
+        DP_HIP(c, s->pkeys.reserve((size_t)nsplit * stride + 1));
+        out = s->pkeys.p;
+    }
+    dpk::KnnArgs ka{s->desc.p, s->jobs.p, s->blocks.p, out, stride};
+    if (timed)
+        DP_HIP(c, hipEventRecord(c->e0, c->stream));
+    DP_HIP(c, dpk::launch_knn(ka, (int)blocks.size(), c->stream));
+    if (nsplit > 1)
+        DP_HIP(c, dpk::launch_knn_merge(out, nsplit, stride, q_total, keys, c->stream));
+    if (timed) {
+        DP_HIP(c, hipEventRecord(c->e1, c->stream));
+        c->timed = true;
+    }
+    return DP_OK;
 }
 
 extern "C" int dp_knn_match(dp_ctx *c, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt,
@@ -229,18 +286,11 @@ extern "C" int dp_knn_match(dp_ctx *c, const uint8_t *query, int64_t nq, const u
     jobs[0].out_off = 0;
     jobs[0].nq = (int32_t)nq;
     jobs[0].nt = (int32_t)nt;
-    std::vector<int2> blocks;
-    knn_blocks(jobs, blocks);
     DP_HIP(c, s->jobs.reserve(1));
-    DP_HIP(c, s->blocks.reserve(blocks.size()));
     DP_HIP(c, hipMemcpyAsync(s->jobs.p, jobs.data(), sizeof(dpk::KnnJob), hipMemcpyHostToDevice, c->stream));
-    DP_HIP(c, hipMemcpyAsync(s->blocks.p, blocks.data(), blocks.size() * sizeof(int2), hipMemcpyHostToDevice,
-                             c->stream));
-    dpk::KnnArgs ka{s->desc.p, s->jobs.p, s->blocks.p, s->keys.p};
-    DP_HIP(c, hipEventRecord(c->e0, c->stream));
-    DP_HIP(c, dpk::launch_knn(ka, (int)blocks.size(), c->stream));
-    DP_HIP(c, hipEventRecord(c->e1, c->stream));
-    c->timed = true;
+    int rc = run_knn(c, s, jobs, nq, s->keys.p, true);
+    if (rc != DP_OK)
+        return rc;
     DP_HIP(c, dpk::launch_knn_decode(s->desc.p, 0, nq, s->keys.p, s->i2.p, s->d2.p, c->stream));
     DP_HIP(c, hipMemcpyAsync(idx2, s->i2.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
     DP_HIP(c, hipMemcpyAsync(dist2, s->d2.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
@@ -595,14 +645,9 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     if (mo.epipolar_matching) {
         DP_HIP(c, dpk::launch_epipolar_match(ma, st));
     } else {
-        std::vector<int2> blocks;
-        knn_blocks(s->h_jobs, blocks);
-        DP_HIP(c, s->blocks.reserve(blocks.size() + 1));
-        if (!blocks.empty())
-            DP_HIP(c, hipMemcpyAsync(s->blocks.p, blocks.data(), blocks.size() * sizeof(int2), hipMemcpyHostToDevice,
-                                     st));
-        dpk::KnnArgs ka{s->desc.p, s->jobs.p, s->blocks.p, s->keys.p};
-        DP_HIP(c, dpk::launch_knn(ka, (int)blocks.size(), st));
+        rc = run_knn(c, s, s->h_jobs, q_total, s->keys.p, false);
+        if (rc != DP_OK)
+            return rc;
         DP_HIP(c, dpk::launch_match(ma, st));
     }
     DP_HIP(c, hipEventRecord(t3.e, st));

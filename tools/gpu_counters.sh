@@ -5,7 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-ARGS=${PROF_ARGS:-"--steps 1 --warmup 0 --no-cpu --no-densify"}
+ARGS=${PROF_ARGS:-"--steps 1 --warmup 0 --no-cpu --no-densify --no-seeds"}
 i=0
 mkdir -p gpurun_out/ctr_$TAG
 while read -r line; do

@@ -5,7 +5,7 @@ set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-ARGS=${PROF_ARGS:-"--steps 3 --warmup 1 --no-cpu --no-densify"}
+ARGS=${PROF_ARGS:-"--steps 3 --warmup 1 --no-cpu --no-densify --no-seeds"}
 mkdir -p gpurun_out/prof_$TAG
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG/trace -o run -- python3 bench.py $ARGS > gpurun_out/prof_$TAG/trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
