@@ -29,6 +29,11 @@ FLAGS = [
     "-Wall",
     "-Wno-unused-value",
     "-Wno-unused-result",
+    # MFMA results in VGPRs (gfx950's unified register file): the knnMatch
+    # epilogue reads every accumulator with VALU, so the AGPR form would add one
+    # v_accvgpr_read per element (the refine kernels have no MFMA)
+    "-mllvm",
+    "-amdgpu-mfma-vgpr-form=1",
 ]
 
 

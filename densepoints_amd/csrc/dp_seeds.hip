@@ -145,8 +145,11 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
 #pragma unroll
             for (int s = 0; s < 8; ++s)
                 af[s] = tileA[ti][s][l];
-            // key base per accumulator register: rows (r&3) + 8 (r>>2) + 4 h
-            const uint32_t base = (256u << 22) + (uint32_t)(tb + 4 * h);
+            // key base per accumulator register: rows tb + (r&3) + 8 (r>>2) + 4 h.
+            // The lane-half term 4 h is left out of every key of this lane (the
+            // same offset for all of its rows, so its order is unchanged) and
+            // added back at the half merge: the 16 bases are wave-uniform (SGPRs).
+            const uint32_t base = (256u << 22) + (uint32_t)tb;
             const bool partial = tb + 32 > t_end;
             // the blocks' accumulation chains interleaved (independent MFMAs back to back)
             v16i acc[kKnnQB];
@@ -170,7 +173,8 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
                 for (int b = 0; b < kKnnQB; ++b)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const uint32_t k = ((uint32_t)acc[b][r] << 22) + R[r];
+                        uint32_t k; // (acc << 22) + R[r] (the compiler otherwise emits shift + add3)
+                        asm("v_lshl_add_u32 %0, %1, 22, %2" : "=v"(k) : "v"(acc[b][r]), "s"(R[r]));
                         m1[b] = med3u(m0[b], k, m1[b]);
                         m0[b] = min(m0[b], k);
                     }
@@ -190,9 +194,14 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
         }
         __syncthreads();
     }
-    // merge the two row halves of each column (lanes l and l ^ 32)
+    // merge the two row halves of each column (lanes l and l ^ 32), restoring
+    // the lane-half row offset 4 h left out of the keys
 #pragma unroll
     for (int b = 0; b < kKnnQB; ++b) {
+        if (m0[b] != 0xFFFFFFFFu)
+            m0[b] += 4 * h;
+        if (m1[b] != 0xFFFFFFFFu)
+            m1[b] += 4 * h;
         const uint32_t p0 = (uint32_t)__shfl_xor((int)m0[b], 32);
         const uint32_t p1 = (uint32_t)__shfl_xor((int)m1[b], 32);
         const uint32_t n0 = min(m0[b], p0);
