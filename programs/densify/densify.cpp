@@ -3,12 +3,13 @@
 // Mirrors the reference's programs/densify/main.cpp (-i scene.json, -s
 // settings.json; PMVS::AddCamera per view, then PMVS::Run) and adds what
 // SURVEY 8b asks of the build: -o out.ply (PMVS::PrintCloud format), --seeds
-// (feature matching is out of scope, so seed points come from a file),
-// --device, option overrides.  All compute goes through the C ABI of
-// libdensepoints.so (include/densepoints.h): dp_set_views + dp_densify.
+// (seed points from a file instead of Matcher::GenerateSeeds), --device,
+// option overrides.  All compute goes through the C ABI of libdensepoints.so
+// (include/densepoints.h): dp_set_views, dp_generate_seeds, dp_densify.
 //
-//   densify -i scene.json --seeds seeds.xyz [-s settings.json] [-o points.ply]
+//   densify -i scene.json [--seeds seeds.xyz] [-s settings.json] [-o points.ply]
 //           [--device N] [--max-pops N] [--level L] [--filter] [--check-only]
+//           [--features N] [--fast-threshold T] [--epipolar-matching]
 //   densify --synthetic V,W,H,KIND --write-scene DIR   (deterministic test scene
 //           written as scene.json + PPM images + seeds.xyz; no GPU needed)
 #include "scene_io.h"
@@ -29,8 +30,9 @@ namespace {
 void usage()
 {
     std::fprintf(stderr,
-                 "usage: densify -i scene.json --seeds seeds.xyz [-s settings.json] [-o points.ply]\n"
+                 "usage: densify -i scene.json [--seeds seeds.xyz] [-s settings.json] [-o points.ply]\n"
                  "               [--device N] [--max-pops N] [--level L] [--filter] [--check-only]\n"
+                 "               [--features N] [--fast-threshold T] [--epipolar-matching]\n"
                  "       densify --synthetic V,W,H,KIND --write-scene DIR\n");
 }
 
@@ -130,6 +132,8 @@ int main(int argc, char **argv)
     long long max_pops = -1;
     int level = 0;
     bool check_only = false, do_filter = false;
+    dp_matcher_options mopt; // MatcherOptions defaults (matcher.h:21-32), ORB::create(40000)
+    dp_default_matcher_options(&mopt);
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> std::string {
@@ -148,6 +152,9 @@ int main(int argc, char **argv)
         else if (a == "--level") level = std::atoi(next().c_str());
         else if (a == "--filter") do_filter = true;
         else if (a == "--check-only") check_only = true;
+        else if (a == "--features") mopt.n_features = std::atoi(next().c_str());
+        else if (a == "--fast-threshold") mopt.fast_threshold = std::atoi(next().c_str());
+        else if (a == "--epipolar-matching") mopt.epipolar_matching = 1;
         else if (a == "--synthetic") synth = next();
         else if (a == "--write-scene") scene_dir = next();
         else if (a == "-h" || a == "--help") {
@@ -164,7 +171,7 @@ int main(int argc, char **argv)
                 throw std::runtime_error("--synthetic needs --write-scene DIR");
             return write_synthetic(synth, scene_dir);
         }
-        if (input.empty() || seeds_path.empty()) {
+        if (input.empty()) {
             usage();
             return 2;
         }
@@ -182,7 +189,7 @@ int main(int argc, char **argv)
             imgs.push_back(dpio::load_image(v.filename)); // PMVS::AddCamera -> View::Load
             P.insert(P.end(), v.P, v.P + 12);
         }
-        const std::vector<double> seeds = dpio::read_seeds(seeds_path);
+        const std::vector<double> seeds = seeds_path.empty() ? std::vector<double>() : dpio::read_seeds(seeds_path);
         if (check_only) {
             // parsed scene summary + FNV-1a of each decoded BGR8 image (no GPU)
             std::printf("{\"views\": %zu, \"width\": %d, \"height\": %d, \"seeds\": %zu, \"image_fnv\": [",
@@ -219,11 +226,23 @@ int main(int argc, char **argv)
             check(dp_build_pyramid(ctx, level + 1), "dp_build_pyramid");
             check(dp_set_level(ctx, level), "dp_set_level");
         }
+        // PMVS::InsertSeeds (pmvs.cpp:29-34): without --seeds the seeds come from
+        // Matcher::GenerateSeeds on the device (level-0 views)
+        std::vector<double> gen_seeds;
+        dp_seed_stats sst;
+        std::memset(&sst, 0, sizeof sst);
+        if (seeds_path.empty()) {
+            const double *xyz = nullptr;
+            int64_t n = 0;
+            check(dp_generate_seeds(ctx, &mopt, &xyz, &n, &sst), "dp_generate_seeds");
+            gen_seeds.assign(xyz, xyz + 3 * n);
+        }
+        const std::vector<double> &use = seeds_path.empty() ? gen_seeds : seeds;
         const dp_patch *out = nullptr;
         int64_t n_out = 0;
         dp_densify_stats st;
         std::memset(&st, 0, sizeof st);
-        check(dp_densify(ctx, seeds.data(), (int)(seeds.size() / 3), &out, &n_out, &st), "dp_densify");
+        check(dp_densify(ctx, use.data(), (int)(use.size() / 3), &out, &n_out, &st), "dp_densify");
         // PMVS::FilterPatches (pmvs.h:27, undefined in the reference): dp_filter_patches spec
         std::vector<uint8_t> keep((size_t)n_out, 1);
         if (do_filter && n_out > 0) {
@@ -248,11 +267,14 @@ int main(int argc, char **argv)
         dpio::write_ply(output, cloud);
         const double wall =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        std::printf("{\"output\": \"%s\", \"patches\": %lld, \"written\": %zu, \"seed_patches\": %lld, \"pops\": %lld, "
-                    "\"candidates\": %lld, \"evals\": %lld, \"generations\": %d, \"refine_ms\": %.3f, "
+        std::printf("{\"output\": \"%s\", \"patches\": %lld, \"written\": %zu, \"seeds\": %zu, \"generated_seeds\": %s, "
+                    "\"keypoints\": %lld, \"matches\": %lld, \"seed_ms\": %.3f, \"seed_patches\": %lld, "
+                    "\"pops\": %lld, \"candidates\": %lld, \"evals\": %lld, \"generations\": %d, \"refine_ms\": %.3f, "
                     "\"densify_ms\": %.3f, \"wall_ms\": %.3f}\n",
-                    output.c_str(), (long long)st.patches, cloud.size(), (long long)st.seed_patches, (long long)st.pops,
-                    (long long)st.candidates, (long long)st.evals, st.generations, st.refine_ms, st.total_ms, wall);
+                    output.c_str(), (long long)st.patches, cloud.size(), use.size() / 3,
+                    seeds_path.empty() ? "true" : "false", (long long)sst.keypoints, (long long)sst.matches,
+                    sst.total_ms, (long long)st.seed_patches, (long long)st.pops, (long long)st.candidates,
+                    (long long)st.evals, st.generations, st.refine_ms, st.total_ms, wall);
         return 0;
     } catch (const std::exception &e) {
         std::fprintf(stderr, "densify: %s\n", e.what());
