@@ -361,6 +361,8 @@ double ev_ms(hipEvent_t a, hipEvent_t b)
         DP_HIP(c, (call_with_tmp));                                                                \
         DP_HIP(c, (s)->cub_tmp.reserve(_bytes + 16));                                              \
         _tmp = (s)->cub_tmp.p;                                                                     \
+        /* a select over 0 items must still report 0 selected */                                  \
+        DP_HIP(c, hipMemsetAsync((s)->n_sel.p, 0, sizeof(int64_t), c->stream));                   \
         DP_HIP(c, (call_with_tmp));                                                                \
     } while (0)
 
@@ -430,6 +432,7 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
             max_h = std::max(max_h, o.h);
         }
     }
+    DP_HIP(c, s->n_sel.reserve(1));
     DP_HIP(c, s->lv.reserve(lv.size()));
     DP_HIP(c, hipMemcpyAsync(s->lv.p, lv.data(), lv.size() * sizeof(dpk::OrbLevel), hipMemcpyHostToDevice, st));
     DP_HIP(c, s->planes0.reserve(V));

@@ -38,7 +38,8 @@ def compare_run(eng, r, mo_kw, V):
         kp, d = m.keypoints(v)
         ok, od = r["keypoints"][v], r["descriptors"][v]
         assert len(kp) == len(ok), f"view {v}: {len(kp)} vs {len(ok)} keypoints"
-        bad = np.flatnonzero((bits(kp).reshape(len(kp), -1) != bits(ok).reshape(len(ok), -1)).any(axis=1))
+        nb = kp.dtype.itemsize
+        bad = np.flatnonzero((bits(kp).reshape(-1, nb) != bits(ok).reshape(-1, nb)).any(axis=1))
         assert bad.size == 0, f"view {v}: keypoints differ at {bad[:5]}: {kp[bad[:3]]} vs {ok[bad[:3]]}"
         assert np.array_equal(d, od), f"view {v}: descriptors differ"
     for p, (a, b) in enumerate(r["pairs"]):
@@ -175,3 +176,48 @@ def test_pmvs_run_generates_its_own_seeds(orc):
     assert len(got) == len(want) and len(got) > 0
     for f in ("pos", "normal", "ref", "vis", "rgb"):
         assert np.array_equal(bits(got[f]), bits(want[f])), f
+
+
+def _run_both(orc, P, imgs, kw):
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    with engine_with(P, imgs) as eng:
+        m = compare_run(eng, r, kw, len(imgs))
+    return r, m
+
+
+def test_seeds_edge_blank_and_single_view(orc):
+    cfg = synth.config(n_views=3, width=320, height=240, kind=1)
+    P, imgs, _ = synth.scene_host(cfg)
+    blank = [np.full_like(im, 128) for im in imgs]
+    r, m = _run_both(orc, P, blank, dict(n_features=1000, n_levels=3))
+    assert m.stats["keypoints_detected"] == 0 and len(m.points) == 0
+    # one textured view among blank ones: keypoints but no matches
+    r, m = _run_both(orc, P, [imgs[0], blank[1], blank[2]], dict(n_features=1000, n_levels=3, fast_threshold=8))
+    assert m.stats["keypoints"] > 0 and m.stats["points"] == 0
+    # a single view: no pairs at all
+    r, m = _run_both(orc, P[:1], imgs[:1], dict(n_features=1000, n_levels=3, fast_threshold=8))
+    assert m.stats["pairs"] == 0 and m.stats["points"] == 0
+
+
+def test_seeds_edge_mixed_sizes_levels_and_cells(orc):
+    cfg = synth.config(n_views=3, width=480, height=360, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    # view 2 cropped to 400x300 (same camera, the ORB pyramids differ per view)
+    imgs = [imgs[0], imgs[1], np.ascontiguousarray(imgs[2][:300, :400])]
+    _run_both(orc, P, imgs, dict(n_features=1500, n_levels=5, fast_threshold=8))
+    _run_both(orc, P, imgs, dict(n_features=1500, n_levels=1, fast_threshold=8, cell_size=8,
+                                 max_keypoints_per_cell=1))
+    r, m = _run_both(orc, P, imgs, dict(n_features=1500, n_levels=2, fast_threshold=8, max_keypoints_per_cell=0))
+    assert m.stats["keypoints"] == 0
+
+
+def test_seeds_bad_options_fail_loudly():
+    cfg = synth.config(n_views=2, width=160, height=120, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    with engine_with(P, imgs) as eng:
+        for kw in (dict(n_levels=0), dict(edge_threshold=5), dict(scale_factor=1.0), dict(n_levels=17)):
+            with pytest.raises(dp.DensePointsError):
+                M.Matcher(eng, M.MatcherOptions(**kw)).generate_seeds()
+    with dp.Engine() as eng:  # no views set
+        with pytest.raises(dp.DensePointsError):
+            M.Matcher(eng).generate_seeds()
