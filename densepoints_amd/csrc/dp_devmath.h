@@ -71,10 +71,11 @@ __device__ __forceinline__ double div32_safe(double w) { return div_rn_core(32.0
 // where q0 = a * r = r needs no multiply
 __device__ __forceinline__ double recip_safe(double b)
 {
+    // with a == 1 the correction is itself a Newton step, so one before it
+    // suffices: seed error 1.5*2^-23 -> 2^-44.8 -> 2^-89.6 before the final
+    // rounding (DESIGN.md "Exactness caveat")
     double r = (double)__builtin_amdgcn_rcpf((float)b);
-    double e = __builtin_fma(-b, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-b, r, 1.0);
+    const double e = __builtin_fma(-b, r, 1.0);
     r = __builtin_fma(r, e, r);
     const double rem = __builtin_fma(-b, r, 1.0);
     return __builtin_fma(rem, r, r);

@@ -33,8 +33,6 @@ struct OrbGeom {
     const OrbLevel *lv;   // V * n_levels
     int32_t V, L;
     uint8_t *gray;        // pool
-    uint8_t *blur;        // pool (GaussianBlur 7x7, sigma 2)
-    uint16_t *tmp;        // horizontal blur pass (pool-sized)
 };
 
 hipError_t launch_orb_gray(const PyrPlane *planes, const OrbGeom &g, int max_w, int max_h, hipStream_t s);
@@ -65,7 +63,7 @@ hipError_t launch_cell_keep(const uint64_t *key, int64_t n, int maxk, uint8_t *f
 // compute(): runByImageBorder at level 0 + stable bucketing by octave
 hipError_t launch_desc_prep(const dp_keypoint *kp, const int32_t *kp_view, const int32_t *vw, const int32_t *vh,
                             int64_t n, int edge, uint8_t *flag, uint32_t *okey, hipStream_t s);
-hipError_t launch_orb_blur(const OrbGeom &g, int level, int max_w, int max_h, hipStream_t s);
+// GaussianBlur(7x7, sigma 2) of each keypoint's patch in LDS + rBRIEF
 hipError_t launch_orb_desc(const OrbGeom &g, const dp_keypoint *kp, const int32_t *kp_view, int64_t n,
                            const int8_t *pattern, uint32_t *desc, hipStream_t s);
 hipError_t launch_gather_kp(const dp_keypoint *src, const int32_t *src_view, const int32_t *idx, int64_t n,

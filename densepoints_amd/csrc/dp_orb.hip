@@ -533,84 +533,83 @@ __device__ __forceinline__ int reflect101(int i, int n)
         i = -i;
     if (i >= n)
         i = 2 * (n - 1) - i;
-    return i;
-}
-
-__global__ void orb_blur_h_kernel(OrbGeom g, int level)
-{
-    const int v = blockIdx.z, y = blockIdx.y;
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const OrbLevel L = g.lv[v * g.L + level];
-    if (x >= L.w || y >= L.h)
-        return;
-    const uint8_t *r = g.gray + L.off + (size_t)y * L.w;
-    int s = 0;
-#pragma unroll
-    for (int k = 0; k < 7; ++k)
-        s += kGauss7[k] * r[reflect101(x + k - 3, L.w)];
-    g.tmp[L.off + (size_t)y * L.w + x] = (uint16_t)s;
-}
-
-__global__ void orb_blur_v_kernel(OrbGeom g, int level)
-{
-    const int v = blockIdx.z, y = blockIdx.y;
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const OrbLevel L = g.lv[v * g.L + level];
-    if (x >= L.w || y >= L.h)
-        return;
-    int s = 0;
-#pragma unroll
-    for (int k = 0; k < 7; ++k)
-        s += kGauss7[k] * (int)g.tmp[L.off + (size_t)reflect101(y + k - 3, L.h) * L.w + x];
-    g.blur[L.off + (size_t)y * L.w + x] = (uint8_t)((s + 32768) >> 16);
-}
-
-hipError_t launch_orb_blur(const OrbGeom &g, int level, int max_w, int max_h, hipStream_t s)
-{
-    hipLaunchKernelGGL(orb_blur_h_kernel, dim3((max_w + 255) / 256, max_h, g.V), dim3(256), 0, s, g, level);
-    hipLaunchKernelGGL(orb_blur_v_kernel, dim3((max_w + 255) / 256, max_h, g.V), dim3(256), 0, s, g, level);
-    return hipGetLastError();
+    return min(max(i, 0), n - 1); // one reflection covers every read below; clamp for safety
 }
 
 // ---------------------------------------------------------------------------
 // rBRIEF (computeOrbDescriptors, WTA_K 2): pattern steered by the keypoint
 // angle, centre cvRound(pt / layerScale) on the blurred level image; bit j of
-// byte i = value(16 i + 2 j) < value(16 i + 2 j + 1)
+// byte i = value(16 i + 2 j) < value(16 i + 2 j + 1).
+// The descriptor reads the blurred level only within kDescR of its centre
+// (|cvRound(rotated pattern point)| <= cvRound(13 sqrt 2) = 18), so each
+// workgroup blurs just its (2 kDescR + 1)^2 patch in LDS instead of the whole
+// pyramid being blurred: ~20k multiply-adds per keypoint against 14 per
+// pyramid pixel.  Every patch pixel the pattern reaches lies inside the level
+// (centres are >= edge_threshold >= 19 px from its border), so the reflected
+// source taps give exactly the full-image blur there.
 // ---------------------------------------------------------------------------
-__global__ void orb_desc_kernel(OrbGeom g, const dp_keypoint *kp, const int32_t *kv, int64_t n,
-                                const int8_t *pattern, uint32_t *desc)
+constexpr int kDescR = 19;
+constexpr int kDescP = 2 * kDescR + 1; // blurred patch side
+constexpr int kDescS = kDescP + 6;     // source patch side (3 taps each way)
+static_assert(kOrbPatternPairs == 256, "one pattern pair per thread");
+
+__global__ __launch_bounds__(256) void orb_desc_kernel(OrbGeom g, const dp_keypoint *kp, const int32_t *kv,
+                                                       const int8_t *pattern, uint32_t *desc)
 {
-    __shared__ int8_t pat[2 * 2 * kOrbPatternPairs];
-    for (int i = threadIdx.x; i < 4 * kOrbPatternPairs; i += blockDim.x)
-        pat[i] = pattern[i];
-    __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
+    __shared__ uint8_t src[kDescS][kDescS + 3];
+    __shared__ uint16_t hb[kDescS][kDescP + 1];
+    __shared__ uint8_t blr[kDescP][kDescP + 1];
+    const int64_t i = blockIdx.x;
+    const int tid = threadIdx.x;
     const dp_keypoint k = kp[i];
     const OrbLevel L = g.lv[kv[i] * g.L + k.octave];
     const float inv = 1.0f / L.scale;
     const int cy = (int)rintf(k.y * inv), cx = (int)rintf(k.x * inv);
+    const uint8_t *img = g.gray + L.off;
+    for (int t = tid; t < kDescS * kDescS; t += 256) {
+        const int yy = t / kDescS, xx = t - yy * kDescS;
+        const int gy = reflect101(cy - kDescR - 3 + yy, L.h), gx = reflect101(cx - kDescR - 3 + xx, L.w);
+        src[yy][xx] = img[(size_t)gy * L.w + gx];
+    }
+    __syncthreads();
+    // horizontal pass: sum_x w_x p (<= 256 * 255, u16)
+    for (int t = tid; t < kDescS * kDescP; t += 256) {
+        const int yy = t / kDescP, xx = t - yy * kDescP;
+        int s = 0;
+#pragma unroll
+        for (int q = 0; q < 7; ++q)
+            s += kGauss7[q] * src[yy][xx + q];
+        hb[yy][xx] = (uint16_t)s;
+    }
+    __syncthreads();
+    // vertical pass: (sum_y w_y h + 2^15) >> 16
+    for (int t = tid; t < kDescP * kDescP; t += 256) {
+        const int yy = t / kDescP, xx = t - yy * kDescP;
+        int s = 0;
+#pragma unroll
+        for (int q = 0; q < 7; ++q)
+            s += kGauss7[q] * (int)hb[yy + q][xx];
+        blr[yy][xx] = (uint8_t)((s + 32768) >> 16);
+    }
+    __syncthreads();
+    // pair tid = points 2 tid, 2 tid + 1 -> word tid / 32, bit tid % 32: the
+    // low / high ballot halves of wave w are words 2 w and 2 w + 1
     const float ang = k.angle * (float)(3.14159265358979323846 / 180.0f);
     double sd, cd;
     dpm::sincos((double)ang, sd, cd);
     const float a = (float)cd, b = (float)sd;
-    const uint8_t *ctr = g.blur + L.off + (size_t)cy * L.w + cx;
-    for (int w = 0; w < 8; ++w) {
-        uint32_t word = 0;
-        for (int q = 0; q < 32; ++q) {
-            const int pi = (w * 32 + q) * 2; // pair index -> points 2 pi, 2 pi + 1
-            int val[2];
-            for (int e = 0; e < 2; ++e) {
-                const float px = (float)pat[2 * (pi + e)], py = (float)pat[2 * (pi + e) + 1];
-                const float xr = px * a - py * b, yr = px * b + py * a;
-                const int ix = (int)rintf(xr), iy = (int)rintf(yr);
-                val[e] = ctr[iy * L.w + ix];
-            }
-            word |= (uint32_t)(val[0] < val[1]) << q;
-        }
-        desc[(size_t)i * 8 + w] = word;
+    int val[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const float px = (float)pattern[2 * (2 * tid + e)], py = (float)pattern[2 * (2 * tid + e) + 1];
+        const float xr = px * a - py * b, yr = px * b + py * a;
+        const int ix = (int)rintf(xr), iy = (int)rintf(yr);
+        val[e] = blr[kDescR + iy][kDescR + ix];
     }
+    const uint64_t m = __ballot(val[0] < val[1]);
+    const int lane = tid & 63;
+    if (lane < 2)
+        desc[(size_t)i * 8 + (tid >> 6) * 2 + lane] = (uint32_t)(m >> (32 * lane));
 }
 
 hipError_t launch_orb_desc(const OrbGeom &g, const dp_keypoint *kp, const int32_t *kv, int64_t n,
@@ -618,8 +617,7 @@ hipError_t launch_orb_desc(const OrbGeom &g, const dp_keypoint *kp, const int32_
 {
     if (n <= 0)
         return hipSuccess;
-    hipLaunchKernelGGL(orb_desc_kernel, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, g, kp, kv, n, pattern,
-                       desc);
+    hipLaunchKernelGGL(orb_desc_kernel, dim3((unsigned)n), dim3(256), 0, s, g, kp, kv, pattern, desc);
     return hipGetLastError();
 }
 

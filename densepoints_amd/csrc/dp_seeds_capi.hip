@@ -28,8 +28,7 @@ struct dp_seedgen {
     // GenerateSeeds
     DevBuf<dpk::OrbLevel> lv;
     DevBuf<dpk::PyrPlane> planes0;
-    DevBuf<uint8_t> gray, score, blur;
-    DevBuf<uint16_t> htmp;
+    DevBuf<uint8_t> gray, score;
     DevBuf<int64_t> row_cnt, row_off;
     DevBuf<dpk::OrbCand> cand, cand2;
     DevBuf<uint32_t> hist, hkey, hkey_sorted, seg_cnt;
@@ -75,11 +74,10 @@ void dp_seedgen_free(dp_seedgen *s)
     s->jobs.release();
     s->blocks.release();
     s->pkeys.release();
-    for (auto *b : {&s->gray, &s->score, &s->blur, &s->keep_all, &s->flag})
+    for (auto *b : {&s->gray, &s->score, &s->keep_all, &s->flag})
         b->release();
     s->lv.release();
     s->planes0.release();
-    s->htmp.release();
     s->row_cnt.release();
     s->row_off.release();
     s->cand.release();
@@ -440,11 +438,9 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
                              st));
     DP_HIP(c, s->gray.reserve(pool));
     DP_HIP(c, s->score.reserve(pool));
-    DP_HIP(c, s->blur.reserve(pool));
-    DP_HIP(c, s->htmp.reserve(pool));
     DP_HIP(c, s->row_cnt.reserve(rows + 1));
     DP_HIP(c, s->row_off.reserve(rows + 1));
-    dpk::OrbGeom g{s->lv.p, V, L, s->gray.p, s->blur.p, s->htmp.p};
+    dpk::OrbGeom g{s->lv.p, V, L, s->gray.p};
 
     Timer t0, t1, t2, t3, t4;
     DP_HIP(c, hipEventRecord(t0.e, st));
@@ -585,8 +581,6 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     DP_HIP(c, hipMemcpyAsync(h_kv.data(), s->kv_b.p, n5 * 4, hipMemcpyDeviceToHost, st));
     DP_HIP(c, hipEventRecord(t1.e, st));
     // descriptors
-    for (int l = 0; l < L; ++l)
-        DP_HIP(c, dpk::launch_orb_blur(g, l, max_w, max_h, st));
     std::vector<int8_t> pat(4 * dpk::kOrbPatternPairs);
     dpk::orb_pattern(pat.data());
     DP_HIP(c, s->pattern.reserve(pat.size()));
