@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="cfg3_32view_4k")
-    ap.add_argument("--batch", type=int, default=65536, help="expansion candidates per step per GPU")
+    ap.add_argument("--batch", type=int, default=262144, help="expansion candidates per step per GPU")
     ap.add_argument("--cell", type=int, default=11)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline wall time")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -233,8 +233,10 @@ def main():
     if tj and os.path.exists(tj):
         with open(tj) as f:
             t = json.load(f)
-        result["roofline"]["traffic"] = t.get("hbm_bytes_per_launch")
-        result["roofline"]["traffic_source"] = os.path.relpath(tj, ROOT)
+        # PMC bytes are per launch, so they only apply to the batch they were measured on
+        if t.get("batch") == result["config"]["batch_per_gpu"]:
+            result["roofline"]["traffic"] = t.get("hbm_bytes_per_launch")
+            result["roofline"]["traffic_source"] = os.path.relpath(tj, ROOT)
 
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out)

@@ -56,7 +56,8 @@ def main():
         if cand:
             k, e = max(cand.items(), key=lambda kv: kv[1].get("stats", {}).get("total_ns", 0.0))
             open(sys.argv[3], "w").write(json.dumps({
-                "kernel": k, "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
+                "kernel": k, "batch": int(sys.argv[4]) if len(sys.argv) > 4 else None,
+                "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
                 "hbm_bytes_per_launch_raw": e["hbm_bytes_per_launch_raw"],
                 "avg_ns": e.get("stats", {}).get("avg_ns"),
                 "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM/rocprofv3), "
