@@ -20,6 +20,7 @@ struct OrbLevel {
     int64_t row0;     // first global row index (row counters)
     float scale;      // layerScale = (float)pow(scale_factor, level)
     int32_t nfeat;    // nfeaturesPerLevel
+    double rsx, rsy;  // resize from level - 1: 1 / ((double)w / w_prev), same for h (0 at level 0)
 };
 
 // FAST candidate / detected keypoint in level coordinates

@@ -39,9 +39,9 @@ hipError_t launch_orb_gray(const PyrPlane *planes, const OrbGeom &g, int max_w, 
 // pyramid level l from level l-1: resize(INTER_LINEAR), 11-bit coefficients,
 // (b0*S0 + b1*S1 + 2^21) >> 22
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void lin_coef(int d, int sn, int dn, int &s0, int &a0, int &a1)
+// scale = 1 / ((double)dn / (double)sn), precomputed per level (OrbLevel::rsx/rsy)
+__device__ __forceinline__ void lin_coef(int d, int sn, double scale, int &s0, int &a0, int &a1)
 {
-    const double scale = 1.0 / ((double)dn / (double)sn);
     float f = (float)(((double)d + 0.5) * scale - 0.5);
     int si = (int)floorf(f);
     f = f - (float)si;
@@ -66,8 +66,8 @@ __global__ void orb_resize_kernel(OrbGeom g, int level)
     if (x >= D.w || y >= D.h)
         return;
     int sx, ax0, ax1, sy, ay0, ay1;
-    lin_coef(x, S.w, D.w, sx, ax0, ax1);
-    lin_coef(y, S.h, D.h, sy, ay0, ay1);
+    lin_coef(x, S.w, D.rsx, sx, ax0, ax1);
+    lin_coef(y, S.h, D.rsy, sy, ay0, ay1);
     const int sx1 = min(sx + 1, S.w - 1), sy1 = min(sy + 1, S.h - 1);
     const uint8_t *r0 = g.gray + S.off + (size_t)sy * S.w;
     const uint8_t *r1 = g.gray + S.off + (size_t)sy1 * S.w;

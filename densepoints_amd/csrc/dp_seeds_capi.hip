@@ -421,6 +421,9 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
             o.h = l == 0 ? vh[v] : (int)std::lrint((float)vh[v] / sc);
             if (o.w < 4 || o.h < 4)
                 return fail(c, DP_E_ARG, "dp_generate_seeds: pyramid level smaller than 4 px (reduce n_levels)");
+            // INTER_LINEAR's inverse scale, once per level instead of per pixel
+            o.rsx = l == 0 ? 0.0 : 1.0 / ((double)o.w / (double)lv[(size_t)v * L + l - 1].w);
+            o.rsy = l == 0 ? 0.0 : 1.0 / ((double)o.h / (double)lv[(size_t)v * L + l - 1].h);
             o.off = pool;
             o.row0 = rows;
             o.nfeat = nfeat[l];
