@@ -98,8 +98,20 @@ __global__ void orb_fast_kernel(OrbGeom g, int level, int t, uint8_t *score)
     if (x >= L.w || y >= L.h)
         return;
     int out = 0;
+    bool cand = false;
+    const uint8_t *p = g.gray + L.off + (size_t)y * L.w + x;
     if (x >= 3 && x < L.w - 3 && y >= 3 && y < L.h - 3) {
-        const uint8_t *p = g.gray + L.off + (size_t)y * L.w + x;
+        // every arc of 9 contains two compass pixels 4 apart (0/4, 4/8, 8/12,
+        // 12/0), so a corner needs such a pair both brighter or both darker by
+        // more than t; pixels without one score 0 exactly, and waves where no
+        // lane has one skip the arc network
+        const int c = p[0];
+        const int e0 = c - p[3 * L.w], e4 = c - p[3], e8 = c - p[-3 * L.w], e12 = c - p[-3];
+        const bool b0 = e0 > t, b4 = e4 > t, b8 = e8 > t, b12 = e12 > t;
+        const bool k0 = e0 < -t, k4 = e4 < -t, k8 = e8 < -t, k12 = e12 < -t;
+        cand = ((b0 || b8) && (b4 || b12)) || ((k0 || k8) && (k4 || k12));
+    }
+    if (cand) {
         const int c = p[0];
         int d[16];
 #pragma unroll
