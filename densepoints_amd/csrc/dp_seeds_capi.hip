@@ -409,6 +409,7 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     std::vector<dpk::OrbLevel> lv((size_t)V * L);
     int64_t pool = 0, rows = 0;
     int max_w = 0, max_h = 0;
+    std::vector<int> lw(L, 0), lh(L, 0); // per-level launch extents (max over views)
     std::vector<int32_t> vw(V), vh(V);
     for (int v = 0; v < V; ++v) {
         vw[v] = c->hv[v].W;
@@ -431,6 +432,8 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
             rows += o.h;
             max_w = std::max(max_w, o.w);
             max_h = std::max(max_h, o.h);
+            lw[l] = std::max(lw[l], o.w);
+            lh[l] = std::max(lh[l], o.h);
         }
     }
     DP_HIP(c, s->n_sel.reserve(1));
@@ -450,15 +453,15 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     // ---- DetectKeypoints (matcher.cpp:45-87)
     DP_HIP(c, dpk::launch_orb_gray(s->planes0.p, g, lv[0].w > 0 ? max_w : 0, max_h, st));
     for (int l = 1; l < L; ++l)
-        DP_HIP(c, dpk::launch_orb_resize(g, l, max_w, max_h, st));
+        DP_HIP(c, dpk::launch_orb_resize(g, l, lw[l], lh[l], st));
     for (int l = 0; l < L; ++l)
-        DP_HIP(c, dpk::launch_orb_fast(g, l, mo.fast_threshold, s->score.p, max_w, max_h, st));
+        DP_HIP(c, dpk::launch_orb_fast(g, l, mo.fast_threshold, s->score.p, lw[l], lh[l], st));
     DP_HIP(c, hipMemsetAsync(s->row_cnt.p, 0, (size_t)(rows + 1) * sizeof(int64_t), st));
     // row counts as int32 into the low half of an int64 buffer would alias: count into idx_a
     DP_HIP(c, s->idx_a.reserve(rows + 1));
     DP_HIP(c, hipMemsetAsync(s->idx_a.p, 0, (size_t)(rows + 1) * sizeof(int32_t), st));
     for (int l = 0; l < L; ++l)
-        DP_HIP(c, dpk::launch_orb_nms(g, l, s->score.p, mo.edge_threshold, nullptr, s->idx_a.p, nullptr, max_h, st));
+        DP_HIP(c, dpk::launch_orb_nms(g, l, s->score.p, mo.edge_threshold, nullptr, s->idx_a.p, nullptr, lh[l], st));
     DP_CUB(c, s, hipcub::DeviceScan::ExclusiveSum(_tmp, _bytes, s->idx_a.p, s->row_off.p, (int)(rows + 1), st));
     int64_t n_cand = 0;
     DP_HIP(c, hipMemcpyAsync(&n_cand, s->row_off.p + rows, sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -468,7 +471,7 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     DP_HIP(c, s->flag.reserve(n_cand + 1));
     DP_HIP(c, s->n_sel.reserve(1));
     for (int l = 0; l < L; ++l)
-        DP_HIP(c, dpk::launch_orb_nms(g, l, s->score.p, mo.edge_threshold, s->row_off.p, nullptr, s->cand.p, max_h, st));
+        DP_HIP(c, dpk::launch_orb_nms(g, l, s->score.p, mo.edge_threshold, s->row_off.p, nullptr, s->cand.p, lh[l], st));
     // retainBest(2 n_l) by FAST score
     const int nseg = V * L;
     DP_HIP(c, s->hist.reserve((size_t)nseg * 256));
