@@ -163,36 +163,61 @@ __global__ __launch_bounds__(256) void orb_nms_kernel(OrbGeom g, int level, cons
     int64_t base = out ? row_off[L.row0 + y] : 0;
     int total = 0;
     const bool row_ok = y >= edge && y < L.h - edge;
-    for (int x0 = 0; x0 < L.w; x0 += 256) {
-        const int x = x0 + tid;
-        bool keep = false;
-        int s = 0;
-        if (row_ok && x >= edge && x < L.w - edge) {
-            const uint8_t *p = score + L.off + (size_t)y * L.w + x;
-            s = p[0];
-            if (s > 0) {
-                const int W = L.w;
-                keep = s > p[-W - 1] && s > p[-W] && s > p[-W + 1] && s > p[-1] && s > p[1] && s > p[W - 1] &&
-                       s > p[W] && s > p[W + 1];
+    if (!row_ok) {
+        if (!out && tid == 0)
+            row_cnt[L.row0 + y] = 0;
+        return;
+    }
+    // 4 consecutive pixels per thread (1024 per step): x order = (thread, j),
+    // so a kept pixel's rank is the kept pixels of lower lanes over all four
+    // ballots plus its own lower j
+    constexpr int kPx = 4;
+    const uint64_t below = (1ull << l) - 1ull;
+    for (int x0 = 0; x0 < L.w; x0 += 256 * kPx) {
+        bool keep[kPx];
+        int sv[kPx];
+        uint64_t m[kPx];
+        int mine = 0, lower = 0, wave_all = 0;
+#pragma unroll
+        for (int j = 0; j < kPx; ++j) {
+            const int x = x0 + tid * kPx + j;
+            keep[j] = false;
+            sv[j] = 0;
+            if (x >= edge && x < L.w - edge) {
+                const uint8_t *p = score + L.off + (size_t)y * L.w + x;
+                const int s = p[0];
+                sv[j] = s;
+                if (s > 0) {
+                    const int W = L.w;
+                    keep[j] = s > p[-W - 1] && s > p[-W] && s > p[-W + 1] && s > p[-1] && s > p[1] &&
+                              s > p[W - 1] && s > p[W] && s > p[W + 1];
+                }
             }
+            m[j] = __ballot(keep[j]);
+            lower += __popcll(m[j] & below);
+            wave_all += __popcll(m[j]);
         }
-        const uint64_t m = __ballot(keep);
         if (l == 0)
-            wsum[w] = __popcll(m);
+            wsum[w] = wave_all;
         __syncthreads();
         int before = 0, all = 0;
         for (int i = 0; i < 4; ++i) {
             before += i < w ? wsum[i] : 0;
             all += wsum[i];
         }
-        if (out && keep) {
-            const int rank = before + __popcll(m & ((1ull << l) - 1ull));
-            OrbCand c;
-            c.x = x;
-            c.y = y;
-            c.seg = v * g.L + level;
-            c.resp = (float)s;
-            out[base + total + rank] = c;
+        if (out) {
+#pragma unroll
+            for (int j = 0; j < kPx; ++j) {
+                if (keep[j]) {
+                    OrbCand c;
+                    c.x = x0 + tid * kPx + j;
+                    c.y = y;
+                    c.seg = v * g.L + level;
+                    c.resp = (float)sv[j];
+                    out[base + total + before + lower + mine] = c;
+                    ++mine;
+                }
+            }
         }
         total += all;
         __syncthreads();
