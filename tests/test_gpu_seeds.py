@@ -221,3 +221,19 @@ def test_seeds_bad_options_fail_loudly():
     with dp.Engine() as eng:  # no views set
         with pytest.raises(dp.DensePointsError):
             M.Matcher(eng).generate_seeds()
+
+
+def test_seeds_min_edge_threshold(orc):
+    """edge_threshold 19 (the minimum): keypoint centres 19 px from a level's
+    border, so the descriptor's patch blur reflects (BORDER_REFLECT_101) at the
+    image edge exactly as the full-image blur does."""
+    cfg = synth.config(n_views=3, width=320, height=240, kind=1)
+    P, imgs, _ = synth.scene_host(cfg)
+    r, m = _run_both(orc, P, imgs, dict(n_features=3000, n_levels=4, fast_threshold=6, edge_threshold=19))
+    kp = np.concatenate([r["keypoints"][v] for v in range(3)])  # equal to the GPU's (checked above)
+    assert len(kp) > 0
+    # some keypoint's blur patch reaches past its level's border (reflection exercised)
+    s = 1.2 ** kp["octave"].astype(np.float64)
+    x, y = kp["x"] / s, kp["y"] / s
+    w, h = np.rint(320 / s), np.rint(240 / s)
+    assert np.any(np.minimum(np.minimum(x, y), np.minimum(w - 1 - x, h - 1 - y)) < 22)
