@@ -221,6 +221,7 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     dp_seedgen_free(c->seeds);
     c->seeds = nullptr;
     c->grid.release();
+    c->lpt.release();
     c->front.release();
     c->f_alive.release();
     c->f_keep.release();
@@ -656,6 +657,15 @@ static dpk::RefineArgs refine_args(dp_ctx *c, dp_patch *d, int n, int cell, int 
     a.max_pops = c->opt.max_pops;
     a.img_base = c->img_base;
     a.narrow = c->narrow ? 1 : 0;
+    // longest-first order (off with DP_NO_LPT=1, for A/B timing); without the
+    // scratch the kernel dequeues in index order
+    static const bool lpt_off = getenv("DP_NO_LPT") && getenv("DP_NO_LPT")[0] == '1';
+    a.order = nullptr;
+    a.order_scratch = nullptr;
+    if (!lpt_off && n > 0 && c->lpt.reserve((size_t)n + 2 * dpk::kLptBuckets) == hipSuccess) {
+        a.order = c->lpt.p;
+        a.order_scratch = c->lpt.p + n;
+    }
     return a;
 }
 

@@ -87,6 +87,7 @@ struct dp_ctx {
     bool timed = false;
     int64_t grid_cells = 0;
     DevBuf<uint32_t> grid;
+    DevBuf<uint32_t> lpt;    // refine dequeue order + its counters
     DevBuf<dp_patch> pat, store, cand;
     DevBuf<uint8_t> ok, acc;
     DevBuf<uint32_t> prefix;

@@ -35,7 +35,15 @@ struct RefineArgs {
     // a window tap is img_base (SGPR) + a 32-bit byte offset (ViewDev::img_off)
     const char *img_base;
     int32_t narrow;
+    // optional longest-first dequeue order, filled by launch_refine: groups
+    // (one parent's 4 children, or one patch) by descending visible-view count
+    // (a candidate costs ~E |V| texel passes), so the longest run first and
+    // the launch does not end on a few long stragglers.  Scheduling only:
+    // every candidate's output is independent of the order.
+    uint32_t *order;         // >= ceil(n / group size) entries, or null
+    uint32_t *order_scratch; // kLptBuckets * 2 counters
 };
+constexpr int kLptBuckets = 129; // visible-view counts 0..128
 
 // organizer / BFS kernels
 struct ClaimArgs {

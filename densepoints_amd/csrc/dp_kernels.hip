@@ -1105,11 +1105,13 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
     // evaluations of a patch), then help the other ranges in order.
     int cur = (int)(xcc_id() & (kXcds - 1));
     int left = kXcds;
+    const uint32_t gs = a.parents ? 4u : 1u;                     // LPT group size
+    const int npos = a.order ? (int)(((uint32_t)a.n + gs - 1) / gs * gs) : a.n; // dequeue positions
     for (;;) {
-        uint32_t idx = (uint32_t)a.n;
+        uint32_t idx = (uint32_t)npos;
         if (lane == 0) {
             while (left > 0) {
-                const uint32_t lo = range_lo(a.n, cur), hi = range_lo(a.n, cur + 1);
+                const uint32_t lo = range_lo(npos, cur), hi = range_lo(npos, cur + 1);
                 const uint32_t t = lo + atomicAdd(a.work + kWorkStride * cur, 1u);
                 if (t < hi) {
                     idx = t;
@@ -1120,8 +1122,13 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
             }
         }
         idx = (uint32_t)uni((int)idx);
-        if (idx >= (uint32_t)a.n)
+        if (idx >= (uint32_t)npos)
             break;
+        if (a.order) {
+            idx = (uint32_t)uni((int)(a.order[idx / gs] * gs + idx % gs));
+            if (idx >= (uint32_t)a.n) // the last group's missing children
+                continue;
+        }
         dp_patch *out = a.patches + idx;
         bool live = true;
 #ifdef DP_STAMPS
@@ -1459,6 +1466,40 @@ int read_stamps(unsigned long long *out)
 #endif
 }
 
+// LPT order: a counting sort of the groups by 128 - |V| (the parent's visible
+// views for expansion children, the patch's own otherwise)
+__device__ __forceinline__ int lpt_key(const RefineArgs &a, int64_t g)
+{
+    const dp_patch &p = a.parents ? a.parents[a.parent0 + g] : a.patches[g];
+    return kLptBuckets - 1 - (__popcll(p.vis[0]) + __popcll(p.vis[1]));
+}
+
+__global__ void lpt_hist_kernel(RefineArgs a, int ng)
+{
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < ng)
+        atomicAdd(a.order_scratch + lpt_key(a, g), 1u);
+}
+
+// exclusive scan of the bucket counts into the cursors (one wave)
+__global__ void lpt_scan_kernel(RefineArgs a)
+{
+    if (threadIdx.x != 0)
+        return;
+    uint32_t run = 0;
+    for (int b = 0; b < kLptBuckets; ++b) {
+        a.order_scratch[kLptBuckets + b] = run;
+        run += a.order_scratch[b];
+    }
+}
+
+__global__ void lpt_scatter_kernel(RefineArgs a, int ng)
+{
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < ng)
+        a.order[atomicAdd(a.order_scratch + kLptBuckets + lpt_key(a, g), 1u)] = (uint32_t)g;
+}
+
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s)
 {
     if (a.n <= 0)
@@ -1476,6 +1517,15 @@ hipError_t launch_refine(const RefineArgs &a, hipStream_t s)
     const int g = pass_width(a.cell);
     if (g <= 0)
         return hipErrorInvalidValue;
+    if (a.order) {
+        const int ng = a.parents ? (a.n + 3) / 4 : a.n;
+        e = hipMemsetAsync(a.order_scratch, 0, 2 * kLptBuckets * sizeof(uint32_t), s);
+        if (e != hipSuccess)
+            return e;
+        hipLaunchKernelGGL(lpt_hist_kernel, dim3((ng + 255) / 256), dim3(256), 0, s, a, ng);
+        hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(lpt_scatter_kernel, dim3((ng + 255) / 256), dim3(256), 0, s, a, ng);
+    }
     switch (a.mode * 16 + g) {
 #define DP_LAUNCH_REFINE(M, GG)                                                                               \
     case M * 16 + GG:                                                                                          \
