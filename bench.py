@@ -41,8 +41,11 @@ def parse():
     ap.add_argument("--config", default="cfg3_32view_4k")
     ap.add_argument("--batch", type=int, default=262144, help="expansion candidates per step per GPU")
     ap.add_argument("--cell", type=int, default=11)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline wall time")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-parents", type=int, default=5000,
+                    help="CPU baseline sample: first N parents (4N candidates) of the batch")
+    ap.add_argument("--cpu-parents-1thread", type=int, default=5000,
+                    help="single-thread CPU baseline sample (a prefix of the same sample)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-densify", action="store_true", help="skip the informational end-to-end densify")
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes/launch from profiles/")
@@ -235,8 +238,14 @@ def main():
             t = json.load(f)
         # PMC bytes are per launch, so they only apply to the batch they were measured on
         if t.get("batch") == result["config"]["batch_per_gpu"]:
+            # both readings: FETCH_SIZE as counted, and doubled per the gfx950
+            # correction that MI355X_MICROARCH.md calibrates for 16-B/lane
+            # streams (these are 8-B gathers: see "traffic_calibration")
             result["roofline"]["traffic"] = t.get("hbm_bytes_per_launch")
+            result["roofline"]["traffic_raw"] = t.get("hbm_bytes_per_launch_raw")
             result["roofline"]["traffic_source"] = os.path.relpath(tj, ROOT)
+            if t.get("calibration"):
+                result["roofline"]["traffic_calibration"] = t["calibration"]
 
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out)
@@ -299,10 +308,26 @@ def latest_traffic_json():
     return found[-1] if found else None
 
 
+def host_cores():
+    """CPUs this process may actually run on: the affinity mask, capped by a
+    cgroup v2 CPU quota when one is set (on the GPU box os.cpu_count() reports
+    the whole machine, of which the job gets a share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(args, cfg, P, planes, parents, gpu_out):
-    """The oracle (CPU restatement, test infrastructure) on a bounded sample of
-    the same parents, timed on this host's cores; also a parity spot-check of
-    the GPU children on that sample."""
+    """The oracle (CPU restatement, test infrastructure) on a FIXED sample --
+    the first --cpu-parents parents (4x as many candidates) of the same batch --
+    timed on all of this host's usable cores and on one thread (SURVEY 8d CPU
+    timing); also a bit-exact parity check of the GPU children on that sample."""
     from oracle import pyoracle as orc
 
     imgs = []
@@ -310,24 +335,27 @@ def cpu_baseline(args, cfg, P, planes, parents, gpu_out):
         a = pl.cpu().numpy().view(np.uint8).reshape(cfg.height, cfg.width, 4)
         imgs.append(np.ascontiguousarray(a[:, :, :3]))
     S = orc.Scene(P, imgs)
-    threads = args.cpu_threads
-    n = 16
-    while True:
-        t0 = time.perf_counter()
-        kids, acc = S.expand(parents[:n], threads)
-        t = time.perf_counter() - t0
-        if t >= args.cpu_seconds * 0.5 or n >= len(parents):
-            break
-        n = min(len(parents), max(n * 2, int(n * args.cpu_seconds / max(t, 1e-3) * 0.9)))
+    cores = args.cpu_threads or host_cores()
+    n = min(args.cpu_parents, len(parents))
+    t0 = time.perf_counter()
+    kids, acc = S.expand(parents[:n], cores)
+    t = time.perf_counter() - t0
+    n1 = min(args.cpu_parents_1thread, n)
+    t0 = time.perf_counter()
+    S.expand(parents[:n1], 1)
+    t1 = time.perf_counter() - t0
     g = gpu_out[: 4 * n]
     fields = ("pos", "normal", "ref", "vis", "cand", "score", "evals", "flags", "parent")
     same = all(kids[f].tobytes() == g[f].tobytes() for f in fields)
     return {
         "value": round(4 * n / t / 1e6, 6),
         "unit": "Mpatches/s",
-        "cores": threads,
+        "cores": cores,
         "kind": "port",
-        "sample": f"first {n} parents ({4 * n} candidates) of the GPU batch, same cell, {t:.1f} s",
+        "sample": f"first {n} parents ({4 * n} candidates) of the GPU batch, same cell, {t:.1f} s on {cores} threads",
+        "value_1thread": round(4 * n1 / t1 / 1e6, 6),
+        "sample_1thread": f"first {n1} parents ({4 * n1} candidates), {t1:.1f} s on 1 thread",
+        "host_cpus_reported": os.cpu_count(),
         "parity_bit_exact_on_sample": bool(same),
     }
 

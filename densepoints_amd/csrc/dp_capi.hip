@@ -165,6 +165,10 @@ extern "C" int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out)
     if (!c)
         return DP_E_OOM;
     c->device = device;
+    {
+        const char *e = getenv("DP_NO_LPT");
+        c->lpt_off = e && e[0] == '1';
+    }
     if (opt)
         c->opt = *opt;
     else
@@ -657,14 +661,21 @@ static dpk::RefineArgs refine_args(dp_ctx *c, dp_patch *d, int n, int cell, int 
     a.max_pops = c->opt.max_pops;
     a.img_base = c->img_base;
     a.narrow = c->narrow ? 1 : 0;
-    // longest-first order (off with DP_NO_LPT=1, for A/B timing); without the
-    // scratch the kernel dequeues in index order
-    static const bool lpt_off = getenv("DP_NO_LPT") && getenv("DP_NO_LPT")[0] == '1';
+    // longest-first order (off in a context created with DP_NO_LPT=1, for A/B
+    // timing and the order-independence test); without the scratch buffer the
+    // kernel dequeues in index order
     a.order = nullptr;
     a.order_scratch = nullptr;
-    if (!lpt_off && n > 0 && c->lpt.reserve((size_t)n + 2 * dpk::kLptBuckets) == hipSuccess) {
-        a.order = c->lpt.p;
-        a.order_scratch = c->lpt.p + n;
+    if (!c->lpt_off && n > 0) {
+        if (c->lpt.reserve((size_t)n + 2 * dpk::kLptBuckets) == hipSuccess) {
+            a.order = c->lpt.p;
+            a.order_scratch = c->lpt.p + n;
+        } else {
+            // the failed hipMalloc is recorded as the thread's last error: clear
+            // it, or launch_refine's hipGetLastError() would report the
+            // index-order launch that follows as failed
+            (void)hipGetLastError();
+        }
     }
     return a;
 }

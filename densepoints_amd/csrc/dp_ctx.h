@@ -88,6 +88,7 @@ struct dp_ctx {
     int64_t grid_cells = 0;
     DevBuf<uint32_t> grid;
     DevBuf<uint32_t> lpt;    // refine dequeue order + its counters
+    bool lpt_off = false;    // DP_NO_LPT=1 at dp_ctx_create: index-order dequeue
     DevBuf<dp_patch> pat, store, cand;
     DevBuf<uint8_t> ok, acc;
     DevBuf<uint32_t> prefix;

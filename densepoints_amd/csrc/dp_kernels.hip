@@ -1474,14 +1474,25 @@ __device__ __forceinline__ int lpt_key(const RefineArgs &a, int64_t g)
     return kLptBuckets - 1 - (__popcll(p.vis[0]) + __popcll(p.vis[1]));
 }
 
+// Per-block LDS histogram, flushed with one global atomic per non-empty
+// bucket (only a dozen of the 129 buckets are hot in practice, so per-thread
+// global atomics serialised on them).
 __global__ void lpt_hist_kernel(RefineArgs a, int ng)
 {
+    __shared__ uint32_t h[kLptBuckets];
+    for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
+        h[b] = 0;
+    __syncthreads();
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < ng)
-        atomicAdd(a.order_scratch + lpt_key(a, g), 1u);
+        atomicAdd(&h[lpt_key(a, g)], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
+        if (h[b])
+            atomicAdd(a.order_scratch + b, h[b]);
 }
 
-// exclusive scan of the bucket counts into the cursors (one wave)
+// exclusive scan of the bucket counts into the cursors (one thread: 129 adds)
 __global__ void lpt_scan_kernel(RefineArgs a)
 {
     if (threadIdx.x != 0)
@@ -1493,11 +1504,30 @@ __global__ void lpt_scan_kernel(RefineArgs a)
     }
 }
 
+// Each block ranks its groups inside their bucket in LDS, reserves one range
+// per non-empty bucket from the global cursor, then writes.  Positions inside
+// a bucket depend on block timing; only the bucket order matters (the order
+// schedules the dequeue and never changes a candidate's output).
 __global__ void lpt_scatter_kernel(RefineArgs a, int ng)
 {
+    __shared__ uint32_t h[kLptBuckets];
+    for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
+        h[b] = 0;
+    __syncthreads();
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    int key = 0;
+    uint32_t rank = 0;
+    if (g < ng) {
+        key = lpt_key(a, g);
+        rank = atomicAdd(&h[key], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
+        if (h[b])
+            h[b] = atomicAdd(a.order_scratch + kLptBuckets + b, h[b]);
+    __syncthreads();
     if (g < ng)
-        a.order[atomicAdd(a.order_scratch + kLptBuckets + lpt_key(a, g), 1u)] = (uint32_t)g;
+        a.order[h[key] + rank] = (uint32_t)g;
 }
 
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s)

@@ -168,3 +168,31 @@ def test_cli_full_pipeline_generates_seeds(tmp_path_factory, tmp_path, orc):
     ref = tmp_path / "oracle.ply"
     write_ply(str(ref), op)
     assert out.read_bytes() == ref.read_bytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("views", [2, 4])
+def test_cli_baseline_cfg1_vga(tmp_path_factory, tmp_path, orc, views):
+    """BASELINE config 1 through programs/densify: the 640x480 synthetic plane.
+    With 2 views every patch has fewer than 3 visible non-reference views, so
+    the reference writes an empty cloud; the 4-view variant's PLY
+    equals the oracle's densify byte for byte (main.cpp:12-40, pmvs.cpp:22-43)."""
+    from densepoints_amd.pmvs import write_ply
+
+    d = str(tmp_path_factory.mktemp(f"cfg1_{views}"))
+    run("--synthetic", f"{views},640,480,0", "--write-scene", d)
+    out = tmp_path / "points.ply"
+    res = json.loads(run("-i", os.path.join(d, "scene.json"), "--seeds", os.path.join(d, "seeds.xyz"),
+                         "-o", str(out)).stdout)
+    cfg = synth.config(views, 640, 480, 0)
+    P = synth.cameras(cfg)
+    imgs = [synth.render_host(cfg, P, v) for v in range(views)]
+    op, ost = orc.Scene(P, imgs).densify(synth.seeds(cfg, P))
+    assert res["patches"] == ost["patches"]
+    if views == 2:
+        assert res["patches"] == 0
+    else:
+        assert res["patches"] > 100
+    ref = tmp_path / "oracle.ply"
+    write_ply(str(ref), op)
+    assert out.read_bytes() == ref.read_bytes()

@@ -342,3 +342,48 @@ def test_filter_bit_exact(orc, passes):
     assert np.array_equal(got, want)
     if passes & 1:
         assert got[:40].sum() < 40
+
+
+@pytest.mark.parametrize("cell", [16, 11, 7])
+def test_eval_batch_scores_equal_oracle(engine, orc, cell):
+    """dp_eval_batch (scores only, include/densepoints.h) against the oracle's
+    per-patch objective evaluation at the stored pose: mean NCCScore over the
+    visible views against texture 0 (error_measurements.cpp:36-60,
+    optimization.cpp:14-56), -1 where no view scores; the records are not
+    mutated."""
+    sc = scene("hf6")
+    engine.set_views(sc.views)
+    S = orc.Scene(sc.P, sc.imgs)
+    gp = engine.seeds_to_patches(sc.seeds[:240])
+    gp["vis"][:3] = 0  # no visible view: score -1
+    before = gp.tobytes()
+    got = engine.evaluate(gp, cell)
+    assert gp.tobytes() == before
+    op = gp.copy()
+    S.refine(op, cell, orc.MODE_EVAL)
+    assert np.array_equal(got.view(np.uint32), op["score"].view(np.uint32))
+    assert (got[:3] == -1.0).all() and (got[3:] > -1.0).any()
+
+
+@pytest.mark.parametrize("n_parents", [37, 96])
+def test_dequeue_order_does_not_change_output(orc, monkeypatch, n_parents):
+    """Longest-first dequeue (the default) and index order (a context created
+    with DP_NO_LPT=1) give byte-identical children and accept flags, for a
+    parent count that is not a multiple of the 4-group block."""
+    sc = scene("hf6")
+    S = orc.Scene(sc.P, sc.imgs)
+    parents = S.seeds_to_patches(sc.seeds[:n_parents])
+    S.refine(parents, 16, orc.MODE_SEED)
+    with dp.Engine(device=0) as eng:
+        eng.set_views(sc.views)
+        k1, a1 = eng.expand(parents)
+        r1 = parents.copy()
+        f1 = eng.refine(r1, 11, N.MODE_EXPAND)
+    monkeypatch.setenv("DP_NO_LPT", "1")
+    with dp.Engine(device=0) as eng:
+        eng.set_views(sc.views)
+        k2, a2 = eng.expand(parents)
+        r2 = parents.copy()
+        f2 = eng.refine(r2, 11, N.MODE_EXPAND)
+    assert k1.tobytes() == k2.tobytes() and np.array_equal(a1, a2)
+    assert r1.tobytes() == r2.tobytes() and np.array_equal(f1, f2)
