@@ -109,7 +109,7 @@ def _seed_and_expand(orc, name, n_seeds, n_parents, pyramid_views=()):
         assert_same(gp, op)
         # the bench step on this scene: ExpandPatch of refined parents at n = 11
         parents = gp[ga == 1]
-        assert len(parents) >= n_parents // 4, len(parents)
+        assert len(parents) > 100, len(parents)
         parents = np.ascontiguousarray(np.resize(parents, n_parents))
         gk, gacc = eng.expand(parents)
         ok, oacc = S.expand(parents)
