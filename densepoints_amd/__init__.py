@@ -8,6 +8,8 @@ library has not been built: there is no CPU fallback.
 from ._native import (  # noqa: F401
     MODE_EVAL,
     MODE_EXPAND,
+    MODE_FAST_EVAL,
+    MODE_FAST_REFINE,
     MODE_FILTER,
     MODE_NM,
     MODE_SEED,
@@ -20,6 +22,7 @@ from ._native import (  # noqa: F401
 from .pmvs import (  # noqa: F401
     PMVS,
     Engine,
+    FastOptions,
     Options,
     View,
     empty_patches,

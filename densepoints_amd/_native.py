@@ -41,6 +41,7 @@ DP_E_STATE = -5
 DP_E_NODEVICE = -6
 
 MODE_EVAL, MODE_FILTER, MODE_NM, MODE_SEED, MODE_EXPAND = range(5)
+MODE_FAST_EVAL, MODE_FAST_REFINE = 5, 6  # performance mode (dp_fast_options)
 PATCH_ACCEPTED = 1
 PATCH_DEGENERATE = 2
 
@@ -159,6 +160,20 @@ class DpSeedStats(ctypes.Structure):
     ]
 
 
+class DpFastOptions(ctypes.Structure):
+    """dp_fast_options: the performance mode's knobs (include/densepoints.h)."""
+    _fields_ = [
+        ("iters", ctypes.c_int32),
+        ("margin", ctypes.c_int32),
+        ("tile_budget", ctypes.c_int32),
+        ("max_views", ctypes.c_int32),
+        ("fd_step", ctypes.c_float),
+        ("ls_step", ctypes.c_float),
+        ("densify", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
 # dp_keypoint: the cv::KeyPoint fields the matcher reads
 KEYPOINT_DTYPE = np.dtype(
     [("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("angle", "<f4"), ("octave", "<i4"), ("reserved", "<i4")]
@@ -213,12 +228,20 @@ SIGNATURES = [
     ("dp_synth_render_host", _I, [_P, _P, _I, _P]),
     ("dp_synth_render_device", _I, [_P, _P, _P, _I, _P, _P]),
     ("dp_synth_seeds", ctypes.c_int64, [_P, _P, _P, ctypes.c_int64]),
+    ("dp_synth_surface", _I, [_P, ctypes.c_int64, _P, _P, _P]),
+    ("dp_default_fast_options", None, [_P]),
+    ("dp_set_fast_options", _I, [_P, _P]),
+    ("dp_build_gray", _I, [_P]),
+    ("dp_read_gray", _I, [_P, _I, _P]),
+    ("dp_fast_expand_batch", _I, [_P, _P, _I, _P, _P]),
+    ("dp_fast_expand_batch_device", _I, [_P, _P, _I, _P, _P, _P]),
     ("dp_probe_sincos", None, [_D, _P, _P]),
     ("dp_probe_acos", _D, [_D]),
     ("dp_probe_texture", _I, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, _I, _P]),
     ("dp_probe_ncc", _D, [ctypes.c_int32] * 6 + [_D]),
     ("dp_probe_math_device", _I, [_P, _I, _P]),
     ("dp_probe_texel_device", _I, [_P, _P, _P, _I, _P]),
+    ("dp_probe_recip_f32_device", _I, [_P, _I, _P]),
     ("dp_debug_stamps", _I, [_P]),
 ]
 

@@ -238,6 +238,10 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->acc.release();
     c->prefix.release();
     c->scan_tmp.release();
+    if (c->gray_pool)
+        hipFree(c->gray_pool);
+    if (c->d_gray)
+        hipFree(c->d_gray);
     if (c->d_work)
         hipFree(c->d_work);
     if (c->d_evals)
@@ -306,6 +310,7 @@ static int upload_view_table(dp_ctx *c)
 
 static void record_level0(dp_ctx *c, const double *P)
 {
+    c->gray_ready = false; // performance-mode gray planes follow the views
     c->P0.assign(P, P + 12 * (size_t)c->V);
     c->planes.assign(1, std::vector<dpk::PyrPlane>(c->V));
     for (int v = 0; v < c->V; ++v)
@@ -389,6 +394,7 @@ extern "C" int dp_build_pyramid(dp_ctx *c, int levels)
         return fail(c, DP_E_ARG, "dp_build_pyramid: levels must be in [1, DP_MAX_LEVELS]");
     if (c->V <= 0 || c->planes.empty())
         return fail(c, DP_E_STATE, "dp_build_pyramid: no views set");
+    c->gray_ready = false;
     hipSetDevice(c->device);
     DP_HIP(c, hipStreamSynchronize(c->stream));
     if (c->level != 0) {
@@ -471,6 +477,7 @@ extern "C" int dp_set_level(dp_ctx *c, int level)
     c->d_views = nullptr;
     c->hv = std::move(hv);
     c->level = level;
+    c->gray_ready = false;
     return upload_view_table(c);
 }
 
@@ -695,7 +702,7 @@ static int check_refine(dp_ctx *c, int n, int cell, int mode)
         return DP_E_ARG;
     if (!c->V)
         return fail(c, DP_E_STATE, "no views set");
-    if (n < 0 || cell < 2 || cell > DP_MAX_CELL || mode < DP_MODE_EVAL || mode > DP_MODE_EXPAND)
+    if (n < 0 || cell < 2 || cell > DP_MAX_CELL || mode < DP_MODE_EVAL || mode > DP_MODE_FAST_REFINE)
         return fail(c, DP_E_ARG, "refine: bad n/cell/mode");
     return DP_OK;
 }
@@ -710,6 +717,8 @@ extern "C" int dp_refine_batch_device(dp_ctx *c, dp_patch *d_inout, int n, int c
         return DP_OK;
     hipSetDevice(c->device);
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (mode >= DP_MODE_FAST_EVAL)
+        return dp_fast_launch(c, d_inout, n, cell, mode, d_accept, nullptr, s);
     dpk::RefineArgs a = refine_args(c, d_inout, n, cell, mode, d_accept);
     return launch_timed(c, a, s);
 }
@@ -733,8 +742,12 @@ extern "C" int dp_refine_batch(dp_ctx *c, dp_patch *inout, int n, int cell, int 
     DP_HIP(c, c->pat.reserve(n));
     DP_HIP(c, c->ok.reserve(n));
     DP_HIP(c, hipMemcpyAsync(c->pat.p, inout, sizeof(dp_patch) * n, hipMemcpyHostToDevice, c->stream));
-    dpk::RefineArgs a = refine_args(c, c->pat.p, n, cell, mode, c->ok.p);
-    rc = launch_timed(c, a, c->stream);
+    if (mode >= DP_MODE_FAST_EVAL) {
+        rc = dp_fast_launch(c, c->pat.p, n, cell, mode, c->ok.p, nullptr, c->stream);
+    } else {
+        dpk::RefineArgs a = refine_args(c, c->pat.p, n, cell, mode, c->ok.p);
+        rc = launch_timed(c, a, c->stream);
+    }
     if (rc != DP_OK)
         return rc;
     DP_HIP(c, hipMemcpyAsync(inout, c->pat.p, sizeof(dp_patch) * n, hipMemcpyDeviceToHost, c->stream));
@@ -1322,6 +1335,33 @@ extern "C" int64_t dp_synth_seeds(const dp_synth_config *cfg, const double *P, d
             }
     }
     return cnt;
+}
+
+extern "C" int dp_synth_surface(const dp_synth_config *cfg, int64_t n, const double *xy, double *z_out,
+                                double *normal_out)
+{
+    if (!cfg || n < 0 || (n > 0 && (!xy || !z_out)))
+        return DP_E_ARG;
+    for (int64_t q = 0; q < n; ++q) {
+        const double x = xy[2 * q], y = xy[2 * q + 1];
+        double z = 0.0, nx = 0.0, ny = 0.0, nz = 1.0;
+        if (cfg->kind != 0) {
+            double h, a, b, cx, cy;
+            dps::facet(cfg->seed, dps::facet_index(x), dps::facet_index(y), h, a, b, cx, cy);
+            z = (h + a * (x - cx)) + b * (y - cy);
+            const double l = std::sqrt((a * a + b * b) + 1.0);
+            nx = -a / l;
+            ny = -b / l;
+            nz = 1.0 / l;
+        }
+        z_out[q] = z;
+        if (normal_out) {
+            normal_out[3 * q] = nx;
+            normal_out[3 * q + 1] = ny;
+            normal_out[3 * q + 2] = nz;
+        }
+    }
+    return DP_OK;
 }
 
 // ---------------------------------------------------------------------------

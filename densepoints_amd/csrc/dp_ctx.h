@@ -108,7 +108,19 @@ struct dp_ctx {
     std::chrono::steady_clock::time_point g_t0;
     // seed generation (Features::Matcher, dp_seeds.hip)
     dp_seedgen *seeds = nullptr;
+    // performance mode (dp_fast.hip): options and the fp16 gray planes of one level
+    dp_fast_options fopt{4, 3, 16384, 32, 0.5f, 1.0f, 0, 0};
+    void *gray_pool = nullptr; // __half planes, pitch = width rounded up to 64
+    size_t gray_cap = 0;       // elements
+    void *d_gray = nullptr;    // device GrayPlane table
+    bool gray_ready = false;
+    int gray_level = -1, gray_V = 0;
 };
+
+// performance-mode launch (dp_fast.hip): refine/eval of n patches in device
+// memory, or the 4n expansion children of d_parents
+int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
+                   hipStream_t s);
 
 static inline int fail(dp_ctx *c, int code, const std::string &msg)
 {

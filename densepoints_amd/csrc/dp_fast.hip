@@ -1,0 +1,1149 @@
+// dp_fast.hip -- the performance mode of the patch refine (gfx950).
+//
+// North star: "each wavefront owns one candidate patch, bilinearly samples its
+// n x n window from LDS-staged image-pyramid tiles across the visible views,
+// reduces the NCC photometric score with wavefront shuffles, and refines
+// depth/normal via fused conjugate-gradient steps in the same kernel ...
+// image pyramids laid out as coalesced SoA in HBM".  Spec: include/densepoints.h
+// (dp_fast_options) and oracle/or_fast.c, which this file implements
+// independently, bit for bit.
+//
+//   gray_kernel   BGRA8 plane -> fp16 gray plane (BGR2GRAY, 14-bit fixed point),
+//                 every view of the current level in one launch (SoA planes)
+//   fast_kernel   one WAVEFRONT per patch, persistent waves on a work counter:
+//                 stage the patch's per-view gray tiles into LDS once, run the
+//                 whole conjugate-gradient refine against them (every
+//                 evaluation samples LDS only), InitRelatedImages, re-stage at
+//                 the new pose and filter.
+//
+// Replaces methods/pmvs/optimization_opencv.cpp:44-78 (DownhillSolver refine);
+// keeps the functor calc objective (optimization_opencv.cpp:14-39) and the
+// NCCScore formula (modules/core/error_measurements.cpp:36-60).
+#include "dp_ctx.h"
+
+#include <hip/hip_fp16.h>
+
+namespace dpk {
+namespace {
+
+constexpr int kFastMaxV = 32;     // staged views per patch (per-view tables)
+constexpr int kFastMaxBbox = 48;  // window bounding-box side cap (grazing views)
+constexpr int kFastMaxMargin = 7; // keeps a tile row <= 64 entries (one lane each)
+constexpr int kFastSlots = 4;     // samples per lane per view pass
+
+struct GrayPlane {
+    const __half *p;
+    int32_t w, h, pitch, pad;
+};
+
+struct FastArgs {
+    const dpg::ViewDev *views;
+    const GrayPlane *gray;
+    int32_t V, cell, mode, n;
+    dp_options opt;
+    dp_fast_options fo;
+    dp_patch *patches;
+    uint8_t *accept;
+    uint32_t *work;
+    unsigned long long *evals;
+    const dp_patch *parents; // expansion: child c = parents[c / 4], direction c % 4
+};
+
+// per staged view, written once per staging (rank order)
+struct StageRec {
+    float v[15];      // H0, Hd, He1, He2, Hn (folded, scaled, fp32)
+    float umax, vmax; // 32 (tw - 1), 32 (th - 1)
+    uint32_t info;    // tile byte offset | (tw + 1) << 16
+    int32_t view, x0t, y0t, tw, th;
+    int32_t pad;
+};
+
+// per evaluation, per staged view: A.xyz umax | B1.xyz vmax | B2.xyz info
+struct EvalRec {
+    float4 q[3];
+};
+
+// patch frame (uniform, fp64): or_fast.c fast_stage
+struct Frame {
+    double X0[3], r[3];
+    double e1[3], e2[3], nn[3]; // times the pixel size
+    double u1[3], u2[3], un[3]; // unit
+    double sd, st;
+    bool degenerate;
+};
+
+// conjugate-gradient state between evaluations (uniform, kept in LDS so the
+// sampling passes have the registers)
+struct CgState {
+    double x[3], x1[3], g[3], gp[3], d[3], dp[3], u[3];
+    double f, f1, gg, ggp, alpha;
+};
+
+template <int kBudget> struct FastLds {
+    uint32_t tiles[kBudget / 4];
+    union {
+        StageRec st[kFastMaxV]; // during staging
+        struct {
+            EvalRec par[kFastMaxV];
+            uint32_t mom[kFastMaxV][4];
+            double score[kFastMaxV];
+        } ev;
+    } u;
+    uint64_t vis[2], cand[2];
+    Frame F;
+    CgState cg;
+    dp_patch p;
+    uint8_t vlist[64];
+};
+
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lane_id()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ double uni_f64(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffff));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// exact integer wave sum (xor butterfly through the LDS crossbar; staging only)
+__device__ __forceinline__ int wave_sum_i32(int v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// inclusive prefix sum over the wave in lane order
+__device__ __forceinline__ int wave_incl_i32(int v)
+{
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o)
+            v += t;
+    }
+    return v;
+}
+
+// sum over each group of LP = 64/G lanes (DPP); the total of group j lands in
+// lane LP (j + 1) - 1
+template <int G> __device__ __forceinline__ uint32_t group_total(uint32_t v)
+{
+    constexpr int LP = 64 / G;
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false); // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false); // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xe, false); // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xc, false); // row_shr:8
+    if (LP >= 32)
+        v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    if (LP == 64)
+        v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return v;
+}
+
+// RN(1 / b) for b >= 2^-20: v_rcp_f32 seed and one Newton step (checked
+// bitwise against IEEE division on the GPU, tests/test_gpu_fast.py)
+__device__ __forceinline__ float recip_rn(float b)
+{
+    const float r = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, r, 1.0f);
+    return __builtin_fmaf(r, e, r);
+}
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
+{
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// all lanes compute the same values; F is the wave's LDS copy
+__device__ __forceinline__ void make_frame(const dpg::ViewDev &rv, const float *pos, const float *nrm, int cell,
+                                           Frame &F)
+{
+    const double X0[3] = {(double)pos[0], (double)pos[1], (double)pos[2]};
+    const double n0[3] = {(double)nrm[0], (double)nrm[1], (double)nrm[2]};
+    double cu, cw, qu, qw;
+    dpg::project(rv.P, X0[0], X0[1], X0[2], cu, cw);
+    dpg::project(rv.P, X0[0] + rv.xr[0], X0[1] + rv.xr[1], X0[2] + rv.xr[2], qu, qw);
+    const double du = qu - cu, dv = qw - cw;
+    const double dx = sqrt(du * du + dv * dv);
+    const double nl = sqrt(dpg::dot3(n0, n0));
+    F.degenerate = !(dx > 0.0) || !(nl > 0.0) || dx != dx;
+    if (F.degenerate)
+        return;
+    const double ps = 1.0 / dx;
+    const double nn[3] = {n0[0] / nl, n0[1] / nl, n0[2] / nl};
+    const double xn = dpg::dot3(rv.xr, nn);
+    double e1[3] = {rv.xr[0] - xn * nn[0], rv.xr[1] - xn * nn[1], rv.xr[2] - xn * nn[2]};
+    const double el = sqrt(dpg::dot3(e1, e1));
+    if (!(el > 0.0)) {
+        F.degenerate = true;
+        return;
+    }
+    for (int k = 0; k < 3; ++k)
+        e1[k] = e1[k] / el;
+    double e2[3];
+    dpg::cross3(nn, e1, e2);
+    const double r[3] = {X0[0] - rv.C[0], X0[1] - rv.C[1], X0[2] - rv.C[2]};
+    const double rl = sqrt(dpg::dot3(r, r));
+    F.sd = ps / rl;
+    F.st = 2.0 / (double)(cell - 1);
+    for (int k = 0; k < 3; ++k) {
+        F.X0[k] = X0[k];
+        F.r[k] = r[k];
+        F.u1[k] = e1[k];
+        F.u2[k] = e2[k];
+        F.un[k] = nn[k];
+        F.e1[k] = e1[k] * ps;
+        F.e2[k] = e2[k] * ps;
+        F.nn[k] = nn[k] * ps;
+    }
+}
+
+__device__ __forceinline__ double rowdot(const double *P, const double *w)
+{
+    return (P[0] * w[0] + P[1] * w[1]) + P[2] * w[2];
+}
+
+// the lane's view geometry before the budget (or_fast.c view_geo)
+struct Geo {
+    double g[5][3];
+    int xa, xb, ya, yb;
+    bool ok;
+};
+
+__device__ Geo view_geo(const dpg::ViewDev &v, const Frame &F, int cell)
+{
+    Geo G;
+    G.ok = false;
+    const double *w[5] = {F.X0, F.r, F.e1, F.e2, F.nn};
+    double H[5][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double *Pr = v.P + 4 * k;
+        H[0][k] = rowdot(Pr, w[0]) + Pr[3];
+#pragma unroll
+        for (int i = 1; i < 5; ++i)
+            H[i][k] = rowdot(Pr, w[i]);
+    }
+    const double s = H[0][2];
+    if (!(s > 0.0))
+        return G;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        G.g[i][0] = (32.0 * H[i][0]) / s;
+        G.g[i][1] = (32.0 * H[i][1]) / s;
+        G.g[i][2] = H[i][2] / s;
+    }
+    const double c = 0.5 * (double)(cell - 1);
+    double umin = 0, umax = 0, vmin = 0, vmax = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double ti = (q & 1) ? c : -c, tj = (q & 2) ? c : -c;
+        double h[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            h[k] = (G.g[0][k] + ti * G.g[2][k]) + tj * G.g[3][k];
+        if (!(h[2] > 0.0))
+            return G;
+        const double u = h[0] / h[2], ww = h[1] / h[2];
+        if (!(u > 0.0 && u < 32.0 * v.W && ww > 0.0 && ww < 32.0 * v.H))
+            return G;
+        if (q == 0 || u < umin)
+            umin = u;
+        if (q == 0 || u > umax)
+            umax = u;
+        if (q == 0 || ww < vmin)
+            vmin = ww;
+        if (q == 0 || ww > vmax)
+            vmax = ww;
+    }
+    G.xa = (int)floor(umin / 32.0);
+    G.xb = (int)floor(umax / 32.0) + 1;
+    G.ya = (int)floor(vmin / 32.0);
+    G.yb = (int)floor(vmax / 32.0) + 1;
+    G.ok = G.xb - G.xa + 1 <= kFastMaxBbox && G.yb - G.ya + 1 <= kFastMaxBbox;
+    return G;
+}
+
+struct Rect {
+    int x0, y0, tw, th, bytes;
+};
+
+__device__ __forceinline__ Rect tile_rect(const Geo &g, int W, int H, int M)
+{
+    Rect t;
+    int x0 = g.xa - M, x1 = g.xb + M, y0 = g.ya - M, y1 = g.yb + M;
+    x0 = x0 < 0 ? 0 : x0;
+    y0 = y0 < 0 ? 0 : y0;
+    x1 = x1 > W - 1 ? W - 1 : x1;
+    y1 = y1 > H - 1 ? H - 1 : y1;
+    t.x0 = x0;
+    t.y0 = y0;
+    t.tw = x1 - x0 + 1;
+    t.th = y1 - y0 + 1;
+    t.bytes = (2 * (t.tw + 1) * t.th + 3) & ~3;
+    return t;
+}
+
+// per-lane staged view (lanes 0 .. m-1 hold ranks 0 .. m-1)
+struct Staged {
+    float v[15];
+    float umax, vmax;
+    uint32_t info;
+    int view;
+};
+
+// Stage the wave's patch: frame, usable views, margin, tiles into LDS.
+// Returns m (uniform); the lane of rank r holds that view's vectors in S.
+template <int kBudget>
+__device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged &S)
+{
+    const int lane = lane_id();
+    const int cell = a.cell;
+    const uint64_t v0 = L.vis[0], v1 = L.vis[1];
+    const int nvis = __popcll(v0) + __popcll(v1);
+    // visible list (ascending), first 64
+    {
+        const uint64_t below = (1ull << lane) - 1ull;
+        const int c0 = __popcll(v0);
+        if ((v0 >> lane) & 1ull)
+            L.vlist[__popcll(v0 & below)] = (uint8_t)lane;
+        if (((v1 >> lane) & 1ull) && c0 + __popcll(v1 & below) < 64)
+            L.vlist[c0 + __popcll(v1 & below)] = (uint8_t)(64 + lane);
+    }
+    wave_sync();
+    const int nconsider = nvis < 64 ? nvis : 64;
+    const int maxv = a.fo.max_views < kFastMaxV ? a.fo.max_views : kFastMaxV;
+    const int view = lane < nconsider ? (int)L.vlist[lane] : 0;
+    const dpg::ViewDev &vw = a.views[view];
+    Geo g;
+    g.ok = false;
+    if (lane < nconsider)
+        g = view_geo(vw, L.F, cell);
+    const uint64_t usable = __ballot(g.ok);
+    const int rank = __popcll(usable & ((1ull << lane) - 1ull));
+    const bool staged = g.ok && rank < maxv;
+    int M = margin;
+    Rect t;
+    for (;;) {
+        t = tile_rect(g, vw.W, vw.H, M);
+        const int tot = uni(wave_sum_i32(staged ? t.bytes : 0));
+        if (tot <= a.fo.tile_budget || M == 0)
+            break;
+        --M;
+    }
+    const int incl = wave_incl_i32(staged ? t.bytes : 0);
+    const bool keep = staged && incl <= a.fo.tile_budget;
+    const int m = __popcll(__ballot(keep));
+    if (keep) {
+        StageRec &R = L.u.st[rank];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const double ga = g.g[i][0] - (32.0 * (double)t.x0) * g.g[i][2];
+            const double gb = g.g[i][1] - (32.0 * (double)t.y0) * g.g[i][2];
+            R.v[3 * i] = (float)ga;
+            R.v[3 * i + 1] = (float)gb;
+            R.v[3 * i + 2] = (float)g.g[i][2];
+        }
+        R.umax = (float)(32 * (t.tw - 1));
+        R.vmax = (float)(32 * (t.th - 1));
+        R.info = (uint32_t)(incl - t.bytes) | ((uint32_t)(t.tw + 1) << 16);
+        R.view = view;
+        R.x0t = t.x0;
+        R.y0t = t.y0;
+        R.tw = t.tw;
+        R.th = t.th;
+    }
+    wave_sync();
+    if (lane < m) {
+        const StageRec &R = L.u.st[lane];
+#pragma unroll
+        for (int i = 0; i < 15; ++i)
+            S.v[i] = R.v[i];
+        S.umax = R.umax;
+        S.vmax = R.vmax;
+        S.info = R.info;
+        S.view = R.view;
+    }
+    // tiles: entry (x, y) = g(x0t + x, y0t + y) | g(x0t + x, y0t + y + 1) << 8,
+    // x in [0, tw], y in [0, th); R = 64 / (tw + 1) rows per wave step
+    for (int r = 0; r < m; ++r) {
+        const int vv = uni(L.u.st[r].view), x0t = uni(L.u.st[r].x0t), y0t = uni(L.u.st[r].y0t);
+        const int tw = uni(L.u.st[r].tw), th = uni(L.u.st[r].th);
+        const uint32_t off = (uint32_t)uni((int)(L.u.st[r].info & 0xffffu));
+        const GrayPlane gp = a.gray[vv];
+        const int cols = tw + 1;
+        const int R = 64 / cols;
+        const int rr = (int)(((float)lane + 0.5f) * (1.0f / (float)cols));
+        const int x = lane - rr * cols;
+        const int X = x0t + x < gp.w - 1 ? x0t + x : gp.w - 1;
+        if (rr < R) {
+            for (int y = rr; y < th; y += R) {
+                const int Y0 = y0t + y < gp.h - 1 ? y0t + y : gp.h - 1;
+                const int Y1 = y0t + y + 1 < gp.h - 1 ? y0t + y + 1 : gp.h - 1;
+                const int p0 = (int)__half2float(gp.p[(size_t)Y0 * gp.pitch + X]);
+                const int p1 = (int)__half2float(gp.p[(size_t)Y1 * gp.pitch + X]);
+                uint16_t *dst = (uint16_t *)((char *)L.tiles + off) + (y * cols + x);
+                *dst = (uint16_t)(p0 | (p1 << 8));
+            }
+        }
+    }
+    wave_sync();
+    return m;
+}
+
+// per-lane sample slots of a view pass (fixed per launch)
+struct Slots {
+    float ti[kFastSlots], tj[kFastSlots];
+    uint32_t live[kFastSlots];
+};
+
+template <int G> __device__ Slots make_slots(int cell)
+{
+    constexpr int LP = 64 / G;
+    const int g = lane_id() & (LP - 1);
+    const int N = cell * cell;
+    const float c = 0.5f * (float)(cell - 1);
+    Slots s;
+#pragma unroll
+    for (int k = 0; k < kFastSlots; ++k) {
+        const int t = g + LP * k;
+        const bool live = t < N;
+        const int te = live ? t : N - 1;
+        const int jj = te / cell, ii = te - jj * cell;
+        s.ti[k] = (float)ii - c;
+        s.tj[k] = (float)jj - c;
+        s.live[k] = live ? 0xffffffffu : 0u;
+    }
+    return s;
+}
+
+// one view's sample in 1/16 gray levels (or_fast.c fast_sample)
+__device__ __forceinline__ uint32_t sample(const char *tiles, const float4 &qa,
+                                           const float4 &qb, const float4 &qc, float ti, float tj)
+{
+    const float hx = __builtin_fmaf(tj, qc.x, __builtin_fmaf(ti, qb.x, qa.x));
+    const float hy = __builtin_fmaf(tj, qc.y, __builtin_fmaf(ti, qb.y, qa.y));
+    float hz = __builtin_fmaf(tj, qc.z, __builtin_fmaf(ti, qb.z, qa.z));
+    hz = __builtin_fmaxf(hz, 0x1p-20f);
+    const float rz = recip_rn(hz);
+    const float U = __builtin_amdgcn_fmed3f(hx * rz, 0.0f, qa.w);
+    const float V = __builtin_amdgcn_fmed3f(hy * rz, 0.0f, qb.w);
+    const uint32_t iu = __float_as_uint(U + 8388608.0f) - 0x4B000000u;
+    const uint32_t iv = __float_as_uint(V + 8388608.0f) - 0x4B000000u;
+    const uint32_t info = __float_as_uint(qc.w);
+    const uint32_t cols = info >> 16;
+    const uint32_t x0 = iu >> 5, fx = iu & 31u, y0 = iv >> 5, fy = iv & 31u;
+    const uint32_t addr = (info & 0xffffu) + ((__umul24(y0, cols) + x0) << 1);
+    const uint16_t *tp = (const uint16_t *)(tiles + addr);
+    const uint32_t e0 = tp[0], e1 = tp[1];
+    const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
+    const uint32_t w0 = __umul24(wx, 32u - fy), w1 = __umul24(wx, fy);
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const uint32_t r0 = perm(e1, e0, 0x0c040c00u); // p00 | p01 << 16
+    const uint32_t r1 = perm(e1, e0, 0x0c050c01u); // p10 | p11 << 16
+    const uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r0), __builtin_bit_cast(us2, w0),
+                                              __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r1),
+                                                                     __builtin_bit_cast(us2, w1), 32u, false),
+                                              false);
+    return b >> 6;
+}
+
+// One objective evaluation at scaled pose x (or_fast.c fast_objective).
+// Leaves NCC of rank r (r >= 1) in L.u.ev.score[r]; returns F (uniform).
+template <int G, int kBudget>
+__device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m, double x0,
+                           double x1, double x2)
+{
+    constexpr int LP = 64 / G;
+    const int lane = lane_id();
+    if (m < 2)
+        return 2.0;
+    const float df = (float)(x0 * L.F.sd), af = (float)(x1 * L.F.st), bf = (float)(x2 * L.F.st);
+    if (lane < m) {
+        EvalRec &E = L.u.ev.par[lane];
+        E.q[0] = make_float4(__builtin_fmaf(df, S.v[3], S.v[0]), __builtin_fmaf(df, S.v[4], S.v[1]),
+                             __builtin_fmaf(df, S.v[5], S.v[2]), S.umax);
+        E.q[1] = make_float4(__builtin_fmaf(-af, S.v[12], S.v[6]), __builtin_fmaf(-af, S.v[13], S.v[7]),
+                             __builtin_fmaf(-af, S.v[14], S.v[8]), S.vmax);
+        E.q[2] = make_float4(__builtin_fmaf(-bf, S.v[12], S.v[9]), __builtin_fmaf(-bf, S.v[13], S.v[10]),
+                             __builtin_fmaf(-bf, S.v[14], S.v[11]), __uint_as_float(S.info));
+    }
+    wave_sync();
+    const int j = lane / LP, g = lane & (LP - 1);
+    const char *tiles = (const char *)L.tiles;
+    uint32_t av[kFastSlots];
+    const int passes = (m + G - 1) / G;
+    for (int p = 0; p < passes; ++p) {
+        const int r = p * G + j;
+        const bool act = r < m;
+        const EvalRec &E = L.u.ev.par[act ? r : 0];
+        const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
+        uint32_t b[kFastSlots];
+#pragma unroll
+        for (int k = 0; k < kFastSlots; ++k)
+            b[k] = sample(tiles, qa, qb, qc, sl.ti[k], sl.tj[k]) & sl.live[k];
+        if (p == 0) {
+            // texture 0 = rank 0 = group 0 of the first pass: its samples reach
+            // every group through the LDS crossbar and stay in registers
+#pragma unroll
+            for (int k = 0; k < kFastSlots; ++k)
+                av[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(g << 2, (int)b[k]);
+        }
+        uint32_t s = 0, ss = 0, sx = 0;
+#pragma unroll
+        for (int k = 0; k < kFastSlots; ++k) {
+            s += b[k];
+            ss += __umul24(b[k], b[k]);
+            sx += __umul24(av[k], b[k]);
+        }
+        s = group_total<G>(s);
+        ss = group_total<G>(ss);
+        sx = group_total<G>(sx);
+        if (g == LP - 1 && act) {
+            L.u.ev.mom[r][0] = s;
+            L.u.ev.mom[r][1] = ss;
+            L.u.ev.mom[r][2] = sx;
+        }
+    }
+    wave_sync();
+    const int N = a.cell * a.cell;
+    if (lane >= 1 && lane < m) {
+        const int64_t Sa = L.u.ev.mom[0][0], Saa = L.u.ev.mom[0][1];
+        const int64_t Sb = L.u.ev.mom[lane][0], Sbb = L.u.ev.mom[lane][1], Sab = L.u.ev.mom[lane][2];
+        const int64_t num = (int64_t)N * Sab - Sa * Sb;
+        const int64_t va = (int64_t)N * Saa - Sa * Sa;
+        const int64_t vb = (int64_t)N * Sbb - Sb * Sb;
+        const double dmin = ((a.opt.ncc_denom_min * 256.0) * (double)N) * (double)N;
+        const double den = sqrt((double)va * (double)vb);
+        const double d = den > dmin ? den : dmin;
+        L.u.ev.score[lane] = (double)num / d;
+    }
+    wave_sync();
+    double sum = 0.0;
+    for (int k = 1; k < m; ++k)
+        sum = sum + (1.0 - L.u.ev.score[k]);
+    return uni_f64(sum / (double)(m - 1));
+}
+
+// Nonlinear CG (or_fast.c fast_cg) as a state machine around ONE evaluation
+// call site (the sampling passes are inlined once); its state lives in LDS.
+// Returns evaluations; L.cg.x = the scaled pose.
+template <int G, int kBudget>
+__device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m)
+{
+    enum { kStart = 0, kFd0 = 1, kFd2 = 3, kProbe1 = 4, kProbe2 = 5 };
+    CgState &C = L.cg;
+    const double h = (double)a.fo.fd_step;
+    for (int k = 0; k < 3; ++k) {
+        C.x[k] = 0.0;
+        C.gp[k] = 0.0;
+        C.dp[k] = 0.0;
+    }
+    C.alpha = (double)a.fo.ls_step;
+    C.ggp = 0.0;
+    int E = 0, it = 0, phase = kStart;
+    for (;;) {
+        double xt0 = C.x[0], xt1 = C.x[1], xt2 = C.x[2];
+        if (phase >= kFd0 && phase <= kFd2) {
+            const int i = phase - kFd0;
+            xt0 = i == 0 ? C.x[0] + h : xt0;
+            xt1 = i == 1 ? C.x[1] + h : xt1;
+            xt2 = i == 2 ? C.x[2] + h : xt2;
+        } else if (phase >= kProbe1) {
+            const double st = phase == kProbe1 ? C.alpha : (C.f1 < C.f ? 2.0 * C.alpha : 0.5 * C.alpha);
+            xt0 = C.x[0] + st * C.u[0];
+            xt1 = C.x[1] + st * C.u[1];
+            xt2 = C.x[2] + st * C.u[2];
+        }
+        const double ft = evaluate<G>(a, L, S, sl, m, xt0, xt1, xt2);
+        if (phase == kStart) {
+            C.f = ft;
+            E = 1;
+            if (a.fo.iters <= 0)
+                break;
+            phase = kFd0;
+        } else if (phase >= kFd0 && phase <= kFd2) {
+            C.g[phase - kFd0] = (ft - C.f) / h;
+            if (phase < kFd2) {
+                ++phase;
+                continue;
+            }
+            E += 3;
+            const double g0 = C.g[0], g1 = C.g[1], g2 = C.g[2];
+            const double gg = (g0 * g0 + g1 * g1) + g2 * g2;
+            C.gg = gg;
+            if (gg == 0.0)
+                break;
+            double beta = 0.0;
+            if (it > 0 && C.ggp > 0.0) {
+                beta = ((g0 * (g0 - C.gp[0]) + g1 * (g1 - C.gp[1])) + g2 * (g2 - C.gp[2])) / C.ggp;
+                beta = beta > 0.0 ? beta : 0.0;
+            }
+            double d0 = beta * C.dp[0] - g0, d1 = beta * C.dp[1] - g1, d2 = beta * C.dp[2] - g2;
+            if ((d0 * g0 + d1 * g1) + d2 * g2 >= 0.0) {
+                d0 = 0.0 - g0;
+                d1 = 0.0 - g1;
+                d2 = 0.0 - g2;
+            }
+            const double nd = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+            C.d[0] = d0;
+            C.d[1] = d1;
+            C.d[2] = d2;
+            C.u[0] = d0 / nd;
+            C.u[1] = d1 / nd;
+            C.u[2] = d2 / nd;
+            phase = kProbe1;
+        } else if (phase == kProbe1) {
+            C.f1 = ft;
+            C.x1[0] = xt0;
+            C.x1[1] = xt1;
+            C.x1[2] = xt2;
+            phase = kProbe2;
+        } else {
+            const double f2 = ft;
+            if (C.f1 < C.f) {
+                if (f2 < C.f1) {
+                    C.x[0] = xt0;
+                    C.x[1] = xt1;
+                    C.x[2] = xt2;
+                    C.f = f2;
+                    C.alpha = 2.0 * C.alpha;
+                } else {
+                    for (int k = 0; k < 3; ++k)
+                        C.x[k] = C.x1[k];
+                    C.f = C.f1;
+                }
+            } else {
+                if (f2 < C.f) {
+                    C.x[0] = xt0;
+                    C.x[1] = xt1;
+                    C.x[2] = xt2;
+                    C.f = f2;
+                }
+                C.alpha = 0.5 * C.alpha;
+            }
+            E += 2;
+            for (int k = 0; k < 3; ++k) {
+                C.gp[k] = C.g[k];
+                C.dp[k] = C.d[k];
+            }
+            C.ggp = C.gg;
+            if (++it >= a.fo.iters)
+                break;
+            phase = kFd0;
+        }
+        wave_sync();
+    }
+    wave_sync();
+    return E;
+}
+
+// Patch::InitRelatedImages (patch.cpp:19-49), one lane per view
+template <int kBudget> __device__ void init_related(const FastArgs &a, FastLds<kBudget> &L, const dp_patch &p)
+{
+    const int lane = lane_id();
+    const int ref = (int)p.ref;
+    const double X[3] = {p.pos[0], p.pos[1], p.pos[2]};
+    const double n[3] = {p.normal[0], p.normal[1], p.normal[2]};
+    int c0 = 0, c1 = 0;
+    if (lane < a.V && lane != ref)
+        c0 = dpg::classify_view(a.views[lane], X, n, a.opt.visible_angle, a.opt.candidate_angle);
+    if (64 + lane < a.V && 64 + lane != ref)
+        c1 = dpg::classify_view(a.views[64 + lane], X, n, a.opt.visible_angle, a.opt.candidate_angle);
+    const uint64_t v0 = __ballot(c0 == 1), v1 = __ballot(c1 == 1);
+    const uint64_t k0 = __ballot(c0 == 2), k1 = __ballot(c1 == 2);
+    wave_sync();
+    L.vis[0] = v0;
+    L.vis[1] = v1;
+    L.cand[0] = k0;
+    L.cand[1] = k1;
+    wave_sync();
+}
+
+// Expand::ExpandPatch child centre (expand.cpp:107-125)
+__device__ void child_position(const FastArgs &a, const dp_patch &par, int dir, float *out)
+{
+    const dpg::ViewDev &rv = a.views[par.ref];
+    const double X[3] = {par.pos[0], par.pos[1], par.pos[2]};
+    const double nrm[3] = {par.normal[0], par.normal[1], par.normal[2]};
+    double yax[3];
+    dpg::cross3(nrm, rv.xr, yax);
+    double cu, cv, qu, qv;
+    dpg::project(rv.P, X[0], X[1], X[2], cu, cv);
+    dpg::project(rv.P, X[0] + rv.xr[0], X[1] + rv.xr[1], X[2] + rv.xr[2], qu, qv);
+    const double du = qu - cu, dv = qv - cv;
+    const double dx = sqrt(du * du + dv * dv);
+    const double scale = (double)a.opt.grid_scale / dx;
+    for (int i = 0; i < 3; ++i) {
+        const double d = dir == 0 ? rv.xr[i] : dir == 1 ? -rv.xr[i] : dir == 2 ? yax[i] : -yax[i];
+        out[i] = (float)(X[i] + scale * d);
+    }
+}
+
+template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void fast_kernel(FastArgs a)
+{
+    __shared__ FastLds<kBudget> L;
+    const int lane = lane_id();
+    const Slots sl = make_slots<G>(a.cell);
+    unsigned long long wave_evals = 0;
+    dp_patch &p = L.p;
+    for (;;) {
+        uint32_t idx = 0;
+        if (lane == 0)
+            idx = atomicAdd(a.work, 1u);
+        idx = (uint32_t)uni((int)idx);
+        if (idx >= (uint32_t)a.n)
+            break;
+        bool live = true;
+        if (a.parents) {
+            const dp_patch &par = a.parents[idx >> 2];
+            p = par;
+            p.evals = 0;
+            p.flags = 0;
+            p.parent = idx >> 2;
+            const int pm = __popcll(par.vis[0]) + __popcll(par.vis[1]);
+            live = pm >= a.opt.min_expand_visible && par.ref < (uint32_t)a.V;
+            if (live) {
+                float cp[3];
+                child_position(a, par, (int)(idx & 3u), cp);
+                p.pos[0] = cp[0];
+                p.pos[1] = cp[1];
+                p.pos[2] = cp[2];
+            }
+        } else {
+            p = a.patches[idx];
+        }
+        wave_sync();
+        {
+            const uint64_t m0 = a.V >= 64 ? ~0ull : ((1ull << a.V) - 1ull);
+            const uint64_t m1 = a.V >= 128 ? ~0ull : (a.V <= 64 ? 0ull : ((1ull << (a.V - 64)) - 1ull));
+            if (p.ref >= (uint32_t)a.V || (p.vis[0] & ~m0) || (p.vis[1] & ~m1))
+                live = false;
+        }
+        bool ok = false;
+        if (live) {
+            L.vis[0] = p.vis[0];
+            L.vis[1] = p.vis[1];
+            const int ref = uni((int)p.ref);
+            const dpg::ViewDev &rv = a.views[ref];
+            make_frame(rv, p.pos, p.normal, a.cell, L.F);
+            wave_sync();
+            if (kMode == DP_MODE_FAST_EVAL) {
+                Staged S;
+                const bool degen = L.F.degenerate;
+                const int m = degen ? 0 : stage(a, L, 0, S);
+                p.evals += 1;
+                if (degen)
+                    p.flags |= DP_PATCH_DEGENERATE;
+                ok = m >= 2;
+                if (ok) {
+                    evaluate<G>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                    double sum = 0.0;
+                    for (int k = 1; k < m; ++k)
+                        sum = sum + L.u.ev.score[k];
+                    p.score = (float)(sum / (double)(m - 1));
+                } else {
+                    p.score = -1.0f;
+                }
+            } else {
+                bool rejected = false;
+                if (L.F.degenerate) {
+                    p.flags |= DP_PATCH_DEGENERATE;
+                    p.score = -1.0f;
+                    rejected = true;
+                } else {
+                    Staged S;
+                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S);
+                    if (m >= 2) {
+                        p.evals += (uint32_t)cg_refine<G>(a, L, S, sl, m);
+                        const Frame &F = L.F;
+                        const double d = L.cg.x[0] * F.sd, aa = L.cg.x[1] * F.st, bb = L.cg.x[2] * F.st;
+                        double nrm[3];
+                        for (int k = 0; k < 3; ++k)
+                            nrm[k] = (F.un[k] + aa * F.u1[k]) + bb * F.u2[k];
+                        const double ml = sqrt(dpg::dot3(nrm, nrm));
+                        float np[3], nn[3];
+                        for (int k = 0; k < 3; ++k) {
+                            np[k] = (float)(F.X0[k] + d * F.r[k]);
+                            nn[k] = (float)(nrm[k] / ml);
+                        }
+                        wave_sync();
+                        for (int k = 0; k < 3; ++k) {
+                            p.pos[k] = np[k];
+                            p.normal[k] = nn[k];
+                        }
+                    }
+                }
+                wave_sync();
+                if (!rejected) {
+                    init_related(a, L, p);
+                    p.vis[0] = L.vis[0];
+                    p.vis[1] = L.vis[1];
+                    p.cand[0] = L.cand[0];
+                    p.cand[1] = L.cand[1];
+                    // fast filter: re-staged at the new pose, margin 0
+                    make_frame(rv, p.pos, p.normal, a.cell, L.F);
+                    wave_sync();
+                    Staged S;
+                    const bool degen = L.F.degenerate;
+                    const int m = degen ? 0 : stage(a, L, 0, S);
+                    p.evals += 1;
+                    if (degen)
+                        p.flags |= DP_PATCH_DEGENERATE;
+                    if (m < 2) {
+                        p.score = -1.0f;
+                        const int v = uni(S.view);
+                        p.vis[0] = (m == 1 && v < 64) ? (1ull << v) : 0ull;
+                        p.vis[1] = (m == 1 && v >= 64) ? (1ull << (v - 64)) : 0ull;
+                        ok = m >= a.opt.min_visible;
+                    } else {
+                        evaluate<G>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                        double sum = 0.0;
+                        for (int k = 1; k < m; ++k)
+                            sum = sum + L.u.ev.score[k];
+                        p.score = (float)(sum / (double)(m - 1));
+                        const bool kept = lane < m && (lane == 0 || !(L.u.ev.score[lane] < a.opt.ncc_threshold));
+                        const uint64_t k0 = __ballot(kept && S.view < 64);
+                        const uint64_t k1 = __ballot(kept && S.view >= 64);
+                        uint64_t n0 = 0, n1 = 0;
+                        for (uint64_t q = k0 | k1; q; q &= q - 1) {
+                            const int l = __builtin_ctzll(q);
+                            const int v = __builtin_amdgcn_readlane(S.view, l);
+                            if (v < 64)
+                                n0 |= 1ull << v;
+                            else
+                                n1 |= 1ull << (v - 64);
+                        }
+                        p.vis[0] = n0;
+                        p.vis[1] = n1;
+                        ok = __popcll(k0 | k1) >= a.opt.min_visible;
+                    }
+                }
+            }
+            if (ok)
+                p.flags |= DP_PATCH_ACCEPTED;
+            else
+                p.flags &= (uint8_t)~DP_PATCH_ACCEPTED;
+        }
+        wave_sync();
+        wave_evals += p.evals;
+        if (lane == 0) {
+            if (a.parents || kMode != DP_MODE_FAST_EVAL) {
+                a.patches[idx] = p;
+            } else {
+                // FAST_EVAL: score, evals and flags only (no pose / mask change)
+                a.patches[idx].score = p.score;
+                a.patches[idx].evals = p.evals;
+                a.patches[idx].flags = p.flags;
+            }
+            if (a.accept)
+                a.accept[idx] = ok ? 1 : 0;
+        }
+        wave_sync();
+    }
+    if (lane == 0 && a.evals)
+        atomicAdd(a.evals, wave_evals);
+}
+
+// BGRA8 -> fp16 gray (BGR2GRAY 14-bit fixed point, exact integers in fp16)
+__global__ __launch_bounds__(256) void gray_kernel(const PyrPlane *src, const GrayPlane *dst)
+{
+    const PyrPlane s = src[blockIdx.z];
+    const GrayPlane d = dst[blockIdx.z];
+    const int y = blockIdx.y;
+    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (y >= s.h || x0 >= s.w)
+        return;
+    const uint32_t *row = s.img + (size_t)y * s.pitch;
+    __half *out = (__half *)d.p + (size_t)y * d.pitch;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (x0 + k < s.w) {
+            const uint32_t px = row[x0 + k];
+            const uint32_t g = (1868u * (px & 255u) + 9617u * ((px >> 8) & 255u) + 4899u * ((px >> 16) & 255u) + 8192u) >> 14;
+            out[x0 + k] = __float2half((float)g);
+        }
+    }
+}
+
+__global__ void recip_probe_kernel(const float *x, int n, float *out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        out[i] = recip_rn(x[i]);
+}
+
+} // namespace
+
+hipError_t launch_recip_probe(const float *x, int n, float *out)
+{
+    hipLaunchKernelGGL(recip_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, x, n, out);
+    return hipGetLastError();
+}
+
+template <int G, int kBudget> static hipError_t launch_fast_t(const FastArgs &a, hipStream_t s)
+{
+    int dev = 0, cus = 256;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int per_cu = (160 * 1024) / (int)sizeof(FastLds<kBudget>);
+    const int64_t want = a.n;
+    const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
+    const int grid = (int)(want < cap ? want : cap);
+    if (a.mode == DP_MODE_FAST_EVAL)
+        hipLaunchKernelGGL((fast_kernel<G, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((fast_kernel<G, kBudget, DP_MODE_FAST_REFINE>), dim3(grid), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+} // namespace dpk
+
+// ---------------------------------------------------------------------------
+// host side: gray planes, options, launches (C ABI)
+// ---------------------------------------------------------------------------
+
+namespace {
+
+constexpr int kFastBudget = 16384; // the kernel's tile arena (dp_fast_options.tile_budget max)
+
+int fast_check_options(dp_ctx *c, const dp_fast_options &f)
+{
+    if (f.iters < 0 || f.iters > 64 || f.margin < 0 || f.margin > dpk::kFastMaxMargin || f.tile_budget < 64 ||
+        f.tile_budget > kFastBudget || f.max_views < 2 || f.max_views > dpk::kFastMaxV || !(f.fd_step > 0.0f) ||
+        !(f.ls_step > 0.0f) || (f.densify != 0 && f.densify != 1))
+        return fail(c, DP_E_ARG, "dp_fast_options out of range (margin <= 7, tile_budget <= 16384, 2 <= max_views <= 32)");
+    return DP_OK;
+}
+
+int ensure_gray(dp_ctx *c)
+{
+    if (!c->V)
+        return fail(c, DP_E_STATE, "no views set");
+    if (c->gray_ready && c->gray_level == c->level && c->gray_V == c->V)
+        return DP_OK;
+    hipSetDevice(c->device);
+    std::vector<dpk::GrayPlane> gp(c->V);
+    size_t total = 0;
+    std::vector<size_t> off(c->V);
+    for (int v = 0; v < c->V; ++v) {
+        const int pitch = (c->hv[v].W + 63) & ~63;
+        off[v] = total;
+        total += (size_t)pitch * (size_t)c->hv[v].H;
+        gp[v].w = c->hv[v].W;
+        gp[v].h = c->hv[v].H;
+        gp[v].pitch = pitch;
+        gp[v].pad = 0;
+    }
+    if (total > c->gray_cap) {
+        if (c->gray_pool)
+            hipFree(c->gray_pool);
+        c->gray_pool = nullptr;
+        c->gray_cap = 0;
+        DP_HIP(c, hipMalloc(&c->gray_pool, total * sizeof(__half)));
+        c->gray_cap = total;
+    }
+    for (int v = 0; v < c->V; ++v)
+        gp[v].p = (const __half *)c->gray_pool + off[v];
+    std::vector<dpk::PyrPlane> src(c->V);
+    int mw = 0, mh = 0;
+    for (int v = 0; v < c->V; ++v) {
+        src[v] = dpk::PyrPlane{(uint32_t *)c->hv[v].img, c->hv[v].W, c->hv[v].H, c->hv[v].pitch, 0};
+        mw = c->hv[v].W > mw ? c->hv[v].W : mw;
+        mh = c->hv[v].H > mh ? c->hv[v].H : mh;
+    }
+    if (c->d_gray)
+        hipFree(c->d_gray);
+    c->d_gray = nullptr;
+    dpk::PyrPlane *d_src = nullptr;
+    DP_HIP(c, hipMalloc(&c->d_gray, sizeof(dpk::GrayPlane) * c->V));
+    DP_HIP(c, hipMalloc(&d_src, sizeof(dpk::PyrPlane) * c->V));
+    DP_HIP(c, hipMemcpy(c->d_gray, gp.data(), sizeof(dpk::GrayPlane) * c->V, hipMemcpyHostToDevice));
+    DP_HIP(c, hipMemcpy(d_src, src.data(), sizeof(dpk::PyrPlane) * c->V, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(dpk::gray_kernel, dim3((mw + 1023) / 1024, mh, c->V), dim3(256), 0, c->stream, d_src,
+                       (const dpk::GrayPlane *)c->d_gray);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(c->stream);
+    hipFree(d_src);
+    DP_HIP(c, e);
+    c->gray_ready = true;
+    c->gray_level = c->level;
+    c->gray_V = c->V;
+    return DP_OK;
+}
+
+} // namespace
+
+int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
+                   hipStream_t s)
+{
+    int rc = ensure_gray(c);
+    if (rc != DP_OK)
+        return rc;
+    dpk::FastArgs a{};
+    a.views = c->d_views;
+    a.gray = (const dpk::GrayPlane *)c->d_gray;
+    a.V = c->V;
+    a.cell = cell;
+    a.mode = mode;
+    a.n = n;
+    a.opt = c->opt;
+    a.fo = c->fopt;
+    a.patches = d;
+    a.accept = acc;
+    a.work = c->d_work;
+    a.evals = c->d_evals;
+    a.parents = d_parents;
+    DP_HIP(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), s));
+    DP_HIP(c, hipEventRecord(c->e0, s));
+    const int N = cell * cell;
+    hipError_t e;
+    if (N <= 64)
+        e = dpk::launch_fast_t<4, kFastBudget>(a, s);
+    else if (N <= 128)
+        e = dpk::launch_fast_t<2, kFastBudget>(a, s);
+    else
+        e = dpk::launch_fast_t<1, kFastBudget>(a, s);
+    DP_HIP(c, e);
+    DP_HIP(c, hipEventRecord(c->e1, s));
+    c->timed = true;
+    return DP_OK;
+}
+
+extern "C" void dp_default_fast_options(dp_fast_options *f)
+{
+    if (!f)
+        return;
+    *f = dp_fast_options{};
+    f->iters = 4;
+    f->margin = 3;
+    f->tile_budget = kFastBudget;
+    f->max_views = dpk::kFastMaxV;
+    f->fd_step = 0.5f;
+    f->ls_step = 1.0f;
+    f->densify = 0;
+}
+
+extern "C" int dp_set_fast_options(dp_ctx *c, const dp_fast_options *f)
+{
+    if (!c || !f)
+        return DP_E_ARG;
+    int rc = fast_check_options(c, *f);
+    if (rc != DP_OK)
+        return rc;
+    c->fopt = *f;
+    return DP_OK;
+}
+
+extern "C" int dp_build_gray(dp_ctx *c)
+{
+    if (!c)
+        return DP_E_ARG;
+    c->gray_ready = false;
+    return ensure_gray(c);
+}
+
+extern "C" int dp_read_gray(dp_ctx *c, int view, uint16_t *out)
+{
+    if (!c || !out)
+        return DP_E_ARG;
+    if (view < 0 || view >= c->V)
+        return fail(c, DP_E_ARG, "dp_read_gray: bad view");
+    int rc = ensure_gray(c);
+    if (rc != DP_OK)
+        return rc;
+    const int W = c->hv[view].W, H = c->hv[view].H, pitch = (W + 63) & ~63;
+    size_t off = 0;
+    for (int v = 0; v < view; ++v)
+        off += (size_t)((c->hv[v].W + 63) & ~63) * (size_t)c->hv[v].H;
+    DP_HIP(c, hipMemcpy2D(out, (size_t)W * 2, (const __half *)c->gray_pool + off, (size_t)pitch * 2, (size_t)W * 2,
+                          (size_t)H, hipMemcpyDeviceToHost));
+    return DP_OK;
+}
+
+extern "C" int dp_fast_expand_batch_device(dp_ctx *c, const dp_patch *d_parents, int n, dp_patch *d_children,
+                                           uint8_t *d_accept, void *stream)
+{
+    if (!c)
+        return DP_E_ARG;
+    if (!c->V)
+        return fail(c, DP_E_STATE, "no views set");
+    const int cell = c->opt.expand_cell_size;
+    if (n < 0 || cell < 2 || cell > DP_MAX_CELL)
+        return fail(c, DP_E_ARG, "fast expand: bad n/cell");
+    if (n == 0)
+        return DP_OK;
+    if ((int64_t)n * 4 > INT32_MAX || !d_parents || !d_children)
+        return fail(c, DP_E_ARG, "fast expand: bad arguments");
+    hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return dp_fast_launch(c, d_children, 4 * n, cell, DP_MODE_FAST_REFINE, d_accept, d_parents, s);
+}
+
+extern "C" int dp_fast_expand_batch(dp_ctx *c, const dp_patch *parents, int n, dp_patch *children,
+                                    uint8_t *accept_out)
+{
+    if (!c)
+        return DP_E_ARG;
+    if (n < 0)
+        return fail(c, DP_E_ARG, "fast expand: bad n");
+    if (n == 0)
+        return DP_OK;
+    if (!parents || !children)
+        return fail(c, DP_E_ARG, "fast expand: null arrays");
+    hipSetDevice(c->device);
+    DP_HIP(c, c->cand.reserve((size_t)n));
+    DP_HIP(c, c->pat.reserve((size_t)4 * n));
+    DP_HIP(c, c->ok.reserve((size_t)4 * n));
+    DP_HIP(c, hipMemcpyAsync(c->cand.p, parents, sizeof(dp_patch) * n, hipMemcpyHostToDevice, c->stream));
+    int rc = dp_fast_expand_batch_device(c, c->cand.p, n, c->pat.p, c->ok.p, c->stream);
+    if (rc != DP_OK)
+        return rc;
+    DP_HIP(c, hipMemcpyAsync(children, c->pat.p, sizeof(dp_patch) * 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (accept_out)
+        DP_HIP(c, hipMemcpyAsync(accept_out, c->ok.p, (size_t)4 * n, hipMemcpyDeviceToHost, c->stream));
+    DP_HIP(c, hipStreamSynchronize(c->stream));
+    return DP_OK;
+}
+
+extern "C" int dp_probe_recip_f32_device(const float *x, int n, float *out)
+{
+    if (n < 0 || (n > 0 && (!x || !out)))
+        return DP_E_ARG;
+    if (n == 0)
+        return DP_OK;
+    float *dx = nullptr, *dy = nullptr;
+    if (hipMalloc(&dx, sizeof(float) * n) != hipSuccess)
+        return DP_E_OOM;
+    if (hipMalloc(&dy, sizeof(float) * n) != hipSuccess) {
+        hipFree(dx);
+        return DP_E_OOM;
+    }
+    hipError_t e = hipMemcpy(dx, x, sizeof(float) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = dpk::launch_recip_probe(dx, n, dy);
+    if (e == hipSuccess)
+        e = hipMemcpy(out, dy, sizeof(float) * n, hipMemcpyDeviceToHost);
+    hipFree(dx);
+    hipFree(dy);
+    return e == hipSuccess ? DP_OK : DP_E_HIP;
+}

@@ -27,6 +27,7 @@ from ._native import PATCH_DTYPE, check, lib, ptr
 
 __all__ = [
     "Options",
+    "FastOptions",
     "View",
     "Engine",
     "PMVS",
@@ -37,6 +38,28 @@ __all__ = [
     "visible_list",
     "mask_from_list",
 ]
+
+
+@dataclass
+class FastOptions:
+    """Performance-mode knobs (dp_fast_options; no reference counterpart: the
+    mode replaces OptimizationOpenCV::Optimize, optimization_opencv.cpp:44-78,
+    with a conjugate-gradient refine on LDS-staged gray tiles)."""
+
+    iters: int = 4            # CG iterations: E = 1 + 5 iters (+1 filter evaluation)
+    margin: int = 3           # tile margin around the initial window, pixels (<= 7)
+    tile_budget: int = 16384  # bytes of LDS tiles per patch (<= 16384)
+    max_views: int = 32       # staged views per patch (<= 32)
+    fd_step: float = 0.5      # forward-difference step, scaled units
+    ls_step: float = 1.0      # initial line-search step, scaled units
+    densify: int = 0          # 1: dp_densify expands with the fast refine
+
+    def to_c(self) -> N.DpFastOptions:
+        o = N.DpFastOptions()
+        for name, _ in N.DpFastOptions._fields_:
+            if name != "reserved":
+                setattr(o, name, getattr(self, name))
+        return o
 
 
 @dataclass
@@ -272,6 +295,42 @@ class Engine:
         ms = ctypes.c_double()
         self._check(lib.dp_last_kernel_ms(self._ctx, ctypes.byref(ms)))
         return ms.value
+
+    # ---- performance mode (include/densepoints.h dp_fast_options) ----
+    def set_fast_options(self, fo: FastOptions):
+        c = fo.to_c()
+        self._check(lib.dp_set_fast_options(self._ctx, ctypes.byref(c)))
+
+    def build_gray(self):
+        """fp16 gray planes of the current level (built on demand otherwise)."""
+        self._check(lib.dp_build_gray(self._ctx))
+
+    def read_gray(self, view: int) -> np.ndarray:
+        vw = self.views[view] if self.views else None
+        w, h, _ = self.level_info(0, view) if vw is None else (vw.width, vw.height, 0)
+        out = np.zeros((h, w), dtype=np.float16)
+        self._check(lib.dp_read_gray(self._ctx, view, ptr(out)))
+        return out
+
+    def fast_refine(self, patches: np.ndarray, cell: int, mode: int = N.MODE_FAST_REFINE) -> np.ndarray:
+        """Performance-mode refine (or one fast evaluation) in place; accept flags."""
+        return self.refine(patches, cell, mode)
+
+    def fast_expand(self, parents: np.ndarray):
+        """Expand::ExpandPatch children refined in performance mode."""
+        parents = np.ascontiguousarray(parents)
+        assert parents.dtype == PATCH_DTYPE
+        kids = empty_patches(4 * len(parents))
+        acc = np.zeros(4 * len(parents), dtype=np.uint8)
+        self._check(lib.dp_fast_expand_batch(self._ctx, ptr(parents), len(parents), ptr(kids), ptr(acc)))
+        return kids, acc
+
+    def fast_expand_device(self, d_parents: int, n: int, d_children: int, d_accept: int | None,
+                           stream: int | None = None):
+        self._check(lib.dp_fast_expand_batch_device(self._ctx, ctypes.c_void_p(d_parents), n,
+                                                    ctypes.c_void_p(d_children),
+                                                    ctypes.c_void_p(d_accept) if d_accept else None,
+                                                    ctypes.c_void_p(stream) if stream else None))
 
     def evaluate(self, patches: np.ndarray, cell: int) -> np.ndarray:
         out = np.zeros(len(patches), dtype=np.float32)

@@ -79,3 +79,13 @@ def scene_host(cfg: N.DpSynthConfig):
     P = cameras(cfg)
     imgs = [render_host(cfg, P, v) for v in range(cfg.n_views)]
     return P, imgs, seeds(cfg, P)
+
+
+def surface(cfg: N.DpSynthConfig, xy: np.ndarray):
+    """Ground truth of the synthetic surface at points xy (n x 2): height z and
+    unit normal (dp_synth_surface) -- for scoring refine quality."""
+    xy = np.ascontiguousarray(np.asarray(xy, dtype=np.float64).reshape(-1, 2))
+    z = np.zeros(len(xy))
+    nrm = np.zeros((len(xy), 3))
+    N.check(lib.dp_synth_surface(ctypes.byref(cfg), len(xy), ptr(xy), ptr(z), ptr(nrm)))
+    return z, nrm

@@ -88,6 +88,9 @@ typedef struct dp_patch {
 #define DP_MODE_NM 2      /* OptimizationOpenCV::Optimize (opencv.cpp:44-78)     */
 #define DP_MODE_SEED 3    /* Seed::FilterPatches then OptimizePatches            */
 #define DP_MODE_EXPAND 4  /* Optimize -> InitRelatedImages -> Filter (expand.cpp:127-135) */
+/* performance mode (no reference counterpart; spec below, dp_fast_options) */
+#define DP_MODE_FAST_EVAL 5    /* one fast evaluation at the stored pose: score only */
+#define DP_MODE_FAST_REFINE 6  /* fast CG refine -> InitRelatedImages -> fast filter */
 
 /* ---- images: BGR8 as cv::imread returns it (types.cpp:9) ----------------- */
 typedef struct dp_image {
@@ -345,6 +348,62 @@ int dp_fundamental_matrix(const double P1[12], const double P2[12], double F[9])
 int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const double *P, const double *obs,
                    double *X);
 
+/* ---- performance mode (north star: "LDS-staged image-pyramid tiles", "fused
+ * conjugate-gradient steps", "fp16 pyramids") ---------------------------------
+ * A second refine of the patch loop for throughput; parity mode (DP_MODE_EVAL
+ * .. DP_MODE_EXPAND) stays the reference restatement.  It replaces
+ * OptimizationOpenCV::Optimize (optimization_opencv.cpp:44-78, DownhillSolver
+ * over depth/roll/pitch) and keeps the objective of the functor calc
+ * (optimization_opencv.cpp:14-39: mean of 1 - NCC against texture 0, the
+ * lowest-index scored view) and NCCScore's formula (error_measurements.cpp:
+ * 36-60, 0.1 denominator floor).  The full arithmetic is oracle/or_fast.c;
+ * in short, per patch:
+ *  - gray planes: BGR2GRAY of the current level (the 14-bit fixed point of the
+ *    parity path) stored as fp16, one plane per view (dp_build_gray);
+ *  - frame: e1 = the reference camera's x-axis projected onto the patch plane,
+ *    e2 = n x e1, sample spacing one reference pixel (1/dx); pose (d, a, b):
+ *    X = X0 + d (X0 - C_ref), plane normal n + a e1 + b e2, in scaled units
+ *    d = x0 / (dx |X0 - C_ref|), a = x1 * 2/(n-1), b = x2 * 2/(n-1);
+ *  - staging: per visible view (ascending, at most max_views) whose initial
+ *    window corners project inside the image, a tile = the window's pixel
+ *    bounding box + `margin` px (reduced until all tiles fit tile_budget bytes,
+ *    then the longest fitting prefix of views), held in LDS for the whole
+ *    refine; samples clamp to the tile (BORDER_REPLICATE);
+ *  - sample: projective map in fp32 (fmaf), 1/32 px, bilinear on 8-bit gray,
+ *    result in 1/16 gray levels; exact integer moments; fp64 NCC finish;
+ *  - refine: `iters` Polak-Ribiere+ conjugate-gradient steps with a forward-
+ *    difference gradient (step fd_step) and a two-probe line search (initial
+ *    step ls_step, doubled on success, halved on failure): E = 1 + 5 iters;
+ *  - then Patch::InitRelatedImages (patch.cpp:19-49) at the new pose and the
+ *    fast filter: re-staged at the new pose (margin 0), one evaluation, views
+ *    with NCC < ncc_threshold or that cannot be staged are dropped (no
+ *    off-by-one), accepted iff >= min_visible views remain; score = mean NCC.
+ * dp_refine_batch[_device] run DP_MODE_FAST_* with `cell` in [2, 16]. */
+typedef struct dp_fast_options {
+    int32_t iters;        /* 4     CG iterations                                    */
+    int32_t margin;       /* 3     tile margin around the initial window, px       */
+    int32_t tile_budget;  /* 16384 bytes of LDS tiles per patch (kernel arena)     */
+    int32_t max_views;    /* 32    staged views per patch (<= 32)                   */
+    float fd_step;        /* 0.5   forward-difference step, scaled units            */
+    float ls_step;        /* 1.0   initial line-search step, scaled units           */
+    int32_t densify;      /* 0     1: dp_densify expands with the fast refine       */
+    int32_t reserved;
+} dp_fast_options;
+
+void dp_default_fast_options(dp_fast_options *fo);
+int dp_set_fast_options(dp_ctx *ctx, const dp_fast_options *fo);
+/* fp16 gray planes of the current level for every view (built on demand by
+ * the first fast call; explicit here so callers can time it). */
+int dp_build_gray(dp_ctx *ctx);
+/* host copy (width*height fp16 bits) of view `view`'s gray plane */
+int dp_read_gray(dp_ctx *ctx, int view, uint16_t *fp16_out);
+/* Expand::ExpandPatch children (as dp_expand_batch) refined in performance
+ * mode: DP_MODE_FAST_REFINE on the parent's visible set, cell =
+ * expand_cell_size. */
+int dp_fast_expand_batch(dp_ctx *ctx, const dp_patch *parents, int n, dp_patch *children, uint8_t *accept_out);
+int dp_fast_expand_batch_device(dp_ctx *ctx, const dp_patch *d_parents, int n, dp_patch *d_children,
+                                uint8_t *d_accept, void *stream);
+
 /* Elapsed device milliseconds of the most recent refine kernel launch, timed
  * with HIP events on the stream the kernel ran on. */
 int dp_last_kernel_ms(dp_ctx *ctx, double *ms);
@@ -371,6 +430,10 @@ int dp_synth_render_device(dp_ctx *ctx, const dp_synth_config *cfg, const double
 /* Seed points on the true surface with depth noise; returns count written
  * (at most cap); xyz_out may be NULL to query the count. */
 int64_t dp_synth_seeds(const dp_synth_config *cfg, const double *P, double *xyz_out, int64_t cap);
+/* Ground truth of the synthetic surface: height z(x, y) and the unit normal
+ * (facing +z) at n points xy (n x 2); normal_out may be NULL.  Used to score
+ * refine quality (tests, bench), never by the patch loop. */
+int dp_synth_surface(const dp_synth_config *cfg, int64_t n, const double *xy, double *z_out, double *normal_out);
 
 #ifdef __cplusplus
 }

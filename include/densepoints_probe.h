@@ -29,6 +29,9 @@ int dp_probe_math_device(const double *x, int n, double *out);
  * taps_a/taps_b = BGRA8 pixel pairs (x0, x0+1) of rows y0 / y1, fxy = fx | fy << 5 */
 int dp_probe_texel_device(const uint64_t *taps_a, const uint64_t *taps_b, const uint32_t *fxy, int n,
                           int32_t *gray);
+/* device run of the performance mode's fp32 reciprocal (v_rcp_f32 + one
+ * Newton step) on n inputs >= 2^-20; the kernel's spec is IEEE 1.0f / x */
+int dp_probe_recip_f32_device(const float *x, int n, float *out);
 /* diagnostic builds (-DDP_STAMPS) only: per-phase s_memtime cycle sums of the
  * refine kernel since the last call (0 maps, 1 texture 0, 2 other views,
  * 3 NCC finish, 6 patches, 7 whole patch); DP_E_STATE otherwise */

@@ -17,6 +17,7 @@
  */
 #include "oracle.h"
 #include "or_detmath.h"
+#include "or_internal.h"
 
 #include <math.h>
 #include <stdint.h>
@@ -52,44 +53,8 @@ void or_default_options(or_options *o)
 }
 
 /* ------------------------------------------------------------------------ */
-/* small vector algebra (fixed evaluation order)                             */
-/* ------------------------------------------------------------------------ */
-
-static inline double dot3(const double a[3], const double b[3])
-{
-    return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
-}
-static inline double norm3(const double a[3]) { return sqrt(dot3(a, a)); }
-static inline void cross3(const double a[3], const double b[3], double o[3])
-{
-    o[0] = a[1] * b[2] - a[2] * b[1];
-    o[1] = a[2] * b[0] - a[0] * b[2];
-    o[2] = a[0] * b[1] - a[1] * b[0];
-}
-static inline double det3c(const double a[3], const double b[3], const double c[3])
-{
-    /* determinant of the matrix with columns a, b, c */
-    return (a[0] * (b[1] * c[2] - b[2] * c[1]) - b[0] * (a[1] * c[2] - a[2] * c[1])) +
-           c[0] * (a[1] * b[2] - a[2] * b[1]);
-}
-
-/* ------------------------------------------------------------------------ */
 /* View (modules/core/types.cpp)                                             */
 /* ------------------------------------------------------------------------ */
-
-typedef struct or_view {
-    double P[12];
-    double C[3];
-    double xr[3]; /* GetXAxis().normalized(), patch.cpp:95 */
-    int W, H;
-    const uint8_t *bgr; /* H x W x 3, BGR8 as cv::imread */
-} or_view;
-
-struct or_scene {
-    int V;
-    or_options opt;
-    or_view v[OR_MAX_VIEWS];
-};
 
 /*
  * View::SetProjectionMatrix, types.cpp:28-68.  C = null(P) (JacobiSVD in the
@@ -147,29 +112,6 @@ int or_view_geometry(const double P[12], double C[3], double K[9], double E[12],
         }
     }
     return 0;
-}
-
-/* View::ProjectPoint, types.cpp:70-75 */
-static inline void proj(const or_view *v, const double X[3], double *u, double *w)
-{
-    const double *P = v->P;
-    double h0 = ((P[0] * X[0] + P[1] * X[1]) + P[2] * X[2]) + P[3];
-    double h1 = ((P[4] * X[0] + P[5] * X[1]) + P[6] * X[2]) + P[7];
-    double h2 = ((P[8] * X[0] + P[9] * X[1]) + P[10] * X[2]) + P[11];
-    *u = h0 / h2;
-    *w = h1 / h2;
-}
-
-/* View::IsPointInside, types.cpp:77-84: open interval on the loaded image */
-static inline int inside_uv(const or_view *v, double u, double w)
-{
-    return u > 0.0 && u < (double)v->W && w > 0.0 && w < (double)v->H;
-}
-static inline int inside(const or_view *v, const double X[3])
-{
-    double u, w;
-    proj(v, X, &u, &w);
-    return inside_uv(v, u, w);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -363,30 +305,6 @@ int or_texture(const or_scene *s, int view, const double corners[12], int cell, 
 /* ------------------------------------------------------------------------ */
 /* patch helpers                                                             */
 /* ------------------------------------------------------------------------ */
-
-static int decode_mask(const uint64_t m[2], int *list)
-{
-    int n = 0;
-    for (int w = 0; w < 2; ++w)
-        for (int b = 0; b < 64; ++b)
-            if ((m[w] >> b) & 1u)
-                list[n++] = w * 64 + b;
-    return n;
-}
-static void encode_mask(const int *list, int n, uint64_t m[2])
-{
-    m[0] = m[1] = 0;
-    for (int i = 0; i < n; ++i)
-        m[list[i] >> 6] |= 1ull << (list[i] & 63);
-}
-static inline void get_pos(const or_patch *p, double X[3])
-{
-    X[0] = p->pos[0]; X[1] = p->pos[1]; X[2] = p->pos[2];
-}
-static inline void get_nrm(const or_patch *p, double n[3])
-{
-    n[0] = p->normal[0]; n[1] = p->normal[1]; n[2] = p->normal[2];
-}
 
 /* Patch::InitRelatedImages, patch.cpp:19-49 */
 int or_init_related(const or_scene *s, or_patch *p)
@@ -829,8 +747,9 @@ static int try_insert(const or_scene *s, grid_t *g, const or_patch *p)
     return claims > 1;
 }
 
-/* Expand::ExpandPatch, expand.cpp:103-143 */
-int or_expand_children(const or_scene *s, const or_patch *parent, or_patch out[4], uint8_t acc[4])
+/* Expand::ExpandPatch child centres, expand.cpp:107-125: X + (grid_scale/dx) *
+ * (+x, -x, +y, -y), y = n x xaxis (not normalised) */
+void or_child_positions(const or_scene *s, const or_patch *parent, double pos[4][3])
 {
     const or_view *rv = &s->v[parent->ref];
     double X[3], n[3];
@@ -845,18 +764,24 @@ int or_expand_children(const or_scene *s, const or_patch *parent, or_patch out[4
     double du = pu - cu, dw = pw - cw;
     double dx = sqrt(du * du + dw * dw);
     double scale = (double)s->opt.grid_scale / dx;
-    double dirs[4][3];
     for (int i = 0; i < 3; ++i) {
-        dirs[0][i] = rv->xr[i];
-        dirs[1][i] = -rv->xr[i];
-        dirs[2][i] = y[i];
-        dirs[3][i] = -y[i];
+        pos[0][i] = X[i] + scale * rv->xr[i];
+        pos[1][i] = X[i] + scale * -rv->xr[i];
+        pos[2][i] = X[i] + scale * y[i];
+        pos[3][i] = X[i] + scale * -y[i];
     }
+}
+
+/* Expand::ExpandPatch, expand.cpp:103-143 */
+int or_expand_children(const or_scene *s, const or_patch *parent, or_patch out[4], uint8_t acc[4])
+{
+    double pos[4][3];
+    or_child_positions(s, parent, pos);
     int na = 0;
     for (int d = 0; d < 4; ++d) {
         or_patch c = *parent;
         for (int i = 0; i < 3; ++i)
-            c.pos[i] = (float)(X[i] + scale * dirs[d][i]);
+            c.pos[i] = (float)pos[d][i];
         c.evals = 0;
         c.flags = 0;
         int ok = refine_one(s, &c, s->opt.expand_cell_size, OR_MODE_EXPAND);

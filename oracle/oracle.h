@@ -66,6 +66,20 @@ typedef struct or_scene or_scene;
 #define OR_MODE_NM 2          /* OptimizationOpenCV::Optimize                        */
 #define OR_MODE_SEED 3        /* Seed::FilterPatches then OptimizePatches (seed.cpp) */
 #define OR_MODE_EXPAND 4      /* Optimize -> InitRelatedImages -> Filter (expand.cpp)*/
+#define OR_MODE_FAST_EVAL 5   /* performance mode: one evaluation (or_fast.c)        */
+#define OR_MODE_FAST_REFINE 6 /* performance mode: CG -> InitRelatedImages -> filter */
+
+/* performance-mode options (layout of include/densepoints.h dp_fast_options) */
+typedef struct or_fast_options {
+    int32_t iters;        /* conjugate-gradient iterations (E = 1 + 5 iters) */
+    int32_t margin;       /* tile margin around the initial window, pixels   */
+    int32_t tile_budget;  /* bytes of gray tiles per patch                   */
+    int32_t max_views;    /* staged views per patch (<= 32)                  */
+    float fd_step;        /* forward-difference step, scaled units           */
+    float ls_step;        /* initial line-search step, scaled units          */
+    int32_t densify;      /* product only: fast expansions in dp_densify     */
+    int32_t reserved;
+} or_fast_options;
 
 #ifdef __cplusplus
 extern "C" {
@@ -112,6 +126,14 @@ int or_pyr_down(const uint8_t *bgr, int W, int H, uint8_t *out);
 #define OR_FILTER_NEIGHBORS 2
 int or_filter_patches(const or_scene *s, const or_patch *p, int64_t n, int passes, double min_neighbor_frac,
                       uint8_t *keep);
+
+/* performance mode (or_fast.c) */
+void or_fast_default_options(or_fast_options *f);
+int or_gray_plane(const or_scene *s, int view, uint8_t *out);
+int or_fast_refine_batch(const or_scene *s, or_patch *p, int n, int cell, int mode, const or_fast_options *fo,
+                         uint8_t *accept, int nthreads);
+int or_fast_expand_batch(const or_scene *s, const or_patch *parents, int n, const or_fast_options *fo,
+                         or_patch *children, uint8_t *acc, int nthreads);
 
 #ifdef __cplusplus
 }

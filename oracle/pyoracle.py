@@ -14,7 +14,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liboracle.so")
 
-MODE_EVAL, MODE_FILTER, MODE_NM, MODE_SEED, MODE_EXPAND = range(5)
+MODE_EVAL, MODE_FILTER, MODE_NM, MODE_SEED, MODE_EXPAND, MODE_FAST_EVAL, MODE_FAST_REFINE = range(7)
 
 PATCH_DTYPE = np.dtype(
     [
@@ -54,6 +54,20 @@ class OrOptions(ctypes.Structure):
     ]
 
 
+class OrFastOptions(ctypes.Structure):
+    """or_fast_options (layout of include/densepoints.h dp_fast_options)."""
+    _fields_ = [
+        ("iters", ctypes.c_int32),
+        ("margin", ctypes.c_int32),
+        ("tile_budget", ctypes.c_int32),
+        ("max_views", ctypes.c_int32),
+        ("fd_step", ctypes.c_float),
+        ("ls_step", ctypes.c_float),
+        ("densify", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB
@@ -88,6 +102,11 @@ def _load():
         "or_org_insert": (ctypes.c_int, [P, P, ctypes.c_uint32, ctypes.c_uint32, P]),
         "or_pyr_down": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, P]),
         "or_filter_patches": (ctypes.c_int, [P, P, ctypes.c_int64, ctypes.c_int, ctypes.c_double, P]),
+        # performance mode (or_fast.c)
+        "or_fast_default_options": (None, [P]),
+        "or_gray_plane": (ctypes.c_int, [P, ctypes.c_int, P]),
+        "or_fast_refine_batch": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int]),
+        "or_fast_expand_batch": (ctypes.c_int, [P, P, ctypes.c_int, P, P, P, ctypes.c_int]),
         # seed generation (or_seeds.c)
         "or_orb_pattern": (None, [P]),
         "or_features_per_level": (None, [ctypes.c_int, ctypes.c_double, ctypes.c_int, P]),
@@ -200,6 +219,50 @@ class Scene:
         pops = ctypes.c_int64()
         n = lib.or_densify(self._h, _p(seeds), len(seeds), _p(out), cap, ctypes.byref(nseed), ctypes.byref(pops))
         return out[: min(n, cap)].copy(), {"patches": n, "seed_patches": nseed.value, "pops": pops.value}
+
+
+def fast_options(opts=None, **kw) -> OrFastOptions:
+    """Copy a densepoints_amd FastOptions (identical layout), or defaults + kw."""
+    o = OrFastOptions()
+    if opts is not None:
+        raw = bytes(opts.to_c() if hasattr(opts, "to_c") else opts)
+        ctypes.memmove(ctypes.byref(o), raw, ctypes.sizeof(o))
+    else:
+        lib.or_fast_default_options(ctypes.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def _scene_fast_refine(self, patches, cell, mode=MODE_FAST_REFINE, fo=None, nthreads=0):
+    """Performance-mode refine (or_fast.c spec) in place; returns accept flags."""
+    fo = fast_options() if fo is None else fast_options(fo)
+    acc = np.zeros(len(patches), dtype=np.uint8)
+    if lib.or_fast_refine_batch(self._h, _p(patches), len(patches), cell, mode, ctypes.byref(fo), _p(acc),
+                                nthreads) != 0:
+        raise ValueError("or_fast_refine_batch failed")
+    return acc
+
+
+def _scene_fast_expand(self, parents, fo=None, nthreads=0):
+    fo = fast_options() if fo is None else fast_options(fo)
+    parents = np.ascontiguousarray(parents)
+    kids = np.zeros(4 * len(parents), dtype=PATCH_DTYPE)
+    acc = np.zeros(4 * len(parents), dtype=np.uint8)
+    lib.or_fast_expand_batch(self._h, _p(parents), len(parents), ctypes.byref(fo), _p(kids), _p(acc), nthreads)
+    return kids, acc
+
+
+def _scene_gray(self, view):
+    W, H = self._keep[1][view], self._keep[2][view]
+    out = np.zeros((H, W), dtype=np.uint8)
+    lib.or_gray_plane(self._h, view, _p(out))
+    return out
+
+
+Scene.fast_refine = _scene_fast_refine
+Scene.fast_expand = _scene_fast_expand
+Scene.gray = _scene_gray
 
 
 def _scene_filter(self, patches, passes=3, min_neighbor_frac=0.25):

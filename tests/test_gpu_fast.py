@@ -1,0 +1,138 @@
+"""Performance mode on the GPU (dp_fast.hip) against its specification, the
+oracle's or_fast.c, bit-exact on every field: gray planes, one fast
+evaluation, the CG refine -> InitRelatedImages -> fast filter sequence, and
+Expand::ExpandPatch children (expand.cpp:103-143) refined in performance mode,
+from toy scenes to BASELINE config 3 at full size."""
+import numpy as np
+import pytest
+
+import densepoints_amd as dp
+from densepoints_amd import _native as N
+from densepoints_amd import synth
+
+from test_gpu_parity import FIELDS, assert_same, scene
+
+pytestmark = pytest.mark.gpu
+
+
+def test_recip_newton_equals_ieee_division():
+    """The kernel's 1/hz (v_rcp_f32 + one Newton step) is IEEE 1.0f/hz on 4M+
+    inputs over the range the spec allows (hz >= 2^-20)."""
+    rng = np.random.default_rng(11)
+    x = np.concatenate([
+        np.exp2(rng.uniform(-20, 20, 2_000_000)).astype(np.float32),
+        rng.uniform(0.25, 4.0, 2_000_000).astype(np.float32),
+        # significands near all-ones / all-zeros
+        (np.float32(1.0) + np.arange(1, 40001, dtype=np.float32) * np.float32(2.0 ** -23)),
+        (np.float32(2.0) - np.arange(1, 40001, dtype=np.float32) * np.float32(2.0 ** -23)),
+        np.array([2.0 ** -20, 1.0, 2.0, 3.0, 0.1, 1e6], dtype=np.float32),
+    ]).astype(np.float32)
+    out = np.zeros_like(x)
+    N.check(N.lib.dp_probe_recip_f32_device(N.ptr(x), len(x), N.ptr(out)))
+    want = np.float32(1.0) / x
+    bad = np.flatnonzero(out.view(np.uint32) != want.view(np.uint32))
+    assert bad.size == 0, f"{bad.size} mismatches, e.g. {x[bad[:5]]}"
+
+
+@pytest.fixture(scope="module")
+def engine():
+    with dp.Engine(device=0) as eng:
+        yield eng
+
+
+def test_gray_planes_equal_spec(engine, orc):
+    sc = scene("hf6")
+    engine.set_views(sc.views)
+    S = orc.Scene(sc.P, sc.imgs)
+    for v in range(len(sc.views)):
+        g = engine.read_gray(v)
+        assert np.array_equal(g.astype(np.int32), S.gray(v).astype(np.int32)), f"view {v}"
+
+
+@pytest.mark.parametrize("cell", [16, 11, 7, 5])
+@pytest.mark.parametrize("mode", [N.MODE_FAST_EVAL, N.MODE_FAST_REFINE])
+def test_fast_modes_bit_exact(engine, orc, cell, mode):
+    sc = scene("hf6")
+    engine.set_views(sc.views)
+    S = orc.Scene(sc.P, sc.imgs)
+    seeds = sc.seeds[:200]
+    gp = engine.seeds_to_patches(seeds)
+    op = S.seeds_to_patches(seeds)
+    ga = engine.fast_refine(gp, cell, mode)
+    oa = S.fast_refine(op, cell, mode)
+    assert np.array_equal(ga, oa)
+    assert_same(gp, op)
+    if mode == N.MODE_FAST_REFINE:
+        assert gp["evals"].mean() > 10 and ga.sum() > 0
+
+
+@pytest.mark.parametrize("opts", [dict(), dict(iters=0), dict(iters=7, margin=7), dict(margin=0, tile_budget=2048),
+                                  dict(max_views=3, fd_step=0.25, ls_step=2.0)])
+def test_fast_expand_bit_exact_options(orc, opts):
+    sc = scene("hf6")
+    S = orc.Scene(sc.P, sc.imgs)
+    parents = S.seeds_to_patches(sc.seeds[:120])
+    S.refine(parents, 16, orc.MODE_SEED)
+    fo = dp.FastOptions(**opts)
+    with dp.Engine(device=0) as eng:
+        eng.set_views(sc.views)
+        eng.set_fast_options(fo)
+        gk, ga = eng.fast_expand(parents)
+    ok, oa = S.fast_expand(parents, orc.fast_options(fo))
+    assert np.array_equal(ga, oa)
+    assert_same(gk, ok, FIELDS + ("parent",))
+
+
+def test_fast_edge_cases(engine, orc):
+    sc = scene("wide70")
+    engine.set_views(sc.views)
+    S = orc.Scene(sc.P, sc.imgs)
+    p = engine.seeds_to_patches(sc.seeds[::7][:64])
+    p["vis"][0] = 0                          # no visible view
+    p["vis"][1] = dp.mask_from_list(dp.visible_list(p["vis"][1])[:1])
+    p["pos"][2] = [50.0, 50.0, 50.0]         # off every image
+    p["normal"][3] = [0.0, 0.0, 0.0]         # degenerate normal
+    for mode in (N.MODE_FAST_EVAL, N.MODE_FAST_REFINE):
+        for cell in (5, 9):
+            gp, op = p.copy(), p.copy()
+            ga = engine.fast_refine(gp, cell, mode)
+            oa = S.fast_refine(op, cell, mode)
+            assert np.array_equal(ga, oa)
+            assert_same(gp, op)
+    assert len(engine.fast_refine(dp.empty_patches(0), 11)) == 0
+    with pytest.raises(dp.DensePointsError):
+        engine.set_fast_options(dp.FastOptions(margin=8))
+    with pytest.raises(dp.DensePointsError):
+        engine.set_fast_options(dp.FastOptions(tile_budget=32768))
+
+
+def test_fast_expand_cfg3_full_scene(orc):
+    """BASELINE config 3 (32 views 3840x2160): performance-mode expansion of
+    2,000 refined parents equals the spec bit for bit, and its geometry beats
+    the parity mode's against the synthetic ground truth."""
+    from test_gpu_configs import DeviceScene, spread
+
+    with dp.Engine(device=0) as eng:
+        sc = DeviceScene("cfg3_32view_4k", eng)
+        S = orc.Scene(sc.P, sc.host_images())
+        seeds = spread(sc.seeds, 600)
+        par = eng.seeds_to_patches(seeds)
+        acc = eng.refine(par, 16, N.MODE_SEED)
+        par = np.ascontiguousarray(np.resize(par[acc == 1], 2000))
+        for cell in (11, 7):
+            o = dp.Options(expand_cell_size=cell)
+            eng.set_options(o)
+            gk, ga = eng.fast_expand(par)
+            S2 = orc.Scene(sc.P, sc.host_images(), o)
+            ok, oa = S2.fast_expand(par)
+            assert np.array_equal(ga, oa)
+            assert_same(gk, ok, FIELDS + ("parent",))
+            assert 0.2 < ga.mean() < 0.95
+        eng.set_options(dp.Options())
+        nk, na = eng.expand(par)
+    def err(k, a):
+        k = k[a == 1]
+        z, _ = synth.surface(sc.cfg, k["pos"][:, :2].astype(np.float64))
+        return float(np.median(np.abs(k["pos"][:, 2] - z)))
+    # cell 7 children vs the parity (Nelder-Mead, cell 11) children
+    assert err(gk, ga) < err(nk, na)
