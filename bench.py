@@ -51,6 +51,12 @@ def parse():
     ap.add_argument("--traffic-json", default=None, help="measured HBM bytes/launch from profiles/")
     ap.add_argument("--no-seeds", action="store_true", help="skip the informational seed generation")
     ap.add_argument("--knn-rows", type=int, default=40000, help="descriptors per side of the kNN kernel timing")
+    ap.add_argument("--mode", choices=["parity", "fast"], default="parity",
+                    help="headline refine: parity (the reference's Nelder-Mead, bit-exact) or the performance "
+                         "mode (LDS-staged fp16 gray tiles + fused CG, dp_fast_options)")
+    ap.add_argument("--fast-cells", default="7,11", help="windows of the informational perf_mode sub-object")
+    ap.add_argument("--no-fast", action="store_true", help="skip the perf_mode sub-object")
+    ap.add_argument("--seed-stride", type=float, default=32.0, help="synthetic seed grid stride (px)")
     return ap.parse_args()
 
 
@@ -72,7 +78,7 @@ def main():
     dist = D.init(backend, torch.device("cuda", local))
     coll_dev = torch.device("cuda", local) if backend == "nccl" else None
 
-    cfg = synth.named(args.config)
+    cfg = synth.named(args.config, seed_stride_px=args.seed_stride)
     V, W, H = cfg.n_views, cfg.width, cfg.height
     P = synth.cameras(cfg)
     eng = dp.Engine(dp.Options(), device=local)
@@ -114,10 +120,15 @@ def main():
     work = torch.empty(B * N.PATCH_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
     accept = torch.empty(B, dtype=torch.uint8, device="cuda")
 
+    fast = args.mode == "fast"
+    if fast:
+        eng.set_options(dp.Options(expand_cell_size=args.cell))
+    expand_fn = eng.fast_expand_device if fast else eng.expand_device
+
     def step(ev=None):
         if ev:
             ev[0].record(stream)
-        eng.expand_device(d_parents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
+        expand_fn(d_parents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
         if ev:
             ev[1].record(stream)
 
@@ -150,8 +161,14 @@ def main():
     pvis = np.array([bin(int(m[0])).count("1") + bin(int(m[1])).count("1") for m in parents["vis"]])
     nvis = np.repeat(pvis, 4)  # children refine on the parent's visible set
     n1 = args.cell + 1
-    # algorithmic bytes: E * sum_v (n+1)^2 * 4 B (BGRA8) + 128 B record in/out
-    bytes_alg = float((evals * nvis * n1 * n1 * 4).sum() + 128 * B)
+    if fast:
+        # algorithmic bytes with fp16 texels: sum over evaluations of
+        # the staged views sampled (device-counted) * (n+1)^2 * 2 B + 128 B record
+        fst = eng.fast_last_stats()
+        bytes_alg = float(fst["view_evals"] * n1 * n1 * 2 + 128 * B)
+    else:
+        # algorithmic bytes: E * sum_v (n+1)^2 * 4 B (BGRA8) + 128 B record in/out
+        bytes_alg = float((evals * nvis * n1 * n1 * 4).sum() + 128 * B)
     achieved = bytes_alg / (launch_ms * 1e-3) / 1e9  # GB/s of the dominant kernel
     peak = 8000.0
     total_patches = B * args.steps * world
@@ -168,12 +185,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8 texels, fp64 geometry, int32 moments",
+        "dtype": "u8 gray texels in LDS (fp16 planes), fp32 sampling, int32 moments, fp64 CG" if fast else
+                 "u8 texels, fp64 geometry, int32 moments",
         "data": "synthetic (deterministic 3x3-facet heightfield, rendered on device)",
         "config": {
             "workload": f"{args.config}: {V} views {W}x{H}, {B} expansion candidates/GPU/step "
                         f"({NP} refined seed parents x 4 directions), n={args.cell}, "
-                        f"Nelder-Mead + InitRelatedImages + NCC filter (parity mode)",
+                        + ("performance mode: LDS-staged fp16 gray tiles + fused CG + InitRelatedImages + fast "
+                           "filter" if fast else "Nelder-Mead + InitRelatedImages + NCC filter (parity mode)"),
             "views": V,
             "width": W,
             "height": H,
@@ -200,7 +219,14 @@ def main():
             "bytes_per_launch_algorithmic": bytes_alg,
         },
     }
-    if rank == 0 and not args.no_densify:
+    if fast:
+        result["fast_stats"] = {k: int(v) for k, v in fst.items()}
+        result["roofline"]["bytes_per_launch_compulsory"] = float(fst["staged_bytes"] + 128 * B)
+        result["quality"] = quality(cfg, out, acc)
+    if rank == 0 and not fast and not args.no_fast:
+        result["perf_mode"] = perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, out, acc, parents, P,
+                                        planes)
+    if rank == 0 and not args.no_densify and not fast:
         # informational: the full PMVS::Run minus matching (dp_densify) on the same scene, untimed by the contract
         t0 = time.perf_counter()
         _, dst = eng.densify(seeds)
@@ -209,7 +235,7 @@ def main():
                                  "patches": int(dst["patches"]), "candidates": int(dst["candidates"]),
                                  "generations": int(dst["generations"]), "evals": int(dst["evals"]),
                                  "refine_ms": round(dst["refine_ms"], 1), "wall_s": round(wall, 3)}
-    if world > 1 and not args.no_densify:
+    if world > 1 and not args.no_densify and not fast:
         # informational: the same densify sharded over the ranks --
         # per generation each rank refines its item range into HBM, the
         # candidate shards are all-gathered over RCCL (all_gather_into_tensor),
@@ -237,7 +263,7 @@ def main():
         with open(tj) as f:
             t = json.load(f)
         # PMC bytes are per launch, so they only apply to the batch they were measured on
-        if t.get("batch") == result["config"]["batch_per_gpu"]:
+        if t.get("batch") == result["config"]["batch_per_gpu"] and not fast:
             # both readings: FETCH_SIZE as counted, and doubled per the gfx950
             # correction that MI355X_MICROARCH.md calibrates for 16-B/lane
             # streams (these are 8-B gathers: see "traffic_calibration")
@@ -248,7 +274,7 @@ def main():
                 result["roofline"]["traffic_calibration"] = t["calibration"]
 
     if rank == 0 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out)
+        result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out, fast)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
@@ -299,6 +325,91 @@ def seed_generation(eng, args):
     return out
 
 
+def quality(cfg, kids, acc):
+    """Median |z - z_true| (world units) and normal error (deg) of the accepted
+    children against the synthetic ground truth (dp_synth_surface)."""
+    from densepoints_amd import synth
+
+    k = kids[acc == 1]
+    if len(k) == 0:
+        return {"accepted": 0}
+    z, nrm = synth.surface(cfg, k["pos"][:, :2].astype(np.float64))
+    nn = k["normal"].astype(np.float64)
+    nn /= np.maximum(np.linalg.norm(nn, axis=1, keepdims=True), 1e-30)
+    ang = np.degrees(np.arccos(np.clip(np.abs((nn * nrm).sum(1)), 0.0, 1.0)))
+    return {"accepted": int(len(k)), "median_abs_dz": float(np.median(np.abs(k["pos"][:, 2] - z))),
+            "median_normal_err_deg": round(float(np.median(ang)), 3)}
+
+
+def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, parity_acc, parents, P, planes):
+    """Informational: the performance mode (DP_MODE_FAST_REFINE, dp_fast.hip --
+    LDS-staged fp16 gray tiles, fused CG, one wavefront per candidate) on the
+    same parents, per window size: Mpatches/s from HIP events on the launch
+    stream, E, the roofline on the algorithmic (every evaluation re-reads its
+    windows) and compulsory (tiles staged once) byte models, geometry against
+    the ground truth next to the parity mode's, and a CPU baseline of its spec
+    (oracle/or_fast.c) with a bit-exact check on that sample."""
+    import densepoints_amd as dp
+    from oracle import pyoracle as orc
+
+    B = 4 * NP
+    res = {"parity_quality_n%d" % args.cell: quality(cfg, parity_out, parity_acc)}
+    imgs = None
+    for cell in [int(c) for c in args.fast_cells.split(",") if c]:
+        eng.set_options(dp.Options(expand_cell_size=cell))
+        eng.fast_expand_device(d_parents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        ms = []
+        for _ in range(max(3, args.steps)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            eng.fast_expand_device(d_parents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
+            e1.record(stream)
+            ms.append((e0, e1))
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in ms]
+        kms = float(np.mean(ms))
+        st = eng.fast_last_stats()
+        out = np.frombuffer(work.cpu().numpy().tobytes(), dtype=dp.PATCH_DTYPE)
+        acc = accept.cpu().numpy()
+        n1 = cell + 1
+        alg = float(st["view_evals"] * n1 * n1 * 2 + 128 * B)
+        comp = float(st["staged_bytes"] + 128 * B)
+        r = {"Mpatches_per_s": round(B / kms / 1e3, 3), "kernel_ms_per_launch": round(kms, 3),
+             "kernel_ms_events": [round(x, 3) for x in ms],
+             "E_mean_evals_per_patch": round(st["evals"] / max(st["patches"], 1), 3),
+             "mean_staged_views_per_eval": round(st["view_evals"] / max(st["evals"], 1), 3),
+             "accept_rate": round(float(acc.mean()), 4),
+             "Mevals_per_s": round(st["evals"] / kms / 1e3, 3),
+             "roofline": {"bound": "hbm", "achieved": round(alg / kms / 1e6, 2), "peak": 8000.0, "unit": "GB/s",
+                          "frac": round(alg / kms / 1e6 / 8000.0, 4), "traffic": None,
+                          "bytes_per_launch_algorithmic": alg, "bytes_per_launch_compulsory": comp,
+                          "compulsory_GBps": round(comp / kms / 1e6, 2)},
+             "quality": quality(cfg, out, acc), "stats": {k: int(v) for k, v in st.items()}}
+        if not args.no_cpu:
+            if imgs is None:
+                imgs = []
+                for pl in planes:
+                    a = pl.cpu().numpy().view(np.uint8).reshape(cfg.height, cfg.width, 4)
+                    imgs.append(np.ascontiguousarray(a[:, :, :3]))
+            S = orc.Scene(P, imgs, dp.Options(expand_cell_size=cell))
+            n = min(args.cpu_parents, len(parents))
+            cores = args.cpu_threads or host_cores()
+            t0 = time.perf_counter()
+            kids, kacc = S.fast_expand(parents[:n], None, cores)
+            t = time.perf_counter() - t0
+            g = out[: 4 * n]
+            fields = ("pos", "normal", "ref", "vis", "cand", "score", "evals", "flags", "parent")
+            r["cpu_baseline"] = {"value": round(4 * n / t / 1e6, 6), "unit": "Mpatches/s", "cores": cores,
+                                 "kind": "port", "sample": f"first {n} parents ({4 * n} candidates), {t:.1f} s",
+                                 "parity_bit_exact_on_sample": bool(all(kids[f].tobytes() == g[f].tobytes()
+                                                                        for f in fields) and
+                                                                    np.array_equal(kacc, acc[: 4 * n]))}
+        res["n%d" % cell] = r
+    eng.set_options(dp.Options(expand_cell_size=args.cell))
+    return res
+
+
 def latest_traffic_json():
     """profiles/<latest round>/refine_traffic.json: rocprofv3 PMC HBM bytes per
     launch of the expansion kernel, collected by tools/gpu_profile.sh"""
@@ -323,7 +434,7 @@ def host_cores():
     return n
 
 
-def cpu_baseline(args, cfg, P, planes, parents, gpu_out):
+def cpu_baseline(args, cfg, P, planes, parents, gpu_out, fast=False):
     """The oracle (CPU restatement, test infrastructure) on a FIXED sample --
     the first --cpu-parents parents (4x as many candidates) of the same batch --
     timed on all of this host's usable cores and on one thread (SURVEY 8d CPU
@@ -334,15 +445,18 @@ def cpu_baseline(args, cfg, P, planes, parents, gpu_out):
     for pl in planes:
         a = pl.cpu().numpy().view(np.uint8).reshape(cfg.height, cfg.width, 4)
         imgs.append(np.ascontiguousarray(a[:, :, :3]))
-    S = orc.Scene(P, imgs)
+    import densepoints_amd as dp
+
+    S = orc.Scene(P, imgs, dp.Options(expand_cell_size=args.cell))
     cores = args.cpu_threads or host_cores()
     n = min(args.cpu_parents, len(parents))
+    expand = (lambda par, th: S.fast_expand(par, None, th)) if fast else S.expand
     t0 = time.perf_counter()
-    kids, acc = S.expand(parents[:n], cores)
+    kids, acc = expand(parents[:n], cores)
     t = time.perf_counter() - t0
     n1 = min(args.cpu_parents_1thread, n)
     t0 = time.perf_counter()
-    S.expand(parents[:n1], 1)
+    expand(parents[:n1], 1)
     t1 = time.perf_counter() - t0
     g = gpu_out[: 4 * n]
     fields = ("pos", "normal", "ref", "vis", "cand", "score", "evals", "flags", "parent")
@@ -357,6 +471,7 @@ def cpu_baseline(args, cfg, P, planes, parents, gpu_out):
         "sample_1thread": f"first {n1} parents ({4 * n1} candidates), {t1:.1f} s on 1 thread",
         "host_cpus_reported": os.cpu_count(),
         "parity_bit_exact_on_sample": bool(same),
+        "spec": "oracle/or_fast.c (performance mode)" if fast else "oracle/oracle.c (reference restatement)",
     }
 
 

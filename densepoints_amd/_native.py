@@ -174,6 +174,11 @@ class DpFastOptions(ctypes.Structure):
     ]
 
 
+class DpFastStats(ctypes.Structure):
+    _fields_ = [("patches", ctypes.c_int64), ("evals", ctypes.c_int64), ("view_evals", ctypes.c_int64),
+                ("staged_bytes", ctypes.c_int64)]
+
+
 # dp_keypoint: the cv::KeyPoint fields the matcher reads
 KEYPOINT_DTYPE = np.dtype(
     [("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("angle", "<f4"), ("octave", "<i4"), ("reserved", "<i4")]
@@ -235,6 +240,7 @@ SIGNATURES = [
     ("dp_read_gray", _I, [_P, _I, _P]),
     ("dp_fast_expand_batch", _I, [_P, _P, _I, _P, _P]),
     ("dp_fast_expand_batch_device", _I, [_P, _P, _I, _P, _P, _P]),
+    ("dp_fast_last_stats", _I, [_P, _P]),
     ("dp_probe_sincos", None, [_D, _P, _P]),
     ("dp_probe_acos", _D, [_D]),
     ("dp_probe_texture", _I, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, _I, _P]),

@@ -240,6 +240,8 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->scan_tmp.release();
     if (c->gray_pool)
         hipFree(c->gray_pool);
+    if (c->d_fstats)
+        hipFree(c->d_fstats);
     if (c->d_gray)
         hipFree(c->d_gray);
     if (c->d_work)

@@ -114,6 +114,7 @@ struct dp_ctx {
     size_t gray_cap = 0;       // elements
     void *d_gray = nullptr;    // device GrayPlane table
     bool gray_ready = false;
+    unsigned long long *d_fstats = nullptr; // dp_fast_stats counters of the last launch
     int gray_level = -1, gray_V = 0;
 };
 

@@ -47,6 +47,7 @@ struct FastArgs {
     uint32_t *work;
     unsigned long long *evals;
     const dp_patch *parents; // expansion: child c = parents[c / 4], direction c % 4
+    unsigned long long *stats; // dp_fast_stats: patches, evals, view_evals, staged_bytes
 };
 
 // per staged view, written once per staging (rank order)
@@ -313,7 +314,7 @@ struct Staged {
 // Stage the wave's patch: frame, usable views, margin, tiles into LDS.
 // Returns m (uniform); the lane of rank r holds that view's vectors in S.
 template <int kBudget>
-__device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged &S)
+__device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged &S, unsigned long long &staged_bytes)
 {
     const int lane = lane_id();
     const int cell = a.cell;
@@ -352,6 +353,8 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     const int incl = wave_incl_i32(staged ? t.bytes : 0);
     const bool keep = staged && incl <= a.fo.tile_budget;
     const int m = __popcll(__ballot(keep));
+    // fp16 texels the tile reads from the gray plane: (tw + 1) x (th + 1)
+    staged_bytes += (unsigned long long)uni(wave_sum_i32(keep ? 2 * (t.tw + 1) * (t.th + 1) : 0));
     if (keep) {
         StageRec &R = L.u.st[rank];
 #pragma unroll
@@ -703,7 +706,7 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
     __shared__ FastLds<kBudget> L;
     const int lane = lane_id();
     const Slots sl = make_slots<G>(a.cell);
-    unsigned long long wave_evals = 0;
+    unsigned long long wave_evals = 0, wave_vev = 0, wave_bytes = 0, wave_patches = 0;
     dp_patch &p = L.p;
     for (;;) {
         uint32_t idx = 0;
@@ -749,11 +752,12 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
             if (kMode == DP_MODE_FAST_EVAL) {
                 Staged S;
                 const bool degen = L.F.degenerate;
-                const int m = degen ? 0 : stage(a, L, 0, S);
+                const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes);
                 p.evals += 1;
                 if (degen)
                     p.flags |= DP_PATCH_DEGENERATE;
                 ok = m >= 2;
+                wave_vev += ok ? (unsigned long long)m : 0ull;
                 if (ok) {
                     evaluate<G>(a, L, S, sl, m, 0.0, 0.0, 0.0);
                     double sum = 0.0;
@@ -771,9 +775,11 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
                     rejected = true;
                 } else {
                     Staged S;
-                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S);
+                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S, wave_bytes);
                     if (m >= 2) {
-                        p.evals += (uint32_t)cg_refine<G>(a, L, S, sl, m);
+                        const int E = cg_refine<G>(a, L, S, sl, m);
+                        p.evals += (uint32_t)E;
+                        wave_vev += (unsigned long long)E * (unsigned long long)m;
                         const Frame &F = L.F;
                         const double d = L.cg.x[0] * F.sd, aa = L.cg.x[1] * F.st, bb = L.cg.x[2] * F.st;
                         double nrm[3];
@@ -804,10 +810,11 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
                     wave_sync();
                     Staged S;
                     const bool degen = L.F.degenerate;
-                    const int m = degen ? 0 : stage(a, L, 0, S);
+                    const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes);
                     p.evals += 1;
                     if (degen)
                         p.flags |= DP_PATCH_DEGENERATE;
+                    wave_vev += m >= 2 ? (unsigned long long)m : 0ull;
                     if (m < 2) {
                         p.score = -1.0f;
                         const int v = uni(S.view);
@@ -845,6 +852,7 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
         }
         wave_sync();
         wave_evals += p.evals;
+        wave_patches += 1;
         if (lane == 0) {
             if (a.parents || kMode != DP_MODE_FAST_EVAL) {
                 a.patches[idx] = p;
@@ -861,6 +869,12 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
     }
     if (lane == 0 && a.evals)
         atomicAdd(a.evals, wave_evals);
+    if (lane == 0 && a.stats) {
+        atomicAdd(a.stats + 0, wave_patches);
+        atomicAdd(a.stats + 1, wave_evals);
+        atomicAdd(a.stats + 2, wave_vev);
+        atomicAdd(a.stats + 3, wave_bytes);
+    }
 }
 
 // BGRA8 -> fp16 gray (BGR2GRAY 14-bit fixed point, exact integers in fp16)
@@ -1013,6 +1027,10 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.work = c->d_work;
     a.evals = c->d_evals;
     a.parents = d_parents;
+    if (!c->d_fstats)
+        DP_HIP(c, hipMalloc(&c->d_fstats, 4 * sizeof(unsigned long long)));
+    a.stats = c->d_fstats;
+    DP_HIP(c, hipMemsetAsync(c->d_fstats, 0, 4 * sizeof(unsigned long long), s));
     DP_HIP(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), s));
     DP_HIP(c, hipEventRecord(c->e0, s));
     const int N = cell * cell;
@@ -1146,4 +1164,21 @@ extern "C" int dp_probe_recip_f32_device(const float *x, int n, float *out)
     hipFree(dx);
     hipFree(dy);
     return e == hipSuccess ? DP_OK : DP_E_HIP;
+}
+
+extern "C" int dp_fast_last_stats(dp_ctx *c, dp_fast_stats *out)
+{
+    if (!c || !out)
+        return DP_E_ARG;
+    *out = dp_fast_stats{};
+    if (!c->d_fstats)
+        return DP_OK;
+    unsigned long long v[4];
+    DP_HIP(c, hipDeviceSynchronize());
+    DP_HIP(c, hipMemcpy(v, c->d_fstats, sizeof(v), hipMemcpyDeviceToHost));
+    out->patches = (int64_t)v[0];
+    out->evals = (int64_t)v[1];
+    out->view_evals = (int64_t)v[2];
+    out->staged_bytes = (int64_t)v[3];
+    return DP_OK;
 }

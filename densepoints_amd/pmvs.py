@@ -332,6 +332,11 @@ class Engine:
                                                     ctypes.c_void_p(d_accept) if d_accept else None,
                                                     ctypes.c_void_p(stream) if stream else None))
 
+    def fast_last_stats(self) -> dict:
+        st = N.DpFastStats()
+        self._check(lib.dp_fast_last_stats(self._ctx, ctypes.byref(st)))
+        return {name: getattr(st, name) for name, _ in N.DpFastStats._fields_}
+
     def evaluate(self, patches: np.ndarray, cell: int) -> np.ndarray:
         out = np.zeros(len(patches), dtype=np.float32)
         self._check(lib.dp_eval_batch(self._ctx, ptr(patches), len(patches), cell, ptr(out)))

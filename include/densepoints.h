@@ -401,6 +401,18 @@ int dp_read_gray(dp_ctx *ctx, int view, uint16_t *fp16_out);
  * mode: DP_MODE_FAST_REFINE on the parent's visible set, cell =
  * expand_cell_size. */
 int dp_fast_expand_batch(dp_ctx *ctx, const dp_patch *parents, int n, dp_patch *children, uint8_t *accept_out);
+/* Work counters of the most recent performance-mode launch (device-counted):
+ * view_evals = sum over patches and evaluations of the staged views sampled,
+ * i.e. algorithmic bytes = view_evals * (n+1)^2 * 2 (fp16 texels);
+ * staged_bytes = fp16 bytes the tiles read from the gray planes (the
+ * compulsory HBM traffic of the windows). */
+typedef struct dp_fast_stats {
+    int64_t patches;
+    int64_t evals;
+    int64_t view_evals;
+    int64_t staged_bytes;
+} dp_fast_stats;
+int dp_fast_last_stats(dp_ctx *ctx, dp_fast_stats *out);
 int dp_fast_expand_batch_device(dp_ctx *ctx, const dp_patch *d_parents, int n, dp_patch *d_children,
                                 uint8_t *d_accept, void *stream);
 
