@@ -1160,6 +1160,141 @@ extern "C" int dp_densify_commit_device(dp_ctx *c, dp_generation *gen, const dp_
     return densify_commit_impl(c, gen, d_cand, d_accept, n_cand, true, (hipStream_t)stream);
 }
 
+// ---- partitioned generations (reference-view super-tiles) -------
+
+extern "C" int dp_densify_owners(dp_ctx *c, const dp_generation *gen, int world, int tile_px, int32_t *owner_out,
+                                 int32_t *fallback_out)
+{
+    if (!c || !gen || world < 1 || tile_px < 1 || (gen->items > 0 && !owner_out))
+        return fail(c, DP_E_ARG, "dp_densify_owners: bad arguments");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_owners: generation out of sequence");
+    const int64_t n = gen->items;
+    if (fallback_out)
+        *fallback_out = 0;
+    if (n == 0)
+        return DP_OK;
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const dp_patch *items = gen->index == 0 ? c->seedp.p : c->store.p + gen->head;
+    DP_HIP(c, c->owners.reserve((size_t)n));
+    DP_HIP(c, dpk::launch_owners(c->d_views, items, n, world, (double)tile_px, c->owners.p, s));
+    DP_HIP(c, hipMemcpyAsync(owner_out, c->owners.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipStreamSynchronize(s));
+    // round robin when the largest share exceeds 1.1x the mean
+    std::vector<int64_t> cnt((size_t)world, 0);
+    for (int64_t i = 0; i < n; ++i)
+        cnt[(size_t)owner_out[i]] += 1;
+    int64_t mx = 0;
+    for (int64_t v : cnt)
+        mx = v > mx ? v : mx;
+    if ((double)mx > 1.1 * (double)n / (double)world) {
+        for (int64_t i = 0; i < n; ++i)
+            owner_out[i] = (int32_t)(i % world);
+        if (fallback_out)
+            *fallback_out = 1;
+    }
+    return DP_OK;
+}
+
+static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const int64_t *d_items, int64_t n,
+                                     dp_patch *work, uint8_t *okp, hipStream_t s)
+{
+    const int64_t nc64 = n * gen->per_item;
+    if (nc64 > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_refine_items: shard too large");
+    const int32_t nc = (int32_t)nc64;
+    dpk::RefineArgs a{};
+    if (gen->index == 0) {
+        DP_HIP(c, dpk::launch_gather_patches(c->seedp.p, d_items, n, work, s));
+        a = refine_args(c, work, nc, gen->cell, DP_MODE_SEED, okp);
+    } else {
+        a = refine_args(c, work, nc, gen->cell, DP_MODE_EXPAND, okp);
+        a.parents = c->store.p;
+        a.parent0 = gen->head;
+        a.items = d_items;
+    }
+    int rc = launch_timed(c, a, s);
+    if (rc != DP_OK)
+        return rc;
+    double ms = 0.0;
+    if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
+        return rc;
+    c->g_st.refine_ms += ms;
+    return DP_OK;
+}
+
+static int check_items(dp_ctx *c, const dp_generation *gen, int64_t n)
+{
+    if (!c || !gen || n < 0 || n > gen->items)
+        return fail(c, DP_E_ARG, "dp_densify_refine_items: bad item count");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_refine_items: generation out of sequence");
+    return DP_OK;
+}
+
+extern "C" int dp_densify_refine_items(dp_ctx *c, const dp_generation *gen, const int64_t *items, int64_t n,
+                                       dp_patch *cand_out, uint8_t *accept_out)
+{
+    int rc = check_items(c, gen, n);
+    if (rc != DP_OK || n == 0)
+        return rc;
+    if (!items || !cand_out || !accept_out)
+        return fail(c, DP_E_ARG, "dp_densify_refine_items: null arrays");
+    for (int64_t i = 0; i < n; ++i)
+        if (items[i] < 0 || items[i] >= gen->items)
+            return fail(c, DP_E_ARG, "dp_densify_refine_items: item out of range");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const size_t nc = (size_t)n * gen->per_item;
+    DP_HIP(c, c->items.reserve((size_t)n));
+    DP_HIP(c, c->cand.reserve(nc));
+    DP_HIP(c, c->ok.reserve(nc));
+    DP_HIP(c, hipMemcpyAsync(c->items.p, items, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
+    rc = densify_refine_items_impl(c, gen, c->items.p, n, c->cand.p, c->ok.p, s);
+    if (rc != DP_OK)
+        return rc;
+    DP_HIP(c, hipMemcpyAsync(cand_out, c->cand.p, sizeof(dp_patch) * nc, hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipMemcpyAsync(accept_out, c->ok.p, nc, hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipStreamSynchronize(s));
+    return DP_OK;
+}
+
+extern "C" int dp_densify_refine_items_device(dp_ctx *c, const dp_generation *gen, const int64_t *d_items, int64_t n,
+                                              dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream)
+{
+    int rc = check_items(c, gen, n);
+    if (rc != DP_OK || n == 0)
+        return rc;
+    if (!d_items || !d_cand_out || !d_accept_out)
+        return fail(c, DP_E_ARG, "dp_densify_refine_items_device: null arrays");
+    hipSetDevice(c->device);
+    return densify_refine_items_impl(c, gen, d_items, n, d_cand_out, d_accept_out,
+                                     stream ? (hipStream_t)stream : c->stream);
+}
+
+extern "C" int dp_densify_commit_items_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_cand,
+                                              const uint8_t *d_accept, const int64_t *d_items, int64_t n_items,
+                                              void *stream)
+{
+    if (!c || !gen || n_items != gen->items || (n_items > 0 && (!d_cand || !d_accept || !d_items)))
+        return fail(c, DP_E_ARG, "dp_densify_commit_items_device: need every item of the generation");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_commit_items_device: generation out of sequence");
+    hipSetDevice(c->device);
+    hipStream_t us = (hipStream_t)stream;
+    const size_t nc = (size_t)n_items * gen->per_item;
+    if (nc > 0) {
+        if (us != c->stream)
+            DP_HIP(c, hipStreamSynchronize(us));
+        DP_HIP(c, c->cand.reserve(nc));
+        DP_HIP(c, c->ok.reserve(nc));
+        DP_HIP(c, dpk::launch_scatter_items(d_cand, d_accept, d_items, n_items, gen->per_item, c->cand.p, c->ok.p,
+                                            c->stream));
+    }
+    return densify_commit_impl(c, gen, c->cand.p, c->ok.p, (int64_t)nc, true, c->stream);
+}
+
 extern "C" int dp_densify_result(dp_ctx *c, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats)
 {
     if (!c || !out || !n_out)

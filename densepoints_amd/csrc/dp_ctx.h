@@ -101,6 +101,8 @@ struct dp_ctx {
     std::vector<dp_patch> result;
     // generation-at-a-time densify (dp_densify_begin/refine/commit/result)
     DevBuf<dp_patch> seedp;  // seed patches of generation 0
+    DevBuf<int64_t> items;   // item list of a partitioned refine / commit
+    DevBuf<int32_t> owners;  // owner rank per item (dp_densify_owners)
     int64_t g_np = 0;        // patches in the replicated store
     int64_t g_nseeds = 0;
     int64_t g_expected = -1; // generation index the next commit must carry

@@ -42,6 +42,9 @@ struct RefineArgs {
     // every candidate's output is independent of the order.
     uint32_t *order;         // >= ceil(n / group size) entries, or null
     uint32_t *order_scratch; // kLptBuckets * 2 counters
+    // optional item list of a partitioned generation: child c
+    // expands queue entry parent0 + items[c / 4] instead of parent0 + c / 4
+    const int64_t *items;
 };
 constexpr int kLptBuckets = 129; // visible-view counts 0..128
 
@@ -94,5 +97,11 @@ hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand,
                          int64_t parent0, int is_seed, hipStream_t s);
 hipError_t launch_render(const dp_synth_config &cfg, const double *P, uint32_t *out, int v,
                          hipStream_t s);
+// multi-GPU partition of a generation's items (dp_densify_owners)
+hipError_t launch_owners(const dpg::ViewDev *views, const dp_patch *items, int64_t n, int world, double tile,
+                         int32_t *owner, hipStream_t s);
+hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s);
+hipError_t launch_scatter_items(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n, int per,
+                                dp_patch *cand_out, uint8_t *acc_out, hipStream_t s);
 
 } // namespace dpk

@@ -1140,7 +1140,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
             float cpos[3] = {0.f, 0.f, 0.f};
             int64_t qi = 0;
             if (a.parents) {
-                qi = a.parent0 + (int64_t)(idx >> 2);
+                qi = a.parent0 + (a.items ? a.items[idx >> 2] : (int64_t)(idx >> 2));
                 src = a.parents + qi;
                 const int pm = __popcll(src->vis[0]) + __popcll(src->vis[1]);
                 live = qi < a.max_pops && pm >= a.opt.min_expand_visible && src->ref < (uint32_t)a.V;
@@ -1470,7 +1470,7 @@ int read_stamps(unsigned long long *out)
 // views for expansion children, the patch's own otherwise)
 __device__ __forceinline__ int lpt_key(const RefineArgs &a, int64_t g)
 {
-    const dp_patch &p = a.parents ? a.parents[a.parent0 + g] : a.patches[g];
+    const dp_patch &p = a.parents ? a.parents[a.parent0 + (a.items ? a.items[g] : g)] : a.patches[g];
     return kLptBuckets - 1 - (__popcll(p.vis[0]) + __popcll(p.vis[1]));
 }
 
@@ -1572,6 +1572,82 @@ hipError_t launch_refine(const RefineArgs &a, hipStream_t s)
     default:
         return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// Owner rank of each item: the centre projected into its
+// reference view, super-tile (ref, floor(v / tile), floor(u / tile)) hashed.
+__device__ __forceinline__ uint32_t owner_hash(uint32_t ref, uint32_t ty, uint32_t tx)
+{
+    uint32_t h = (ref * 73856093u) ^ (ty * 19349663u) ^ (tx * 83492791u);
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    return h;
+}
+
+__device__ __forceinline__ uint32_t tile_coord(double q)
+{
+    // floor to int32 (wraps through uint32); NaN and out-of-range go to 0
+    return (q > -2.0e9 && q < 2.0e9) ? (uint32_t)(int32_t)floor(q) : 0u;
+}
+
+__global__ void owners_kernel(const dpg::ViewDev *views, const dp_patch *items, int64_t n, int world, double tile,
+                              int32_t *owner)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const dp_patch &p = items[i];
+    const dpg::ViewDev &v = views[p.ref];
+    double u, w;
+    dpg::project(v.P, (double)p.pos[0], (double)p.pos[1], (double)p.pos[2], u, w);
+    owner[i] = (int32_t)(owner_hash(p.ref, tile_coord(w / tile), tile_coord(u / tile)) % (uint32_t)world);
+}
+
+__global__ void gather_patches_kernel(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        dst[i] = src[idx[i]];
+}
+
+__global__ void scatter_items_kernel(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n,
+                                     int per, dp_patch *cand_out, uint8_t *acc_out)
+{
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n * per)
+        return;
+    const int64_t dst = items[j / per] * per + j % per;
+    cand_out[dst] = cand[j];
+    acc_out[dst] = acc[j];
+}
+
+hipError_t launch_owners(const dpg::ViewDev *views, const dp_patch *items, int64_t n, int world, double tile,
+                         int32_t *owner, hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(owners_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, views, items, n, world,
+                       tile, owner);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(gather_patches_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, idx, n, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_items(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n, int per,
+                                dp_patch *cand_out, uint8_t *acc_out, hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(scatter_items_kernel, dim3((unsigned)((n * per + 255) / 256)), dim3(256), 0, s, cand, acc,
+                       items, n, per, cand_out, acc_out);
     return hipGetLastError();
 }
 

@@ -9,6 +9,12 @@ The refine/expand step has no data-path collective. Candidates are independent
     exchange of a sharded densify).
 Shards are contiguous ranges of the candidate sequence, so concatenating the
 gathered shards in rank order restores the 1-GPU order bit for bit.
+
+The densify BFS is also sharded by REFERENCE-VIEW SUPER-TILE (north star:
+"reference-view grid cells shard across the 8 GPUs"):
+densify_partitioned[_device] hand each rank the generation items whose centre
+falls in its hashed (ref, v/64, u/64) tiles (dp_densify_owners), all-gather the
+candidates, put them back in sequence order and commit -- still bit-exact.
 """
 from __future__ import annotations
 
@@ -184,6 +190,107 @@ def densify_sharded_device(eng, seeds_xyz, dist, device: torch.device):
         del buf, acc, all_c, all_a
     patches, stats = eng.densify_result()
     return patches, _reduce_stats(stats, dist, device)
+
+
+def partition(owners: np.ndarray, world: int):
+    """Rank-major item order of a generation: (order, counts, offsets), items
+    of rank r = order[offsets[r]:offsets[r] + counts[r]], ascending."""
+    owners = np.asarray(owners, dtype=np.int64)
+    order = np.argsort(owners, kind="stable").astype(np.int64)
+    counts = np.bincount(owners, minlength=world).astype(np.int64)
+    offsets = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+    return order, counts, offsets
+
+
+def densify_partitioned(eng, seeds_xyz, dist, device: torch.device | None = None, tile_px: int = 64):
+    """dp_densify with every generation partitioned by reference-view super-tile
+    (dp_densify_owners: (ref, floor(v/tile), floor(u/tile)) hashed to a rank,
+    round robin when the largest share exceeds 1.1x the mean).  Each rank
+    refines its own items (dp_densify_refine_items), the candidates are
+    all-gathered in rank order, scattered back to sequence order and committed
+    by every rank (dp_densify_commit): the replicated store equals dp_densify's
+    bit for bit.  Host arrays: `eng` is an Engine or the oracle's
+    GenerationEngine (gloo tests on the CPU).  stats gains "partition": per
+    generation (items, largest share, fallback)."""
+    rank = dist.get_rank() if dist is not None else 0
+    world = dist.get_world_size() if dist is not None else 1
+    gen = eng.densify_begin(seeds_xyz)
+    parts = []
+    while gen.items > 0:
+        owners, fallback = eng.densify_owners(gen, world, tile_px)
+        order, counts, offsets = partition(owners, world)
+        mine = order[offsets[rank]: offsets[rank] + counts[rank]]
+        cand, acc = eng.densify_refine_items(gen, mine)
+        all_cand = allgather_array(cand, dist, device)
+        all_acc = allgather_array(acc, dist, device)
+        per = gen.per_item
+        pos = (order[:, None] * per + np.arange(per)[None, :]).ravel()
+        item_cand = np.empty_like(all_cand)
+        item_acc = np.empty_like(all_acc)
+        item_cand[pos] = all_cand
+        item_acc[pos] = all_acc
+        parts.append((int(gen.items), int(counts.max()), bool(fallback)))
+        gen = eng.densify_commit(gen, item_cand, item_acc)
+    patches, stats = eng.densify_result()
+    stats = _reduce_stats(stats, dist, device)
+    stats["partition"] = parts
+    return patches, stats
+
+
+def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64):
+    """densify_partitioned with the records in HBM: per generation the owners
+    (identical on every rank), this rank's item list to the device, one refine
+    launch over it (dp_densify_refine_items_device), ONE all_gather_into_tensor
+    per array of the padded shards (RCCL over xGMI on "nccl"), trim to the true
+    shard sizes, and one commit that scatters the gathered candidates back to
+    sequence order on the device (dp_densify_commit_items_device).  stats gains
+    "partition" (items, largest share, fallback) and "gathered_bytes" per
+    generation (81 B per candidate slot incl. padding)."""
+    rank = dist.get_rank() if dist is not None else 0
+    world = dist.get_world_size() if dist is not None else 1
+    rccl = dist is not None and dist.get_backend() == "nccl"
+    rec = PATCH_DTYPE.itemsize
+    stream = torch.cuda.current_stream(device)
+    gen = eng.densify_begin(seeds_xyz)
+    parts, gathered = [], []
+    while gen.items > 0:
+        per = gen.per_item
+        owners, fallback = eng.densify_owners(gen, world, tile_px)
+        order, counts, offsets = partition(owners, world)
+        sizes = [int(c) * per for c in counts]
+        cap = max(max(sizes), 1)
+        mine = torch.from_numpy(order[offsets[rank]: offsets[rank] + counts[rank]].copy()).to(device)
+        buf = torch.empty(cap * rec, dtype=torch.uint8, device=device)
+        acc = torch.zeros(cap, dtype=torch.uint8, device=device)
+        eng.densify_refine_items_device(gen, mine.data_ptr(), int(counts[rank]), buf.data_ptr(), acc.data_ptr(),
+                                        stream.cuda_stream)
+        if dist is None:
+            all_c, all_a = buf[: sizes[0] * rec], acc[: sizes[0]]
+        else:
+            if rccl:
+                gb = torch.empty(world * cap * rec, dtype=torch.uint8, device=device)
+                ga = torch.empty(world * cap, dtype=torch.uint8, device=device)
+                dist.all_gather_into_tensor(gb, buf)
+                dist.all_gather_into_tensor(ga, acc)
+            else:
+                gb = torch.empty(world * cap * rec, dtype=torch.uint8)
+                ga = torch.empty(world * cap, dtype=torch.uint8)
+                dist.all_gather_into_tensor(gb, buf.cpu())
+                dist.all_gather_into_tensor(ga, acc.cpu())
+                gb, ga = gb.to(device), ga.to(device)
+            all_c = torch.cat([gb[r * cap * rec: r * cap * rec + sizes[r] * rec] for r in range(world)])
+            all_a = torch.cat([ga[r * cap: r * cap + sizes[r]] for r in range(world)])
+        d_order = torch.from_numpy(order).to(device)
+        parts.append((int(gen.items), int(counts.max()), bool(fallback)))
+        gathered.append(world * cap * (rec + 1))
+        gen = eng.densify_commit_items_device(gen, all_c.data_ptr(), all_a.data_ptr(), d_order.data_ptr(),
+                                              len(order), stream.cuda_stream)
+        del buf, acc, all_c, all_a, mine, d_order
+    patches, stats = eng.densify_result()
+    stats = _reduce_stats(stats, dist, device)
+    stats["partition"] = parts
+    stats["gathered_bytes"] = gathered
+    return patches, stats
 
 
 def max_over_ranks(x: float, dist, device: torch.device | None = None) -> float:

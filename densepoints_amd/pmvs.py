@@ -399,6 +399,36 @@ class Engine:
                                                  ctypes.c_void_p(stream) if stream else None))
         return gen
 
+    # ---- partitioned generations (reference-view super-tiles) ----
+    def densify_owners(self, gen: N.DpGeneration, world: int, tile_px: int = 64):
+        """(owner rank per item, round-robin fallback flag) of the generation."""
+        own = np.zeros(gen.items, dtype=np.int32)
+        fb = ctypes.c_int32()
+        self._check(lib.dp_densify_owners(self._ctx, ctypes.byref(gen), world, tile_px, ptr(own), ctypes.byref(fb)))
+        return own, bool(fb.value)
+
+    def densify_refine_items(self, gen: N.DpGeneration, items: np.ndarray):
+        items = np.ascontiguousarray(items, dtype=np.int64)
+        n = len(items) * gen.per_item
+        cand = empty_patches(n)
+        acc = np.zeros(n, dtype=np.uint8)
+        self._check(lib.dp_densify_refine_items(self._ctx, ctypes.byref(gen), ptr(items), len(items), ptr(cand),
+                                                ptr(acc)))
+        return cand, acc
+
+    def densify_refine_items_device(self, gen: N.DpGeneration, d_items: int, n: int, d_cand: int, d_accept: int,
+                                    stream: int | None = None):
+        self._check(lib.dp_densify_refine_items_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_items), n,
+                                                       ctypes.c_void_p(d_cand), ctypes.c_void_p(d_accept),
+                                                       ctypes.c_void_p(stream) if stream else None))
+
+    def densify_commit_items_device(self, gen: N.DpGeneration, d_cand: int, d_accept: int, d_items: int, n: int,
+                                    stream: int | None = None) -> N.DpGeneration:
+        self._check(lib.dp_densify_commit_items_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_cand),
+                                                       ctypes.c_void_p(d_accept), ctypes.c_void_p(d_items), n,
+                                                       ctypes.c_void_p(stream) if stream else None))
+        return gen
+
     def densify_result(self):
         out = ctypes.c_void_p()
         n = ctypes.c_int64()

@@ -240,6 +240,26 @@ int dp_densify_refine_device(dp_ctx *ctx, const dp_generation *gen, int64_t item
                              dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream);
 int dp_densify_commit_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_cand,
                              const uint8_t *d_accept, int64_t n_cand, void *stream);
+/* Partitioned generations (north star: "reference-view grid cells shard across
+ * the 8 GPUs").  owner_out[i] (host, gen->items) = the rank that
+ * refines item i: the item's centre (seed patch or parent) projected into its
+ * reference view, super-tile (ref, floor(v/tile_px), floor(u/tile_px)) hashed to
+ * [0, world); if the largest share exceeds 1.1x the mean, round robin
+ * (i % world) instead and *fallback_out = 1.  Every rank computes the same
+ * owners from its replicated store.  Each rank then refines its own items
+ * (ascending) with dp_densify_refine_items[_device] -- candidates in list
+ * order -- the caller all-gathers them in rank order, and
+ * dp_densify_commit_items_device scatters the gathered candidates back to item
+ * order (d_items = the concatenated item lists, a permutation of the
+ * generation) and commits: the store equals dp_densify's bit for bit. */
+int dp_densify_owners(dp_ctx *ctx, const dp_generation *gen, int world, int tile_px, int32_t *owner_out,
+                      int32_t *fallback_out);
+int dp_densify_refine_items(dp_ctx *ctx, const dp_generation *gen, const int64_t *items, int64_t n,
+                            dp_patch *cand_out, uint8_t *accept_out);
+int dp_densify_refine_items_device(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
+                                   dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream);
+int dp_densify_commit_items_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_cand, const uint8_t *d_accept,
+                                   const int64_t *d_items, int64_t n_items, void *stream);
 
 /* ---- patch filter ----------------------------------------
  * PMVS::FilterPatches is declared (methods/pmvs/pmvs.h:27) but never defined

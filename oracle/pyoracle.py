@@ -296,6 +296,7 @@ class GenerationEngine:
         self.S = scene
         self.threads = threads
         self.org = None
+        self._P = scene._keep[0]
 
     def __del__(self):
         if self.org:
@@ -319,6 +320,49 @@ class GenerationEngine:
         parents = np.array(self.store[g.head + lo: g.head + hi], dtype=PATCH_DTYPE)
         kids, acc = self.S.expand(parents, self.threads)
         q = g.head + lo + np.repeat(np.arange(hi - lo), 4)
+        kids["parent"] = q.astype(np.uint32)
+        acc[q >= self.S.opt.max_pops] = 0  # past the pop cap (expand.cpp:95)
+        return kids, acc
+
+    # ---- partitioned generations (dp_densify_owners spec) ----
+    def densify_owners(self, g, world, tile_px=64):
+        """Owner rank per item: centre projected into the reference view (fp64,
+        ((p0 x + p1 y) + p2 z) + p3 then one division), super-tile hash, round
+        robin when the largest share exceeds 1.1x the mean."""
+        items = self.sp if g.index == 0 else np.array(self.store[g.head: g.head + g.items], dtype=PATCH_DTYPE)
+        P = np.stack([self._P[int(r)] for r in items["ref"]]) if len(items) else np.zeros((0, 12))
+        X = items["pos"].astype(np.float64)
+        h = [((P[:, 4 * k] * X[:, 0] + P[:, 4 * k + 1] * X[:, 1]) + P[:, 4 * k + 2] * X[:, 2]) + P[:, 4 * k + 3]
+             for k in range(3)]
+        u, w = h[0] / h[2], h[1] / h[2]
+
+        def tc(q):
+            q = q / float(tile_px)
+            ok = (q > -2.0e9) & (q < 2.0e9)
+            return np.where(ok, np.floor(np.where(ok, q, 0.0)), 0.0).astype(np.int64).astype(np.int32).view(np.uint32)
+
+        with np.errstate(over="ignore"):
+            ref = items["ref"].astype(np.uint32)
+            hh = (ref * np.uint32(73856093)) ^ (tc(w) * np.uint32(19349663)) ^ (tc(u) * np.uint32(83492791))
+            hh ^= hh >> np.uint32(16)
+            hh *= np.uint32(0x85EBCA6B)
+            hh ^= hh >> np.uint32(13)
+        own = (hh % np.uint32(world)).astype(np.int32)
+        cnt = np.bincount(own, minlength=world)
+        fb = len(own) > 0 and cnt.max() > 1.1 * len(own) / world
+        if fb:
+            own = (np.arange(len(own)) % world).astype(np.int32)
+        return own, bool(fb)
+
+    def densify_refine_items(self, g, items):
+        items = np.asarray(items, dtype=np.int64)
+        if g.index == 0:
+            r = self.sp[items].copy()
+            acc = self.S.refine(r, g.cell, 3, self.threads)  # MODE_SEED
+            return r, acc
+        parents = np.array([self.store[g.head + int(i)] for i in items], dtype=PATCH_DTYPE)
+        kids, acc = self.S.expand(parents, self.threads)
+        q = g.head + np.repeat(items, 4)
         kids["parent"] = q.astype(np.uint32)
         acc[q >= self.S.opt.max_pops] = 0  # past the pop cap (expand.cpp:95)
         return kids, acc

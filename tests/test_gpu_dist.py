@@ -78,7 +78,7 @@ def test_two_ranks_sharded_densify_equals_dp_densify(tmp_path):
         assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
 
 
-def _worker_dev(rank, world, port, out_path, backend):
+def _worker_dev(rank, world, port, out_path, backend, partitioned=False):
     import torch
     import torch.distributed as tdist
 
@@ -94,7 +94,10 @@ def _worker_dev(rank, world, port, out_path, backend):
     P, imgs, seeds = _scene("hf6")
     with dp.Engine(device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
-        got, st = D.densify_sharded_device(eng, seeds, group, torch.device("cuda", 0))
+        if partitioned:
+            got, st = D.densify_partitioned_device(eng, seeds, group, torch.device("cuda", 0))
+        else:
+            got, st = D.densify_sharded_device(eng, seeds, group, torch.device("cuda", 0))
     np.save(out_path + f".r{rank}.npy", got.view(np.uint8), allow_pickle=False)
     with open(out_path + f".r{rank}.evals", "w") as f:
         f.write(str(st["evals"]))
@@ -119,3 +122,48 @@ def test_device_resident_sharded_densify(tmp_path, backend, world):
         got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
         assert got.tobytes() == ref.tobytes(), f"rank {r}"
         assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
+
+
+@pytest.mark.parametrize("backend,world", [(None, 1), ("nccl", 1), ("gloo", 2), ("gloo", 3)])
+def test_partitioned_densify_device(tmp_path, backend, world):
+    """Reference-view super-tile partition of every generation
+    (dp_densify_owners -> dp_densify_refine_items_device -> all-gather ->
+    dp_densify_commit_items_device): every rank's store equals dp_densify."""
+    out = str(tmp_path / "dense")
+    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, True), nprocs=world, join=True)
+    P, imgs, seeds = _scene("hf6")
+    with dp.Engine(device=0) as eng:
+        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+        ref, rst = eng.densify(seeds)
+    for r in range(world):
+        got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
+        assert got.tobytes() == ref.tobytes(), f"rank {r}"
+        assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_owners_equal_oracle_and_host_path(orc, world):
+    """dp_densify_owners (device projection + hash) equals the oracle's numpy
+    statement generation by generation, and the host-array partitioned driver
+    equals dp_densify (with the pop cap)."""
+    P, imgs, seeds = _scene("wide70")
+    S = orc.Scene(P, imgs)
+    G = orc.GenerationEngine(S)
+    with dp.Engine(device=0) as eng:
+        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+        g = eng.densify_begin(seeds)
+        og = G.densify_begin(seeds)
+        gens = 0
+        while g.items > 0:
+            own, fb = eng.densify_owners(g, world)
+            oown, ofb = G.densify_owners(og, world)
+            assert fb == ofb and np.array_equal(own, oown), f"generation {gens}"
+            cand, acc = eng.densify_refine(g, 0, g.items)
+            g = eng.densify_commit(g, cand, acc)
+            oc, oa = G.densify_refine(og, 0, og.items)
+            og = G.densify_commit(og, oc, oa)
+            gens += 1
+        assert gens > 3
+        ref, _ = eng.densify(seeds)
+        got, st = D.densify_partitioned(eng, seeds, None)
+    assert got.tobytes() == ref.tobytes()
