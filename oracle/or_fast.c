@@ -426,11 +426,13 @@ static int fast_filter(const or_scene *s, or_patch *p, int cell, const or_fast_o
     p->evals += 1;
     if (fp.degenerate) p->flags |= OR_FLAG_DEGENERATE;
     if (fp.m < 2) {
+        /* only the anchor (or nothing) could be staged: it stays, unscored */
+        const int m = fp.m, v0 = m == 1 ? fp.fv[0].view : 0;
         p->score = -1.0f;
         fast_free(&fp);
         p->vis[0] = p->vis[1] = 0;
-        if (fp.m == 1) p->vis[fp.fv[0].view >> 6] |= 1ull << (fp.fv[0].view & 63);
-        return fp.m >= s->opt.min_visible;
+        if (m == 1) p->vis[v0 >> 6] |= 1ull << (v0 & 63);
+        return m >= s->opt.min_visible;
     }
     double sc[FAST_MAX_VIEWS];
     const double x[3] = {0.0, 0.0, 0.0};

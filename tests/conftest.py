@@ -25,6 +25,19 @@ def pytest_configure(config):
     _build_all()
 
 
+def pytest_sessionstart(session):
+    # on a GPU box, torch's bundled HIP runtime initialises the device before
+    # libdensepoints' contexts (tests that put views into torch tensors need
+    # it; bench.py uses the same order); a no-op without a GPU
+    try:
+        import torch
+
+        if torch.cuda.device_count() > 0:
+            torch.cuda.init()
+    except Exception:
+        pass
+
+
 @pytest.fixture(scope="session")
 def orc():
     from oracle import pyoracle
