@@ -898,6 +898,22 @@ __global__ __launch_bounds__(256) void gray_kernel(const PyrPlane *src, const Gr
     }
 }
 
+// 32-bit LDS reads at 2-byte alignment (unaligned DS access mode): out[k*64+l]
+// = the u32 at byte offset 2 (l + k) of an LDS array of u16 values i
+__global__ void lds_unaligned_probe_kernel(uint32_t *out)
+{
+    __shared__ uint16_t a[512];
+    for (int i = threadIdx.x; i < 512; i += 64)
+        a[i] = (uint16_t)(i * 3 + 1);
+    __syncthreads();
+    for (int k = 0; k < 4; ++k) {
+        const char *p = (const char *)a + 2 * (threadIdx.x + k);
+        uint32_t v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(uintptr_t)p));
+        out[k * 64 + threadIdx.x] = v;
+    }
+}
+
 __global__ void recip_probe_kernel(const float *x, int n, float *out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -906,6 +922,12 @@ __global__ void recip_probe_kernel(const float *x, int n, float *out)
 }
 
 } // namespace
+
+hipError_t launch_lds_probe(uint32_t *out)
+{
+    hipLaunchKernelGGL(lds_unaligned_probe_kernel, dim3(1), dim3(64), 0, 0, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_recip_probe(const float *x, int n, float *out)
 {
@@ -1181,4 +1203,18 @@ extern "C" int dp_fast_last_stats(dp_ctx *c, dp_fast_stats *out)
     out->view_evals = (int64_t)v[2];
     out->staged_bytes = (int64_t)v[3];
     return DP_OK;
+}
+
+extern "C" int dp_probe_lds_unaligned_device(uint32_t *out256)
+{
+    if (!out256)
+        return DP_E_ARG;
+    uint32_t *d = nullptr;
+    if (hipMalloc(&d, 256 * sizeof(uint32_t)) != hipSuccess)
+        return DP_E_OOM;
+    hipError_t e = dpk::launch_lds_probe(d);
+    if (e == hipSuccess)
+        e = hipMemcpy(out256, d, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    hipFree(d);
+    return e == hipSuccess ? DP_OK : DP_E_HIP;
 }
