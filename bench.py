@@ -55,6 +55,9 @@ def parse():
                     help="headline refine: parity (the reference's Nelder-Mead, bit-exact) or the performance "
                          "mode (LDS-staged fp16 gray tiles + fused CG, dp_fast_options)")
     ap.add_argument("--fast-cells", default="7,11", help="windows of the informational perf_mode sub-object")
+    ap.add_argument("--fast-budgets", default="", help="tile budgets (bytes) to sweep in perf_mode; default: the "
+                                                         "FastOptions default")
+    ap.add_argument("--fast-iters", type=int, default=None, help="performance-mode CG iterations (default: FastOptions)")
     ap.add_argument("--no-fast", action="store_true", help="skip the perf_mode sub-object")
     ap.add_argument("--seed-stride", type=float, default=32.0, help="synthetic seed grid stride (px)")
     return ap.parse_args()
@@ -123,6 +126,12 @@ def main():
     fast = args.mode == "fast"
     if fast:
         eng.set_options(dp.Options(expand_cell_size=args.cell))
+        fo = dp.FastOptions()
+        if args.fast_budgets:
+            fo.tile_budget = int(args.fast_budgets.split(",")[0])
+        if args.fast_iters is not None:
+            fo.iters = args.fast_iters
+        eng.set_fast_options(fo)
     expand_fn = eng.fast_expand_device if fast else eng.expand_device
 
     def step(ev=None):
@@ -355,7 +364,15 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
     B = 4 * NP
     res = {"parity_quality_n%d" % args.cell: quality(cfg, parity_out, parity_acc)}
     imgs = None
-    for cell in [int(c) for c in args.fast_cells.split(",") if c]:
+    budgets = [int(b) for b in args.fast_budgets.split(",") if b] or [None]
+    combos = [(int(c), b) for c in args.fast_cells.split(",") if c for b in budgets]
+    for cell, tb in combos:
+        fo = dp.FastOptions()
+        if tb:
+            fo.tile_budget = tb
+        if args.fast_iters is not None:
+            fo.iters = args.fast_iters
+        eng.set_fast_options(fo)
         eng.set_options(dp.Options(expand_cell_size=cell))
         eng.fast_expand_device(d_parents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
         torch.cuda.synchronize()
@@ -385,7 +402,8 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                           "frac": round(alg / kms / 1e6 / 8000.0, 4), "traffic": None,
                           "bytes_per_launch_algorithmic": alg, "bytes_per_launch_compulsory": comp,
                           "compulsory_GBps": round(comp / kms / 1e6, 2)},
-             "quality": quality(cfg, out, acc), "stats": {k: int(v) for k, v in st.items()}}
+             "quality": quality(cfg, out, acc), "stats": {k: int(v) for k, v in st.items()},
+             "fast_options": {k: getattr(fo, k) for k in ("iters", "margin", "tile_budget", "max_views")}}
         if not args.no_cpu:
             if imgs is None:
                 imgs = []
@@ -396,7 +414,7 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
             n = min(args.cpu_parents, len(parents))
             cores = args.cpu_threads or host_cores()
             t0 = time.perf_counter()
-            kids, kacc = S.fast_expand(parents[:n], None, cores)
+            kids, kacc = S.fast_expand(parents[:n], fo, cores)
             t = time.perf_counter() - t0
             g = out[: 4 * n]
             fields = ("pos", "normal", "ref", "vis", "cand", "score", "evals", "flags", "parent")
@@ -405,8 +423,9 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                                  "parity_bit_exact_on_sample": bool(all(kids[f].tobytes() == g[f].tobytes()
                                                                         for f in fields) and
                                                                     np.array_equal(kacc, acc[: 4 * n]))}
-        res["n%d" % cell] = r
+        res["n%d" % cell + ("_b%d" % tb if tb and len(budgets) > 1 else "")] = r
     eng.set_options(dp.Options(expand_cell_size=args.cell))
+    eng.set_fast_options(dp.FastOptions())
     return res
 
 

@@ -176,7 +176,7 @@ class DpFastOptions(ctypes.Structure):
 
 class DpFastStats(ctypes.Structure):
     _fields_ = [("patches", ctypes.c_int64), ("evals", ctypes.c_int64), ("view_evals", ctypes.c_int64),
-                ("staged_bytes", ctypes.c_int64)]
+                ("staged_bytes", ctypes.c_int64), ("clipped_stagings", ctypes.c_int64)]
 
 
 # dp_keypoint: the cv::KeyPoint fields the matcher reads

@@ -54,7 +54,7 @@ struct FastArgs {
 struct StageRec {
     float v[15];      // H0, Hd, He1, He2, Hn (folded, scaled, fp32)
     float umax, vmax; // 32 (tw - 1), 32 (th - 1)
-    uint32_t info;    // tile byte offset | (tw + 1) << 16
+    uint32_t info;    // tile byte offset | row bytes << 16
     int32_t view, x0t, y0t, tw, th;
     int32_t pad;
 };
@@ -222,36 +222,45 @@ __device__ __forceinline__ double rowdot(const double *P, const double *w)
     return (P[0] * w[0] + P[1] * w[1]) + P[2] * w[2];
 }
 
-// the lane's view geometry before the budget (or_fast.c view_geo)
+// the lane's view geometry before the budget (or_fast.c view_geo): only the
+// window box (the fp64 vectors are recomputed for the views that are kept, so
+// they are not live across the budget loop)
 struct Geo {
-    double g[5][3];
     int xa, xb, ya, yb;
     bool ok;
 };
+
+// vector i of the view (H0, Hd, He1, He2, Hn: P applied to the frame vectors),
+// in 1/32 px for rows 0-1, divided by the centre's depth H0[2] (times inv)
+__device__ __forceinline__ void geo_vec(const dpg::ViewDev &v, const Frame &F, int i, double inv, double *g)
+{
+    const double *w = i == 0 ? F.X0 : i == 1 ? F.r : i == 2 ? F.e1 : i == 3 ? F.e2 : F.nn;
+    double H[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        H[k] = i == 0 ? rowdot(v.P + 4 * k, w) + v.P[4 * k + 3] : rowdot(v.P + 4 * k, w);
+    g[0] = (32.0 * H[0]) * inv;
+    g[1] = (32.0 * H[1]) * inv;
+    g[2] = H[2] * inv;
+}
+
+__device__ __forceinline__ double geo_inv(const dpg::ViewDev &v, const Frame &F)
+{
+    return 1.0 / (rowdot(v.P + 8, F.X0) + v.P[11]);
+}
 
 __device__ Geo view_geo(const dpg::ViewDev &v, const Frame &F, int cell)
 {
     Geo G;
     G.ok = false;
-    const double *w[5] = {F.X0, F.r, F.e1, F.e2, F.nn};
-    double H[5][3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const double *Pr = v.P + 4 * k;
-        H[0][k] = rowdot(Pr, w[0]) + Pr[3];
-#pragma unroll
-        for (int i = 1; i < 5; ++i)
-            H[i][k] = rowdot(Pr, w[i]);
-    }
-    const double s = H[0][2];
+    const double s = rowdot(v.P + 8, F.X0) + v.P[11];
     if (!(s > 0.0))
         return G;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        G.g[i][0] = (32.0 * H[i][0]) / s;
-        G.g[i][1] = (32.0 * H[i][1]) / s;
-        G.g[i][2] = H[i][2] / s;
-    }
+    const double inv = 1.0 / s;
+    double g0[3], g2[3], g3[3];
+    geo_vec(v, F, 0, inv, g0);
+    geo_vec(v, F, 2, inv, g2);
+    geo_vec(v, F, 3, inv, g3);
     const double c = 0.5 * (double)(cell - 1);
     double umin = 0, umax = 0, vmin = 0, vmax = 0;
 #pragma unroll
@@ -260,7 +269,7 @@ __device__ Geo view_geo(const dpg::ViewDev &v, const Frame &F, int cell)
         double h[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k)
-            h[k] = (G.g[0][k] + ti * G.g[2][k]) + tj * G.g[3][k];
+            h[k] = (g0[k] + ti * g2[k]) + tj * g3[k];
         if (!(h[2] > 0.0))
             return G;
         const double u = h[0] / h[2], ww = h[1] / h[2];
@@ -291,7 +300,7 @@ __device__ __forceinline__ Rect tile_rect(const Geo &g, int W, int H, int M)
 {
     Rect t;
     int x0 = g.xa - M, x1 = g.xb + M, y0 = g.ya - M, y1 = g.yb + M;
-    x0 = x0 < 0 ? 0 : x0;
+    x0 = x0 < 0 ? 0 : x0 & ~1; // even: rows are copied as 32-bit fp16 pairs
     y0 = y0 < 0 ? 0 : y0;
     x1 = x1 > W - 1 ? W - 1 : x1;
     y1 = y1 > H - 1 ? H - 1 : y1;
@@ -299,7 +308,8 @@ __device__ __forceinline__ Rect tile_rect(const Geo &g, int W, int H, int M)
     t.y0 = y0;
     t.tw = x1 - x0 + 1;
     t.th = y1 - y0 + 1;
-    t.bytes = (2 * (t.tw + 1) * t.th + 3) & ~3;
+    // (tw + 1) columns (right tap) as words of two pixels, th + 1 rows (lower tap)
+    t.bytes = 4 * ((t.tw + 2) / 2) * (t.th + 1);
     return t;
 }
 
@@ -314,7 +324,8 @@ struct Staged {
 // Stage the wave's patch: frame, usable views, margin, tiles into LDS.
 // Returns m (uniform); the lane of rank r holds that view's vectors in S.
 template <int kBudget>
-__device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged &S, unsigned long long &staged_bytes)
+__device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged &S, unsigned long long &staged_bytes,
+                     unsigned long long &clipped)
 {
     const int lane = lane_id();
     const int cell = a.cell;
@@ -353,21 +364,25 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     const int incl = wave_incl_i32(staged ? t.bytes : 0);
     const bool keep = staged && incl <= a.fo.tile_budget;
     const int m = __popcll(__ballot(keep));
-    // fp16 texels the tile reads from the gray plane: (tw + 1) x (th + 1)
-    staged_bytes += (unsigned long long)uni(wave_sum_i32(keep ? 2 * (t.tw + 1) * (t.th + 1) : 0));
+    clipped += (M < margin || m < __popcll(__ballot(staged))) ? 1ull : 0ull;
+    // bytes the tiles copy from the gray planes (whole 32-bit pixel pairs)
+    staged_bytes += (unsigned long long)uni(wave_sum_i32(keep ? t.bytes : 0));
     if (keep) {
         StageRec &R = L.u.st[rank];
+        const double inv = geo_inv(vw, L.F);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            const double ga = g.g[i][0] - (32.0 * (double)t.x0) * g.g[i][2];
-            const double gb = g.g[i][1] - (32.0 * (double)t.y0) * g.g[i][2];
+            double gv[3];
+            geo_vec(vw, L.F, i, inv, gv);
+            const double ga = gv[0] - (32.0 * (double)t.x0) * gv[2];
+            const double gb = gv[1] - (32.0 * (double)t.y0) * gv[2];
             R.v[3 * i] = (float)ga;
             R.v[3 * i + 1] = (float)gb;
-            R.v[3 * i + 2] = (float)g.g[i][2];
+            R.v[3 * i + 2] = (float)gv[2];
         }
         R.umax = (float)(32 * (t.tw - 1));
         R.vmax = (float)(32 * (t.th - 1));
-        R.info = (uint32_t)(incl - t.bytes) | ((uint32_t)(t.tw + 1) << 16);
+        R.info = (uint32_t)(incl - t.bytes) | ((uint32_t)(4 * ((t.tw + 2) / 2)) << 16);
         R.view = view;
         R.x0t = t.x0;
         R.y0t = t.y0;
@@ -385,29 +400,34 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
         S.info = R.info;
         S.view = R.view;
     }
-    // tiles: entry (x, y) = g(x0t + x, y0t + y) | g(x0t + x, y0t + y + 1) << 8,
-    // x in [0, tw], y in [0, th); R = 64 / (tw + 1) rows per wave step
+    // tiles: rows y0t .. y0t + th (clamped to the image) of biased-fp16 gray,
+    // columns x0t .. x0t + 2 W2 - 1 (the plane's padding columns replicate
+    // the last pixel), copied straight into LDS by global_load_lds_dword: the
+    // tiles are one contiguous LDS range in rank order, so lane l of a copy
+    // instruction moves word 64 i + l of its view.  All copies are issued
+    // before a single wait.
+    typedef __attribute__((address_space(3))) void *lds_ptr_t;
+    typedef __attribute__((address_space(1))) const void *gptr_t;
+    const uint32_t tbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)L.tiles;
     for (int r = 0; r < m; ++r) {
         const int vv = uni(L.u.st[r].view), x0t = uni(L.u.st[r].x0t), y0t = uni(L.u.st[r].y0t);
         const int tw = uni(L.u.st[r].tw), th = uni(L.u.st[r].th);
         const uint32_t off = (uint32_t)uni((int)(L.u.st[r].info & 0xffffu));
         const GrayPlane gp = a.gray[vv];
-        const int cols = tw + 1;
-        const int R = 64 / cols;
-        const int rr = (int)(((float)lane + 0.5f) * (1.0f / (float)cols));
-        const int x = lane - rr * cols;
-        const int X = x0t + x < gp.w - 1 ? x0t + x : gp.w - 1;
-        if (rr < R) {
-            for (int y = rr; y < th; y += R) {
-                const int Y0 = y0t + y < gp.h - 1 ? y0t + y : gp.h - 1;
-                const int Y1 = y0t + y + 1 < gp.h - 1 ? y0t + y + 1 : gp.h - 1;
-                const int p0 = (int)__half2float(gp.p[(size_t)Y0 * gp.pitch + X]);
-                const int p1 = (int)__half2float(gp.p[(size_t)Y1 * gp.pitch + X]);
-                uint16_t *dst = (uint16_t *)((char *)L.tiles + off) + (y * cols + x);
-                *dst = (uint16_t)(p0 | (p1 << 8));
-            }
+        const int W2 = (tw + 2) / 2;
+        const int nw = W2 * (th + 1);
+        const float inv = 1.0f / (float)W2;
+        for (int i = 0; i < nw; i += 64) {
+            const int d = i + lane;
+            const int y = (int)(((float)d + 0.5f) * inv);
+            const int c = d - y * W2;
+            const int Y = y0t + y < gp.h - 1 ? y0t + y : gp.h - 1;
+            const __half *src = gp.p + (size_t)Y * gp.pitch + x0t + 2 * c;
+            if (d < nw)
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)(uintptr_t)(tbase + off + 4u * (uint32_t)i), 4, 0, 0);
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
     return m;
 }
@@ -452,19 +472,22 @@ __device__ __forceinline__ uint32_t sample(const char *tiles, const float4 &qa,
     const uint32_t iu = __float_as_uint(U + 8388608.0f) - 0x4B000000u;
     const uint32_t iv = __float_as_uint(V + 8388608.0f) - 0x4B000000u;
     const uint32_t info = __float_as_uint(qc.w);
-    const uint32_t cols = info >> 16;
+    const uint32_t rowb = info >> 16;
     const uint32_t x0 = iu >> 5, fx = iu & 31u, y0 = iv >> 5, fy = iv & 31u;
-    const uint32_t addr = (info & 0xffffu) + ((__umul24(y0, cols) + x0) << 1);
-    const uint16_t *tp = (const uint16_t *)(tiles + addr);
-    const uint32_t e0 = tp[0], e1 = tp[1];
+    const uint32_t addr = (info & 0xffffu) + __umul24(y0, rowb) + (x0 << 1);
+    // (p(x0), p(x0+1)) of rows y0 and y0 + 1 as u16 pairs: 32-bit LDS reads at
+    // 2-byte alignment (the unaligned DS mode, probed on the device); each
+    // value is 0x6400 + gray (fp16 of 1024 + gray)
+    const uint32_t r0 = *(const uint32_t *)(tiles + addr);
+    const uint32_t r1 = *(const uint32_t *)(tiles + addr + rowb);
     const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
     const uint32_t w0 = __umul24(wx, 32u - fy), w1 = __umul24(wx, fy);
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const uint32_t r0 = perm(e1, e0, 0x0c040c00u); // p00 | p01 << 16
-    const uint32_t r1 = perm(e1, e0, 0x0c050c01u); // p10 | p11 << 16
+    // sum w (0x6400 + p) + 32 = sum w p + 32 + 0x6400 * 1024 (weights sum to 1024)
     const uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r0), __builtin_bit_cast(us2, w0),
                                               __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r1),
-                                                                     __builtin_bit_cast(us2, w1), 32u, false),
+                                                                     __builtin_bit_cast(us2, w1),
+                                                                     32u - 0x6400u * 1024u, false),
                                               false);
     return b >> 6;
 }
@@ -701,12 +724,19 @@ __device__ void child_position(const FastArgs &a, const dp_patch &par, int dir, 
     }
 }
 
-template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void fast_kernel(FastArgs a)
+// occupancy the LDS arena allows (1-wave workgroups, 160 KiB per CU): 16 KiB
+// tiles -> 2 waves/SIMD, 8 KiB -> 3, 6 KiB -> 4; the register budget follows
+template <int kBudget> struct FastOcc {
+    static constexpr int value = kBudget <= 6144 ? 4 : kBudget <= 8192 ? 3 : 2;
+};
+
+template <int G, int kBudget, int kMode>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBudget>::value))) void fast_kernel(FastArgs a)
 {
     __shared__ FastLds<kBudget> L;
     const int lane = lane_id();
     const Slots sl = make_slots<G>(a.cell);
-    unsigned long long wave_evals = 0, wave_vev = 0, wave_bytes = 0, wave_patches = 0;
+    unsigned long long wave_evals = 0, wave_vev = 0, wave_bytes = 0, wave_patches = 0, wave_clip = 0;
     dp_patch &p = L.p;
     for (;;) {
         uint32_t idx = 0;
@@ -752,7 +782,7 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
             if (kMode == DP_MODE_FAST_EVAL) {
                 Staged S;
                 const bool degen = L.F.degenerate;
-                const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes);
+                const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes, wave_clip);
                 p.evals += 1;
                 if (degen)
                     p.flags |= DP_PATCH_DEGENERATE;
@@ -775,7 +805,7 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
                     rejected = true;
                 } else {
                     Staged S;
-                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S, wave_bytes);
+                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S, wave_bytes, wave_clip);
                     if (m >= 2) {
                         const int E = cg_refine<G>(a, L, S, sl, m);
                         p.evals += (uint32_t)E;
@@ -810,7 +840,7 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
                     wave_sync();
                     Staged S;
                     const bool degen = L.F.degenerate;
-                    const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes);
+                    const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes, wave_clip);
                     p.evals += 1;
                     if (degen)
                         p.flags |= DP_PATCH_DEGENERATE;
@@ -874,32 +904,34 @@ template <int G, int kBudget, int kMode> __global__ __launch_bounds__(64) void f
         atomicAdd(a.stats + 1, wave_evals);
         atomicAdd(a.stats + 2, wave_vev);
         atomicAdd(a.stats + 3, wave_bytes);
+        atomicAdd(a.stats + 4, wave_clip);
     }
 }
 
-// BGRA8 -> fp16 gray (BGR2GRAY 14-bit fixed point, exact integers in fp16)
+// BGRA8 -> biased fp16 gray: fp16(1024 + BGR2GRAY) (14-bit fixed point), whose
+// bits are 0x6400 | gray; the padding columns [w, pitch) replicate column w-1
 __global__ __launch_bounds__(256) void gray_kernel(const PyrPlane *src, const GrayPlane *dst)
 {
     const PyrPlane s = src[blockIdx.z];
     const GrayPlane d = dst[blockIdx.z];
     const int y = blockIdx.y;
     const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    if (y >= s.h || x0 >= s.w)
+    if (y >= s.h || x0 >= d.pitch)
         return;
     const uint32_t *row = s.img + (size_t)y * s.pitch;
-    __half *out = (__half *)d.p + (size_t)y * d.pitch;
+    uint16_t *out = (uint16_t *)d.p + (size_t)y * d.pitch;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        if (x0 + k < s.w) {
-            const uint32_t px = row[x0 + k];
-            const uint32_t g = (1868u * (px & 255u) + 9617u * ((px >> 8) & 255u) + 4899u * ((px >> 16) & 255u) + 8192u) >> 14;
-            out[x0 + k] = __float2half((float)g);
+        const int x = x0 + k;
+        if (x < d.pitch) {
+            const uint32_t px = row[x < s.w ? x : s.w - 1];
+            const uint32_t g =
+                (1868u * (px & 255u) + 9617u * ((px >> 8) & 255u) + 4899u * ((px >> 16) & 255u) + 8192u) >> 14;
+            out[x] = (uint16_t)(0x6400u | g);
         }
     }
 }
 
-// 32-bit LDS reads at 2-byte alignment (unaligned DS access mode): out[k*64+l]
-// = the u32 at byte offset 2 (l + k) of an LDS array of u16 values i
 __global__ void lds_unaligned_probe_kernel(uint32_t *out)
 {
     __shared__ uint16_t a[512];
@@ -961,6 +993,10 @@ namespace {
 
 constexpr int kFastBudget = 16384; // the kernel's tile arena (dp_fast_options.tile_budget max)
 
+// gray plane pitch (pixels): a tile row may read two pixels past the image
+// edge (a whole 32-bit pair after the right tap), 128-B aligned rows
+inline int gray_pitch(int W) { return (W + 2 + 63) & ~63; }
+
 int fast_check_options(dp_ctx *c, const dp_fast_options &f)
 {
     if (f.iters < 0 || f.iters > 64 || f.margin < 0 || f.margin > dpk::kFastMaxMargin || f.tile_budget < 64 ||
@@ -981,7 +1017,7 @@ int ensure_gray(dp_ctx *c)
     size_t total = 0;
     std::vector<size_t> off(c->V);
     for (int v = 0; v < c->V; ++v) {
-        const int pitch = (c->hv[v].W + 63) & ~63;
+        const int pitch = gray_pitch(c->hv[v].W);
         off[v] = total;
         total += (size_t)pitch * (size_t)c->hv[v].H;
         gp[v].w = c->hv[v].W;
@@ -1014,7 +1050,7 @@ int ensure_gray(dp_ctx *c)
     DP_HIP(c, hipMalloc(&d_src, sizeof(dpk::PyrPlane) * c->V));
     DP_HIP(c, hipMemcpy(c->d_gray, gp.data(), sizeof(dpk::GrayPlane) * c->V, hipMemcpyHostToDevice));
     DP_HIP(c, hipMemcpy(d_src, src.data(), sizeof(dpk::PyrPlane) * c->V, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(dpk::gray_kernel, dim3((mw + 1023) / 1024, mh, c->V), dim3(256), 0, c->stream, d_src,
+    hipLaunchKernelGGL(dpk::gray_kernel, dim3((gray_pitch(mw) + 1023) / 1024, mh, c->V), dim3(256), 0, c->stream, d_src,
                        (const dpk::GrayPlane *)c->d_gray);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess)
@@ -1050,19 +1086,23 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.evals = c->d_evals;
     a.parents = d_parents;
     if (!c->d_fstats)
-        DP_HIP(c, hipMalloc(&c->d_fstats, 4 * sizeof(unsigned long long)));
+        DP_HIP(c, hipMalloc(&c->d_fstats, 8 * sizeof(unsigned long long)));
     a.stats = c->d_fstats;
-    DP_HIP(c, hipMemsetAsync(c->d_fstats, 0, 4 * sizeof(unsigned long long), s));
+    DP_HIP(c, hipMemsetAsync(c->d_fstats, 0, 8 * sizeof(unsigned long long), s));
     DP_HIP(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), s));
     DP_HIP(c, hipEventRecord(c->e0, s));
     const int N = cell * cell;
+    const int tb = c->fopt.tile_budget;
     hipError_t e;
-    if (N <= 64)
-        e = dpk::launch_fast_t<4, kFastBudget>(a, s);
-    else if (N <= 128)
-        e = dpk::launch_fast_t<2, kFastBudget>(a, s);
+#define DP_FAST_ARENA(B)                                                                                      \
+    (N <= 64 ? dpk::launch_fast_t<4, B>(a, s) : N <= 128 ? dpk::launch_fast_t<2, B>(a, s) : dpk::launch_fast_t<1, B>(a, s))
+    if (tb <= 6144)
+        e = DP_FAST_ARENA(6144);
+    else if (tb <= 8192)
+        e = DP_FAST_ARENA(8192);
     else
-        e = dpk::launch_fast_t<1, kFastBudget>(a, s);
+        e = DP_FAST_ARENA(kFastBudget);
+#undef DP_FAST_ARENA
     DP_HIP(c, e);
     DP_HIP(c, hipEventRecord(c->e1, s));
     c->timed = true;
@@ -1111,10 +1151,10 @@ extern "C" int dp_read_gray(dp_ctx *c, int view, uint16_t *out)
     int rc = ensure_gray(c);
     if (rc != DP_OK)
         return rc;
-    const int W = c->hv[view].W, H = c->hv[view].H, pitch = (W + 63) & ~63;
+    const int W = c->hv[view].W, H = c->hv[view].H, pitch = gray_pitch(W);
     size_t off = 0;
     for (int v = 0; v < view; ++v)
-        off += (size_t)((c->hv[v].W + 63) & ~63) * (size_t)c->hv[v].H;
+        off += (size_t)gray_pitch(c->hv[v].W) * (size_t)c->hv[v].H;
     DP_HIP(c, hipMemcpy2D(out, (size_t)W * 2, (const __half *)c->gray_pool + off, (size_t)pitch * 2, (size_t)W * 2,
                           (size_t)H, hipMemcpyDeviceToHost));
     return DP_OK;
@@ -1195,9 +1235,10 @@ extern "C" int dp_fast_last_stats(dp_ctx *c, dp_fast_stats *out)
     *out = dp_fast_stats{};
     if (!c->d_fstats)
         return DP_OK;
-    unsigned long long v[4];
+    unsigned long long v[5];
     DP_HIP(c, hipDeviceSynchronize());
     DP_HIP(c, hipMemcpy(v, c->d_fstats, sizeof(v), hipMemcpyDeviceToHost));
+    out->clipped_stagings = (int64_t)v[4];
     out->patches = (int64_t)v[0];
     out->evals = (int64_t)v[1];
     out->view_evals = (int64_t)v[2];

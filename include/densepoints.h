@@ -379,16 +379,19 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  * 36-60, 0.1 denominator floor).  The full arithmetic is oracle/or_fast.c;
  * in short, per patch:
  *  - gray planes: BGR2GRAY of the current level (the 14-bit fixed point of the
- *    parity path) stored as fp16, one plane per view (dp_build_gray);
+ *    parity path) stored as fp16 (biased by 1024), one SoA plane per view
+ *    (dp_build_gray);
  *  - frame: e1 = the reference camera's x-axis projected onto the patch plane,
  *    e2 = n x e1, sample spacing one reference pixel (1/dx); pose (d, a, b):
  *    X = X0 + d (X0 - C_ref), plane normal n + a e1 + b e2, in scaled units
  *    d = x0 / (dx |X0 - C_ref|), a = x1 * 2/(n-1), b = x2 * 2/(n-1);
  *  - staging: per visible view (ascending, at most max_views) whose initial
  *    window corners project inside the image, a tile = the window's pixel
- *    bounding box + `margin` px (reduced until all tiles fit tile_budget bytes,
- *    then the longest fitting prefix of views), held in LDS for the whole
- *    refine; samples clamp to the tile (BORDER_REPLICATE);
+ *    bounding box + `margin` px (left edge even; footprint 4 ceil((tw+1)/2)
+ *    (th+1) bytes; the margin is reduced until all tiles fit tile_budget
+ *    bytes, then the longest fitting prefix of views is kept), copied once
+ *    into LDS and used for the whole refine; samples clamp to the tile
+ *    (BORDER_REPLICATE);
  *  - sample: projective map in fp32 (fmaf), 1/32 px, bilinear on 8-bit gray,
  *    result in 1/16 gray levels; exact integer moments; fp64 NCC finish;
  *  - refine: `iters` Polak-Ribiere+ conjugate-gradient steps with a forward-
@@ -415,7 +418,9 @@ int dp_set_fast_options(dp_ctx *ctx, const dp_fast_options *fo);
 /* fp16 gray planes of the current level for every view (built on demand by
  * the first fast call; explicit here so callers can time it). */
 int dp_build_gray(dp_ctx *ctx);
-/* host copy (width*height fp16 bits) of view `view`'s gray plane */
+/* host copy (width*height fp16 values) of view `view`'s gray plane; the
+ * planes hold 1024 + gray (biased fp16: the bits are 0x6400 | gray, so the
+ * sampler reads integer taps without a conversion) */
 int dp_read_gray(dp_ctx *ctx, int view, uint16_t *fp16_out);
 /* Expand::ExpandPatch children (as dp_expand_batch) refined in performance
  * mode: DP_MODE_FAST_REFINE on the parent's visible set, cell =
@@ -424,13 +429,15 @@ int dp_fast_expand_batch(dp_ctx *ctx, const dp_patch *parents, int n, dp_patch *
 /* Work counters of the most recent performance-mode launch (device-counted):
  * view_evals = sum over patches and evaluations of the staged views sampled,
  * i.e. algorithmic bytes = view_evals * (n+1)^2 * 2 (fp16 texels);
- * staged_bytes = fp16 bytes the tiles read from the gray planes (the
- * compulsory HBM traffic of the windows). */
+ * staged_bytes = bytes the tiles copy from the gray planes (the compulsory
+ * HBM traffic of the windows). */
 typedef struct dp_fast_stats {
     int64_t patches;
     int64_t evals;
     int64_t view_evals;
     int64_t staged_bytes;
+    int64_t clipped_stagings; /* stagings whose tiles did not fit tile_budget at the
+                                 full margin (margin reduced or views dropped) */
 } dp_fast_stats;
 int dp_fast_last_stats(dp_ctx *ctx, dp_fast_stats *out);
 int dp_fast_expand_batch_device(dp_ctx *ctx, const dp_patch *d_parents, int n, dp_patch *d_children,

@@ -77,7 +77,7 @@ int or_gray_plane(const or_scene *s, int view, uint8_t *out)
 typedef struct fast_view {
     int view;
     int x0t, y0t, tw, th;  /* tile origin and size (pixels)           */
-    int bytes;             /* 2 * (tw + 1) * th rounded up to 4        */
+    int bytes;             /* LDS footprint: 4 ceil((tw+1)/2) (th+1)   */
     float vec[5][3];       /* H0, Hd, He1, He2, Hn (folded, scaled)    */
     float umax, vmax;      /* 32 * (tw - 1), 32 * (th - 1)             */
     uint16_t *tile;        /* (tw + 1) x th entries: p[y][x] | p[y+1][x] << 8 */
@@ -119,10 +119,11 @@ static int view_geo(const or_view *v, const fast_patch *fp, int cell, fast_geo *
     }
     const double s = H[0][2];
     if (!(s > 0.0)) return 0;
+    const double inv = 1.0 / s; /* one reciprocal of the centre's depth */
     for (int i = 0; i < 5; ++i) {
-        g->vec[i][0] = (32.0 * H[i][0]) / s;
-        g->vec[i][1] = (32.0 * H[i][1]) / s;
-        g->vec[i][2] = H[i][2] / s;
+        g->vec[i][0] = (32.0 * H[i][0]) * inv;
+        g->vec[i][1] = (32.0 * H[i][1]) * inv;
+        g->vec[i][2] = H[i][2] * inv;
     }
     /* initial window corners (x = 0): tau in {-c, +c} */
     const double c = 0.5 * (double)(cell - 1);
@@ -149,10 +150,14 @@ static int view_geo(const or_view *v, const fast_patch *fp, int cell, fast_geo *
     return 1;
 }
 
+/* tile rectangle: the window's pixel box grown by M, clipped to the image,
+ * left edge rounded down to an even column (the device copies the rows as
+ * 32-bit words of two fp16 pixels); the footprint counts tw + 1 columns
+ * (right tap) and th + 1 rows (lower tap) */
 static void tile_rect(const or_view *v, const fast_geo *g, int M, fast_view *t)
 {
     int x0 = g->xa - M, x1 = g->xb + M, y0 = g->ya - M, y1 = g->yb + M;
-    x0 = x0 < 0 ? 0 : x0;
+    x0 = x0 < 0 ? 0 : x0 & ~1;
     y0 = y0 < 0 ? 0 : y0;
     x1 = x1 > v->W - 1 ? v->W - 1 : x1;
     y1 = y1 > v->H - 1 ? v->H - 1 : y1;
@@ -160,7 +165,7 @@ static void tile_rect(const or_view *v, const fast_geo *g, int M, fast_view *t)
     t->y0t = y0;
     t->tw = x1 - x0 + 1;
     t->th = y1 - y0 + 1;
-    t->bytes = (2 * (t->tw + 1) * t->th + 3) & ~3;
+    t->bytes = 4 * ((t->tw + 2) / 2) * (t->th + 1);
 }
 
 /*

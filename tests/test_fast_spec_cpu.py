@@ -73,7 +73,8 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
         s = H[0][2]
         if not s > 0:
             continue
-        g = [np.array([32.0 * h[0] / s, 32.0 * h[1] / s, h[2] / s]) for h in H]
+        inv = 1.0 / s
+        g = [np.array([(32.0 * h[0]) * inv, (32.0 * h[1]) * inv, h[2] * inv]) for h in H]
         us, ws, ok = [], [], True
         for ti in (-c, c):
             for tj in (-c, c):
@@ -96,9 +97,9 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
         if xb - xa + 1 > 48 or yb - ya + 1 > 48:
             continue
         Hh, Ww = imgs[v].shape[:2]
-        x0, y0 = max(xa, 0), max(ya, 0)
+        x0, y0 = max(xa, 0) & ~1, max(ya, 0)  # even left edge (32-bit fp16 pairs on the device)
         tw, th = min(xb, Ww - 1) - x0 + 1, min(yb, Hh - 1) - y0 + 1
-        staged.append((v, g, x0, y0, tw, th, (2 * (tw + 1) * th + 3) & ~3))
+        staged.append((v, g, x0, y0, tw, th, 4 * ((tw + 2) // 2) * (th + 1)))
         if len(staged) == fo.max_views:
             break
     tot, keep = 0, []
