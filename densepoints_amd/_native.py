@@ -193,6 +193,7 @@ _D = ctypes.c_double
 SIGNATURES = [
     ("dp_default_options", None, [_P]),
     ("dp_abi_version", _I, []),
+    ("dp_device_count", _I, []),
     ("dp_ctx_create", _I, [_P, _I, _P]),
     ("dp_ctx_destroy", _I, [_P]),
     ("dp_last_error", ctypes.c_char_p, [_P]),

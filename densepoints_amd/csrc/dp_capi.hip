@@ -151,6 +151,12 @@ static int check_options(dp_ctx *c, const dp_options &o)
     return DP_OK;
 }
 
+extern "C" int dp_device_count(void)
+{
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 extern "C" int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out)
 {
     if (!out)

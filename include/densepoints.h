@@ -119,6 +119,8 @@ typedef struct dp_ctx dp_ctx;
 /* defaults identical to the reference constructors (list in dp_options) */
 void dp_default_options(dp_options *opt);
 int dp_abi_version(void);
+/* number of HIP devices visible to the process (0 if none) */
+int dp_device_count(void);
 
 /* Create a context bound to HIP device `device`. */
 int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out);

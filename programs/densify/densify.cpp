@@ -22,7 +22,9 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <algorithm>
 #include <sys/stat.h>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -33,6 +35,8 @@ void usage()
                  "usage: densify -i scene.json [--seeds seeds.xyz] [-s settings.json] [-o points.ply]\n"
                  "               [--device N] [--max-pops N] [--level L] [--filter] [--check-only]\n"
                  "               [--features N] [--fast-threshold T] [--epipolar-matching]\n"
+                 "               [--gpus N]   (one context per GPU, generations partitioned by\n"
+                 "                             reference-view super-tile; output identical to 1 GPU)\n"
                  "       densify --synthetic V,W,H,KIND --write-scene DIR\n");
 }
 
@@ -123,12 +127,98 @@ int write_synthetic(const std::string &spec, const std::string &dir)
     return 0;
 }
 
+// dp_densify over `ctxs.size()` contexts (one per GPU): every generation's
+// items are partitioned by reference-view super-tile (dp_densify_owners), each
+// context refines its own items in its own host thread, the candidates are
+// gathered in host memory (one process: shared memory is the all-gather) and
+// put back in item order, and every context commits the whole generation to
+// its replicated organizer -- the store equals dp_densify's bit for bit.
+// Returns the stats of context 0 (evals / refine_ms summed / maxed).
+int densify_multi(std::vector<dp_ctx *> &ctxs, const std::vector<double> &seeds, std::vector<dp_patch> &out,
+                  dp_densify_stats &st, std::string &err)
+{
+    const int G = (int)ctxs.size();
+    const int n = (int)(seeds.size() / 3);
+    std::vector<dp_generation> gen((size_t)G);
+    std::vector<int> rcs((size_t)G, DP_OK);
+    auto all = [&](auto f) {
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; ++g)
+            th.emplace_back([&, g]() { rcs[(size_t)g] = f(g); });
+        for (auto &t : th)
+            t.join();
+        for (int g = 0; g < G; ++g)
+            if (rcs[(size_t)g] != DP_OK) {
+                err = dp_last_error(ctxs[(size_t)g]);
+                return rcs[(size_t)g];
+            }
+        return DP_OK;
+    };
+    int rc = all([&](int g) { return dp_densify_begin(ctxs[(size_t)g], seeds.data(), n, &gen[(size_t)g]); });
+    if (rc != DP_OK)
+        return rc;
+    while (gen[0].items > 0) {
+        const int64_t items = gen[0].items;
+        const int per = gen[0].per_item;
+        std::vector<int32_t> owner((size_t)items);
+        int32_t fallback = 0;
+        if ((rc = dp_densify_owners(ctxs[0], &gen[0], G, 64, owner.data(), &fallback)) != DP_OK) {
+            err = dp_last_error(ctxs[0]);
+            return rc;
+        }
+        std::vector<std::vector<int64_t>> mine((size_t)G);
+        for (int64_t i = 0; i < items; ++i)
+            mine[(size_t)owner[(size_t)i]].push_back(i);
+        std::vector<std::vector<dp_patch>> cand((size_t)G);
+        std::vector<std::vector<uint8_t>> acc((size_t)G);
+        rc = all([&](int g) {
+            const size_t k = mine[(size_t)g].size() * (size_t)per;
+            cand[(size_t)g].resize(k);
+            acc[(size_t)g].resize(k);
+            return dp_densify_refine_items(ctxs[(size_t)g], &gen[(size_t)g], mine[(size_t)g].data(),
+                                           (int64_t)mine[(size_t)g].size(), cand[(size_t)g].data(),
+                                           acc[(size_t)g].data());
+        });
+        if (rc != DP_OK)
+            return rc;
+        std::vector<dp_patch> all_c((size_t)(items * per));
+        std::vector<uint8_t> all_a((size_t)(items * per));
+        for (int g = 0; g < G; ++g)
+            for (size_t j = 0; j < mine[(size_t)g].size(); ++j)
+                for (int d = 0; d < per; ++d) {
+                    const size_t dst = (size_t)mine[(size_t)g][j] * per + d;
+                    all_c[dst] = cand[(size_t)g][j * per + d];
+                    all_a[dst] = acc[(size_t)g][j * per + d];
+                }
+        rc = all([&](int g) {
+            return dp_densify_commit(ctxs[(size_t)g], &gen[(size_t)g], all_c.data(), all_a.data(), items * per);
+        });
+        if (rc != DP_OK)
+            return rc;
+    }
+    std::vector<dp_densify_stats> sts((size_t)G);
+    const dp_patch *res = nullptr;
+    int64_t np = 0;
+    for (int g = G - 1; g >= 0; --g)
+        if ((rc = dp_densify_result(ctxs[(size_t)g], &res, &np, &sts[(size_t)g])) != DP_OK) {
+            err = dp_last_error(ctxs[(size_t)g]);
+            return rc;
+        }
+    out.assign(res, res + np);
+    st = sts[0];
+    for (int g = 1; g < G; ++g) {
+        st.evals += sts[(size_t)g].evals;
+        st.refine_ms = std::max(st.refine_ms, sts[(size_t)g].refine_ms);
+    }
+    return DP_OK;
+}
+
 } // namespace
 
 int main(int argc, char **argv)
 {
     std::string input, settings, output = "points.ply", seeds_path, synth, scene_dir;
-    int device = 0;
+    int device = 0, gpus = 1;
     long long max_pops = -1;
     int level = 0;
     bool check_only = false, do_filter = false;
@@ -148,6 +238,7 @@ int main(int argc, char **argv)
         else if (a == "-o" || a == "--output") output = next();
         else if (a == "--seeds") seeds_path = next();
         else if (a == "--device") device = std::atoi(next().c_str());
+        else if (a == "--gpus") gpus = std::atoi(next().c_str());
         else if (a == "--max-pops") max_pops = std::atoll(next().c_str());
         else if (a == "--level") level = std::atoi(next().c_str());
         else if (a == "--filter") do_filter = true;
@@ -242,7 +333,35 @@ int main(int argc, char **argv)
         int64_t n_out = 0;
         dp_densify_stats st;
         std::memset(&st, 0, sizeof st);
-        check(dp_densify(ctx, use.data(), (int)(use.size() / 3), &out, &n_out, &st), "dp_densify");
+        std::vector<dp_patch> multi_out;
+        if (gpus > 1) {
+            // contexts 1..N-1 on the next devices (wrapping: several ranks may share a GPU)
+            const int ndev = dp_device_count();
+            std::vector<dp_ctx *> ctxs{ctx};
+            for (int g = 1; g < gpus; ++g) {
+                dp_ctx *cg = nullptr;
+                check(dp_ctx_create(&opt, (device + g) % (ndev > 0 ? ndev : 1), &cg), "dp_ctx_create");
+                ctxs.push_back(cg);
+                check(dp_set_views(cg, (int)imgs.size(), P.data(), dimg.data()), "dp_set_views");
+                if (level > 0) {
+                    check(dp_build_pyramid(cg, level + 1), "dp_build_pyramid");
+                    check(dp_set_level(cg, level), "dp_set_level");
+                }
+            }
+            std::string err;
+            const int mrc = densify_multi(ctxs, use, multi_out, st, err);
+            for (int g = 1; g < gpus; ++g)
+                dp_ctx_destroy(ctxs[(size_t)g]);
+            if (mrc != DP_OK) {
+                std::fprintf(stderr, "densify: multi-GPU densify failed (%d): %s\n", mrc, err.c_str());
+                dp_ctx_destroy(ctx);
+                return 1;
+            }
+            out = multi_out.data();
+            n_out = (int64_t)multi_out.size();
+        } else {
+            check(dp_densify(ctx, use.data(), (int)(use.size() / 3), &out, &n_out, &st), "dp_densify");
+        }
         // PMVS::FilterPatches (pmvs.h:27, undefined in the reference): dp_filter_patches spec
         std::vector<uint8_t> keep((size_t)n_out, 1);
         if (do_filter && n_out > 0) {
@@ -270,11 +389,11 @@ int main(int argc, char **argv)
         std::printf("{\"output\": \"%s\", \"patches\": %lld, \"written\": %zu, \"seeds\": %zu, \"generated_seeds\": %s, "
                     "\"keypoints\": %lld, \"matches\": %lld, \"seed_ms\": %.3f, \"seed_patches\": %lld, "
                     "\"pops\": %lld, \"candidates\": %lld, \"evals\": %lld, \"generations\": %d, \"refine_ms\": %.3f, "
-                    "\"densify_ms\": %.3f, \"wall_ms\": %.3f}\n",
+                    "\"densify_ms\": %.3f, \"wall_ms\": %.3f, \"gpus\": %d}\n",
                     output.c_str(), (long long)st.patches, cloud.size(), use.size() / 3,
                     seeds_path.empty() ? "true" : "false", (long long)sst.keypoints, (long long)sst.matches,
                     sst.total_ms, (long long)st.seed_patches, (long long)st.pops, (long long)st.candidates,
-                    (long long)st.evals, st.generations, st.refine_ms, st.total_ms, wall);
+                    (long long)st.evals, st.generations, st.refine_ms, st.total_ms, wall, gpus);
         return 0;
     } catch (const std::exception &e) {
         std::fprintf(stderr, "densify: %s\n", e.what());

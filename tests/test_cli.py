@@ -196,3 +196,18 @@ def test_cli_baseline_cfg1_vga(tmp_path_factory, tmp_path, orc, views):
     ref = tmp_path / "oracle.ply"
     write_ply(str(ref), op)
     assert out.read_bytes() == ref.read_bytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_cli_gpus_partitioned_equals_one_gpu(scene_dir, tmp_path, gpus):
+    """densify --gpus N: N contexts (wrapping onto the available devices),
+    every generation partitioned by reference-view super-tile; the PLY is
+    byte-identical to the 1-GPU run."""
+    one, many = tmp_path / "one.ply", tmp_path / "many.ply"
+    args = ["-i", os.path.join(scene_dir, "scene.json"), "--seeds", os.path.join(scene_dir, "seeds.xyz")]
+    r1 = json.loads(run(*args, "-o", str(one)).stdout)
+    rn = json.loads(run(*args, "-o", str(many), "--gpus", str(gpus)).stdout)
+    assert rn["gpus"] == gpus and rn["patches"] == r1["patches"] > 0
+    assert rn["evals"] == r1["evals"]
+    assert many.read_bytes() == one.read_bytes()
