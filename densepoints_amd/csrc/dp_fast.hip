@@ -458,9 +458,17 @@ template <int G> __device__ Slots make_slots(int cell)
     return s;
 }
 
-// one view's sample in 1/16 gray levels (or_fast.c fast_sample)
-__device__ __forceinline__ uint32_t sample(const char *tiles, const float4 &qa,
-                                           const float4 &qb, const float4 &qc, float ti, float tj)
+// One view's sample in 1/16 gray levels (or_fast.c fast_sample), in three
+// phases so that a pass issues every lane's LDS reads before it consumes any:
+// tap_addr (projective map, clamp, 1/32-px split), tap_load (the two aligned
+// words around each row's tap pair), tap_blend (funnel shift, bilinear).
+struct Tap {
+    uint32_t a0, a1;   // aligned LDS byte addresses of rows y0, y0 + 1
+    uint32_t sh;       // 16 if the pair starts at an odd pixel
+    uint32_t w0, w1;   // packed bilinear weights of the two rows
+};
+
+__device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, const float4 &qc, float ti, float tj)
 {
     const float hx = __builtin_fmaf(tj, qc.x, __builtin_fmaf(ti, qb.x, qa.x));
     const float hy = __builtin_fmaf(tj, qc.y, __builtin_fmaf(ti, qb.y, qa.y));
@@ -475,18 +483,42 @@ __device__ __forceinline__ uint32_t sample(const char *tiles, const float4 &qa,
     const uint32_t rowb = info >> 16;
     const uint32_t x0 = iu >> 5, fx = iu & 31u, y0 = iv >> 5, fy = iv & 31u;
     const uint32_t addr = (info & 0xffffu) + __umul24(y0, rowb) + (x0 << 1);
-    // (p(x0), p(x0+1)) of rows y0 and y0 + 1 as u16 pairs: 32-bit LDS reads at
-    // 2-byte alignment (the unaligned DS mode, probed on the device); each
-    // value is 0x6400 + gray (fp16 of 1024 + gray)
-    const uint32_t r0 = *(const uint32_t *)(tiles + addr);
-    const uint32_t r1 = *(const uint32_t *)(tiles + addr + rowb);
+    Tap t;
+    t.a0 = addr & ~3u;
+    t.a1 = t.a0 + rowb;
+    t.sh = (addr & 2u) << 3;
     const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
-    const uint32_t w0 = __umul24(wx, 32u - fy), w1 = __umul24(wx, fy);
+    t.w0 = __umul24(wx, 32u - fy);
+    t.w1 = __umul24(wx, fy);
+    return t;
+}
+
+struct TapWords {
+    uint32_t d[4];
+};
+
+__device__ __forceinline__ TapWords tap_load(const char *tiles, const Tap &t)
+{
+    typedef __attribute__((address_space(3))) const uint32_t *lds_u32_t;
+    const lds_u32_t p0 = (lds_u32_t)(tiles + t.a0), p1 = (lds_u32_t)(tiles + t.a1);
+    TapWords w;
+    w.d[0] = p0[0];
+    w.d[1] = p0[1];
+    w.d[2] = p1[0];
+    w.d[3] = p1[1];
+    return w;
+}
+
+// (p(x0), p(x0+1)) of each row as u16 pairs, each value 0x6400 + gray (fp16 of
+// 1024 + gray): sum w (0x6400 + p) + 32 = sum w p + 32 + 0x6400 * 1024
+__device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
+{
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    // sum w (0x6400 + p) + 32 = sum w p + 32 + 0x6400 * 1024 (weights sum to 1024)
-    const uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r0), __builtin_bit_cast(us2, w0),
+    const uint32_t r0 = __builtin_amdgcn_alignbit(w.d[1], w.d[0], t.sh);
+    const uint32_t r1 = __builtin_amdgcn_alignbit(w.d[3], w.d[2], t.sh);
+    const uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r0), __builtin_bit_cast(us2, t.w0),
                                               __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r1),
-                                                                     __builtin_bit_cast(us2, w1),
+                                                                     __builtin_bit_cast(us2, t.w1),
                                                                      32u - 0x6400u * 1024u, false),
                                               false);
     return b >> 6;
@@ -522,10 +554,20 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
         const bool act = r < m;
         const EvalRec &E = L.u.ev.par[act ? r : 0];
         const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
+        Tap tp[kFastSlots];
+#pragma unroll
+        for (int k = 0; k < kFastSlots; ++k)
+            tp[k] = tap_addr(qa, qb, qc, sl.ti[k], sl.tj[k]);
+        __builtin_amdgcn_sched_barrier(0);
+        TapWords tw[kFastSlots];
+#pragma unroll
+        for (int k = 0; k < kFastSlots; ++k)
+            tw[k] = tap_load(tiles, tp[k]);
+        __builtin_amdgcn_sched_barrier(0);
         uint32_t b[kFastSlots];
 #pragma unroll
         for (int k = 0; k < kFastSlots; ++k)
-            b[k] = sample(tiles, qa, qb, qc, sl.ti[k], sl.tj[k]) & sl.live[k];
+            b[k] = tap_blend(tp[k], tw[k]) & sl.live[k];
         if (p == 0) {
             // texture 0 = rank 0 = group 0 of the first pass: its samples reach
             // every group through the LDS crossbar and stay in registers

@@ -137,7 +137,7 @@ def test_fast_expand_cfg3_full_scene(orc):
             ok, oa = S2.fast_expand(par)
             assert np.array_equal(ga, oa)
             assert_same(gk, ok, FIELDS + ("parent",))
-            assert 0.2 < ga.mean() < 0.95
+            assert 0.1 < ga.mean() < 0.95
         eng.set_options(dp.Options())
         nk, na = eng.expand(par)
     def err(k, a):
