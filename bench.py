@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--fast-budgets", default="", help="tile budgets (bytes) to sweep in perf_mode; default: the "
                                                          "FastOptions default")
     ap.add_argument("--fast-iters", type=int, default=None, help="performance-mode CG iterations (default: FastOptions)")
+    ap.add_argument("--fast-margins", default="", help="tile margins (px) to sweep in perf_mode")
     ap.add_argument("--no-fast", action="store_true", help="skip the perf_mode sub-object")
     ap.add_argument("--seed-stride", type=float, default=32.0, help="synthetic seed grid stride (px)")
     return ap.parse_args()
@@ -365,11 +366,14 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
     res = {"parity_quality_n%d" % args.cell: quality(cfg, parity_out, parity_acc)}
     imgs = None
     budgets = [int(b) for b in args.fast_budgets.split(",") if b] or [None]
-    combos = [(int(c), b) for c in args.fast_cells.split(",") if c for b in budgets]
-    for cell, tb in combos:
+    margins = [int(b) for b in args.fast_margins.split(",") if b] or [None]
+    combos = [(int(c), b, mg) for c in args.fast_cells.split(",") if c for b in budgets for mg in margins]
+    for cell, tb, mg in combos:
         fo = dp.FastOptions()
         if tb:
             fo.tile_budget = tb
+        if mg is not None:
+            fo.margin = mg
         if args.fast_iters is not None:
             fo.iters = args.fast_iters
         eng.set_fast_options(fo)
@@ -423,7 +427,8 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                                  "parity_bit_exact_on_sample": bool(all(kids[f].tobytes() == g[f].tobytes()
                                                                         for f in fields) and
                                                                     np.array_equal(kacc, acc[: 4 * n]))}
-        res["n%d" % cell + ("_b%d" % tb if tb and len(budgets) > 1 else "")] = r
+        res["n%d" % cell + ("_b%d" % tb if tb and len(budgets) > 1 else "") +
+            ("_m%d" % mg if mg is not None and len(margins) > 1 else "")] = r
     eng.set_options(dp.Options(expand_cell_size=args.cell))
     eng.set_fast_options(dp.FastOptions())
     return res

@@ -29,7 +29,7 @@ namespace {
 constexpr int kFastMaxV = 32;     // staged views per patch (per-view tables)
 constexpr int kFastMaxBbox = 48;  // window bounding-box side cap (grazing views)
 constexpr int kFastMaxMargin = 7; // keeps a tile row <= 64 entries (one lane each)
-constexpr int kFastSlots = 4;     // samples per lane per view pass
+constexpr int kFastSlots = 4;     // at most this many samples per lane per view pass
 
 struct GrayPlane {
     const __half *p;
@@ -432,13 +432,17 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     return m;
 }
 
-// per-lane sample slots of a view pass (fixed per launch)
+// Per-lane sample slots of a view pass (fixed per launch).  A pass of G views
+// gives each view LP = 64/G lanes x S slots; with kTail the last sample of
+// every view (N = S LP + 1, e.g. 7 x 7 = 3 x 16 + 1) is taken by one extra
+// round over the views instead of a fourth, nearly empty slot per pass.
 struct Slots {
     float ti[kFastSlots], tj[kFastSlots];
     uint32_t live[kFastSlots];
+    float tail;  // (i, j) of the tail sample: n - 1 - c on both axes
 };
 
-template <int G> __device__ Slots make_slots(int cell)
+template <int G, int S> __device__ Slots make_slots(int cell)
 {
     constexpr int LP = 64 / G;
     const int g = lane_id() & (LP - 1);
@@ -446,7 +450,7 @@ template <int G> __device__ Slots make_slots(int cell)
     const float c = 0.5f * (float)(cell - 1);
     Slots s;
 #pragma unroll
-    for (int k = 0; k < kFastSlots; ++k) {
+    for (int k = 0; k < S; ++k) {
         const int t = g + LP * k;
         const bool live = t < N;
         const int te = live ? t : N - 1;
@@ -455,6 +459,7 @@ template <int G> __device__ Slots make_slots(int cell)
         s.tj[k] = (float)jj - c;
         s.live[k] = live ? 0xffffffffu : 0u;
     }
+    s.tail = (float)(cell - 1) - c;
     return s;
 }
 
@@ -477,11 +482,13 @@ __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, cons
     const float rz = recip_rn(hz);
     const float U = __builtin_amdgcn_fmed3f(hx * rz, 0.0f, qa.w);
     const float V = __builtin_amdgcn_fmed3f(hy * rz, 0.0f, qb.w);
-    const uint32_t iu = __float_as_uint(U + 8388608.0f) - 0x4B000000u;
-    const uint32_t iv = __float_as_uint(V + 8388608.0f) - 0x4B000000u;
+    // U + 2^23 holds rint(U) (U < 2^22) in its low mantissa bits: the pixel
+    // and 1/32 fraction are bit fields of it (the exponent bits lie above them)
+    const uint32_t bu = __float_as_uint(U + 8388608.0f), bv = __float_as_uint(V + 8388608.0f);
     const uint32_t info = __float_as_uint(qc.w);
     const uint32_t rowb = info >> 16;
-    const uint32_t x0 = iu >> 5, fx = iu & 31u, y0 = iv >> 5, fy = iv & 31u;
+    const uint32_t x0 = __builtin_amdgcn_ubfe(bu, 5, 17), fx = bu & 31u;
+    const uint32_t y0 = __builtin_amdgcn_ubfe(bv, 5, 17), fy = bv & 31u;
     const uint32_t addr = (info & 0xffffu) + __umul24(y0, rowb) + (x0 << 1);
     Tap t;
     t.a0 = addr & ~3u;
@@ -526,7 +533,7 @@ __device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
 
 // One objective evaluation at scaled pose x (or_fast.c fast_objective).
 // Leaves NCC of rank r (r >= 1) in L.u.ev.score[r]; returns F (uniform).
-template <int G, int kBudget>
+template <int G, int NS, bool kTail, int kBudget>
 __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m, double x0,
                            double x1, double x2)
 {
@@ -547,37 +554,37 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
     wave_sync();
     const int j = lane / LP, g = lane & (LP - 1);
     const char *tiles = (const char *)L.tiles;
-    uint32_t av[kFastSlots];
+    uint32_t av[NS];
     const int passes = (m + G - 1) / G;
     for (int p = 0; p < passes; ++p) {
         const int r = p * G + j;
         const bool act = r < m;
         const EvalRec &E = L.u.ev.par[act ? r : 0];
         const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
-        Tap tp[kFastSlots];
+        Tap tp[NS];
 #pragma unroll
-        for (int k = 0; k < kFastSlots; ++k)
+        for (int k = 0; k < NS; ++k)
             tp[k] = tap_addr(qa, qb, qc, sl.ti[k], sl.tj[k]);
         __builtin_amdgcn_sched_barrier(0);
-        TapWords tw[kFastSlots];
+        TapWords tw[NS];
 #pragma unroll
-        for (int k = 0; k < kFastSlots; ++k)
+        for (int k = 0; k < NS; ++k)
             tw[k] = tap_load(tiles, tp[k]);
         __builtin_amdgcn_sched_barrier(0);
-        uint32_t b[kFastSlots];
+        uint32_t b[NS];
 #pragma unroll
-        for (int k = 0; k < kFastSlots; ++k)
+        for (int k = 0; k < NS; ++k)
             b[k] = tap_blend(tp[k], tw[k]) & sl.live[k];
         if (p == 0) {
             // texture 0 = rank 0 = group 0 of the first pass: its samples reach
             // every group through the LDS crossbar and stay in registers
 #pragma unroll
-            for (int k = 0; k < kFastSlots; ++k)
+            for (int k = 0; k < NS; ++k)
                 av[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(g << 2, (int)b[k]);
         }
         uint32_t s = 0, ss = 0, sx = 0;
 #pragma unroll
-        for (int k = 0; k < kFastSlots; ++k) {
+        for (int k = 0; k < NS; ++k) {
             s += b[k];
             ss += __umul24(b[k], b[k]);
             sx += __umul24(av[k], b[k]);
@@ -591,30 +598,54 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
             L.u.ev.mom[r][2] = sx;
         }
     }
-    wave_sync();
-    const int N = a.cell * a.cell;
-    if (lane >= 1 && lane < m) {
-        const int64_t Sa = L.u.ev.mom[0][0], Saa = L.u.ev.mom[0][1];
-        const int64_t Sb = L.u.ev.mom[lane][0], Sbb = L.u.ev.mom[lane][1], Sab = L.u.ev.mom[lane][2];
-        const int64_t num = (int64_t)N * Sab - Sa * Sb;
-        const int64_t va = (int64_t)N * Saa - Sa * Sa;
-        const int64_t vb = (int64_t)N * Sbb - Sb * Sb;
-        const double dmin = ((a.opt.ncc_denom_min * 256.0) * (double)N) * (double)N;
-        const double den = sqrt((double)va * (double)vb);
-        const double d = den > dmin ? den : dmin;
-        L.u.ev.score[lane] = (double)num / d;
+    if (kTail) {
+        // the last sample of every view, one lane per view (m <= 32)
+        wave_sync();
+        const int r = lane < m ? lane : 0;
+        const EvalRec &E = L.u.ev.par[r];
+        const Tap t = tap_addr(E.q[0], E.q[1], E.q[2], sl.tail, sl.tail);
+        const uint32_t b = tap_blend(t, tap_load(tiles, t));
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b); // the anchor's (lane 0)
+        if (lane < m) {
+            L.u.ev.mom[lane][0] += b;
+            L.u.ev.mom[lane][1] += __umul24(b, b);
+            L.u.ev.mom[lane][2] += __umul24(a0, b);
+        }
     }
     wave_sync();
+    const int N = a.cell * a.cell;
+    // NCC per view, one lane each: the integer moment products are below 2^53,
+    // so these fp64 expressions are exactly the spec's int64 ones
+    double sc = 0.0;
+    if (lane >= 1 && lane < m) {
+        const double Sa = (double)L.u.ev.mom[0][0], Saa = (double)L.u.ev.mom[0][1];
+        const double Sb = (double)L.u.ev.mom[lane][0], Sbb = (double)L.u.ev.mom[lane][1];
+        const double Sab = (double)L.u.ev.mom[lane][2];
+        const double dN = (double)N;
+        const double num = dN * Sab - Sa * Sb;
+        const double va = dN * Saa - Sa * Sa;
+        const double vb = dN * Sbb - Sb * Sb;
+        const double dmin = ((a.opt.ncc_denom_min * 256.0) * dN) * dN;
+        const double den = sqrt(va * vb);
+        sc = num / (den > dmin ? den : dmin);
+        L.u.ev.score[lane] = sc;
+    }
+    // the objective sums the views in order (std::accumulate), lane by lane
     double sum = 0.0;
-    for (int k = 1; k < m; ++k)
-        sum = sum + (1.0 - L.u.ev.score[k]);
+    for (int k = 1; k < m; ++k) {
+        const long long bits = __double_as_longlong(sc);
+        const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffff), k);
+        const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), k);
+        sum = sum + (1.0 - __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo));
+    }
+    wave_sync();
     return uni_f64(sum / (double)(m - 1));
 }
 
 // Nonlinear CG (or_fast.c fast_cg) as a state machine around ONE evaluation
 // call site (the sampling passes are inlined once); its state lives in LDS.
 // Returns evaluations; L.cg.x = the scaled pose.
-template <int G, int kBudget>
+template <int G, int NS, bool kTail, int kBudget>
 __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m)
 {
     enum { kStart = 0, kFd0 = 1, kFd2 = 3, kProbe1 = 4, kProbe2 = 5 };
@@ -641,7 +672,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
             xt1 = C.x[1] + st * C.u[1];
             xt2 = C.x[2] + st * C.u[2];
         }
-        const double ft = evaluate<G>(a, L, S, sl, m, xt0, xt1, xt2);
+        const double ft = evaluate<G, NS, kTail>(a, L, S, sl, m, xt0, xt1, xt2);
         if (phase == kStart) {
             C.f = ft;
             E = 1;
@@ -772,12 +803,12 @@ template <int kBudget> struct FastOcc {
     static constexpr int value = kBudget <= 6144 ? 4 : kBudget <= 8192 ? 3 : 2;
 };
 
-template <int G, int kBudget, int kMode>
+template <int G, int NS, bool kTail, int kBudget, int kMode>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBudget>::value))) void fast_kernel(FastArgs a)
 {
     __shared__ FastLds<kBudget> L;
     const int lane = lane_id();
-    const Slots sl = make_slots<G>(a.cell);
+    const Slots sl = make_slots<G, NS>(a.cell);
     unsigned long long wave_evals = 0, wave_vev = 0, wave_bytes = 0, wave_patches = 0, wave_clip = 0;
     dp_patch &p = L.p;
     for (;;) {
@@ -831,7 +862,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                 ok = m >= 2;
                 wave_vev += ok ? (unsigned long long)m : 0ull;
                 if (ok) {
-                    evaluate<G>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                    evaluate<G, NS, kTail>(a, L, S, sl, m, 0.0, 0.0, 0.0);
                     double sum = 0.0;
                     for (int k = 1; k < m; ++k)
                         sum = sum + L.u.ev.score[k];
@@ -849,7 +880,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                     Staged S;
                     const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S, wave_bytes, wave_clip);
                     if (m >= 2) {
-                        const int E = cg_refine<G>(a, L, S, sl, m);
+                        const int E = cg_refine<G, NS, kTail>(a, L, S, sl, m);
                         p.evals += (uint32_t)E;
                         wave_vev += (unsigned long long)E * (unsigned long long)m;
                         const Frame &F = L.F;
@@ -894,7 +925,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                         p.vis[1] = (m == 1 && v >= 64) ? (1ull << (v - 64)) : 0ull;
                         ok = m >= a.opt.min_visible;
                     } else {
-                        evaluate<G>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                        evaluate<G, NS, kTail>(a, L, S, sl, m, 0.0, 0.0, 0.0);
                         double sum = 0.0;
                         for (int k = 1; k < m; ++k)
                             sum = sum + L.u.ev.score[k];
@@ -1009,7 +1040,7 @@ hipError_t launch_recip_probe(const float *x, int n, float *out)
     return hipGetLastError();
 }
 
-template <int G, int kBudget> static hipError_t launch_fast_t(const FastArgs &a, hipStream_t s)
+template <int G, int NS, bool kTail, int kBudget> static hipError_t launch_fast_t(const FastArgs &a, hipStream_t s)
 {
     int dev = 0, cus = 256;
     hipGetDevice(&dev);
@@ -1019,9 +1050,9 @@ template <int G, int kBudget> static hipError_t launch_fast_t(const FastArgs &a,
     const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
     const int grid = (int)(want < cap ? want : cap);
     if (a.mode == DP_MODE_FAST_EVAL)
-        hipLaunchKernelGGL((fast_kernel<G, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((fast_kernel<G, kBudget, DP_MODE_FAST_REFINE>), dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kBudget, DP_MODE_FAST_REFINE>), dim3(grid), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
@@ -1107,6 +1138,27 @@ int ensure_gray(dp_ctx *c)
 
 } // namespace
 
+template <int B> static hipError_t fast_dispatch(int N, const dpk::FastArgs &a, hipStream_t s)
+{
+    if (N == 49)
+        return dpk::launch_fast_t<4, 3, true, B>(a, s);
+    if (N <= 16)
+        return dpk::launch_fast_t<4, 1, false, B>(a, s);
+    if (N <= 32)
+        return dpk::launch_fast_t<4, 2, false, B>(a, s);
+    if (N <= 48)
+        return dpk::launch_fast_t<4, 3, false, B>(a, s);
+    if (N <= 64)
+        return dpk::launch_fast_t<4, 4, false, B>(a, s);
+    if (N <= 96)
+        return dpk::launch_fast_t<2, 3, false, B>(a, s);
+    if (N <= 128)
+        return dpk::launch_fast_t<2, 4, false, B>(a, s);
+    if (N <= 192)
+        return dpk::launch_fast_t<1, 3, false, B>(a, s);
+    return dpk::launch_fast_t<1, 4, false, B>(a, s);
+}
+
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
                    hipStream_t s)
 {
@@ -1136,8 +1188,9 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     const int N = cell * cell;
     const int tb = c->fopt.tile_budget;
     hipError_t e;
-#define DP_FAST_ARENA(B)                                                                                      \
-    (N <= 64 ? dpk::launch_fast_t<4, B>(a, s) : N <= 128 ? dpk::launch_fast_t<2, B>(a, s) : dpk::launch_fast_t<1, B>(a, s))
+    // views per pass G (LP = 64/G lanes each) and slots S = ceil(N / LP); for
+    // N = 49 three slots plus the one-sample tail round
+#define DP_FAST_ARENA(B) fast_dispatch<B>(N, a, s)
     if (tb <= 6144)
         e = DP_FAST_ARENA(6144);
     else if (tb <= 8192)
