@@ -246,20 +246,28 @@ def main():
                                  "generations": int(dst["generations"]), "evals": int(dst["evals"]),
                                  "refine_ms": round(dst["refine_ms"], 1), "wall_s": round(wall, 3)}
     if world > 1 and not args.no_densify and not fast:
-        # informational: the same densify sharded over the ranks --
-        # per generation each rank refines its item range into HBM, the
-        # candidate shards are all-gathered over RCCL (all_gather_into_tensor),
-        # every rank commits the replicated organizer step
+        # informational: the same densify with every generation partitioned by
+        # reference-view super-tile over the ranks (north star): each
+        # rank refines its tiles' items into HBM, the candidate shards are
+        # all-gathered over RCCL (all_gather_into_tensor), every rank commits
+        # the replicated organizer step in sequence order
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        _, sst = D.densify_sharded_device(eng, seeds, dist, torch.device("cuda", local))
+        _, sst = D.densify_partitioned_device(eng, seeds, dist, torch.device("cuda", local))
         torch.cuda.synchronize()
         wall = D.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
-        result["densify_sharded"] = {"ranks": world, "patches": int(sst["patches"]),
-                                     "generations": int(sst["generations"]), "evals": int(sst["evals"]),
-                                     "refine_ms_max_rank": round(sst["refine_ms"], 1), "wall_s": round(wall, 3),
-                                     "collective": "all_gather_into_tensor (RCCL) of 80-B candidate records"}
+        parts = sst["partition"]
+        result["densify_partitioned"] = {
+            "ranks": world, "patches": int(sst["patches"]), "generations": int(sst["generations"]),
+            "evals": int(sst["evals"]), "refine_ms_max_rank": round(sst["refine_ms"], 1), "wall_s": round(wall, 3),
+            "Mpatches_per_s": round(int(sst["candidates"]) / wall / 1e6, 3),
+            "gathered_MB_total": round(sum(sst["gathered_bytes"]) / 1e6, 2),
+            "gathered_MB_max_generation": round(max(sst["gathered_bytes"]) / 1e6, 2),
+            "tile_partitioned_generations": sum(1 for _, _, fb in parts if not fb),
+            "round_robin_generations": sum(1 for _, _, fb in parts if fb),
+            "max_share_vs_mean": round(max((mx * world / it) for it, mx, _ in parts if it > 0), 3),
+            "collective": "all_gather_into_tensor (RCCL) of 80-B candidate records + accept flags"}
     if rank == 0 and not args.no_seeds:
         result["seed_generation"] = seed_generation(eng, args)
     st = np.zeros(8, dtype=np.uint64)
