@@ -272,7 +272,8 @@ __device__ Geo view_geo(const dpg::ViewDev &v, const Frame &F, int cell)
             h[k] = (g0[k] + ti * g2[k]) + tj * g3[k];
         if (!(h[2] > 0.0))
             return G;
-        const double u = h[0] / h[2], ww = h[1] / h[2];
+        double u, ww;
+        dpg::div2(h[0], h[1], h[2], u, ww); // = h0 / h2, h1 / h2 (IEEE, one shared reciprocal)
         if (!(u > 0.0 && u < 32.0 * v.W && ww > 0.0 && ww < 32.0 * v.H))
             return G;
         if (q == 0 || u < umin)
@@ -475,25 +476,31 @@ struct Tap {
 
 __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, const float4 &qc, float ti, float tj)
 {
-    const float hx = __builtin_fmaf(tj, qc.x, __builtin_fmaf(ti, qb.x, qa.x));
-    const float hy = __builtin_fmaf(tj, qc.y, __builtin_fmaf(ti, qb.y, qa.y));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    // (hx, hy) as packed fp32 FMAs (v_pk_fma_f32: two fmaf roundings each)
+    const f2 hxy = __builtin_elementwise_fma((f2){tj, tj}, (f2){qc.x, qc.y},
+                                             __builtin_elementwise_fma((f2){ti, ti}, (f2){qb.x, qb.y},
+                                                                       (f2){qa.x, qa.y}));
     float hz = __builtin_fmaf(tj, qc.z, __builtin_fmaf(ti, qb.z, qa.z));
     hz = __builtin_fmaxf(hz, 0x1p-20f);
     const float rz = recip_rn(hz);
-    const float U = __builtin_amdgcn_fmed3f(hx * rz, 0.0f, qa.w);
-    const float V = __builtin_amdgcn_fmed3f(hy * rz, 0.0f, qb.w);
+    const f2 uv = hxy * (f2){rz, rz};
+    const float U = __builtin_amdgcn_fmed3f(uv.x, 0.0f, qa.w);
+    const float V = __builtin_amdgcn_fmed3f(uv.y, 0.0f, qb.w);
     // U + 2^23 holds rint(U) (U < 2^22) in its low mantissa bits: the pixel
     // and 1/32 fraction are bit fields of it (the exponent bits lie above them)
-    const uint32_t bu = __float_as_uint(U + 8388608.0f), bv = __float_as_uint(V + 8388608.0f);
+    const f2 m = (f2){U, V} + (f2){8388608.0f, 8388608.0f};
+    const uint32_t bu = __float_as_uint(m.x), bv = __float_as_uint(m.y);
     const uint32_t info = __float_as_uint(qc.w);
     const uint32_t rowb = info >> 16;
-    const uint32_t x0 = __builtin_amdgcn_ubfe(bu, 5, 17), fx = bu & 31u;
-    const uint32_t y0 = __builtin_amdgcn_ubfe(bv, 5, 17), fy = bv & 31u;
-    const uint32_t addr = (info & 0xffffu) + __umul24(y0, rowb) + (x0 << 1);
+    const uint32_t y0 = __builtin_amdgcn_ubfe(bv, 5, 17);
     Tap t;
-    t.a0 = addr & ~3u;
+    // aligned word of the pair: byte (x0 >> 1) * 4 of the row; x0 odd -> the
+    // pair straddles two words, shifted by 16 bits
+    t.a0 = __umul24(y0, rowb) + ((bu >> 4) & 0x3FFFCu) + (info & 0xffffu);
     t.a1 = t.a0 + rowb;
-    t.sh = (addr & 2u) << 3;
+    t.sh = (bu >> 1) & 16u;
+    const uint32_t fx = bu & 31u, fy = bv & 31u;
     const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
     t.w0 = __umul24(wx, 32u - fy);
     t.w1 = __umul24(wx, fy);
@@ -533,7 +540,7 @@ __device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
 
 // One objective evaluation at scaled pose x (or_fast.c fast_objective).
 // Leaves NCC of rank r (r >= 1) in L.u.ev.score[r]; returns F (uniform).
-template <int G, int NS, bool kTail, int kBudget>
+template <int G, int NS, bool kTail, bool kMask, int kBudget>
 __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m, double x0,
                            double x1, double x2)
 {
@@ -574,7 +581,7 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
         uint32_t b[NS];
 #pragma unroll
         for (int k = 0; k < NS; ++k)
-            b[k] = tap_blend(tp[k], tw[k]) & sl.live[k];
+            b[k] = kMask ? (tap_blend(tp[k], tw[k]) & sl.live[k]) : tap_blend(tp[k], tw[k]);
         if (p == 0) {
             // texture 0 = rank 0 = group 0 of the first pass: its samples reach
             // every group through the LDS crossbar and stay in registers
@@ -645,7 +652,7 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
 // Nonlinear CG (or_fast.c fast_cg) as a state machine around ONE evaluation
 // call site (the sampling passes are inlined once); its state lives in LDS.
 // Returns evaluations; L.cg.x = the scaled pose.
-template <int G, int NS, bool kTail, int kBudget>
+template <int G, int NS, bool kTail, bool kMask, int kBudget>
 __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m)
 {
     enum { kStart = 0, kFd0 = 1, kFd2 = 3, kProbe1 = 4, kProbe2 = 5 };
@@ -672,7 +679,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
             xt1 = C.x[1] + st * C.u[1];
             xt2 = C.x[2] + st * C.u[2];
         }
-        const double ft = evaluate<G, NS, kTail>(a, L, S, sl, m, xt0, xt1, xt2);
+        const double ft = evaluate<G, NS, kTail, kMask>(a, L, S, sl, m, xt0, xt1, xt2);
         if (phase == kStart) {
             C.f = ft;
             E = 1;
@@ -803,7 +810,7 @@ template <int kBudget> struct FastOcc {
     static constexpr int value = kBudget <= 6144 ? 4 : kBudget <= 8192 ? 3 : 2;
 };
 
-template <int G, int NS, bool kTail, int kBudget, int kMode>
+template <int G, int NS, bool kTail, bool kMask, int kBudget, int kMode>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBudget>::value))) void fast_kernel(FastArgs a)
 {
     __shared__ FastLds<kBudget> L;
@@ -862,7 +869,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                 ok = m >= 2;
                 wave_vev += ok ? (unsigned long long)m : 0ull;
                 if (ok) {
-                    evaluate<G, NS, kTail>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                    evaluate<G, NS, kTail, kMask>(a, L, S, sl, m, 0.0, 0.0, 0.0);
                     double sum = 0.0;
                     for (int k = 1; k < m; ++k)
                         sum = sum + L.u.ev.score[k];
@@ -880,7 +887,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                     Staged S;
                     const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S, wave_bytes, wave_clip);
                     if (m >= 2) {
-                        const int E = cg_refine<G, NS, kTail>(a, L, S, sl, m);
+                        const int E = cg_refine<G, NS, kTail, kMask>(a, L, S, sl, m);
                         p.evals += (uint32_t)E;
                         wave_vev += (unsigned long long)E * (unsigned long long)m;
                         const Frame &F = L.F;
@@ -925,7 +932,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                         p.vis[1] = (m == 1 && v >= 64) ? (1ull << (v - 64)) : 0ull;
                         ok = m >= a.opt.min_visible;
                     } else {
-                        evaluate<G, NS, kTail>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                        evaluate<G, NS, kTail, kMask>(a, L, S, sl, m, 0.0, 0.0, 0.0);
                         double sum = 0.0;
                         for (int k = 1; k < m; ++k)
                             sum = sum + L.u.ev.score[k];
@@ -1040,7 +1047,8 @@ hipError_t launch_recip_probe(const float *x, int n, float *out)
     return hipGetLastError();
 }
 
-template <int G, int NS, bool kTail, int kBudget> static hipError_t launch_fast_t(const FastArgs &a, hipStream_t s)
+template <int G, int NS, bool kTail, bool kMask, int kBudget>
+static hipError_t launch_fast_m(const FastArgs &a, hipStream_t s)
 {
     int dev = 0, cus = 256;
     hipGetDevice(&dev);
@@ -1050,10 +1058,21 @@ template <int G, int NS, bool kTail, int kBudget> static hipError_t launch_fast_
     const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
     const int grid = (int)(want < cap ? want : cap);
     if (a.mode == DP_MODE_FAST_EVAL)
-        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kBudget, DP_MODE_FAST_REFINE>), dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_REFINE>), dim3(grid), dim3(64), 0, s,
+                           a);
     return hipGetLastError();
+}
+
+// kMask: the last slot has dead lanes (N not a multiple of the pass's lane
+// count and no tail round)
+template <int G, int NS, bool kTail, int kBudget> static hipError_t launch_fast_t(const FastArgs &a, hipStream_t s)
+{
+    const int N = a.cell * a.cell;
+    if (kTail || N == NS * (64 / G))
+        return launch_fast_m<G, NS, kTail, false, kBudget>(a, s);
+    return launch_fast_m<G, NS, kTail, true, kBudget>(a, s);
 }
 
 } // namespace dpk
