@@ -94,6 +94,7 @@ template <int kBudget> struct FastLds {
     Frame F;
     CgState cg;
     dp_patch p;
+    dp_patch par;      // parent of the current chunk (expansion)
     uint8_t vlist[64];
 };
 
@@ -391,6 +392,12 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
         R.th = t.th;
     }
     wave_sync();
+    // lane r takes rank r's vectors (kept in registers for the evaluations)
+    // and its tile rectangle + gray plane descriptor (read with one vector
+    // load for all views, then broadcast per view by readlane)
+    int tx0 = 0, ty0 = 0, ttw = 0, tth = 0;
+    uint32_t toff = 0;
+    GrayPlane gp{};
     if (lane < m) {
         const StageRec &R = L.u.st[lane];
 #pragma unroll
@@ -400,6 +407,12 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
         S.vmax = R.vmax;
         S.info = R.info;
         S.view = R.view;
+        tx0 = R.x0t;
+        ty0 = R.y0t;
+        ttw = R.tw;
+        tth = R.th;
+        toff = R.info & 0xffffu;
+        gp = a.gray[R.view];
     }
     // tiles: rows y0t .. y0t + th (clamped to the image) of biased-fp16 gray,
     // columns x0t .. x0t + 2 W2 - 1 (the plane's padding columns replicate
@@ -410,11 +423,15 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     typedef __attribute__((address_space(3))) void *lds_ptr_t;
     typedef __attribute__((address_space(1))) const void *gptr_t;
     const uint32_t tbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)L.tiles;
+    const uint64_t gpp = (uint64_t)(uintptr_t)gp.p;
     for (int r = 0; r < m; ++r) {
-        const int vv = uni(L.u.st[r].view), x0t = uni(L.u.st[r].x0t), y0t = uni(L.u.st[r].y0t);
-        const int tw = uni(L.u.st[r].tw), th = uni(L.u.st[r].th);
-        const uint32_t off = (uint32_t)uni((int)(L.u.st[r].info & 0xffffu));
-        const GrayPlane gp = a.gray[vv];
+        const int x0t = __builtin_amdgcn_readlane(tx0, r), y0t = __builtin_amdgcn_readlane(ty0, r);
+        const int tw = __builtin_amdgcn_readlane(ttw, r), th = __builtin_amdgcn_readlane(tth, r);
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)toff, r);
+        const int gh = __builtin_amdgcn_readlane(gp.h, r), gpitch = __builtin_amdgcn_readlane(gp.pitch, r);
+        const uint64_t pb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(gpp >> 32), r) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gpp, r);
+        const __half *plane = (const __half *)(uintptr_t)pb;
         const int W2 = (tw + 2) / 2;
         const int nw = W2 * (th + 1);
         const float inv = 1.0f / (float)W2;
@@ -422,8 +439,8 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
             const int d = i + lane;
             const int y = (int)(((float)d + 0.5f) * inv);
             const int c = d - y * W2;
-            const int Y = y0t + y < gp.h - 1 ? y0t + y : gp.h - 1;
-            const __half *src = gp.p + (size_t)Y * gp.pitch + x0t + 2 * c;
+            const int Y = y0t + y < gh - 1 ? y0t + y : gh - 1;
+            const __half *src = plane + (size_t)Y * gpitch + x0t + 2 * c;
             if (d < nw)
                 __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)(uintptr_t)(tbase + off + 4u * (uint32_t)i), 4, 0, 0);
         }
@@ -818,16 +835,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
     const Slots sl = make_slots<G, NS>(a.cell);
     unsigned long long wave_evals = 0, wave_vev = 0, wave_bytes = 0, wave_patches = 0, wave_clip = 0;
     dp_patch &p = L.p;
+    // work is dequeued in chunks of 4 (one atomic per chunk): the 4 children of
+    // one parent, whose record is read once into LDS, or 4 consecutive patches
+    uint32_t chunk_idx = 0xffffffffu, q4 = 4;
     for (;;) {
-        uint32_t idx = 0;
-        if (lane == 0)
-            idx = atomicAdd(a.work, 1u);
-        idx = (uint32_t)uni((int)idx);
-        if (idx >= (uint32_t)a.n)
-            break;
+        if (q4 == 4) {
+            uint32_t c = 0;
+            if (lane == 0)
+                c = atomicAdd(a.work, 1u);
+            chunk_idx = (uint32_t)uni((int)c);
+            q4 = 0;
+            if ((uint64_t)chunk_idx * 4u >= (uint64_t)a.n)
+                break;
+            if (a.parents) {
+                const uint32_t *src = (const uint32_t *)(a.parents + chunk_idx);
+                if (lane < (int)(sizeof(dp_patch) / 4))
+                    ((uint32_t *)&L.par)[lane] = src[lane];
+                wave_sync();
+            }
+        }
+        const uint32_t idx = chunk_idx * 4u + q4++;
+        if (idx >= (uint32_t)a.n) {
+            q4 = 4;
+            continue;
+        }
         bool live = true;
         if (a.parents) {
-            const dp_patch &par = a.parents[idx >> 2];
+            const dp_patch &par = L.par;
             p = par;
             p.evals = 0;
             p.flags = 0;
@@ -1054,7 +1088,7 @@ static hipError_t launch_fast_m(const FastArgs &a, hipStream_t s)
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int per_cu = (160 * 1024) / (int)sizeof(FastLds<kBudget>);
-    const int64_t want = a.n;
+    const int64_t want = ((int64_t)a.n + 3) / 4;
     const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
     const int grid = (int)(want < cap ? want : cap);
     if (a.mode == DP_MODE_FAST_EVAL)
