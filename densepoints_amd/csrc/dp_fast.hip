@@ -96,7 +96,21 @@ template <int kBudget> struct FastLds {
     dp_patch p;
     dp_patch par;      // parent of the current chunk (expansion)
     uint8_t vlist[64];
+#ifdef DP_FAST_TIMING
+    unsigned long long tm[16], tlast;
+#endif
 };
+
+#ifdef DP_FAST_TIMING
+#define TMARK(L, k)                                                                                                    \
+    do {                                                                                                               \
+        const unsigned long long t_ = __builtin_readcyclecounter();                                                  \
+        (L).tm[k] += t_ - (L).tlast;                                                                                   \
+        (L).tlast = t_;                                                                                                \
+    } while (0)
+#else
+#define TMARK(L, k) ((void)0)
+#endif
 
 __device__ __forceinline__ void wave_sync()
 {
@@ -392,6 +406,7 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
         R.th = t.th;
     }
     wave_sync();
+    TMARK(L, 2);
     // lane r takes rank r's vectors (kept in registers for the evaluations)
     // and its tile rectangle + gray plane descriptor (read with one vector
     // load for all views, then broadcast per view by readlane)
@@ -445,8 +460,10 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
                 __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)(uintptr_t)(tbase + off + 4u * (uint32_t)i), 4, 0, 0);
         }
     }
+    TMARK(L, 3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
+    TMARK(L, 4);
     return m;
 }
 
@@ -556,7 +573,9 @@ __device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
 }
 
 // One objective evaluation at scaled pose x (or_fast.c fast_objective).
-// Leaves NCC of rank r (r >= 1) in L.u.ev.score[r]; returns F (uniform).
+// Leaves NCC of rank r (r >= 1) in L.u.ev.score[r]; returns the objective
+// (uniform): the sum over r >= 1 of 1 - NCC_r, NCCs in 2^-24 steps, which is
+// an exact integer reduction across the wave.
 template <int G, int NS, bool kTail, bool kMask, int kBudget>
 __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m, double x0,
                            double x1, double x2)
@@ -576,29 +595,42 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
                              __builtin_fmaf(-bf, S.v[14], S.v[11]), __uint_as_float(S.info));
     }
     wave_sync();
+    TMARK(L, 10);
     const int j = lane / LP, g = lane & (LP - 1);
     const char *tiles = (const char *)L.tiles;
     uint32_t av[NS];
+    // kTail: the last sample of every view (N = NS LP + 1), one lane per view
+    // (m <= 32), computed alongside the first pass and kept in a register
+    uint32_t bt = 0;
     const int passes = (m + G - 1) / G;
     for (int p = 0; p < passes; ++p) {
         const int r = p * G + j;
         const bool act = r < m;
+        const bool tail = kTail && p == 0;
         const EvalRec &E = L.u.ev.par[act ? r : 0];
         const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
-        Tap tp[NS];
+        Tap tp[NS], tt{};
 #pragma unroll
         for (int k = 0; k < NS; ++k)
             tp[k] = tap_addr(qa, qb, qc, sl.ti[k], sl.tj[k]);
+        if (tail) {
+            const EvalRec &T = L.u.ev.par[lane < m ? lane : 0];
+            tt = tap_addr(T.q[0], T.q[1], T.q[2], sl.tail, sl.tail);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        TapWords tw[NS];
+        TapWords tw[NS], twt{};
 #pragma unroll
         for (int k = 0; k < NS; ++k)
             tw[k] = tap_load(tiles, tp[k]);
+        if (tail)
+            twt = tap_load(tiles, tt);
         __builtin_amdgcn_sched_barrier(0);
         uint32_t b[NS];
 #pragma unroll
         for (int k = 0; k < NS; ++k)
             b[k] = kMask ? (tap_blend(tp[k], tw[k]) & sl.live[k]) : tap_blend(tp[k], tw[k]);
+        if (tail)
+            bt = tap_blend(tt, twt);
         if (p == 0) {
             // texture 0 = rank 0 = group 0 of the first pass: its samples reach
             // every group through the LDS crossbar and stay in registers
@@ -622,48 +654,41 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
             L.u.ev.mom[r][2] = sx;
         }
     }
-    if (kTail) {
-        // the last sample of every view, one lane per view (m <= 32)
-        wave_sync();
-        const int r = lane < m ? lane : 0;
-        const EvalRec &E = L.u.ev.par[r];
-        const Tap t = tap_addr(E.q[0], E.q[1], E.q[2], sl.tail, sl.tail);
-        const uint32_t b = tap_blend(t, tap_load(tiles, t));
-        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b); // the anchor's (lane 0)
-        if (lane < m) {
-            L.u.ev.mom[lane][0] += b;
-            L.u.ev.mom[lane][1] += __umul24(b, b);
-            L.u.ev.mom[lane][2] += __umul24(a0, b);
-        }
-    }
     wave_sync();
+    TMARK(L, 11);
     const int N = a.cell * a.cell;
+    // the anchor's tail sample (lane 0 holds rank 0's)
+    const uint32_t a0 = kTail ? (uint32_t)__builtin_amdgcn_readfirstlane((int)bt) : 0u;
     // NCC per view, one lane each: the integer moment products are below 2^53,
     // so these fp64 expressions are exactly the spec's int64 ones
-    double sc = 0.0;
+    int q = 0;
     if (lane >= 1 && lane < m) {
-        const double Sa = (double)L.u.ev.mom[0][0], Saa = (double)L.u.ev.mom[0][1];
-        const double Sb = (double)L.u.ev.mom[lane][0], Sbb = (double)L.u.ev.mom[lane][1];
-        const double Sab = (double)L.u.ev.mom[lane][2];
+        uint32_t sa = L.u.ev.mom[0][0], saa = L.u.ev.mom[0][1];
+        uint32_t sb = L.u.ev.mom[lane][0], sbb = L.u.ev.mom[lane][1], sab = L.u.ev.mom[lane][2];
+        if (kTail) {
+            sa += a0;
+            saa += __umul24(a0, a0);
+            sb += bt;
+            sbb += __umul24(bt, bt);
+            sab += __umul24(a0, bt);
+        }
+        const double Sa = (double)sa, Saa = (double)saa, Sb = (double)sb, Sbb = (double)sbb, Sab = (double)sab;
         const double dN = (double)N;
         const double num = dN * Sab - Sa * Sb;
         const double va = dN * Saa - Sa * Sa;
         const double vb = dN * Sbb - Sb * Sb;
         const double dmin = ((a.opt.ncc_denom_min * 256.0) * dN) * dN;
         const double den = sqrt(va * vb);
-        sc = num / (den > dmin ? den : dmin);
+        const double sc = num / (den > dmin ? den : dmin);
         L.u.ev.score[lane] = sc;
+        q = (int)__builtin_rint(sc * 16777216.0);
     }
-    // the objective sums the views in order (std::accumulate), lane by lane
-    double sum = 0.0;
-    for (int k = 1; k < m; ++k) {
-        const long long bits = __double_as_longlong(sc);
-        const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffff), k);
-        const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), k);
-        sum = sum + (1.0 - __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo));
-    }
+    TMARK(L, 12);
+    // exact: |q| <= 2^24, at most 31 views
+    const int tot = __builtin_amdgcn_readlane((int)group_total<1>((uint32_t)q), 63);
     wave_sync();
-    return uni_f64(sum / (double)(m - 1));
+    TMARK(L, 14);
+    return (double)((long long)(m - 1) * 16777216ll - (long long)tot) * 0x1p-24;
 }
 
 // Nonlinear CG (or_fast.c fast_cg) as a state machine around ONE evaluation
@@ -696,6 +721,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
             xt1 = C.x[1] + st * C.u[1];
             xt2 = C.x[2] + st * C.u[2];
         }
+        TMARK(L, 15);
         const double ft = evaluate<G, NS, kTail, kMask>(a, L, S, sl, m, xt0, xt1, xt2);
         if (phase == kStart) {
             C.f = ft;
@@ -838,6 +864,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
     // work is dequeued in chunks of 4 (one atomic per chunk): the 4 children of
     // one parent, whose record is read once into LDS, or 4 consecutive patches
     uint32_t chunk_idx = 0xffffffffu, q4 = 4;
+#ifdef DP_FAST_TIMING
+    for (int k = 0; k < 16; ++k)
+        L.tm[k] = 0;
+    L.tlast = __builtin_readcyclecounter();
+    const unsigned long long t_start = L.tlast;
+#endif
     for (;;) {
         if (q4 == 4) {
             uint32_t c = 0;
@@ -854,6 +886,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                 wave_sync();
             }
         }
+        TMARK(L, 0);
         const uint32_t idx = chunk_idx * 4u + q4++;
         if (idx >= (uint32_t)a.n) {
             q4 = 4;
@@ -893,6 +926,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
             const dpg::ViewDev &rv = a.views[ref];
             make_frame(rv, p.pos, p.normal, a.cell, L.F);
             wave_sync();
+            TMARK(L, 1);
             if (kMode == DP_MODE_FAST_EVAL) {
                 Staged S;
                 const bool degen = L.F.degenerate;
@@ -922,6 +956,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                     const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S, wave_bytes, wave_clip);
                     if (m >= 2) {
                         const int E = cg_refine<G, NS, kTail, kMask>(a, L, S, sl, m);
+                        TMARK(L, 5);
                         p.evals += (uint32_t)E;
                         wave_vev += (unsigned long long)E * (unsigned long long)m;
                         const Frame &F = L.F;
@@ -949,9 +984,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                     p.vis[1] = L.vis[1];
                     p.cand[0] = L.cand[0];
                     p.cand[1] = L.cand[1];
+                    TMARK(L, 6);
                     // fast filter: re-staged at the new pose, margin 0
                     make_frame(rv, p.pos, p.normal, a.cell, L.F);
                     wave_sync();
+                    TMARK(L, 7);
                     Staged S;
                     const bool degen = L.F.degenerate;
                     const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes, wave_clip);
@@ -989,6 +1026,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                     }
                 }
             }
+            TMARK(L, 8);
             if (ok)
                 p.flags |= DP_PATCH_ACCEPTED;
             else
@@ -1010,7 +1048,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                 a.accept[idx] = ok ? 1 : 0;
         }
         wave_sync();
+        TMARK(L, 9);
     }
+#ifdef DP_FAST_TIMING
+    if (lane == 0 && (blockIdx.x & 511) == 0)
+        printf("TM blk %d patches %llu total %llu r0 %llu r1 %llu r2 %llu r3 %llu r4 %llu r5 %llu r6 %llu r7 %llu r8 %llu "
+               "r9 %llu r10 %llu r11 %llu r12 %llu r13 %llu r14 %llu r15 %llu\n",
+               (int)blockIdx.x, wave_patches, __builtin_readcyclecounter() - t_start, L.tm[0], L.tm[1], L.tm[2], L.tm[3],
+               L.tm[4], L.tm[5], L.tm[6], L.tm[7], L.tm[8], L.tm[9], L.tm[10], L.tm[11], L.tm[12], L.tm[13],
+               L.tm[14], L.tm[15]);
+#endif
     if (lane == 0 && a.evals)
         atomicAdd(a.evals, wave_evals);
     if (lane == 0 && a.stats) {

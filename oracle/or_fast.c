@@ -10,8 +10,9 @@
  * methods/pmvs/optimization_opencv.cpp:44-78 (DownhillSolver over
  * (depth, roll, pitch)) and samples the n x n window of optimization.cpp:14-56
  * from a gray plane, keeping the reference's objective (functor calc,
- * optimization_opencv.cpp:14-39: mean of 1 - NCC against texture 0, the
- * lowest-index scored view) and its NCC formula (error_measurements.cpp:36-60
+ * optimization_opencv.cpp:14-39: 1 - NCC against texture 0, the lowest-index
+ * scored view, over the other views; summed, NCCs in 2^-24 steps) and its NCC
+ * formula (error_measurements.cpp:36-60
  * with the 0.1 denominator floor).  What differs, by design:
  *   - samples come from per-view TILES of the gray plane staged once per patch
  *     (the initial window's bounding box plus `margin` pixels, BORDER_REPLICATE
@@ -323,7 +324,9 @@ static double fast_ncc(int64_t N, int64_t Sa, int64_t Saa, int64_t Sb, int64_t S
     return (double)num / d;
 }
 
-/* objective at scaled pose x; scores[k-1] = NCC of staged view k (k >= 1) */
+/* objective at scaled pose x: the functor calc's sum of (1 - NCC) over the
+ * views scored against texture 0 (without its division by m - 1, a constant
+ * of the refine), NCCs in 2^-24 steps; scores[k-1] = NCC of staged view k */
 static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_min, const double x[3],
                              double *scores)
 {
@@ -339,7 +342,7 @@ static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_mi
         Saa += (int64_t)a[i] * a[i];
     }
     const double dmin = ncc_denom_min * 256.0 * (double)N * (double)N;
-    double sum = 0.0;
+    int64_t qsum = 0;
     for (int k = 1; k < m; ++k) {
         fast_sample(&fp->fv[k], cell, df, af, bf, b);
         int64_t Sb = 0, Sbb = 0, Sab = 0;
@@ -350,9 +353,11 @@ static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_mi
         }
         const double ncc = fast_ncc(N, Sa, Saa, Sb, Sbb, Sab, dmin);
         if (scores) scores[k - 1] = ncc;
-        sum = sum + (1.0 - ncc);
+        qsum += (int64_t)nearbyint(ncc * 16777216.0);
     }
-    return sum / (double)(m - 1);
+    /* sum over the views of (1 - NCC), each NCC rounded to a multiple of 2^-24
+     * and summed exactly (so the value does not depend on the order) */
+    return (double)((int64_t)(m - 1) * 16777216 - qsum) * 0x1p-24;
 }
 
 /* nonlinear CG (Polak-Ribiere+) with forward differences and a two-probe
