@@ -576,7 +576,7 @@ __device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
 // Leaves NCC of rank r (r >= 1) in L.u.ev.score[r]; returns the objective
 // (uniform): the sum over r >= 1 of 1 - NCC_r, NCCs in 2^-24 steps, which is
 // an exact integer reduction across the wave.
-template <int G, int NS, bool kTail, bool kMask, int kBudget>
+template <int G, int NS, bool kTail, bool kMask, bool kScore, int kBudget>
 __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m, double x0,
                            double x1, double x2)
 {
@@ -678,17 +678,27 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
         const double va = dN * Saa - Sa * Sa;
         const double vb = dN * Sbb - Sb * Sb;
         const double dmin = ((a.opt.ncc_denom_min * 256.0) * dN) * dN;
-        const double den = sqrt(va * vb);
-        const double sc = num / (den > dmin ? den : dmin);
-        L.u.ev.score[lane] = sc;
-        q = (int)__builtin_rint(sc * 16777216.0);
+        if (kScore) {
+            // the reported score (filter, FAST_EVAL): fp64 finish
+            const double den = sqrt(va * vb);
+            L.u.ev.score[lane] = num / (den > dmin ? den : dmin);
+        } else {
+            // the refine's objective term: fp32 finish in 2^-24 steps
+            const float den = __builtin_sqrtf((float)va * (float)vb);
+            const float dminf = (float)dmin;
+            q = (int)__builtin_rintf(((float)num / (den > dminf ? den : dminf)) * 16777216.0f);
+        }
     }
     TMARK(L, 12);
+    if (kScore) {
+        wave_sync();
+        return 0.0;
+    }
     // exact: |q| <= 2^24, at most 31 views
     const int tot = __builtin_amdgcn_readlane((int)group_total<1>((uint32_t)q), 63);
     wave_sync();
     TMARK(L, 14);
-    return (double)((long long)(m - 1) * 16777216ll - (long long)tot) * 0x1p-24;
+    return (double)((m - 1) * 16777216 - tot) * 0x1p-24; // < 2^29
 }
 
 // Nonlinear CG (or_fast.c fast_cg) as a state machine around ONE evaluation
@@ -699,7 +709,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
 {
     enum { kStart = 0, kFd0 = 1, kFd2 = 3, kProbe1 = 4, kProbe2 = 5 };
     CgState &C = L.cg;
-    const double h = (double)a.fo.fd_step;
+    const double h = (double)a.fo.fd_step, inv_h = 1.0 / h;
     for (int k = 0; k < 3; ++k) {
         C.x[k] = 0.0;
         C.gp[k] = 0.0;
@@ -722,7 +732,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
             xt2 = C.x[2] + st * C.u[2];
         }
         TMARK(L, 15);
-        const double ft = evaluate<G, NS, kTail, kMask>(a, L, S, sl, m, xt0, xt1, xt2);
+        const double ft = evaluate<G, NS, kTail, kMask, false>(a, L, S, sl, m, xt0, xt1, xt2);
         if (phase == kStart) {
             C.f = ft;
             E = 1;
@@ -730,7 +740,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
                 break;
             phase = kFd0;
         } else if (phase >= kFd0 && phase <= kFd2) {
-            C.g[phase - kFd0] = (ft - C.f) / h;
+            C.g[phase - kFd0] = (ft - C.f) * inv_h;
             if (phase < kFd2) {
                 ++phase;
                 continue;
@@ -752,13 +762,13 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
                 d1 = 0.0 - g1;
                 d2 = 0.0 - g2;
             }
-            const double nd = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+            const double inv_nd = 1.0 / sqrt((d0 * d0 + d1 * d1) + d2 * d2);
             C.d[0] = d0;
             C.d[1] = d1;
             C.d[2] = d2;
-            C.u[0] = d0 / nd;
-            C.u[1] = d1 / nd;
-            C.u[2] = d2 / nd;
+            C.u[0] = d0 * inv_nd;
+            C.u[1] = d1 * inv_nd;
+            C.u[2] = d2 * inv_nd;
             phase = kProbe1;
         } else if (phase == kProbe1) {
             C.f1 = ft;
@@ -937,7 +947,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                 ok = m >= 2;
                 wave_vev += ok ? (unsigned long long)m : 0ull;
                 if (ok) {
-                    evaluate<G, NS, kTail, kMask>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                    evaluate<G, NS, kTail, kMask, true>(a, L, S, sl, m, 0.0, 0.0, 0.0);
                     double sum = 0.0;
                     for (int k = 1; k < m; ++k)
                         sum = sum + L.u.ev.score[k];
@@ -1003,7 +1013,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                         p.vis[1] = (m == 1 && v >= 64) ? (1ull << (v - 64)) : 0ull;
                         ok = m >= a.opt.min_visible;
                     } else {
-                        evaluate<G, NS, kTail, kMask>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                        evaluate<G, NS, kTail, kMask, true>(a, L, S, sl, m, 0.0, 0.0, 0.0);
                         double sum = 0.0;
                         for (int k = 1; k < m; ++k)
                             sum = sum + L.u.ev.score[k];

@@ -24,7 +24,8 @@
  *     `iters` nonlinear conjugate-gradient steps (Polak-Ribiere+, forward-
  *     difference gradient, a two-probe line search); E = 1 + 5 * iters;
  *   - samples are bilinear in 1/32 px with 1/16 gray-level output, moments are
- *     exact integers, the NCC finish is fp64.
+ *     exact integers; the refine's NCC finish is fp32 (quantised to 2^-24),
+ *     the reported scores' is fp64.
  * Arithmetic: fp32 with explicit fmaf where written, every other line one
  * IEEE rounding (-ffp-contract=off); fp64 for the per-patch setup, the NCC
  * finish and the CG state.
@@ -324,9 +325,22 @@ static double fast_ncc(int64_t N, int64_t Sa, int64_t Saa, int64_t Sb, int64_t S
     return (double)num / d;
 }
 
+/* the refine's NCC in 2^-24 steps: the exact moments rounded to fp32, IEEE
+ * fp32 square root and quotient, the 0.1 floor as fp32 */
+static int32_t fast_ncc_q(int64_t N, int64_t Sa, int64_t Saa, int64_t Sb, int64_t Sbb, int64_t Sab, float dminf)
+{
+    const int64_t num = N * Sab - Sa * Sb;
+    const int64_t va = N * Saa - Sa * Sa;
+    const int64_t vb = N * Sbb - Sb * Sb;
+    const float den = sqrtf((float)va * (float)vb);
+    const float d = den > dminf ? den : dminf;
+    return (int32_t)rintf(((float)num / d) * 16777216.0f);
+}
+
 /* objective at scaled pose x: the functor calc's sum of (1 - NCC) over the
  * views scored against texture 0 (without its division by m - 1, a constant
- * of the refine), NCCs in 2^-24 steps; scores[k-1] = NCC of staged view k */
+ * of the refine), NCCs in 2^-24 steps; scores[k-1] = the fp64 NCC of staged
+ * view k (the scores the filter and FAST_EVAL report) */
 static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_min, const double x[3],
                              double *scores)
 {
@@ -342,6 +356,7 @@ static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_mi
         Saa += (int64_t)a[i] * a[i];
     }
     const double dmin = ncc_denom_min * 256.0 * (double)N * (double)N;
+    const float dminf = (float)dmin;
     int64_t qsum = 0;
     for (int k = 1; k < m; ++k) {
         fast_sample(&fp->fv[k], cell, df, af, bf, b);
@@ -351,12 +366,11 @@ static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_mi
             Sbb += (int64_t)b[i] * b[i];
             Sab += (int64_t)a[i] * b[i];
         }
-        const double ncc = fast_ncc(N, Sa, Saa, Sb, Sbb, Sab, dmin);
-        if (scores) scores[k - 1] = ncc;
-        qsum += (int64_t)nearbyint(ncc * 16777216.0);
+        if (scores) scores[k - 1] = fast_ncc(N, Sa, Saa, Sb, Sbb, Sab, dmin);
+        qsum += fast_ncc_q(N, Sa, Saa, Sb, Sbb, Sab, dminf);
     }
-    /* sum over the views of (1 - NCC), each NCC rounded to a multiple of 2^-24
-     * and summed exactly (so the value does not depend on the order) */
+    /* sum over the views of (1 - NCC), each NCC (fp32) rounded to a multiple
+     * of 2^-24 and summed exactly (so the value does not depend on the order) */
     return (double)((int64_t)(m - 1) * 16777216 - qsum) * 0x1p-24;
 }
 
@@ -367,7 +381,7 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
     x[0] = x[1] = x[2] = 0.0;
     double f = fast_objective(fp, cell, dmin0, x, NULL);
     int E = 1;
-    const double h = (double)fo->fd_step;
+    const double h = (double)fo->fd_step, inv_h = 1.0 / h;
     double alpha = (double)fo->ls_step;
     double gp[3] = {0, 0, 0}, dp[3] = {0, 0, 0}, ggp = 0.0;
     for (int it = 0; it < fo->iters; ++it) {
@@ -375,7 +389,7 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
         for (int i = 0; i < 3; ++i) {
             double xt[3] = {x[0], x[1], x[2]};
             xt[i] = x[i] + h;
-            g[i] = (fast_objective(fp, cell, dmin0, xt, NULL) - f) / h;
+            g[i] = (fast_objective(fp, cell, dmin0, xt, NULL) - f) * inv_h;
         }
         E += 3;
         const double gg = (g[0] * g[0] + g[1] * g[1]) + g[2] * g[2];
@@ -389,9 +403,9 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
         for (int i = 0; i < 3; ++i) d[i] = beta * dp[i] - g[i];
         if ((d[0] * g[0] + d[1] * g[1]) + d[2] * g[2] >= 0.0)
             for (int i = 0; i < 3; ++i) d[i] = 0.0 - g[i];
-        const double nd = sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+        const double inv_nd = 1.0 / sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
         double u[3];
-        for (int i = 0; i < 3; ++i) u[i] = d[i] / nd;
+        for (int i = 0; i < 3; ++i) u[i] = d[i] * inv_nd;
         double x1[3], x2[3];
         for (int i = 0; i < 3; ++i) x1[i] = x[i] + alpha * u[i];
         const double f1 = fast_objective(fp, cell, dmin0, x1, NULL);
