@@ -59,10 +59,17 @@ struct StageRec {
     int32_t pad;
 };
 
-// per evaluation, per staged view: A.xyz umax | B1.xyz vmax | B2.xyz info
+// per evaluation, per staged view: A.xyz 2^23+umax | B1.xyz 2^23+vmax | B2.xyz
+// tile byte offset (less the row term of the 2^23 exponent bits)
 struct EvalRec {
     float4 q[3];
 };
+
+// row bytes of a tile from its biased umax = 2^23 + 32 (tw - 1): 4 ((tw + 2) / 2)
+__device__ __forceinline__ uint32_t tile_rowb(float umax_b)
+{
+    return (((__float_as_uint(umax_b) & 0x7fffffu) >> 5) + 3u) >> 1 << 2;
+}
 
 // patch frame (uniform, fp64): or_fast.c fast_stage
 struct Frame {
@@ -508,7 +515,8 @@ struct Tap {
     uint32_t w0, w1;   // packed bilinear weights of the two rows
 };
 
-__device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, const float4 &qc, float ti, float tj)
+__device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, const float4 &qc, uint32_t off,
+                                       uint32_t rowb, float ti, float tj)
 {
     typedef float f2 __attribute__((ext_vector_type(2)));
     // (hx, hy) as packed fp32 FMAs (v_pk_fma_f32: two fmaf roundings each)
@@ -518,20 +526,18 @@ __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, cons
     float hz = __builtin_fmaf(tj, qc.z, __builtin_fmaf(ti, qb.z, qa.z));
     hz = __builtin_fmaxf(hz, 0x1p-20f);
     const float rz = recip_rn(hz);
-    const f2 uv = hxy * (f2){rz, rz};
-    const float U = __builtin_amdgcn_fmed3f(uv.x, 0.0f, qa.w);
-    const float V = __builtin_amdgcn_fmed3f(uv.y, 0.0f, qb.w);
-    // U + 2^23 holds rint(U) (U < 2^22) in its low mantissa bits: the pixel
-    // and 1/32 fraction are bit fields of it (the exponent bits lie above them)
-    const f2 m = (f2){U, V} + (f2){8388608.0f, 8388608.0f};
-    const uint32_t bu = __float_as_uint(m.x), bv = __float_as_uint(m.y);
-    const uint32_t info = __float_as_uint(qc.w);
-    const uint32_t rowb = info >> 16;
-    const uint32_t y0 = __builtin_amdgcn_ubfe(bv, 5, 17);
+    // U, V rounded to integers by one FMA with 2^23 (spacing 1 in [2^23, 2^24))
+    // and clamped to [2^23, 2^23 + umax]: rint(U) and rint(V) are the low
+    // mantissa bits, the pixel and its 1/32 fraction bit fields of them
+    const f2 m = __builtin_elementwise_fma(hxy, (f2){rz, rz}, (f2){0x1p23f, 0x1p23f});
+    const uint32_t bu = __float_as_uint(__builtin_amdgcn_fmed3f(m.x, 0x1p23f, qa.w));
+    const uint32_t bv = __float_as_uint(__builtin_amdgcn_fmed3f(m.y, 0x1p23f, qb.w));
     Tap t;
+    // row: bv >> 5 is y0 plus the exponent bits' 0x2580000, whose 24-bit part
+    // times the row bytes is taken off the view's offset (u32 wrap-around);
     // aligned word of the pair: byte (x0 >> 1) * 4 of the row; x0 odd -> the
     // pair straddles two words, shifted by 16 bits
-    t.a0 = __umul24(y0, rowb) + ((bu >> 4) & 0x3FFFCu) + (info & 0xffffu);
+    t.a0 = __umul24(bv >> 5, rowb) + (((bu >> 4) & 0x3FFFCu) + off);
     t.a1 = t.a0 + rowb;
     t.sh = (bu >> 1) & 16u;
     const uint32_t fx = bu & 31u, fy = bv & 31u;
@@ -588,15 +594,17 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
     if (lane < m) {
         EvalRec &E = L.u.ev.par[lane];
         E.q[0] = make_float4(__builtin_fmaf(df, S.v[3], S.v[0]), __builtin_fmaf(df, S.v[4], S.v[1]),
-                             __builtin_fmaf(df, S.v[5], S.v[2]), S.umax);
+                             __builtin_fmaf(df, S.v[5], S.v[2]), 0x1p23f + S.umax);
         E.q[1] = make_float4(__builtin_fmaf(-af, S.v[12], S.v[6]), __builtin_fmaf(-af, S.v[13], S.v[7]),
-                             __builtin_fmaf(-af, S.v[14], S.v[8]), S.vmax);
+                             __builtin_fmaf(-af, S.v[14], S.v[8]), 0x1p23f + S.vmax);
         E.q[2] = make_float4(__builtin_fmaf(-bf, S.v[12], S.v[9]), __builtin_fmaf(-bf, S.v[13], S.v[10]),
-                             __builtin_fmaf(-bf, S.v[14], S.v[11]), __uint_as_float(S.info));
+                             __builtin_fmaf(-bf, S.v[14], S.v[11]),
+                             __uint_as_float((S.info & 0xffffu) -
+                                             __umul24((0x4B000000u >> 5) & 0xffffffu, S.info >> 16)));
     }
     wave_sync();
     TMARK(L, 10);
-    const int j = lane / LP, g = lane & (LP - 1);
+    const int j = (int)((unsigned)lane / LP), g = lane & (LP - 1);
     const char *tiles = (const char *)L.tiles;
     uint32_t av[NS];
     // kTail: the last sample of every view (N = NS LP + 1), one lane per view
@@ -609,13 +617,15 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
         const bool tail = kTail && p == 0;
         const EvalRec &E = L.u.ev.par[act ? r : 0];
         const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
+        const uint32_t off = __float_as_uint(qc.w), rowb = tile_rowb(qa.w);
         Tap tp[NS], tt{};
 #pragma unroll
         for (int k = 0; k < NS; ++k)
-            tp[k] = tap_addr(qa, qb, qc, sl.ti[k], sl.tj[k]);
+            tp[k] = tap_addr(qa, qb, qc, off, rowb, sl.ti[k], sl.tj[k]);
         if (tail) {
             const EvalRec &T = L.u.ev.par[lane < m ? lane : 0];
-            tt = tap_addr(T.q[0], T.q[1], T.q[2], sl.tail, sl.tail);
+            const float4 ta = T.q[0], tb = T.q[1], tc = T.q[2];
+            tt = tap_addr(ta, tb, tc, __float_as_uint(tc.w), tile_rowb(ta.w), sl.tail, sl.tail);
         }
         __builtin_amdgcn_sched_barrier(0);
         TapWords tw[NS], twt{};
@@ -638,12 +648,12 @@ __device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged 
             for (int k = 0; k < NS; ++k)
                 av[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(g << 2, (int)b[k]);
         }
-        uint32_t s = 0, ss = 0, sx = 0;
+        uint32_t s = b[0], ss = __umul24(b[0], b[0]), sx = __umul24(av[0], b[0]);
 #pragma unroll
-        for (int k = 0; k < NS; ++k) {
+        for (int k = 1; k < NS; ++k) {
             s += b[k];
-            ss += __umul24(b[k], b[k]);
-            sx += __umul24(av[k], b[k]);
+            ss = __umul24(b[k], b[k]) + ss;
+            sx = __umul24(av[k], b[k]) + sx;
         }
         s = group_total<G>(s);
         ss = group_total<G>(ss);

@@ -298,10 +298,12 @@ static void fast_sample(const fast_view *t, int cell, float df, float af, float 
             float hz = fmaf(tj, B2[2], fmaf(ti, B1[2], A[2]));
             hz = fmaxf(hz, 0x1p-20f);
             const float rz = 1.0f / hz;
-            float U = hx * rz, V = hy * rz;
-            U = fminf(fmaxf(U, 0.0f), t->umax);
-            V = fminf(fmaxf(V, 0.0f), t->vmax);
-            const int iu = (int)rintf(U), iv = (int)rintf(V);
+            /* U, V in 1/32 px rounded to integers by one fused multiply-add
+             * with 2^23 (fp32 spacing 1 in [2^23, 2^24)), then clamped to the
+             * tile: iu = rint(clamp(U)) without a second rounding */
+            const float Ub = fminf(fmaxf(fmaf(hx, rz, 0x1p23f), 0x1p23f), 0x1p23f + t->umax);
+            const float Vb = fminf(fmaxf(fmaf(hy, rz, 0x1p23f), 0x1p23f), 0x1p23f + t->vmax);
+            const int iu = (int)(Ub - 0x1p23f), iv = (int)(Vb - 0x1p23f);
             const int x0 = iu >> 5, fx = iu & 31, y0 = iv >> 5, fy = iv & 31;
             const uint16_t e0 = t->tile[y0 * (t->tw + 1) + x0];
             const uint16_t e1 = t->tile[y0 * (t->tw + 1) + x0 + 1];

@@ -127,9 +127,10 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
                 h = [_fmaf(tj, B2[k], _fmaf(ti, B1[k], A[k])) for k in range(3)]
                 hz = max(h[2], np.float32(2.0 ** -20))
                 rz = np.float32(1.0) / hz
-                U = min(max(np.float32(h[0] * rz), np.float32(0)), np.float32(32 * (tw - 1)))
-                W = min(max(np.float32(h[1] * rz), np.float32(0)), np.float32(32 * (th - 1)))
-                iu, iv = int(np.rint(U)), int(np.rint(W))
+                b23 = np.float32(2.0 ** 23)
+                U = min(max(_fmaf(h[0], rz, b23), b23), b23 + np.float32(32 * (tw - 1)))
+                W = min(max(_fmaf(h[1], rz, b23), b23), b23 + np.float32(32 * (th - 1)))
+                iu, iv = int(U - b23), int(W - b23)
                 xx, fx, yy, fy = iu >> 5, iu & 31, iv >> 5, iv & 31
 
                 def px(x, y):
