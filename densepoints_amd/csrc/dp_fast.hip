@@ -1330,8 +1330,8 @@ extern "C" void dp_default_fast_options(dp_fast_options *f)
         return;
     *f = dp_fast_options{};
     f->iters = 4;
-    f->margin = 3;
-    f->tile_budget = kFastBudget;
+    f->margin = 2;
+    f->tile_budget = 6144; // 4 waves per SIMD (the 6 KiB arena); up to kFastBudget
     f->max_views = dpk::kFastMaxV;
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;

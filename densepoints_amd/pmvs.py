@@ -47,8 +47,8 @@ class FastOptions:
     with a conjugate-gradient refine on LDS-staged gray tiles)."""
 
     iters: int = 4            # CG iterations: E = 1 + 5 iters (+1 filter evaluation)
-    margin: int = 3           # tile margin around the initial window, pixels (<= 7)
-    tile_budget: int = 16384  # bytes of LDS tiles per patch (<= 16384)
+    margin: int = 2           # tile margin around the initial window, pixels (<= 7)
+    tile_budget: int = 6144   # bytes of LDS tiles per patch (<= 16384; <= 6144: 4 waves/SIMD)
     max_views: int = 32       # staged views per patch (<= 32)
     fd_step: float = 0.5      # forward-difference step, scaled units
     ls_step: float = 1.0      # initial line-search step, scaled units

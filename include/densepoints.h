@@ -394,8 +394,13 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  *    bytes, then the longest fitting prefix of views is kept), copied once
  *    into LDS and used for the whole refine; samples clamp to the tile
  *    (BORDER_REPLICATE);
- *  - sample: projective map in fp32 (fmaf), 1/32 px, bilinear on 8-bit gray,
- *    result in 1/16 gray levels; exact integer moments; fp64 NCC finish;
+ *  - sample: projective map in fp32 (fmaf), 1/32 px (U, V rounded to
+ *    integers by one fmaf with 2^23, clamped to the tile), bilinear on 8-bit
+ *    gray, result in 1/16 gray levels; exact integer moments;
+ *  - refine objective: the sum over the scored views of 1 - NCC, each NCC
+ *    finished in fp32 and rounded to a multiple of 2^-24, summed exactly (the
+ *    functor calc's mean without its constant 1/(m-1)); reported scores
+ *    (FAST_EVAL, filter) use an fp64 finish;
  *  - refine: `iters` Polak-Ribiere+ conjugate-gradient steps with a forward-
  *    difference gradient (step fd_step) and a two-probe line search (initial
  *    step ls_step, doubled on success, halved on failure): E = 1 + 5 iters;
@@ -406,8 +411,9 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  * dp_refine_batch[_device] run DP_MODE_FAST_* with `cell` in [2, 16]. */
 typedef struct dp_fast_options {
     int32_t iters;        /* 4     CG iterations                                    */
-    int32_t margin;       /* 3     tile margin around the initial window, px       */
-    int32_t tile_budget;  /* 16384 bytes of LDS tiles per patch (kernel arena)     */
+    int32_t margin;       /* 2     tile margin around the initial window, px       */
+    int32_t tile_budget;  /* 6144  bytes of LDS tiles per patch (<= 16384; the
+                                   kernel's arena is 6, 8 or 16 KiB by this value) */
     int32_t max_views;    /* 32    staged views per patch (<= 32)                   */
     float fd_step;        /* 0.5   forward-difference step, scaled units            */
     float ls_step;        /* 1.0   initial line-search step, scaled units           */

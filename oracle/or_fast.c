@@ -49,8 +49,8 @@ void or_fast_default_options(or_fast_options *f)
 {
     memset(f, 0, sizeof(*f));
     f->iters = 4;
-    f->margin = 3;
-    f->tile_budget = 16384;
+    f->margin = 2;
+    f->tile_budget = 6144;
     f->max_views = FAST_MAX_VIEWS;
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;
