@@ -179,6 +179,7 @@ extern "C" int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out)
         c->opt = *opt;
     else
         dp_default_options(&c->opt);
+    dp_default_fast_options(&c->fopt);
     int rc = check_options(c, c->opt);
     if (rc != DP_OK) {
         delete c;

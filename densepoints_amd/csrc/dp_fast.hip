@@ -82,9 +82,13 @@ struct Frame {
 
 // conjugate-gradient state between evaluations (uniform, kept in LDS so the
 // sampling passes have the registers)
+constexpr int kFastPoses = 4;  // poses per batched evaluation (start + 3 differences)
+constexpr int kFastItems = 44; // (view, pose) records per pass set (the staging union's room)
+
 struct CgState {
     double x[3], x1[3], g[3], gp[3], d[3], dp[3], u[3];
     double f, f1, gg, ggp, alpha;
+    double px[kFastPoses][3], fr[kFastPoses]; // poses to evaluate, their objectives
 };
 
 template <int kBudget> struct FastLds {
@@ -92,8 +96,8 @@ template <int kBudget> struct FastLds {
     union {
         StageRec st[kFastMaxV]; // during staging
         struct {
-            EvalRec par[kFastMaxV];
-            uint32_t mom[kFastMaxV][4];
+            EvalRec par[kFastItems];
+            uint32_t mom[kFastItems][4];
             double score[kFastMaxV];
         } ev;
     } u;
@@ -578,146 +582,180 @@ __device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
     return b >> 6;
 }
 
-// One objective evaluation at scaled pose x (or_fast.c fast_objective).
-// Leaves NCC of rank r (r >= 1) in L.u.ev.score[r]; returns the objective
-// (uniform): the sum over r >= 1 of 1 - NCC_r, NCCs in 2^-24 steps, which is
-// an exact integer reduction across the wave.
+// Objective evaluations at up to kFastPoses scaled poses (or_fast.c
+// fast_objective), L.cg.px[0 .. K-1] -> L.cg.fr[0 .. K-1] (uniform).  The
+// poses' (view, pose) items share the sampling passes: item i = r K' + k
+// (view r, pose k of a chunk of K' poses) runs in pass i / G, group i % G, so
+// the K' anchors (r = 0) are the first K' groups of pass 0 and every item's
+// anchor samples come from group k of pass 0 by ds_bpermute.  A chunk holds
+// at most kFastItems items (the LDS records) and K' <= G poses.  kScore (one
+// pose): the fp64 NCC of rank r >= 1 goes to L.u.ev.score[r] instead.
 template <int G, int NS, bool kTail, bool kMask, bool kScore, int kBudget>
-__device__ double evaluate(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m, double x0,
-                           double x1, double x2)
+__device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m, int K)
 {
     constexpr int LP = 64 / G;
     const int lane = lane_id();
-    if (m < 2)
-        return 2.0;
-    const float df = (float)(x0 * L.F.sd), af = (float)(x1 * L.F.st), bf = (float)(x2 * L.F.st);
-    if (lane < m) {
-        EvalRec &E = L.u.ev.par[lane];
-        E.q[0] = make_float4(__builtin_fmaf(df, S.v[3], S.v[0]), __builtin_fmaf(df, S.v[4], S.v[1]),
-                             __builtin_fmaf(df, S.v[5], S.v[2]), 0x1p23f + S.umax);
-        E.q[1] = make_float4(__builtin_fmaf(-af, S.v[12], S.v[6]), __builtin_fmaf(-af, S.v[13], S.v[7]),
-                             __builtin_fmaf(-af, S.v[14], S.v[8]), 0x1p23f + S.vmax);
-        E.q[2] = make_float4(__builtin_fmaf(-bf, S.v[12], S.v[9]), __builtin_fmaf(-bf, S.v[13], S.v[10]),
-                             __builtin_fmaf(-bf, S.v[14], S.v[11]),
-                             __uint_as_float((S.info & 0xffffu) -
-                                             __umul24((0x4B000000u >> 5) & 0xffffffu, S.info >> 16)));
+    if (m < 2) {
+        for (int k = 0; k < K; ++k)
+            L.cg.fr[k] = 2.0;
+        wave_sync();
+        return;
     }
-    wave_sync();
-    TMARK(L, 10);
+    // poses per chunk: K' <= G (anchors in pass 0), K' m <= kFastItems
+    int kc = kFastItems / m;
+    kc = kc < G ? kc : G;
+    kc = kc < kFastPoses ? kc : kFastPoses;
+    kc = kScore ? 1 : kc;
     const int j = (int)((unsigned)lane / LP), g = lane & (LP - 1);
     const char *tiles = (const char *)L.tiles;
-    uint32_t av[NS];
-    // kTail: the last sample of every view (N = NS LP + 1), one lane per view
-    // (m <= 32), computed alongside the first pass and kept in a register
-    uint32_t bt = 0;
-    const int passes = (m + G - 1) / G;
-    for (int p = 0; p < passes; ++p) {
-        const int r = p * G + j;
-        const bool act = r < m;
-        const bool tail = kTail && p == 0;
-        const EvalRec &E = L.u.ev.par[act ? r : 0];
-        const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
-        const uint32_t off = __float_as_uint(qc.w), rowb = tile_rowb(qa.w);
-        Tap tp[NS], tt{};
-#pragma unroll
-        for (int k = 0; k < NS; ++k)
-            tp[k] = tap_addr(qa, qb, qc, off, rowb, sl.ti[k], sl.tj[k]);
-        if (tail) {
-            const EvalRec &T = L.u.ev.par[lane < m ? lane : 0];
-            const float4 ta = T.q[0], tb = T.q[1], tc = T.q[2];
-            tt = tap_addr(ta, tb, tc, __float_as_uint(tc.w), tile_rowb(ta.w), sl.tail, sl.tail);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        TapWords tw[NS], twt{};
-#pragma unroll
-        for (int k = 0; k < NS; ++k)
-            tw[k] = tap_load(tiles, tp[k]);
-        if (tail)
-            twt = tap_load(tiles, tt);
-        __builtin_amdgcn_sched_barrier(0);
-        uint32_t b[NS];
-#pragma unroll
-        for (int k = 0; k < NS; ++k)
-            b[k] = kMask ? (tap_blend(tp[k], tw[k]) & sl.live[k]) : tap_blend(tp[k], tw[k]);
-        if (tail)
-            bt = tap_blend(tt, twt);
-        if (p == 0) {
-            // texture 0 = rank 0 = group 0 of the first pass: its samples reach
-            // every group through the LDS crossbar and stay in registers
-#pragma unroll
-            for (int k = 0; k < NS; ++k)
-                av[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(g << 2, (int)b[k]);
-        }
-        uint32_t s = b[0], ss = __umul24(b[0], b[0]), sx = __umul24(av[0], b[0]);
-#pragma unroll
-        for (int k = 1; k < NS; ++k) {
-            s += b[k];
-            ss = __umul24(b[k], b[k]) + ss;
-            sx = __umul24(av[k], b[k]) + sx;
-        }
-        s = group_total<G>(s);
-        ss = group_total<G>(ss);
-        sx = group_total<G>(sx);
-        if (g == LP - 1 && act) {
-            L.u.ev.mom[r][0] = s;
-            L.u.ev.mom[r][1] = ss;
-            L.u.ev.mom[r][2] = sx;
-        }
-    }
-    wave_sync();
-    TMARK(L, 11);
     const int N = a.cell * a.cell;
-    // the anchor's tail sample (lane 0 holds rank 0's)
-    const uint32_t a0 = kTail ? (uint32_t)__builtin_amdgcn_readfirstlane((int)bt) : 0u;
-    // NCC per view, one lane each: the integer moment products are below 2^53,
-    // so these fp64 expressions are exactly the spec's int64 ones
-    int q = 0;
-    if (lane >= 1 && lane < m) {
-        uint32_t sa = L.u.ev.mom[0][0], saa = L.u.ev.mom[0][1];
-        uint32_t sb = L.u.ev.mom[lane][0], sbb = L.u.ev.mom[lane][1], sab = L.u.ev.mom[lane][2];
-        if (kTail) {
-            sa += a0;
-            saa += __umul24(a0, a0);
-            sb += bt;
-            sbb += __umul24(bt, bt);
-            sab += __umul24(a0, bt);
+    const double dmin = ((a.opt.ncc_denom_min * 256.0) * (double)N) * (double)N;
+    for (int k0 = 0; k0 < K; k0 += kc) {
+        const int kn = K - k0 < kc ? K - k0 : kc;
+        const int Q = kn * m;
+        // 1/kn for item -> (view, pose): floor(i * ceil(2^16 / kn) / 2^16) = i / kn for i < 2^10
+        const uint32_t rk = (65536u + (uint32_t)kn - 1u) / (uint32_t)kn;
+        if (lane < m) {
+            for (int k = 0; k < kn; ++k) {
+                const float df = (float)(L.cg.px[k0 + k][0] * L.F.sd), af = (float)(L.cg.px[k0 + k][1] * L.F.st),
+                            bf = (float)(L.cg.px[k0 + k][2] * L.F.st);
+                EvalRec &E = L.u.ev.par[lane * kn + k];
+                E.q[0] = make_float4(__builtin_fmaf(df, S.v[3], S.v[0]), __builtin_fmaf(df, S.v[4], S.v[1]),
+                                     __builtin_fmaf(df, S.v[5], S.v[2]), 0x1p23f + S.umax);
+                E.q[1] = make_float4(__builtin_fmaf(-af, S.v[12], S.v[6]), __builtin_fmaf(-af, S.v[13], S.v[7]),
+                                     __builtin_fmaf(-af, S.v[14], S.v[8]), 0x1p23f + S.vmax);
+                E.q[2] = make_float4(__builtin_fmaf(-bf, S.v[12], S.v[9]), __builtin_fmaf(-bf, S.v[13], S.v[10]),
+                                     __builtin_fmaf(-bf, S.v[14], S.v[11]),
+                                     __uint_as_float((S.info & 0xffffu) -
+                                                     __umul24((0x4B000000u >> 5) & 0xffffffu, S.info >> 16)));
+            }
         }
-        const double Sa = (double)sa, Saa = (double)saa, Sb = (double)sb, Sbb = (double)sbb, Sab = (double)sab;
-        const double dN = (double)N;
-        const double num = dN * Sab - Sa * Sb;
-        const double va = dN * Saa - Sa * Sa;
-        const double vb = dN * Sbb - Sb * Sb;
-        const double dmin = ((a.opt.ncc_denom_min * 256.0) * dN) * dN;
-        if (kScore) {
-            // the reported score (filter, FAST_EVAL): fp64 finish
-            const double den = sqrt(va * vb);
-            L.u.ev.score[lane] = num / (den > dmin ? den : dmin);
-        } else {
-            // the refine's objective term: fp32 finish in 2^-24 steps
-            const float den = __builtin_sqrtf((float)va * (float)vb);
-            const float dminf = (float)dmin;
-            q = (int)__builtin_rintf(((float)num / (den > dminf ? den : dminf)) * 16777216.0f);
-        }
-    }
-    TMARK(L, 12);
-    if (kScore) {
         wave_sync();
-        return 0.0;
+        TMARK(L, 10);
+        uint32_t a0s[NS]; // pass 0's samples: group k holds pose k's anchor
+        // kTail: the last sample of every item (N = NS LP + 1), one lane per
+        // item (Q <= kFastItems < 64), computed alongside the first pass
+        uint32_t bt = 0;
+        const int passes = (Q + G - 1) / G;
+        for (int p = 0; p < passes; ++p) {
+            const int i = p * G + j;
+            const bool act = i < Q;
+            const bool tail = kTail && p == 0;
+            const int r = (int)(__umul24((uint32_t)i, rk) >> 16);
+            const int k = i - r * kn;
+            const EvalRec &E = L.u.ev.par[act ? i : 0];
+            const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
+            const uint32_t off = __float_as_uint(qc.w), rowb = tile_rowb(qa.w);
+            Tap tp[NS], tt{};
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2)
+                tp[s2] = tap_addr(qa, qb, qc, off, rowb, sl.ti[s2], sl.tj[s2]);
+            if (tail) {
+                const EvalRec &T = L.u.ev.par[lane < Q ? lane : 0];
+                const float4 ta = T.q[0], tb = T.q[1], tc = T.q[2];
+                tt = tap_addr(ta, tb, tc, __float_as_uint(tc.w), tile_rowb(ta.w), sl.tail, sl.tail);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            TapWords tw[NS], twt{};
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2)
+                tw[s2] = tap_load(tiles, tp[s2]);
+            if (tail)
+                twt = tap_load(tiles, tt);
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t b[NS];
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2)
+                b[s2] = kMask ? (tap_blend(tp[s2], tw[s2]) & sl.live[s2]) : tap_blend(tp[s2], tw[s2]);
+            if (tail)
+                bt = tap_blend(tt, twt);
+            if (p == 0) {
+#pragma unroll
+                for (int s2 = 0; s2 < NS; ++s2)
+                    a0s[s2] = b[s2];
+            }
+            // the anchor samples of this item's pose through the LDS crossbar
+            const int src = (k * LP + g) << 2;
+            uint32_t av[NS];
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2)
+                av[s2] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a0s[s2]);
+            uint32_t s = b[0], ss = __umul24(b[0], b[0]), sx = __umul24(av[0], b[0]);
+#pragma unroll
+            for (int s2 = 1; s2 < NS; ++s2) {
+                s += b[s2];
+                ss = __umul24(b[s2], b[s2]) + ss;
+                sx = __umul24(av[s2], b[s2]) + sx;
+            }
+            s = group_total<G>(s);
+            ss = group_total<G>(ss);
+            sx = group_total<G>(sx);
+            if (g == LP - 1 && act) {
+                L.u.ev.mom[i][0] = s;
+                L.u.ev.mom[i][1] = ss;
+                L.u.ev.mom[i][2] = sx;
+            }
+        }
+        wave_sync();
+        TMARK(L, 11);
+        // NCC per item, one lane each (lane t: view t / kn, pose t % kn): the
+        // integer moment products are below 2^53, so these fp64 expressions
+        // are exactly the spec's int64 ones
+        const int rt = (int)(__umul24((uint32_t)lane, rk) >> 16);
+        const int kt = lane - rt * kn;
+        // the tail sample of the item's anchor (lane kt holds item kt's)
+        const uint32_t a0 = kTail ? (uint32_t)__builtin_amdgcn_ds_bpermute(kt << 2, (int)bt) : 0u;
+        int q = 0;
+        if (lane < Q && rt >= 1) {
+            uint32_t sa = L.u.ev.mom[kt][0], saa = L.u.ev.mom[kt][1];
+            uint32_t sb = L.u.ev.mom[lane][0], sbb = L.u.ev.mom[lane][1], sab = L.u.ev.mom[lane][2];
+            if (kTail) {
+                sa += a0;
+                saa += __umul24(a0, a0);
+                sb += bt;
+                sbb += __umul24(bt, bt);
+                sab += __umul24(a0, bt);
+            }
+            const double Sa = (double)sa, Saa = (double)saa, Sb = (double)sb, Sbb = (double)sbb, Sab = (double)sab;
+            const double dN = (double)N;
+            const double num = dN * Sab - Sa * Sb;
+            const double va = dN * Saa - Sa * Sa;
+            const double vb = dN * Sbb - Sb * Sb;
+            if (kScore) {
+                // the reported score (filter, FAST_EVAL): fp64 finish
+                const double den = sqrt(va * vb);
+                L.u.ev.score[rt] = num / (den > dmin ? den : dmin);
+            } else {
+                // the refine's objective term: fp32 finish in 2^-24 steps
+                const float den = __builtin_sqrtf((float)va * (float)vb);
+                const float dminf = (float)dmin;
+                q = (int)__builtin_rintf(((float)num / (den > dminf ? den : dminf)) * 16777216.0f);
+            }
+        }
+        TMARK(L, 12);
+        if (!kScore) {
+            // per pose: the sum over r >= 1 of 1 - NCC, NCCs in 2^-24 steps, an
+            // exact integer reduction across the wave (|q| <= 2^24, <= 31 views)
+            for (int k = 0; k < kn; ++k) {
+                const int tot = __builtin_amdgcn_readlane((int)group_total<1>((uint32_t)(kt == k ? q : 0)), 63);
+                L.cg.fr[k0 + k] = (double)((m - 1) * 16777216 - tot) * 0x1p-24; // < 2^29
+            }
+        }
+        wave_sync();
+        TMARK(L, 14);
     }
-    // exact: |q| <= 2^24, at most 31 views
-    const int tot = __builtin_amdgcn_readlane((int)group_total<1>((uint32_t)q), 63);
-    wave_sync();
-    TMARK(L, 14);
-    return (double)((m - 1) * 16777216 - tot) * 0x1p-24; // < 2^29
 }
 
 // Nonlinear CG (or_fast.c fast_cg) as a state machine around ONE evaluation
 // call site (the sampling passes are inlined once); its state lives in LDS.
-// Returns evaluations; L.cg.x = the scaled pose.
+// The start evaluation and the three forward differences of each iteration
+// are independent, so they share one set of passes (evaluate_poses); the
+// results are those of one evaluation at a time.  Returns evaluations;
+// L.cg.x = the scaled pose.
 template <int G, int NS, bool kTail, bool kMask, int kBudget>
 __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m)
 {
-    enum { kStart = 0, kFd0 = 1, kFd2 = 3, kProbe1 = 4, kProbe2 = 5 };
+    enum { kStart = 0, kFd = 1, kProbe1 = 2, kProbe2 = 3 };
     CgState &C = L.cg;
     const double h = (double)a.fo.fd_step, inv_h = 1.0 / h;
     for (int k = 0; k < 3; ++k) {
@@ -729,32 +767,41 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
     C.ggp = 0.0;
     int E = 0, it = 0, phase = kStart;
     for (;;) {
-        double xt0 = C.x[0], xt1 = C.x[1], xt2 = C.x[2];
-        if (phase >= kFd0 && phase <= kFd2) {
-            const int i = phase - kFd0;
-            xt0 = i == 0 ? C.x[0] + h : xt0;
-            xt1 = i == 1 ? C.x[1] + h : xt1;
-            xt2 = i == 2 ? C.x[2] + h : xt2;
-        } else if (phase >= kProbe1) {
-            const double st = phase == kProbe1 ? C.alpha : (C.f1 < C.f ? 2.0 * C.alpha : 0.5 * C.alpha);
-            xt0 = C.x[0] + st * C.u[0];
-            xt1 = C.x[1] + st * C.u[1];
-            xt2 = C.x[2] + st * C.u[2];
-        }
-        TMARK(L, 15);
-        const double ft = evaluate<G, NS, kTail, kMask, false>(a, L, S, sl, m, xt0, xt1, xt2);
-        if (phase == kStart) {
-            C.f = ft;
-            E = 1;
-            if (a.fo.iters <= 0)
-                break;
-            phase = kFd0;
-        } else if (phase >= kFd0 && phase <= kFd2) {
-            C.g[phase - kFd0] = (ft - C.f) * inv_h;
-            if (phase < kFd2) {
-                ++phase;
-                continue;
+        int K = 1;
+        if (phase == kStart || phase == kFd) {
+            // f(x) (start only), then f(x + h e_i), i = 0, 1, 2
+            const int k0 = phase == kStart ? 1 : 0;
+            if (phase == kStart) {
+                C.px[0][0] = C.x[0];
+                C.px[0][1] = C.x[1];
+                C.px[0][2] = C.x[2];
             }
+            K = phase == kStart ? (a.fo.iters > 0 ? 4 : 1) : 3;
+            for (int i = 0; i < 3; ++i) {
+                C.px[k0 + i][0] = i == 0 ? C.x[0] + h : C.x[0];
+                C.px[k0 + i][1] = i == 1 ? C.x[1] + h : C.x[1];
+                C.px[k0 + i][2] = i == 2 ? C.x[2] + h : C.x[2];
+            }
+        } else {
+            const double st = phase == kProbe1 ? C.alpha : (C.f1 < C.f ? 2.0 * C.alpha : 0.5 * C.alpha);
+            C.px[0][0] = C.x[0] + st * C.u[0];
+            C.px[0][1] = C.x[1] + st * C.u[1];
+            C.px[0][2] = C.x[2] + st * C.u[2];
+        }
+        wave_sync();
+        TMARK(L, 15);
+        evaluate_poses<G, NS, kTail, kMask, false>(a, L, S, sl, m, K);
+        if (phase == kStart || phase == kFd) {
+            int k0 = 0;
+            if (phase == kStart) {
+                C.f = C.fr[0];
+                E = 1;
+                if (a.fo.iters <= 0)
+                    break;
+                k0 = 1;
+            }
+            for (int i = 0; i < 3; ++i)
+                C.g[i] = (C.fr[k0 + i] - C.f) * inv_h;
             E += 3;
             const double g0 = C.g[0], g1 = C.g[1], g2 = C.g[2];
             const double gg = (g0 * g0 + g1 * g1) + g2 * g2;
@@ -781,18 +828,18 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
             C.u[2] = d2 * inv_nd;
             phase = kProbe1;
         } else if (phase == kProbe1) {
-            C.f1 = ft;
-            C.x1[0] = xt0;
-            C.x1[1] = xt1;
-            C.x1[2] = xt2;
+            C.f1 = C.fr[0];
+            C.x1[0] = C.px[0][0];
+            C.x1[1] = C.px[0][1];
+            C.x1[2] = C.px[0][2];
             phase = kProbe2;
         } else {
-            const double f2 = ft;
+            const double f2 = C.fr[0];
             if (C.f1 < C.f) {
                 if (f2 < C.f1) {
-                    C.x[0] = xt0;
-                    C.x[1] = xt1;
-                    C.x[2] = xt2;
+                    C.x[0] = C.px[0][0];
+                    C.x[1] = C.px[0][1];
+                    C.x[2] = C.px[0][2];
                     C.f = f2;
                     C.alpha = 2.0 * C.alpha;
                 } else {
@@ -802,9 +849,9 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
                 }
             } else {
                 if (f2 < C.f) {
-                    C.x[0] = xt0;
-                    C.x[1] = xt1;
-                    C.x[2] = xt2;
+                    C.x[0] = C.px[0][0];
+                    C.x[1] = C.px[0][1];
+                    C.x[2] = C.px[0][2];
                     C.f = f2;
                 }
                 C.alpha = 0.5 * C.alpha;
@@ -817,12 +864,24 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
             C.ggp = C.gg;
             if (++it >= a.fo.iters)
                 break;
-            phase = kFd0;
+            phase = kFd;
         }
         wave_sync();
     }
     wave_sync();
     return E;
+}
+
+// one scoring evaluation at the staged pose (FAST_EVAL, the filter): the fp64
+// NCC of rank r >= 1 in L.u.ev.score[r]
+template <int G, int NS, bool kTail, bool kMask, int kBudget>
+__device__ void evaluate_score(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m)
+{
+    L.cg.px[0][0] = 0.0;
+    L.cg.px[0][1] = 0.0;
+    L.cg.px[0][2] = 0.0;
+    wave_sync();
+    evaluate_poses<G, NS, kTail, kMask, true>(a, L, S, sl, m, 1);
 }
 
 // Patch::InitRelatedImages (patch.cpp:19-49), one lane per view
@@ -957,7 +1016,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                 ok = m >= 2;
                 wave_vev += ok ? (unsigned long long)m : 0ull;
                 if (ok) {
-                    evaluate<G, NS, kTail, kMask, true>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                    evaluate_score<G, NS, kTail, kMask>(a, L, S, sl, m);
                     double sum = 0.0;
                     for (int k = 1; k < m; ++k)
                         sum = sum + L.u.ev.score[k];
@@ -1023,7 +1082,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                         p.vis[1] = (m == 1 && v >= 64) ? (1ull << (v - 64)) : 0ull;
                         ok = m >= a.opt.min_visible;
                     } else {
-                        evaluate<G, NS, kTail, kMask, true>(a, L, S, sl, m, 0.0, 0.0, 0.0);
+                        evaluate_score<G, NS, kTail, kMask>(a, L, S, sl, m);
                         double sum = 0.0;
                         for (int k = 1; k < m; ++k)
                             sum = sum + L.u.ev.score[k];
