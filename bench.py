@@ -416,6 +416,9 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                           "compulsory_GBps": round(comp / kms / 1e6, 2)},
              "quality": quality(cfg, out, acc), "stats": {k: int(v) for k, v in st.items()},
              "fast_options": {k: getattr(fo, k) for k in ("iters", "margin", "tile_budget", "max_views")}}
+        ft = fast_traffic(cell, fo, B)
+        if ft:
+            r["roofline"].update(ft)
         if not args.no_cpu:
             if imgs is None:
                 imgs = []
@@ -440,6 +443,29 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
     eng.set_options(dp.Options(expand_cell_size=args.cell))
     eng.set_fast_options(dp.FastOptions())
     return res
+
+
+def fast_traffic(cell, fo, B):
+    """rocprofv3 PMC bytes per launch of the performance-mode kernel for this
+    window (profiles/<latest round>/traffic_all_kernels.json, tools/gpu_profile.sh),
+    when the recorded launch used the same arena and batch: raw = (FETCH_SIZE +
+    WRITE_SIZE) KiB, traffic = the guide's 2x FETCH correction (uncalibrated for
+    these short tile-row reads; WRITE_SIZE is mostly register-spill scratch)."""
+    import glob
+
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_all_kernels.json")))
+    if not found or B != 4 * 65536 or fo.tile_budget > 6144:
+        return None
+    tag = {7: "fast_kernel<4, 3, true, false, 6144", 11: "fast_kernel<2, 4, false, true, 6144"}.get(cell)
+    if tag is None:
+        return None
+    with open(found[-1]) as f:
+        t = json.load(f)
+    for k, v in t.items():
+        if tag in k:
+            return {"traffic": v["corrected_bytes"], "traffic_raw": v["raw_bytes"],
+                    "traffic_source": os.path.relpath(found[-1], ROOT)}
+    return None
 
 
 def latest_traffic_json():
