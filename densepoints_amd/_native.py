@@ -11,7 +11,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdensepoints.so")
+# DP_LIB_VARIANT=<file name in lib/>: load a differently-compiled build of the
+# same sources (A/B measurements in one GPU session, tools/ab_variants.sh)
+LIB_PATH = os.path.join(_HERE, "lib", os.environ.get("DP_LIB_VARIANT") or "libdensepoints.so")
 
 # dp_patch (include/densepoints.h) -- 80 bytes
 PATCH_DTYPE = np.dtype(

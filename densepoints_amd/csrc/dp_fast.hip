@@ -558,6 +558,7 @@ struct TapWords {
 __device__ __forceinline__ TapWords tap_load(const char *tiles, const Tap &t)
 {
     typedef __attribute__((address_space(3))) const uint32_t *lds_u32_t;
+
     const lds_u32_t p0 = (lds_u32_t)(tiles + t.a0), p1 = (lds_u32_t)(tiles + t.a1);
     TapWords w;
     w.d[0] = p0[0];
