@@ -23,6 +23,8 @@
 
 #include <hip/hip_fp16.h>
 
+#include <cmath>
+
 namespace dpk {
 namespace {
 
@@ -47,6 +49,7 @@ struct FastArgs {
     uint32_t *work;
     unsigned long long *evals;
     const dp_patch *parents; // expansion: child c = parents[c / 4], direction c % 4
+    double cvis, ccand;      // cos(visible_angle), cos(candidate_angle) from the host libm
     unsigned long long *stats; // dp_fast_stats: patches, evals, view_evals, staged_bytes
 };
 
@@ -55,8 +58,7 @@ struct StageRec {
     float v[15];      // H0, Hd, He1, He2, Hn (folded, scaled, fp32)
     float umax, vmax; // 32 (tw - 1), 32 (th - 1)
     uint32_t info;    // tile byte offset | row bytes << 16
-    int32_t view, x0t, y0t, tw, th;
-    int32_t pad;
+    int32_t view;
 };
 
 // per evaluation, per staged view: A.xyz 2^23+umax | B1.xyz 2^23+vmax | B2.xyz
@@ -147,28 +149,6 @@ __device__ __forceinline__ double uni_f64(double v)
     return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-// exact integer wave sum (xor butterfly through the LDS crossbar; staging only)
-__device__ __forceinline__ int wave_sum_i32(int v)
-{
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
-        v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// inclusive prefix sum over the wave in lane order
-__device__ __forceinline__ int wave_incl_i32(int v)
-{
-    const int lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o)
-            v += t;
-    }
-    return v;
-}
-
 // sum over each group of LP = 64/G lanes (DPP); the total of group j lands in
 // lane LP (j + 1) - 1
 template <int G> __device__ __forceinline__ uint32_t group_total(uint32_t v)
@@ -184,6 +164,13 @@ template <int G> __device__ __forceinline__ uint32_t group_total(uint32_t v)
         v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
     return v;
 }
+
+// inclusive prefix sum over the wave in lane order: group_total<1> leaves
+// every lane's inclusive prefix (Hillis-Steele within rows of 16, then the
+// row broadcasts), all in DPP -- no LDS crossbar round trips
+__device__ __forceinline__ int wave_incl_i32(int v) { return (int)group_total<1>((uint32_t)v); }
+
+__device__ __forceinline__ int wave_sum_i32(int v) { return __builtin_amdgcn_readlane(wave_incl_i32(v), 63); }
 
 // RN(1 / b) for b >= 2^-20: v_rcp_f32 seed and one Newton step (checked
 // bitwise against IEEE division on the GPU, tests/test_gpu_fast.py)
@@ -215,7 +202,8 @@ __device__ __forceinline__ void make_frame(const dpg::ViewDev &rv, const float *
     if (F.degenerate)
         return;
     const double ps = 1.0 / dx;
-    const double nn[3] = {n0[0] / nl, n0[1] / nl, n0[2] / nl};
+    const double inl = 1.0 / nl;
+    const double nn[3] = {n0[0] * inl, n0[1] * inl, n0[2] * inl};
     const double xn = dpg::dot3(rv.xr, nn);
     double e1[3] = {rv.xr[0] - xn * nn[0], rv.xr[1] - xn * nn[1], rv.xr[2] - xn * nn[2]};
     const double el = sqrt(dpg::dot3(e1, e1));
@@ -223,8 +211,9 @@ __device__ __forceinline__ void make_frame(const dpg::ViewDev &rv, const float *
         F.degenerate = true;
         return;
     }
+    const double iel = 1.0 / el;
     for (int k = 0; k < 3; ++k)
-        e1[k] = e1[k] / el;
+        e1[k] = e1[k] * iel;
     double e2[3];
     dpg::cross3(nn, e1, e2);
     const double r[3] = {X0[0] - rv.C[0], X0[1] - rv.C[1], X0[2] - rv.C[2]};
@@ -372,6 +361,11 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     const int maxv = a.fo.max_views < kFastMaxV ? a.fo.max_views : kFastMaxV;
     const int view = lane < nconsider ? (int)L.vlist[lane] : 0;
     const dpg::ViewDev &vw = a.views[view];
+    // the view's gray plane descriptor, loaded now so that its latency
+    // overlaps the window geometry
+    GrayPlane gpl{};
+    if (lane < nconsider)
+        gpl = a.gray[view];
     Geo g;
     g.ok = false;
     if (lane < nconsider)
@@ -394,6 +388,22 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     clipped += (M < margin || m < __popcll(__ballot(staged))) ? 1ull : 0ull;
     // bytes the tiles copy from the gray planes (whole 32-bit pixel pairs)
     staged_bytes += (unsigned long long)uni(wave_sum_i32(keep ? t.bytes : 0));
+    // the tile copy's parameters stay in the view's lane (the copy loop
+    // broadcasts them per view by readlane)
+    uint64_t dbase = 0;
+    int dpitch = 0, dW2 = 0, dnw = 0, dylim = 0;
+    float dinv = 0.0f;
+    uint32_t doff = 0;
+    if (keep) {
+        dbase = (uint64_t)(uintptr_t)(gpl.p + (size_t)t.y0 * (size_t)gpl.pitch + t.x0);
+        dpitch = gpl.pitch;
+        dW2 = (t.tw + 2) / 2;
+        dnw = dW2 * (t.th + 1);
+        dinv = 1.0f / (float)dW2;
+        dylim = gpl.h - 1 - t.y0;
+        doff = (uint32_t)(incl - t.bytes);
+    }
+    const uint64_t kept = __ballot(keep);
     if (keep) {
         StageRec &R = L.u.st[rank];
         const double inv = geo_inv(vw, L.F);
@@ -411,19 +421,10 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
         R.vmax = (float)(32 * (t.th - 1));
         R.info = (uint32_t)(incl - t.bytes) | ((uint32_t)(4 * ((t.tw + 2) / 2)) << 16);
         R.view = view;
-        R.x0t = t.x0;
-        R.y0t = t.y0;
-        R.tw = t.tw;
-        R.th = t.th;
     }
     wave_sync();
     TMARK(L, 2);
     // lane r takes rank r's vectors (kept in registers for the evaluations)
-    // and its tile rectangle + gray plane descriptor (read with one vector
-    // load for all views, then broadcast per view by readlane)
-    int tx0 = 0, ty0 = 0, ttw = 0, tth = 0;
-    uint32_t toff = 0;
-    GrayPlane gp{};
     if (lane < m) {
         const StageRec &R = L.u.st[lane];
 #pragma unroll
@@ -433,12 +434,6 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
         S.vmax = R.vmax;
         S.info = R.info;
         S.view = R.view;
-        tx0 = R.x0t;
-        ty0 = R.y0t;
-        ttw = R.tw;
-        tth = R.th;
-        toff = R.info & 0xffffu;
-        gp = a.gray[R.view];
     }
     // tiles: rows y0t .. y0t + th (clamped to the image) of biased-fp16 gray,
     // columns x0t .. x0t + 2 W2 - 1 (the plane's padding columns replicate
@@ -449,24 +444,21 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     typedef __attribute__((address_space(3))) void *lds_ptr_t;
     typedef __attribute__((address_space(1))) const void *gptr_t;
     const uint32_t tbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)L.tiles;
-    const uint64_t gpp = (uint64_t)(uintptr_t)gp.p;
-    for (int r = 0; r < m; ++r) {
-        const int x0t = __builtin_amdgcn_readlane(tx0, r), y0t = __builtin_amdgcn_readlane(ty0, r);
-        const int tw = __builtin_amdgcn_readlane(ttw, r), th = __builtin_amdgcn_readlane(tth, r);
-        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)toff, r);
-        const int gh = __builtin_amdgcn_readlane(gp.h, r), gpitch = __builtin_amdgcn_readlane(gp.pitch, r);
-        const uint64_t pb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(gpp >> 32), r) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gpp, r);
-        const __half *plane = (const __half *)(uintptr_t)pb;
-        const int W2 = (tw + 2) / 2;
-        const int nw = W2 * (th + 1);
-        const float inv = 1.0f / (float)W2;
+    for (uint64_t q = kept; q; q &= q - 1) {
+        const int l = (int)__builtin_ctzll(q);
+        const uint64_t pb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(dbase >> 32), l) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dbase, l);
+        const __half *base = (const __half *)(uintptr_t)pb;
+        const int pitch = __builtin_amdgcn_readlane(dpitch, l), W2 = __builtin_amdgcn_readlane(dW2, l);
+        const int nw = __builtin_amdgcn_readlane(dnw, l), ylim = __builtin_amdgcn_readlane(dylim, l);
+        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dinv), l));
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)doff, l);
         for (int i = 0; i < nw; i += 64) {
             const int d = i + lane;
             const int y = (int)(((float)d + 0.5f) * inv);
             const int c = d - y * W2;
-            const int Y = y0t + y < gh - 1 ? y0t + y : gh - 1;
-            const __half *src = plane + (size_t)Y * gpitch + x0t + 2 * c;
+            const int Y = y < ylim ? y : ylim;
+            const __half *src = base + (__umul24((uint32_t)Y, (uint32_t)pitch) + 2u * (uint32_t)c);
             if (d < nw)
                 __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)(uintptr_t)(tbase + off + 4u * (uint32_t)i), 4, 0, 0);
         }
@@ -885,6 +877,20 @@ __device__ void evaluate_score(const FastArgs &a, FastLds<kBudget> &L, const Sta
     evaluate_poses<G, NS, kTail, kMask, true>(a, L, S, sl, m, 1);
 }
 
+// InitRelatedImages' per-view test (patch.cpp:30-45) with the angle tests as
+// cosine tests (or_fast.c fast_init_related): 1 visible, 2 candidate, 0 none
+__device__ __forceinline__ int classify_cos(const dpg::ViewDev &v, const double *X, const double *n, double cvis,
+                                           double ccand)
+{
+    double u, w;
+    dpg::project(v.P, X[0], X[1], X[2], u, w);
+    if (!dpg::inside(u, w, v.W, v.H))
+        return 0;
+    const double d[3] = {X[0] - v.C[0], X[1] - v.C[1], X[2] - v.C[2]};
+    const double x = dpg::dot3(n, d) / sqrt(dpg::dot3(d, d));
+    return x > cvis ? 1 : x > ccand ? 2 : 0;
+}
+
 // Patch::InitRelatedImages (patch.cpp:19-49), one lane per view
 template <int kBudget> __device__ void init_related(const FastArgs &a, FastLds<kBudget> &L, const dp_patch &p)
 {
@@ -894,9 +900,9 @@ template <int kBudget> __device__ void init_related(const FastArgs &a, FastLds<k
     const double n[3] = {p.normal[0], p.normal[1], p.normal[2]};
     int c0 = 0, c1 = 0;
     if (lane < a.V && lane != ref)
-        c0 = dpg::classify_view(a.views[lane], X, n, a.opt.visible_angle, a.opt.candidate_angle);
+        c0 = classify_cos(a.views[lane], X, n, a.cvis, a.ccand);
     if (64 + lane < a.V && 64 + lane != ref)
-        c1 = dpg::classify_view(a.views[64 + lane], X, n, a.opt.visible_angle, a.opt.candidate_angle);
+        c1 = classify_cos(a.views[64 + lane], X, n, a.cvis, a.ccand);
     const uint64_t v0 = __ballot(c0 == 1), v1 = __ballot(c1 == 1);
     const uint64_t k0 = __ballot(c0 == 2), k1 = __ballot(c1 == 2);
     wave_sync();
@@ -1359,6 +1365,9 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.work = c->d_work;
     a.evals = c->d_evals;
     a.parents = d_parents;
+    // the InitRelatedImages thresholds as cosines, by the host libm (the spec's)
+    a.cvis = std::cos(c->opt.visible_angle);
+    a.ccand = std::cos(c->opt.candidate_angle);
     if (!c->d_fstats)
         DP_HIP(c, hipMalloc(&c->d_fstats, 8 * sizeof(unsigned long long)));
     a.stats = c->d_fstats;

@@ -404,7 +404,9 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  *  - refine: `iters` Polak-Ribiere+ conjugate-gradient steps with a forward-
  *    difference gradient (step fd_step) and a two-probe line search (initial
  *    step ls_step, doubled on success, halved on failure): E = 1 + 5 iters;
- *  - then Patch::InitRelatedImages (patch.cpp:19-49) at the new pose and the
+ *  - then Patch::InitRelatedImages (patch.cpp:19-49) at the new pose (its
+ *    angle tests as cosine tests, x > cos(angle) with the cosines from the
+ *    host libm; frame unit vectors by one reciprocal and products) and the
  *    fast filter: re-staged at the new pose (margin 0), one evaluation, views
  *    with NCC < ncc_threshold or that cannot be staged are dropped (no
  *    off-by-one), accepted iff >= min_visible views remain; score = mean NCC.

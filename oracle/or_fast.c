@@ -25,7 +25,9 @@
  *     difference gradient, a two-probe line search); E = 1 + 5 * iters;
  *   - samples are bilinear in 1/32 px with 1/16 gray-level output, moments are
  *     exact integers; the refine's NCC finish is fp32 (quantised to 2^-24),
- *     the reported scores' is fp64.
+ *     the reported scores' is fp64;
+ *   - InitRelatedImages after the refine tests cos(angle) against the
+ *     thresholds' cosines (host libm) instead of acos(x) against the angles.
  * Arithmetic: fp32 with explicit fmaf where written, every other line one
  * IEEE rounding (-ffp-contract=off); fp64 for the per-patch setup, the NCC
  * finish and the CG state.
@@ -197,7 +199,9 @@ static int fast_stage(const or_scene *s, const or_patch *p, int cell, const or_f
         return 0;
     }
     const double ps = 1.0 / dx; /* world size of one reference pixel */
-    double nn[3] = {n0[0] / nl, n0[1] / nl, n0[2] / nl};
+    /* unit vectors by one reciprocal and three products each */
+    const double inl = 1.0 / nl;
+    double nn[3] = {n0[0] * inl, n0[1] * inl, n0[2] * inl};
     const double xn = dot3(rv->xr, nn);
     double e1[3] = {rv->xr[0] - xn * nn[0], rv->xr[1] - xn * nn[1], rv->xr[2] - xn * nn[2]};
     const double el = sqrt(dot3(e1, e1));
@@ -205,7 +209,8 @@ static int fast_stage(const or_scene *s, const or_patch *p, int cell, const or_f
         fp->degenerate = 1;
         return 0;
     }
-    for (int k = 0; k < 3; ++k) e1[k] = e1[k] / el;
+    const double iel = 1.0 / el;
+    for (int k = 0; k < 3; ++k) e1[k] = e1[k] * iel;
     double e2[3];
     cross3(nn, e1, e2);
     const double r[3] = {X0[0] - rv->C[0], X0[1] - rv->C[1], X0[2] - rv->C[2]};
@@ -475,6 +480,32 @@ static int fast_filter(const or_scene *s, or_patch *p, int cell, const or_fast_o
     return nk >= s->opt.min_visible;
 }
 
+/* Patch::InitRelatedImages (patch.cpp:19-49) with its angle tests as cosine
+ * tests, acos(x) < a <=> x > cos(a): the thresholds' cosines come from the
+ * host libm once (the product passes the same doubles to the device), so
+ * no acos is evaluated per view */
+static void fast_init_related(const or_scene *s, or_patch *p)
+{
+    const double cvis = cos(s->opt.visible_angle), ccand = cos(s->opt.candidate_angle);
+    double X[3], n[3];
+    get_pos(p, X);
+    get_nrm(p, n);
+    int vis[OR_MAX_VIEWS], cand[OR_MAX_VIEWS], nv = 0, nc = 0;
+    for (int vi = 0; vi < s->V; ++vi) {
+        if ((uint32_t)vi == p->ref) continue;
+        const or_view *v = &s->v[vi];
+        if (!inside(v, X)) continue;
+        const double d[3] = {X[0] - v->C[0], X[1] - v->C[1], X[2] - v->C[2]};
+        const double x = dot3(n, d) / norm3(d);
+        if (x > cvis)
+            vis[nv++] = vi;
+        else if (x > ccand)
+            cand[nc++] = vi;
+    }
+    encode_mask(vis, nv, p->vis);
+    encode_mask(cand, nc, p->cand);
+}
+
 /* DP_MODE_FAST_REFINE: CG refine on the current visible set ->
  * InitRelatedImages (patch.cpp:19-49) -> fast filter */
 static int fast_refine_one(const or_scene *s, or_patch *p, int cell, const or_fast_options *fo)
@@ -501,7 +532,7 @@ static int fast_refine_one(const or_scene *s, or_patch *p, int cell, const or_fa
         }
     }
     fast_free(&fp);
-    or_init_related(s, p);
+    fast_init_related(s, p);
     int ok = fast_filter(s, p, cell, fo);
     if (ok) p->flags |= OR_FLAG_ACCEPTED;
     else p->flags &= (uint8_t)~OR_FLAG_ACCEPTED;
