@@ -51,6 +51,13 @@ KERNEL(k_dpp_add, unsigned, "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf ban
 KERNEL(k_cndmask, unsigned, "v_cndmask_b32_e64 %0, %0, %1, vcc")
 KERNEL(k_mul_sdwa, unsigned, "v_mul_u32_u24_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1")
 KERNEL(k_lshr, unsigned, "v_lshrrev_b32 %0, 4, %0")
+KERNEL(k_rcp_f64, double, "v_rcp_f64 %0, %0")
+KERNEL(k_rsq_f64, double, "v_rsq_f64 %0, %0")
+KERNEL(k_sqrt_f64, double, "v_sqrt_f64 %0, %0")
+KERNEL(k_div_fixup_f64, double, "v_div_fixup_f64 %0, %1, %2, %0")
+KERNEL(k_ldexp_f64, double, "v_ldexp_f64 %0, %0, 3")
+KERNEL(k_mul_f64, double, "v_mul_f64 %0, %1, %0")
+
 
 typedef void (*kfn)(unsigned long long *, float, float);
 
@@ -102,5 +109,11 @@ int main()
     run("cndmask", k_cndmask, 3u, 5u, cus);
     run("mul_u24_sdwa", k_mul_sdwa, 3u, 5u, cus);
     run("lshrrev", k_lshr, 3u, 5u, cus);
+    run("rcp_f64", k_rcp_f64, 1.5, 2.0, cus);
+    run("rsq_f64", k_rsq_f64, 1.5, 2.0, cus);
+    run("sqrt_f64", k_sqrt_f64, 1.5, 2.0, cus);
+    run("div_fixup_f64", k_div_fixup_f64, 1.5, 2.0, cus);
+    run("ldexp_f64", k_ldexp_f64, 1.5, 2.0, cus);
+    run("mul_f64", k_mul_f64, 1.0001, 2.0, cus);
     return 0;
 }
