@@ -12,8 +12,8 @@ Expand::ExpandPatch (expand.cpp:103-143) and PMVS::Run minus matching
   cfg3  32 x 3840x2160, 4-level pyramid (two views), seed stage on a spread
         subset, n = 11 expansion of 2,000 refined parents
   cfg4  64 x 3840x2160 (one GPU), the same kind of sample with 1,000 parents
-Config 5 (fp16 gray pyramids) has no parity-mode counterpart; its scene runs
-in tests/test_gpu_perf.py.
+Config 5 (fp16 gray planes, 11x11 window) is the performance mode's: its full
+scene runs in tests/test_gpu_fast.py (test_fast_expand_cfg5_full_scene).
 """
 import ctypes
 

@@ -146,3 +146,32 @@ def test_fast_expand_cfg3_full_scene(orc):
         return float(np.median(np.abs(k["pos"][:, 2] - z)))
     # cell 7 children vs the parity (Nelder-Mead, cell 11) children
     assert err(gk, ga) < err(nk, na)
+
+
+def test_fast_expand_cfg5_full_scene(orc):
+    """BASELINE config 5 (128 views 7680x4320, fp16 gray planes, 11x11 window)
+    on one GPU: performance-mode expansion of 400 refined parents equals the
+    spec bit for bit (the BGRA8 levels are 17 GB, the gray planes 8.5 GB in
+    HBM); geometry within the scene's tolerance of the ground truth."""
+    from test_gpu_configs import DeviceScene, spread
+
+    o = dp.Options(expand_cell_size=11)
+    with dp.Engine(device=0) as eng:
+        sc = DeviceScene("cfg5_128view_8k", eng)
+        seeds = spread(sc.seeds, 800)
+        par = eng.seeds_to_patches(seeds)
+        acc = eng.refine(par, 16, N.MODE_SEED)
+        par = np.ascontiguousarray(par[acc == 1][:400])
+        assert len(par) >= 200
+        eng.set_options(o)
+        gk, ga = eng.fast_expand(par)
+        st = eng.fast_last_stats()
+    S = orc.Scene(sc.P, sc.host_images(), o)
+    ok, oa = S.fast_expand(par)
+    assert np.array_equal(ga, oa)
+    assert_same(gk, ok, FIELDS + ("parent",))
+    assert 0.1 < ga.mean() < 0.95 and st["patches"] == 4 * len(par)
+    k = gk[ga == 1]
+    z, _ = synth.surface(sc.cfg, k["pos"][:, :2].astype(np.float64))
+    print("cfg5 accepted %d of %d, median |dz| %.5f, staged views per eval %.2f"
+          % (len(k), len(gk), float(np.median(np.abs(k["pos"][:, 2] - z))), st["view_evals"] / st["evals"]))
