@@ -66,6 +66,7 @@ struct StageRec {
 struct EvalRec {
     float4 q[3];
 };
+static_assert(sizeof(EvalRec) == 48, "EvalRec is indexed by byte offset i * 48");
 
 // row bytes of a tile from its biased umax = 2^23 + 32 (tw - 1): 4 ((tw + 2) / 2)
 __device__ __forceinline__ uint32_t tile_rowb(float umax_b)
@@ -154,10 +155,12 @@ __device__ __forceinline__ double uni_f64(double v)
 template <int G> __device__ __forceinline__ uint32_t group_total(uint32_t v)
 {
     constexpr int LP = 64 / G;
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false); // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false); // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xe, false); // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xc, false); // row_shr:8
+    // Hillis-Steele within each row of 16: a lane whose source lies before
+    // the row start reads 0 (bound_ctrl), so every step is one v_add_u32_dpp
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true); // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true); // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true); // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true); // row_shr:8
     if (LP >= 32)
         v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
     if (LP == 64)
@@ -636,7 +639,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
             const bool tail = kTail && p == 0;
             const int r = (int)(__umul24((uint32_t)i, rk) >> 16);
             const int k = i - r * kn;
-            const EvalRec &E = L.u.ev.par[act ? i : 0];
+            const EvalRec &E = *(const EvalRec *)((const char *)L.u.ev.par + (act ? (uint32_t)i * 48u : 0u));
             const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
             const uint32_t off = __float_as_uint(qc.w), rowb = tile_rowb(qa.w);
             Tap tp[NS], tt{};
