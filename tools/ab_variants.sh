@@ -13,5 +13,5 @@ for v in ${VARIANTS:-libdensepoints.so}; do
   fi
   DP_LIB_VARIANT=$v timeout -k 10 500 python -u bench.py $ARGS > gpurun_out/ab_$v.log 2>&1; rc=$?
   [ $rc -eq 0 ] || { echo "$v bench rc=$rc"; exit $rc; }
-  tail -1 gpurun_out/ab_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); pm=d['perf_mode']; print('$v', {k: (v['Mpatches_per_s'], v['kernel_ms_per_launch']) for k, v in pm.items() if isinstance(v, dict) and 'Mpatches_per_s' in v})"
+  tail -1 gpurun_out/ab_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); pm=d['perf_mode']; print('$v', 'parity', d['value'], {k: (v['Mpatches_per_s'], v['kernel_ms_per_launch']) for k, v in pm.items() if isinstance(v, dict) and 'Mpatches_per_s' in v})"
 done
