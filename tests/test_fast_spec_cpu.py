@@ -209,3 +209,57 @@ def test_fast_refine_quality_vs_ground_truth(orc):
     e = [err(*S.fast_expand(par, orc.fast_options(iters=it))) for it in (0, 2, 4)]
     assert e[2] < e[1] < e[0]
     assert e[2] < 0.5 * e_nm
+
+
+def test_fast_init_related_cosine_tests(orc, small_scene):
+    """After the refine, InitRelatedImages runs with its angle tests as cosine
+    tests (x > cos(angle), the cosines from the host libm): the candidate mask
+    equals an independent numpy classification at the refined pose, and the
+    filtered visible mask is a subset of the views that test visible."""
+    import math
+
+    _, P, imgs, seeds = small_scene
+    S = orc.Scene(P, imgs)
+    p = S.seeds_to_patches(seeds[:60])
+    S.fast_refine(p, 7, orc.MODE_FAST_REFINE)
+    V = len(imgs)
+    Pm = np.asarray(P, dtype=np.float64).reshape(V, 3, 4)
+    C = [orc.view_geometry(P[v])[1] for v in range(V)]
+    opts = dp_options()
+    cvis, ccand = math.cos(opts.visible_angle), math.cos(opts.candidate_angle)
+
+    def bits(m):
+        return {v for v in range(128) if (int(m[v >> 6]) >> (v & 63)) & 1}
+
+    checked = 0
+    for q in p:
+        if q["flags"] & 2:  # degenerate
+            continue
+        X = [float(t) for t in q["pos"]]
+        n = [float(t) for t in q["normal"]]
+        vis, cand = set(), set()
+        for v in range(V):
+            if v == int(q["ref"]):
+                continue
+            r = Pm[v]
+            h = [((r[k, 0] * X[0] + r[k, 1] * X[1]) + r[k, 2] * X[2]) + r[k, 3] for k in range(3)]
+            u, w = h[0] / h[2], h[1] / h[2]
+            H, W = imgs[v].shape[:2]
+            if not (u > 0.0 and u < W and w > 0.0 and w < H):
+                continue
+            d = [X[k] - C[v][k] for k in range(3)]
+            x = ((n[0] * d[0] + n[1] * d[1]) + n[2] * d[2]) / math.sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2])
+            if x > cvis:
+                vis.add(v)
+            elif x > ccand:
+                cand.add(v)
+        assert bits(q["cand"]) == cand
+        assert bits(q["vis"]) <= vis | {int(q["ref"])}
+        checked += 1
+    assert checked > 40
+
+
+def dp_options():
+    from densepoints_amd import pmvs
+
+    return pmvs.Options()
