@@ -6,6 +6,7 @@ arithmetic spec is one IEEE rounding on both the CPU and CDNA4.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -56,15 +57,41 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """One object per source, compiled in parallel (hipcc -c), then linked
+    into the shared object; an object is rebuilt when its source, a header or
+    this file is newer."""
     if not force and not _stale():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
     extra = os.environ.get("DP_EXTRA_FLAGS", "").split()
-    cmd = [hipcc(), *FLAGS, *extra, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True, cwd=CSRC)
+    # variant builds (DP_EXTRA_FLAGS) keep their objects apart
+    tag = "obj" if not extra else "obj_" + hashlib.sha1(" ".join(extra).encode()).hexdigest()[:10]
+    objdir = os.path.join(HERE, "lib", tag)
+    os.makedirs(objdir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"]
+    common = [os.path.join(CSRC, h) for h in HEADERS] + [__file__]
+    common += [os.path.join(HERE, "..", "include", h) for h in ("densepoints.h", "densepoints_probe.h")]
+    t_common = max(os.path.getmtime(d) for d in common if os.path.exists(d))
+    procs, objs = [], []
+    for s in SOURCES:
+        src, obj = os.path.join(CSRC, s), os.path.join(objdir, s.replace(".hip", ".o"))
+        objs.append(obj)
+        if not force and os.path.exists(obj) and \
+                os.path.getmtime(obj) > max(os.path.getmtime(src), t_common):
+            continue
+        cmd = [hipcc(), *cflags, *extra, "-c", "-o", obj + ".tmp", src]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((subprocess.Popen(cmd, cwd=CSRC), obj))
+    failed = False
+    for pr, obj in procs:
+        if pr.wait() != 0:
+            failed = True
+        else:
+            os.replace(obj + ".tmp", obj)
+    if failed:
+        raise RuntimeError("hipcc failed")
+    tmp = OUT + ".tmp"
+    subprocess.run([hipcc(), *FLAGS, *extra, "-o", tmp, *objs], check=True, cwd=CSRC)
     os.replace(tmp, OUT)
     return OUT
 

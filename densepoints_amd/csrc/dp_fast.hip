@@ -518,17 +518,15 @@ __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, cons
                                        uint32_t rowb, float ti, float tj)
 {
     typedef float f2 __attribute__((ext_vector_type(2)));
-    // (hx, hy) as packed fp32 FMAs (v_pk_fma_f32: two fmaf roundings each)
-    const f2 hxy = __builtin_elementwise_fma((f2){tj, tj}, (f2){qc.x, qc.y},
-                                             __builtin_elementwise_fma((f2){ti, ti}, (f2){qb.x, qb.y},
-                                                                       (f2){qa.x, qa.y}));
-    float hz = __builtin_fmaf(tj, qc.z, __builtin_fmaf(ti, qb.z, qa.z));
-    hz = __builtin_fmaxf(hz, 0x1p-20f);
-    const float rz = recip_rn(hz);
-    // U, V rounded to integers by one FMA with 2^23 (spacing 1 in [2^23, 2^24))
+    // the item's affine window map (U, V) = A + ti Bi + tj Bj as packed fp32
+    // FMAs (v_pk_fma_f32: two fmaf roundings each); no per-sample division
+    const f2 uv = __builtin_elementwise_fma((f2){tj, tj}, (f2){qc.x, qc.y},
+                                            __builtin_elementwise_fma((f2){ti, ti}, (f2){qb.x, qb.y},
+                                                                      (f2){qa.x, qa.y}));
+    // U, V rounded to integers by one add of 2^23 (spacing 1 in [2^23, 2^24))
     // and clamped to [2^23, 2^23 + umax]: rint(U) and rint(V) are the low
     // mantissa bits, the pixel and its 1/32 fraction bit fields of them
-    const f2 m = __builtin_elementwise_fma(hxy, (f2){rz, rz}, (f2){0x1p23f, 0x1p23f});
+    const f2 m = uv + (f2){0x1p23f, 0x1p23f};
     const uint32_t bu = __float_as_uint(__builtin_amdgcn_fmed3f(m.x, 0x1p23f, qa.w));
     const uint32_t bv = __float_as_uint(__builtin_amdgcn_fmed3f(m.y, 0x1p23f, qb.w));
     Tap t;
@@ -616,12 +614,21 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
                 const float df = (float)(L.cg.px[k0 + k][0] * L.F.sd), af = (float)(L.cg.px[k0 + k][1] * L.F.st),
                             bf = (float)(L.cg.px[k0 + k][2] * L.F.st);
                 EvalRec &E = L.u.ev.par[lane * kn + k];
-                E.q[0] = make_float4(__builtin_fmaf(df, S.v[3], S.v[0]), __builtin_fmaf(df, S.v[4], S.v[1]),
-                                     __builtin_fmaf(df, S.v[5], S.v[2]), 0x1p23f + S.umax);
-                E.q[1] = make_float4(__builtin_fmaf(-af, S.v[12], S.v[6]), __builtin_fmaf(-af, S.v[13], S.v[7]),
-                                     __builtin_fmaf(-af, S.v[14], S.v[8]), 0x1p23f + S.vmax);
-                E.q[2] = make_float4(__builtin_fmaf(-bf, S.v[12], S.v[9]), __builtin_fmaf(-bf, S.v[13], S.v[10]),
-                                     __builtin_fmaf(-bf, S.v[14], S.v[11]),
+                // homography columns at the pose (or_fast.c fast_affine), then
+                // its first-order map about the window centre: A/Az and the
+                // quotient rule's (B - (A/Az) Bz) / Az, one IEEE division
+                const float ax = __builtin_fmaf(df, S.v[3], S.v[0]), ay = __builtin_fmaf(df, S.v[4], S.v[1]);
+                const float az = __builtin_fmaxf(__builtin_fmaf(df, S.v[5], S.v[2]), 0x1p-20f);
+                const float ix = __builtin_fmaf(-af, S.v[12], S.v[6]), iy = __builtin_fmaf(-af, S.v[13], S.v[7]),
+                            iz = __builtin_fmaf(-af, S.v[14], S.v[8]);
+                const float jx = __builtin_fmaf(-bf, S.v[12], S.v[9]), jy = __builtin_fmaf(-bf, S.v[13], S.v[10]),
+                            jz = __builtin_fmaf(-bf, S.v[14], S.v[11]);
+                const float rz = 1.0f / az;
+                const float u0 = ax * rz, v0 = ay * rz;
+                E.q[0] = make_float4(u0, v0, 0.0f, 0x1p23f + S.umax);
+                E.q[1] = make_float4(__builtin_fmaf(-u0, iz, ix) * rz, __builtin_fmaf(-v0, iz, iy) * rz, 0.0f,
+                                     0x1p23f + S.vmax);
+                E.q[2] = make_float4(__builtin_fmaf(-u0, jz, jx) * rz, __builtin_fmaf(-v0, jz, jy) * rz, 0.0f,
                                      __uint_as_float((S.info & 0xffffu) -
                                                      __umul24((0x4B000000u >> 5) & 0xffffffu, S.info >> 16)));
             }

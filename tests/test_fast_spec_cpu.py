@@ -118,18 +118,20 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
         gray = _gray(imgs[v])
         Hh, Ww = gray.shape
         A, B1, B2 = vec[0], vec[2], vec[3]
+        # first-order map of the homography about the window centre
+        rz = np.float32(1.0) / max(A[2], np.float32(2.0 ** -20))
+        U0, V0 = A[0] * rz, A[1] * rz
+        Ui, Vi = _fmaf(-U0, B1[2], B1[0]) * rz, _fmaf(-V0, B1[2], B1[1]) * rz
+        Uj, Vj = _fmaf(-U0, B2[2], B2[0]) * rz, _fmaf(-V0, B2[2], B2[1]) * rz
         out = np.zeros(N, dtype=np.int64)
         cf = np.float32(0.5) * np.float32(cell - 1)
         for j in range(cell):
             tj = np.float32(j) - cf
             for i in range(cell):
                 ti = np.float32(i) - cf
-                h = [_fmaf(tj, B2[k], _fmaf(ti, B1[k], A[k])) for k in range(3)]
-                hz = max(h[2], np.float32(2.0 ** -20))
-                rz = np.float32(1.0) / hz
                 b23 = np.float32(2.0 ** 23)
-                U = min(max(_fmaf(h[0], rz, b23), b23), b23 + np.float32(32 * (tw - 1)))
-                W = min(max(_fmaf(h[1], rz, b23), b23), b23 + np.float32(32 * (th - 1)))
+                U = min(max(_fmaf(tj, Uj, _fmaf(ti, Ui, U0)) + b23, b23), b23 + np.float32(32 * (tw - 1)))
+                W = min(max(_fmaf(tj, Vj, _fmaf(ti, Vi, V0)) + b23, b23), b23 + np.float32(32 * (th - 1)))
                 iu, iv = int(U - b23), int(W - b23)
                 xx, fx, yy, fy = iu >> 5, iu & 31, iv >> 5, iv & 31
 
