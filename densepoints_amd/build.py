@@ -60,9 +60,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     """One object per source, compiled in parallel (hipcc -c), then linked
     into the shared object; an object is rebuilt when its source, a header or
     this file is newer."""
-    if not force and not _stale():
-        return OUT
     extra = os.environ.get("DP_EXTRA_FLAGS", "").split()
+    if not force and not extra and not _stale():
+        return OUT
     # variant builds (DP_EXTRA_FLAGS) keep their objects apart
     tag = "obj" if not extra else "obj_" + hashlib.sha1(" ".join(extra).encode()).hexdigest()[:10]
     objdir = os.path.join(HERE, "lib", tag)
@@ -90,10 +90,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
             os.replace(obj + ".tmp", obj)
     if failed:
         raise RuntimeError("hipcc failed")
-    tmp = OUT + ".tmp"
+    # DP_LIB_NAME: a variant's file name under lib/ (loaded by DP_LIB_VARIANT)
+    out = os.path.join(os.path.dirname(OUT), os.environ.get("DP_LIB_NAME") or os.path.basename(OUT))
+    tmp = out + ".tmp"
     subprocess.run([hipcc(), *FLAGS, *extra, "-o", tmp, *objs], check=True, cwd=CSRC)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

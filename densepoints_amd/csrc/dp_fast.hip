@@ -616,14 +616,14 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
                 EvalRec &E = L.u.ev.par[lane * kn + k];
                 // homography columns at the pose (or_fast.c fast_affine), then
                 // its first-order map about the window centre: A/Az and the
-                // quotient rule's (B - (A/Az) Bz) / Az, one IEEE division
+                // quotient rule's (B - (A/Az) Bz) / Az, one reciprocal
                 const float ax = __builtin_fmaf(df, S.v[3], S.v[0]), ay = __builtin_fmaf(df, S.v[4], S.v[1]);
                 const float az = __builtin_fmaxf(__builtin_fmaf(df, S.v[5], S.v[2]), 0x1p-20f);
                 const float ix = __builtin_fmaf(-af, S.v[12], S.v[6]), iy = __builtin_fmaf(-af, S.v[13], S.v[7]),
                             iz = __builtin_fmaf(-af, S.v[14], S.v[8]);
                 const float jx = __builtin_fmaf(-bf, S.v[12], S.v[9]), jy = __builtin_fmaf(-bf, S.v[13], S.v[10]),
                             jz = __builtin_fmaf(-bf, S.v[14], S.v[11]);
-                const float rz = 1.0f / az;
+                const float rz = recip_rn(az); // == 1.0f / az (az >= 2^-20)
                 const float u0 = ax * rz, v0 = ay * rz;
                 E.q[0] = make_float4(u0, v0, 0.0f, 0x1p23f + S.umax);
                 E.q[1] = make_float4(__builtin_fmaf(-u0, iz, ix) * rz, __builtin_fmaf(-v0, iz, iy) * rz, 0.0f,
