@@ -267,7 +267,8 @@ def main():
             "tile_partitioned_generations": sum(1 for _, _, fb in parts if not fb),
             "round_robin_generations": sum(1 for _, _, fb in parts if fb),
             "max_share_vs_mean": round(max((mx * world / it) for it, mx, _ in parts if it > 0), 3),
-            "collective": "all_gather_into_tensor (RCCL) of 80-B candidate records + accept flags"}
+            "collective": f"all_gather_into_tensor ({'RCCL' if backend == 'nccl' else backend}) of 80-B candidate "
+                          "records + accept flags"}
     if rank == 0 and not args.no_seeds:
         result["seed_generation"] = seed_generation(eng, args)
     st = np.zeros(8, dtype=np.uint64)
