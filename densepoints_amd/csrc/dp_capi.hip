@@ -893,6 +893,7 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
     hipSetDevice(c->device);
     hipStream_t s = c->stream;
     const dp_options &o = c->opt;
+    const bool fast = c->fopt.densify != 0;
     dp_densify_stats st{};
     st.seeds_in = n;
     c->result.clear();
@@ -917,9 +918,14 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         DP_HIP(c, c->cand.reserve(n));
         DP_HIP(c, c->ok.reserve(n));
         DP_HIP(c, hipMemcpyAsync(c->cand.p, sp.data(), sizeof(dp_patch) * n, hipMemcpyHostToDevice, s));
-        // seed.cpp:110-144: FilterPatches then OptimizePatches at the seed cell size
-        dpk::RefineArgs a = refine_args(c, c->cand.p, n, o.seed_cell_size, DP_MODE_SEED, c->ok.p);
-        rc = launch_timed(c, a, s);
+        // seed.cpp:110-144: FilterPatches then OptimizePatches at the seed cell
+        // size (performance mode, dp_fast_options.densify: the fast refine)
+        if (fast) {
+            rc = dp_fast_launch(c, c->cand.p, n, o.seed_cell_size, DP_MODE_FAST_REFINE, c->ok.p, nullptr, s);
+        } else {
+            dpk::RefineArgs a = refine_args(c, c->cand.p, n, o.seed_cell_size, DP_MODE_SEED, c->ok.p);
+            rc = launch_timed(c, a, s);
+        }
         if (rc != DP_OK)
             return rc;
         double ms = 0.0;
@@ -946,10 +952,17 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         DP_HIP(c, hipStreamSynchronize(s)); // previous append may still read cand
         DP_HIP(c, c->cand.reserve(nc));
         DP_HIP(c, c->ok.reserve(nc));
-        dpk::RefineArgs a = refine_args(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_EXPAND, c->ok.p);
-        a.parents = c->store.p;
-        a.parent0 = head;
-        int rc = launch_timed(c, a, s);
+        int rc;
+        if (fast) {
+            // Expand::ExpandPatch with the fast refine; parents past the pop cap stay put
+            rc = dp_fast_launch(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_FAST_REFINE, c->ok.p, c->store.p + head,
+                                s, o.max_pops - head);
+        } else {
+            dpk::RefineArgs a = refine_args(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_EXPAND, c->ok.p);
+            a.parents = c->store.p;
+            a.parent0 = head;
+            rc = launch_timed(c, a, s);
+        }
         if (rc != DP_OK)
             return rc;
         double ms = 0.0;
@@ -1008,6 +1021,9 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
         return fail(c, DP_E_ARG, "dp_densify_begin: bad arguments");
     if (!c->V)
         return fail(c, DP_E_STATE, "dp_densify_begin: no views");
+    if (c->fopt.densify)
+        return fail(c, DP_E_ARG, "dp_densify_begin: the performance-mode densify (dp_fast_options.densify) runs in "
+                                 "dp_densify only");
     hipSetDevice(c->device);
     hipStream_t s = c->stream;
     c->g_t0 = std::chrono::steady_clock::now();

@@ -49,6 +49,7 @@ struct FastArgs {
     uint32_t *work;
     unsigned long long *evals;
     const dp_patch *parents; // expansion: child c = parents[c / 4], direction c % 4
+    int64_t live_parents;    // parents[i] expands only for i < live_parents (the pop cap)
     double cvis, ccand;      // cos(visible_angle), cos(candidate_angle) from the host libm
     unsigned long long *stats; // dp_fast_stats: patches, evals, view_evals, staged_bytes
 };
@@ -996,7 +997,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
             p.flags = 0;
             p.parent = idx >> 2;
             const int pm = __popcll(par.vis[0]) + __popcll(par.vis[1]);
-            live = pm >= a.opt.min_expand_visible && par.ref < (uint32_t)a.V;
+            live = pm >= a.opt.min_expand_visible && par.ref < (uint32_t)a.V && (int64_t)(idx >> 2) < a.live_parents;
             if (live) {
                 float cp[3];
                 child_position(a, par, (int)(idx & 3u), cp);
@@ -1356,7 +1357,7 @@ template <int B> static hipError_t fast_dispatch(int N, const dpk::FastArgs &a, 
 }
 
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
-                   hipStream_t s)
+                   hipStream_t s, int64_t live_parents)
 {
     int rc = ensure_gray(c);
     if (rc != DP_OK)
@@ -1375,6 +1376,7 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.work = c->d_work;
     a.evals = c->d_evals;
     a.parents = d_parents;
+    a.live_parents = live_parents;
     // the InitRelatedImages thresholds as cosines, by the host libm (the spec's)
     a.cvis = std::cos(c->opt.visible_angle);
     a.ccand = std::cos(c->opt.candidate_angle);

@@ -394,8 +394,10 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  *    bytes, then the longest fitting prefix of views is kept), copied once
  *    into LDS and used for the whole refine; samples clamp to the tile
  *    (BORDER_REPLICATE);
- *  - sample: projective map in fp32 (fmaf), 1/32 px (U, V rounded to
- *    integers by one fmaf with 2^23, clamped to the tile), bilinear on 8-bit
+ *  - sample: per (view, pose) the window homography's first-order (affine)
+ *    map about the window centre in fp32 (U0 = Ax / Az, axes (B - U0 Bz) / Az,
+ *    one IEEE reciprocal), U = U0 + ti Ui + tj Uj by fmaf, 1/32 px (rounded
+ *    to integers by one add of 2^23, clamped to the tile), bilinear on 8-bit
  *    gray, result in 1/16 gray levels; exact integer moments;
  *  - refine objective: the sum over the scored views of 1 - NCC, each NCC
  *    finished in fp32 and rounded to a multiple of 2^-24, summed exactly (the
@@ -419,7 +421,10 @@ typedef struct dp_fast_options {
     int32_t max_views;    /* 32    staged views per patch (<= 32)                   */
     float fd_step;        /* 0.5   forward-difference step, scaled units            */
     float ls_step;        /* 1.0   initial line-search step, scaled units           */
-    int32_t densify;      /* 0     1: dp_densify expands with the fast refine       */
+    int32_t densify;      /* 0     1: dp_densify runs the seed stage (at
+                                   seed_cell_size) and every expansion (at
+                                   expand_cell_size) with the fast refine; the
+                                   generation-at-a-time API then returns DP_E_ARG */
     int32_t reserved;
 } dp_fast_options;
 

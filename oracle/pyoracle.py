@@ -292,11 +292,33 @@ class GenerationEngine:
     on the CPU.  Same sequence numbering, pop cap and organizer order as
     or_densify (which it must reproduce)."""
 
-    def __init__(self, scene: "Scene", threads: int = 2):
+    def __init__(self, scene: "Scene", threads: int = 2, fast=None):
+        """fast: dp_fast_options / FastOptions with densify = 1 -> the
+        performance-mode densify (seed stage and expansions by the fast refine,
+        or_fast.c), as dp_densify runs it"""
         self.S = scene
         self.threads = threads
         self.org = None
         self._P = scene._keep[0]
+        self.fast = None if fast is None else fast_options(fast)
+
+    def _refine_seeds(self, r, cell):
+        if self.fast is not None:
+            return self.S.fast_refine(r, cell, MODE_FAST_REFINE, self.fast, self.threads)
+        return self.S.refine(r, cell, 3, self.threads)  # MODE_SEED
+
+    def _expand(self, parents):
+        if self.fast is not None:
+            return self.S.fast_expand(parents, self.fast, self.threads)
+        return self.S.expand(parents, self.threads)
+
+    def densify_all(self, seeds):
+        """every generation in turn (dp_densify's result): the store"""
+        g = self.densify_begin(seeds)
+        while g.items:
+            cand, acc = self.densify_refine(g, 0, g.items)
+            g = self.densify_commit(g, cand, acc)
+        return np.array(self.store, dtype=PATCH_DTYPE)
 
     def __del__(self):
         if self.org:
@@ -315,10 +337,10 @@ class GenerationEngine:
     def densify_refine(self, g, lo, hi):
         if g.index == 0:
             r = self.sp[lo:hi].copy()
-            acc = self.S.refine(r, g.cell, 3, self.threads)  # MODE_SEED
+            acc = self._refine_seeds(r, g.cell)
             return r, acc
         parents = np.array(self.store[g.head + lo: g.head + hi], dtype=PATCH_DTYPE)
-        kids, acc = self.S.expand(parents, self.threads)
+        kids, acc = self._expand(parents)
         q = g.head + lo + np.repeat(np.arange(hi - lo), 4)
         kids["parent"] = q.astype(np.uint32)
         acc[q >= self.S.opt.max_pops] = 0  # past the pop cap (expand.cpp:95)
@@ -358,10 +380,10 @@ class GenerationEngine:
         items = np.asarray(items, dtype=np.int64)
         if g.index == 0:
             r = self.sp[items].copy()
-            acc = self.S.refine(r, g.cell, 3, self.threads)  # MODE_SEED
+            acc = self._refine_seeds(r, g.cell)
             return r, acc
         parents = np.array([self.store[g.head + int(i)] for i in items], dtype=PATCH_DTYPE)
-        kids, acc = self.S.expand(parents, self.threads)
+        kids, acc = self._expand(parents)
         q = g.head + np.repeat(items, 4)
         kids["parent"] = q.astype(np.uint32)
         acc[q >= self.S.opt.max_pops] = 0  # past the pop cap (expand.cpp:95)

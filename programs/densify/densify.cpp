@@ -37,6 +37,9 @@ void usage()
                  "               [--features N] [--fast-threshold T] [--epipolar-matching]\n"
                  "               [--gpus N]   (one context per GPU, generations partitioned by\n"
                  "                             reference-view super-tile; output identical to 1 GPU)\n"
+                 "               [--mode parity|fast] [--fast-iters N]  (fast: the performance-mode\n"
+                 "                             refine -- LDS-staged gray tiles, fused CG -- for the seed\n"
+                 "                             stage and every expansion; one GPU)\n"
                  "       densify --synthetic V,W,H,KIND --write-scene DIR\n");
 }
 
@@ -221,7 +224,8 @@ int main(int argc, char **argv)
     int device = 0, gpus = 1;
     long long max_pops = -1;
     int level = 0;
-    bool check_only = false, do_filter = false;
+    bool check_only = false, do_filter = false, fast = false;
+    int fast_iters = -1;
     dp_matcher_options mopt; // MatcherOptions defaults (matcher.h:21-32), ORB::create(40000)
     dp_default_matcher_options(&mopt);
     for (int i = 1; i < argc; ++i) {
@@ -246,6 +250,14 @@ int main(int argc, char **argv)
         else if (a == "--features") mopt.n_features = std::atoi(next().c_str());
         else if (a == "--fast-threshold") mopt.fast_threshold = std::atoi(next().c_str());
         else if (a == "--epipolar-matching") mopt.epipolar_matching = 1;
+        else if (a == "--mode") {
+            const std::string m = next();
+            if (m != "parity" && m != "fast") {
+                usage();
+                return 2;
+            }
+            fast = m == "fast";
+        } else if (a == "--fast-iters") fast_iters = std::atoi(next().c_str());
         else if (a == "--synthetic") synth = next();
         else if (a == "--write-scene") scene_dir = next();
         else if (a == "-h" || a == "--help") {
@@ -312,6 +324,19 @@ int main(int argc, char **argv)
             }
         };
         check(dp_set_views(ctx, (int)imgs.size(), P.data(), dimg.data()), "dp_set_views");
+        if (fast) {
+            if (gpus > 1) {
+                std::fprintf(stderr, "densify: --mode fast runs on one GPU (--gpus 1)\n");
+                dp_ctx_destroy(ctx);
+                return 2;
+            }
+            dp_fast_options fo;
+            dp_default_fast_options(&fo);
+            fo.densify = 1;
+            if (fast_iters >= 0)
+                fo.iters = fast_iters;
+            check(dp_set_fast_options(ctx, &fo), "dp_set_fast_options");
+        }
         if (level > 0) {
             // run on pyramid level L (cv::pyrDown^L on the device, P rows 0-1 / 2^L)
             check(dp_build_pyramid(ctx, level + 1), "dp_build_pyramid");
@@ -389,11 +414,12 @@ int main(int argc, char **argv)
         std::printf("{\"output\": \"%s\", \"patches\": %lld, \"written\": %zu, \"seeds\": %zu, \"generated_seeds\": %s, "
                     "\"keypoints\": %lld, \"matches\": %lld, \"seed_ms\": %.3f, \"seed_patches\": %lld, "
                     "\"pops\": %lld, \"candidates\": %lld, \"evals\": %lld, \"generations\": %d, \"refine_ms\": %.3f, "
-                    "\"densify_ms\": %.3f, \"wall_ms\": %.3f, \"gpus\": %d}\n",
+                    "\"densify_ms\": %.3f, \"wall_ms\": %.3f, \"gpus\": %d, \"mode\": \"%s\"}\n",
                     output.c_str(), (long long)st.patches, cloud.size(), use.size() / 3,
                     seeds_path.empty() ? "true" : "false", (long long)sst.keypoints, (long long)sst.matches,
                     sst.total_ms, (long long)st.seed_patches, (long long)st.pops, (long long)st.candidates,
-                    (long long)st.evals, st.generations, st.refine_ms, st.total_ms, wall, gpus);
+                    (long long)st.evals, st.generations, st.refine_ms, st.total_ms, wall, gpus,
+                    fast ? "fast" : "parity");
         return 0;
     } catch (const std::exception &e) {
         std::fprintf(stderr, "densify: %s\n", e.what());

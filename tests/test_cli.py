@@ -147,6 +147,30 @@ def test_cli_densify_ply_equals_oracle(scene_dir, tmp_path, orc):
 
 
 @pytest.mark.gpu
+def test_cli_fast_mode_ply_equals_oracle(scene_dir, tmp_path, orc):
+    """densify --mode fast: the performance-mode densify (dp_fast_options.densify)
+    through the CLI; the PLY equals the oracle's generation-at-a-time restatement
+    with the fast refine, byte for byte.  --gpus 2 is refused in this mode."""
+    from densepoints_amd import FastOptions
+    from densepoints_amd.pmvs import write_ply
+
+    out = tmp_path / "points.ply"
+    args = ("-i", os.path.join(scene_dir, "scene.json"), "--seeds", os.path.join(scene_dir, "seeds.xyz"))
+    res = json.loads(run(*args, "--mode", "fast", "-o", str(out)).stdout)
+    cfg = synth.config(4, 160, 120, 1)
+    P = synth.cameras(cfg)
+    imgs = [synth.render_host(cfg, P, v) for v in range(4)]
+    S = orc.Scene(P, imgs)
+    op = orc.GenerationEngine(S, threads=8, fast=FastOptions(densify=1)).densify_all(synth.seeds(cfg, P))
+    assert res["mode"] == "fast" and res["patches"] == len(op) > 0
+    ref = tmp_path / "oracle.ply"
+    write_ply(str(ref), op)
+    assert out.read_bytes() == ref.read_bytes()
+    assert run(*args, "--mode", "fast", "--gpus", "2", "-o", str(out), check=False).returncode == 2
+    assert run(*args, "--mode", "turbo", check=False).returncode == 2
+
+
+@pytest.mark.gpu
 def test_cli_full_pipeline_generates_seeds(tmp_path_factory, tmp_path, orc):
     """densify -i scene.json with no --seeds: PMVS::Run's InsertSeeds
     (Matcher::GenerateSeeds on the device) then expansion; the PLY equals the

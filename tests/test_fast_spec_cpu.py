@@ -332,3 +332,19 @@ def test_affine_window_map_error_below_sample_grid(orc, small_scene, cell):
     assert n > 500
     assert worst < 16.0, f"affine map off by {worst:.3f} / 32 px"
     assert np.median(start) < 2.5
+
+
+def test_generation_engine_densify_all(orc):
+    """The oracle's generation-at-a-time densify run to the end equals
+    or_densify (parity mode), and in performance mode (dp_fast_options.densify,
+    the spec dp_densify follows) stores accepted patches in sequence order."""
+    cfg = synth.config(6, 320, 240, 1)
+    P, imgs, seeds = synth.scene_host(cfg)
+    S = orc.Scene(P, imgs)
+    op, ost = S.densify(seeds)
+    gp = orc.GenerationEngine(S, threads=8).densify_all(seeds)
+    assert len(gp) == ost["patches"] and gp.tobytes() == op.tobytes()
+    fp = orc.GenerationEngine(S, threads=8, fast=orc.fast_options(densify=1)).densify_all(seeds)
+    assert len(fp) > 20
+    assert (fp["seq"] == np.arange(len(fp))).all()
+    assert (fp["flags"] & 1).all()

@@ -175,3 +175,25 @@ def test_fast_expand_cfg5_full_scene(orc):
     z, _ = synth.surface(sc.cfg, k["pos"][:, :2].astype(np.float64))
     print("cfg5 accepted %d of %d, median |dz| %.5f, staged views per eval %.2f"
           % (len(k), len(gk), float(np.median(np.abs(k["pos"][:, 2] - z))), st["view_evals"] / st["evals"]))
+
+
+@pytest.mark.parametrize("name,max_pops", [("hf6", None), ("plane4", None), ("hf6", 37)])
+def test_fast_densify_bit_exact(orc, name, max_pops):
+    """dp_densify with dp_fast_options.densify = 1: the seed stage and every
+    expansion generation refined in performance mode, the organizer claims as
+    in the parity densify (PatchOrganizer::TryInsert in sequence order), the
+    pop cap (expand.cpp:95); equal to the oracle's generation-at-a-time
+    restatement on every stored field."""
+    sc = scene(name)
+    opts = dp.Options() if max_pops is None else dp.Options(max_pops=max_pops)
+    fo = dp.FastOptions(densify=1)
+    S = orc.Scene(sc.P, sc.imgs, opts)
+    op = orc.GenerationEngine(S, threads=8, fast=fo).densify_all(sc.seeds)
+    with dp.Engine(opts, device=0) as eng:
+        eng.set_views(sc.views)
+        eng.set_fast_options(fo)
+        gp, gst = eng.densify(sc.seeds)
+    assert gst["patches"] == len(op) > 20
+    if max_pops is not None:
+        assert gst["pops"] == max_pops
+    assert_same(gp, op, FIELDS + ("seq", "parent", "rgb"))
