@@ -245,6 +245,19 @@ def main():
                                  "patches": int(dst["patches"]), "candidates": int(dst["candidates"]),
                                  "generations": int(dst["generations"]), "evals": int(dst["evals"]),
                                  "refine_ms": round(dst["refine_ms"], 1), "wall_s": round(wall, 3)}
+        # informational: the same densify with the performance-mode refine
+        # (dp_fast_options.densify: seed stage at n = 16 and expansions at n = 11)
+        eng.set_fast_options(dp.FastOptions(densify=1))
+        t0 = time.perf_counter()
+        _, fst = eng.densify(seeds)
+        wall = time.perf_counter() - t0
+        eng.set_fast_options(dp.FastOptions())
+        result["densify_e2e_fast"] = {"seed_patches": int(fst["seed_patches"]), "patches": int(fst["patches"]),
+                                      "candidates": int(fst["candidates"]), "generations": int(fst["generations"]),
+                                      "evals": int(fst["evals"]), "refine_ms": round(fst["refine_ms"], 1),
+                                      "wall_s": round(wall, 3),
+                                      "Mpatches_per_s_refine": round(int(fst["candidates"]) / max(fst["refine_ms"], 1e-9)
+                                                                     / 1e3, 3)}
     if world > 1 and not args.no_densify and not fast:
         # informational: the same densify with every generation partitioned by
         # reference-view super-tile over the ranks (north star): each
