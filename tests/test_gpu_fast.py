@@ -197,3 +197,18 @@ def test_fast_densify_bit_exact(orc, name, max_pops):
     if max_pops is not None:
         assert gst["pops"] == max_pops
     assert_same(gp, op, FIELDS + ("seq", "parent", "rgb"))
+
+
+def test_fast_densify_refused_by_generation_api(engine):
+    """The generation-at-a-time densify (multi-GPU protocol) stays in parity
+    mode: with dp_fast_options.densify set, dp_densify_begin returns DP_E_ARG
+    instead of silently mixing modes."""
+    sc = scene("hf6")
+    engine.set_views(sc.views)
+    engine.set_fast_options(dp.FastOptions(densify=1))
+    try:
+        with pytest.raises(dp.DensePointsError):
+            engine.densify_begin(sc.seeds)
+    finally:
+        engine.set_fast_options(dp.FastOptions())
+    engine.densify_begin(sc.seeds)
