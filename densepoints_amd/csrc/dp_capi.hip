@@ -955,8 +955,8 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         int rc;
         if (fast) {
             // Expand::ExpandPatch with the fast refine; parents past the pop cap stay put
-            rc = dp_fast_launch(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_FAST_REFINE, c->ok.p, c->store.p + head,
-                                s, o.max_pops - head);
+            rc = dp_fast_launch(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_FAST_REFINE, c->ok.p, c->store.p, s,
+                                head, nullptr, o.max_pops);
         } else {
             dpk::RefineArgs a = refine_args(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_EXPAND, c->ok.p);
             a.parents = c->store.p;
@@ -1021,9 +1021,6 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
         return fail(c, DP_E_ARG, "dp_densify_begin: bad arguments");
     if (!c->V)
         return fail(c, DP_E_STATE, "dp_densify_begin: no views");
-    if (c->fopt.densify)
-        return fail(c, DP_E_ARG, "dp_densify_begin: the performance-mode densify (dp_fast_options.densify) runs in "
-                                 "dp_densify only");
     hipSetDevice(c->device);
     hipStream_t s = c->stream;
     c->g_t0 = std::chrono::steady_clock::now();
@@ -1081,17 +1078,22 @@ static int densify_refine_impl(dp_ctx *c, const dp_generation *gen, int64_t lo, 
         okp = c->ok.p;
     }
     dpk::RefineArgs a{};
+    const bool fast = c->fopt.densify != 0;
+    int rc;
     if (gen->index == 0) {
         // seed.cpp:110-144 on this shard of the seed patches
         DP_HIP(c, hipMemcpyAsync(work, c->seedp.p + lo, sizeof(dp_patch) * nc, hipMemcpyDeviceToDevice, s));
         a = refine_args(c, work, nc, gen->cell, DP_MODE_SEED, okp);
+        rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, nullptr, s) : launch_timed(c, a, s);
     } else {
         // Expand::ExpandPatch of parents head+lo .. head+hi-1 (queue order)
         a = refine_args(c, work, nc, gen->cell, DP_MODE_EXPAND, okp);
         a.parents = c->store.p;
         a.parent0 = gen->head + lo;
+        rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, c->store.p, s, gen->head + lo,
+                                   nullptr, c->opt.max_pops)
+                  : launch_timed(c, a, s);
     }
-    int rc = launch_timed(c, a, s);
     if (rc != DP_OK)
         return rc;
     double ms = 0.0;
@@ -1228,16 +1230,21 @@ static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const 
         return fail(c, DP_E_OOM, "dp_densify_refine_items: shard too large");
     const int32_t nc = (int32_t)nc64;
     dpk::RefineArgs a{};
+    const bool fast = c->fopt.densify != 0;
+    int rc;
     if (gen->index == 0) {
         DP_HIP(c, dpk::launch_gather_patches(c->seedp.p, d_items, n, work, s));
         a = refine_args(c, work, nc, gen->cell, DP_MODE_SEED, okp);
+        rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, nullptr, s) : launch_timed(c, a, s);
     } else {
         a = refine_args(c, work, nc, gen->cell, DP_MODE_EXPAND, okp);
         a.parents = c->store.p;
         a.parent0 = gen->head;
         a.items = d_items;
+        rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, c->store.p, s, gen->head, d_items,
+                                   c->opt.max_pops)
+                  : launch_timed(c, a, s);
     }
-    int rc = launch_timed(c, a, s);
     if (rc != DP_OK)
         return rc;
     double ms = 0.0;

@@ -121,10 +121,12 @@ struct dp_ctx {
 };
 
 // performance-mode launch (dp_fast.hip): refine/eval of n patches in device
-// memory, or the 4n expansion children of d_parents, of which only the first
-// live_parents may expand (dp_densify's pop cap)
+// memory, or the 4 (n / 4) expansion children of parents
+// d_parents[parent0 + (items ? items[k] : k)], k < n / 4, of which only those
+// with a parent index below max_pops expand (dp_densify's pop cap)
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
-                   hipStream_t s, int64_t live_parents = INT64_MAX);
+                   hipStream_t s, int64_t parent0 = 0, const int64_t *items = nullptr,
+                   int64_t max_pops = INT64_MAX);
 
 static inline int fail(dp_ctx *c, int code, const std::string &msg)
 {

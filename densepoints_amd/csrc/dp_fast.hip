@@ -49,7 +49,9 @@ struct FastArgs {
     uint32_t *work;
     unsigned long long *evals;
     const dp_patch *parents; // expansion: child c = parents[c / 4], direction c % 4
-    int64_t live_parents;    // parents[i] expands only for i < live_parents (the pop cap)
+    int64_t parent0;         // chunk k's parent is parents[parent0 + (items ? items[k] : k)] ...
+    const int64_t *items;
+    int64_t max_pops;        // ... and expands only below this index (the pop cap)
     double cvis, ccand;      // cos(visible_angle), cos(candidate_angle) from the host libm
     unsigned long long *stats; // dp_fast_stats: patches, evals, view_evals, staged_bytes
 };
@@ -961,6 +963,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
     // work is dequeued in chunks of 4 (one atomic per chunk): the 4 children of
     // one parent, whose record is read once into LDS, or 4 consecutive patches
     uint32_t chunk_idx = 0xffffffffu, q4 = 4;
+    bool par_live = true;
 #ifdef DP_FAST_TIMING
     for (int k = 0; k < 16; ++k)
         L.tm[k] = 0;
@@ -977,7 +980,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
             if ((uint64_t)chunk_idx * 4u >= (uint64_t)a.n)
                 break;
             if (a.parents) {
-                const uint32_t *src = (const uint32_t *)(a.parents + chunk_idx);
+                const int64_t q = a.parent0 + (a.items ? a.items[chunk_idx] : (int64_t)chunk_idx);
+                par_live = q < a.max_pops;
+                const uint32_t *src = (const uint32_t *)(a.parents + q);
                 if (lane < (int)(sizeof(dp_patch) / 4))
                     ((uint32_t *)&L.par)[lane] = src[lane];
                 wave_sync();
@@ -997,7 +1002,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
             p.flags = 0;
             p.parent = idx >> 2;
             const int pm = __popcll(par.vis[0]) + __popcll(par.vis[1]);
-            live = pm >= a.opt.min_expand_visible && par.ref < (uint32_t)a.V && (int64_t)(idx >> 2) < a.live_parents;
+            live = pm >= a.opt.min_expand_visible && par.ref < (uint32_t)a.V && par_live;
             if (live) {
                 float cp[3];
                 child_position(a, par, (int)(idx & 3u), cp);
@@ -1357,7 +1362,7 @@ template <int B> static hipError_t fast_dispatch(int N, const dpk::FastArgs &a, 
 }
 
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
-                   hipStream_t s, int64_t live_parents)
+                   hipStream_t s, int64_t parent0, const int64_t *items, int64_t max_pops)
 {
     int rc = ensure_gray(c);
     if (rc != DP_OK)
@@ -1376,7 +1381,9 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.work = c->d_work;
     a.evals = c->d_evals;
     a.parents = d_parents;
-    a.live_parents = live_parents;
+    a.parent0 = parent0;
+    a.items = items;
+    a.max_pops = max_pops;
     // the InitRelatedImages thresholds as cosines, by the host libm (the spec's)
     a.cvis = std::cos(c->opt.visible_angle);
     a.ccand = std::cos(c->opt.candidate_angle);

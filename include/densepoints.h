@@ -423,8 +423,8 @@ typedef struct dp_fast_options {
     float ls_step;        /* 1.0   initial line-search step, scaled units           */
     int32_t densify;      /* 0     1: dp_densify runs the seed stage (at
                                    seed_cell_size) and every expansion (at
-                                   expand_cell_size) with the fast refine; the
-                                   generation-at-a-time API then returns DP_E_ARG */
+                                   expand_cell_size) with the fast refine, and so
+                                   does the generation-at-a-time (multi-GPU) API */
     int32_t reserved;
 } dp_fast_options;
 

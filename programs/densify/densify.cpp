@@ -39,7 +39,7 @@ void usage()
                  "                             reference-view super-tile; output identical to 1 GPU)\n"
                  "               [--mode parity|fast] [--fast-iters N]  (fast: the performance-mode\n"
                  "                             refine -- LDS-staged gray tiles, fused CG -- for the seed\n"
-                 "                             stage and every expansion; one GPU)\n"
+                 "                             stage and every expansion)\n"
                  "       densify --synthetic V,W,H,KIND --write-scene DIR\n");
 }
 
@@ -324,19 +324,13 @@ int main(int argc, char **argv)
             }
         };
         check(dp_set_views(ctx, (int)imgs.size(), P.data(), dimg.data()), "dp_set_views");
-        if (fast) {
-            if (gpus > 1) {
-                std::fprintf(stderr, "densify: --mode fast runs on one GPU (--gpus 1)\n");
-                dp_ctx_destroy(ctx);
-                return 2;
-            }
-            dp_fast_options fo;
-            dp_default_fast_options(&fo);
-            fo.densify = 1;
-            if (fast_iters >= 0)
-                fo.iters = fast_iters;
-            check(dp_set_fast_options(ctx, &fo), "dp_set_fast_options");
-        }
+        // --mode fast: dp_fast_options.densify on every context
+        dp_fast_options fo;
+        dp_default_fast_options(&fo);
+        fo.densify = fast ? 1 : 0;
+        if (fast_iters >= 0)
+            fo.iters = fast_iters;
+        check(dp_set_fast_options(ctx, &fo), "dp_set_fast_options");
         if (level > 0) {
             // run on pyramid level L (cv::pyrDown^L on the device, P rows 0-1 / 2^L)
             check(dp_build_pyramid(ctx, level + 1), "dp_build_pyramid");
@@ -368,6 +362,7 @@ int main(int argc, char **argv)
                 check(dp_ctx_create(&opt, (device + g) % (ndev > 0 ? ndev : 1), &cg), "dp_ctx_create");
                 ctxs.push_back(cg);
                 check(dp_set_views(cg, (int)imgs.size(), P.data(), dimg.data()), "dp_set_views");
+                check(dp_set_fast_options(cg, &fo), "dp_set_fast_options");
                 if (level > 0) {
                     check(dp_build_pyramid(cg, level + 1), "dp_build_pyramid");
                     check(dp_set_level(cg, level), "dp_set_level");

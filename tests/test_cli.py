@@ -150,7 +150,8 @@ def test_cli_densify_ply_equals_oracle(scene_dir, tmp_path, orc):
 def test_cli_fast_mode_ply_equals_oracle(scene_dir, tmp_path, orc):
     """densify --mode fast: the performance-mode densify (dp_fast_options.densify)
     through the CLI; the PLY equals the oracle's generation-at-a-time restatement
-    with the fast refine, byte for byte.  --gpus 2 is refused in this mode."""
+    with the fast refine, byte for byte, on one GPU and partitioned over two
+    contexts (--gpus 2)."""
     from densepoints_amd import FastOptions
     from densepoints_amd.pmvs import write_ply
 
@@ -166,7 +167,9 @@ def test_cli_fast_mode_ply_equals_oracle(scene_dir, tmp_path, orc):
     ref = tmp_path / "oracle.ply"
     write_ply(str(ref), op)
     assert out.read_bytes() == ref.read_bytes()
-    assert run(*args, "--mode", "fast", "--gpus", "2", "-o", str(out), check=False).returncode == 2
+    out2 = tmp_path / "points2.ply"
+    res2 = json.loads(run(*args, "--mode", "fast", "--gpus", "2", "-o", str(out2)).stdout)
+    assert res2["gpus"] == 2 and out2.read_bytes() == ref.read_bytes()
     assert run(*args, "--mode", "turbo", check=False).returncode == 2
 
 

@@ -199,16 +199,30 @@ def test_fast_densify_bit_exact(orc, name, max_pops):
     assert_same(gp, op, FIELDS + ("seq", "parent", "rgb"))
 
 
-def test_fast_densify_refused_by_generation_api(engine):
-    """The generation-at-a-time densify (multi-GPU protocol) stays in parity
-    mode: with dp_fast_options.densify set, dp_densify_begin returns DP_E_ARG
-    instead of silently mixing modes."""
+def test_fast_densify_generation_protocol_bit_exact(orc):
+    """The generation-at-a-time densify (the multi-GPU protocol) in
+    performance mode: every generation's candidates refined by owner shards
+    (dp_densify_owners + dp_densify_refine_items, two simulated ranks) and
+    committed in sequence order equals dp_densify with the same flag."""
     sc = scene("hf6")
-    engine.set_views(sc.views)
-    engine.set_fast_options(dp.FastOptions(densify=1))
-    try:
-        with pytest.raises(dp.DensePointsError):
-            engine.densify_begin(sc.seeds)
-    finally:
-        engine.set_fast_options(dp.FastOptions())
-    engine.densify_begin(sc.seeds)
+    opts = dp.Options(max_pops=90)
+    fo = dp.FastOptions(densify=1)
+    with dp.Engine(opts, device=0) as eng:
+        eng.set_views(sc.views)
+        eng.set_fast_options(fo)
+        gp, gst = eng.densify(sc.seeds)
+        g = eng.densify_begin(sc.seeds)
+        while g.items:
+            own, _ = eng.densify_owners(g, 2)
+            per = g.per_item
+            cand = np.zeros(g.items * per, dtype=N.PATCH_DTYPE)
+            acc = np.zeros(g.items * per, dtype=np.uint8)
+            for r in range(2):
+                it = np.nonzero(own == r)[0].astype(np.int64)
+                c, a = eng.densify_refine_items(g, it)
+                sl = (it[:, None] * per + np.arange(per)).reshape(-1)
+                cand[sl], acc[sl] = c, a
+            g = eng.densify_commit(g, cand, acc)
+        sp, sst = eng.densify_result()
+    assert sst["patches"] == gst["patches"] > 20 and sst["pops"] == gst["pops"]
+    assert sp.tobytes() == gp.tobytes()
