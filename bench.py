@@ -282,6 +282,20 @@ def main():
             "max_share_vs_mean": round(max((mx * world / it) for it, mx, _ in parts if it > 0), 3),
             "collective": f"all_gather_into_tensor ({'RCCL' if backend == 'nccl' else backend}) of 80-B candidate "
                           "records + accept flags"}
+        # the same partitioned densify with the performance-mode refine (dp_fast_options.densify)
+        eng.set_fast_options(dp.FastOptions(densify=1))
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        _, fst = D.densify_partitioned_device(eng, seeds, dist, torch.device("cuda", local))
+        torch.cuda.synchronize()
+        wall = D.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
+        eng.set_fast_options(dp.FastOptions())
+        result["densify_partitioned_fast"] = {
+            "ranks": world, "patches": int(fst["patches"]), "generations": int(fst["generations"]),
+            "refine_ms_max_rank": round(fst["refine_ms"], 1), "wall_s": round(wall, 3),
+            "Mpatches_per_s": round(int(fst["candidates"]) / wall / 1e6, 3),
+            "gathered_MB_total": round(sum(fst["gathered_bytes"]) / 1e6, 2)}
     if rank == 0 and not args.no_seeds:
         result["seed_generation"] = seed_generation(eng, args)
     st = np.zeros(8, dtype=np.uint64)
