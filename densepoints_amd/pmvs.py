@@ -448,9 +448,12 @@ class PMVS:
     reference's Matcher::GenerateSeeds output is just a list of 3-D points).
     """
 
-    def __init__(self, options: Options | None = None, device: int = 0):
+    def __init__(self, options: Options | None = None, device: int = 0, fast: FastOptions | None = None):
+        """fast: FastOptions with densify = 1 runs the whole loop in performance
+        mode (no reference counterpart; dp_fast_options.densify)"""
         self.options = options or Options()
         self.device = device
+        self.fast = fast
         self.views: list[View] = []
         self.patches = empty_patches(0)
         self.stats: dict = {}
@@ -470,6 +473,8 @@ class PMVS:
 
         with Engine(self.options, self.device) as eng:
             eng.set_views(self.views)
+            if self.fast is not None:
+                eng.set_fast_options(self.fast)
             seed_stats = None
             if seeds_xyz is None:
                 m = Matcher(eng, matcher_options)

@@ -226,3 +226,18 @@ def test_fast_densify_generation_protocol_bit_exact(orc):
         sp, sst = eng.densify_result()
     assert sst["patches"] == gst["patches"] > 20 and sst["pops"] == gst["pops"]
     assert sp.tobytes() == gp.tobytes()
+
+
+def test_pmvs_host_mirror_fast_mode(orc):
+    """PMVS(fast=FastOptions(densify=1)).run (the Python mirror of PMVS::Run,
+    pmvs.cpp:22-43) in performance mode equals the oracle's restatement."""
+    sc = scene("plane4")
+    fo = dp.FastOptions(densify=1)
+    pm = dp.PMVS(fast=fo)
+    for v in sc.views:
+        pm.add_camera(v)
+    pm.run(sc.seeds)
+    S = orc.Scene(sc.P, sc.imgs)
+    op = orc.GenerationEngine(S, threads=8, fast=fo).densify_all(sc.seeds)
+    assert len(pm.patches) == len(op) > 20
+    assert_same(pm.patches, op, FIELDS + ("seq", "parent", "rgb"))
