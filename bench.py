@@ -482,9 +482,9 @@ def fast_traffic(cell, fo, B):
     import glob
 
     found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_all_kernels.json")))
-    if not found or B != 4 * 65536 or fo.tile_budget > 6144:
+    if not found or B != 4 * 65536 or fo.tile_budget > 6656:
         return None
-    tag = {7: "fast_kernel<4, 3, true, false, 6144", 11: "fast_kernel<2, 4, false, true, 6144"}.get(cell)
+    tag = {7: "fast_kernel<4, 3, true, false, 6656", 11: "fast_kernel<2, 4, false, true, 6656"}.get(cell)
     if tag is None:
         return None
     with open(found[-1]) as f:

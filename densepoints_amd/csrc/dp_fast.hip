@@ -28,19 +28,31 @@
 namespace dpk {
 namespace {
 
-constexpr int kFastMaxV = 32;     // staged views per patch (per-view tables)
+constexpr int kFastMaxV = 32;     // staged views per patch (per-view records)
 constexpr int kFastMaxBbox = 48;  // window bounding-box side cap (grazing views)
 constexpr int kFastMaxMargin = 7; // keeps a tile row <= 64 entries (one lane each)
 constexpr int kFastSlots = 4;     // at most this many samples per lane per view pass
+constexpr int kFastRec = 64;      // LDS record per staged view (bytes), counted in the budget
+constexpr float kRcpMin = 0x1p-20f, kRcpMax = 0x1p+64f; // operand range of recip_rn
 
 struct GrayPlane {
     const __half *p;
     int32_t w, h, pitch, pad;
 };
 
+// fp32 camera of a view (or_fast.c fcam_of): rows 0-1 of P times 32 (1/32-px
+// units), row 2, the centre and the unit x-axis, each rounded once on the host
+struct FastCam {
+    float Q[12];
+    float C[3], xr[3];
+    int32_t W, H;
+};
+static_assert(sizeof(FastCam) == 80, "FastCam is read as five 16-byte pieces");
+
 struct FastArgs {
     const dpg::ViewDev *views;
     const GrayPlane *gray;
+    const FastCam *cams;
     int32_t V, cell, mode, n;
     dp_options opt;
     dp_fast_options fo;
@@ -52,16 +64,9 @@ struct FastArgs {
     int64_t parent0;         // chunk k's parent is parents[parent0 + (items ? items[k] : k)] ...
     const int64_t *items;
     int64_t max_pops;        // ... and expands only below this index (the pop cap)
-    double cvis, ccand;      // cos(visible_angle), cos(candidate_angle) from the host libm
+    float cvis, ccand;       // cos(visible_angle), cos(candidate_angle) from the host libm, rounded
+    float cvis2, ccand2;     // their squares (fp32)
     unsigned long long *stats; // dp_fast_stats: patches, evals, view_evals, staged_bytes
-};
-
-// per staged view, written once per staging (rank order)
-struct StageRec {
-    float v[15];      // H0, Hd, He1, He2, Hn (folded, scaled, fp32)
-    float umax, vmax; // 32 (tw - 1), 32 (th - 1)
-    uint32_t info;    // tile byte offset | row bytes << 16
-    int32_t view;
 };
 
 // per evaluation, per staged view: A.xyz 2^23+umax | B1.xyz 2^23+vmax | B2.xyz
@@ -77,41 +82,45 @@ __device__ __forceinline__ uint32_t tile_rowb(float umax_b)
     return (((__float_as_uint(umax_b) & 0x7fffffu) >> 5) + 3u) >> 1 << 2;
 }
 
-// patch frame (uniform, fp64): or_fast.c fast_stage
+// patch frame (uniform, fp32): or_fast.c fast_frame
 struct Frame {
-    double X0[3], r[3];
-    double e1[3], e2[3], nn[3]; // times the pixel size
-    double u1[3], u2[3], un[3]; // unit
-    double sd, st;
-    bool degenerate;
+    float X0[3], r[3];
+    float e1[3], e2[3], nn[3]; // times the pixel size
+    float u1[3], u2[3], un[3]; // unit
+    float sd, st;
+    int degenerate;
 };
 
 // conjugate-gradient state between evaluations (uniform, kept in LDS so the
 // sampling passes have the registers)
 constexpr int kFastPoses = 4;  // poses per batched evaluation (start + 3 differences)
-constexpr int kFastItems = 44; // (view, pose) records per pass set (the staging union's room)
+constexpr int kFastItems = 44; // (view, pose) records per pass set
 
 struct CgState {
-    double x[3], x1[3], g[3], gp[3], d[3], dp[3], u[3];
-    double f, f1, gg, ggp, alpha;
-    double px[kFastPoses][3], fr[kFastPoses]; // poses to evaluate, their objectives
+    float4 pf[kFastPoses]; // sampler inputs (df, af, bf, 0) of the poses to evaluate
+    float x[3], x1[3], g[3], gp[3], d[3], dp[3], u[3];
+    float gg, ggp, alpha;
+    int32_t f, f1;
+    float px[kFastPoses][3]; // poses to evaluate (scaled units)
+    int32_t fr[kFastPoses];  // their objectives (exact integers)
 };
 
-template <int kBudget> struct FastLds {
-    uint32_t tiles[kBudget / 4];
+// The wave's LDS.  The arena holds the staged views' 64-byte records (rank
+// order: the 15 folded fp32 vectors and a packed word: view | (tw - 1) << 7 |
+// (th - 1) << 13 | (tile offset / 4) << 19) followed by their tiles.
+template <int kArena> struct FastLds {
+    uint32_t arena[kArena / 4];
     union {
-        StageRec st[kFastMaxV]; // during staging
-        struct {
-            EvalRec par[kFastItems];
-            uint32_t mom[kFastItems][4];
-            double score[kFastMaxV];
-        } ev;
-    } u;
+        EvalRec par[kFastItems]; // a round's (view, pose) items
+        double score[kFastMaxV]; // a scoring evaluation's fp64 NCCs (after its passes)
+    } e;
+    uint32_t mom[kFastItems][4];
     uint64_t vis[2], cand[2];
     Frame F;
     CgState cg;
     dp_patch p;
     dp_patch par;      // parent of the current chunk (expansion)
+    float cpos[4][3];  // its four children's centres
     uint8_t vlist[64];
 #ifdef DP_FAST_TIMING
     unsigned long long tm[16], tlast;
@@ -145,14 +154,6 @@ __device__ __forceinline__ int lane_id()
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__device__ __forceinline__ double uni_f64(double v)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffff));
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-
 // sum over each group of LP = 64/G lanes (DPP); the total of group j lands in
 // lane LP (j + 1) - 1
 template <int G> __device__ __forceinline__ uint32_t group_total(uint32_t v)
@@ -178,8 +179,8 @@ __device__ __forceinline__ int wave_incl_i32(int v) { return (int)group_total<1>
 
 __device__ __forceinline__ int wave_sum_i32(int v) { return __builtin_amdgcn_readlane(wave_incl_i32(v), 63); }
 
-// RN(1 / b) for b >= 2^-20: v_rcp_f32 seed and one Newton step (checked
-// bitwise against IEEE division on the GPU, tests/test_gpu_fast.py)
+// RN(1 / b) for b in [2^-20, 2^64]: v_rcp_f32 seed and one Newton step
+// (checked bitwise against IEEE division on the GPU, tests/test_gpu_fast.py)
 __device__ __forceinline__ float recip_rn(float b)
 {
     const float r = __builtin_amdgcn_rcpf(b);
@@ -187,47 +188,74 @@ __device__ __forceinline__ float recip_rn(float b)
     return __builtin_fmaf(r, e, r);
 }
 
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
+__device__ __forceinline__ float fdot(const float *a, const float *b)
 {
-    return __builtin_amdgcn_perm(hi, lo, sel);
+    return __builtin_fmaf(a[2], b[2], __builtin_fmaf(a[1], b[1], a[0] * b[0]));
 }
 
-// all lanes compute the same values; F is the wave's LDS copy
-__device__ __forceinline__ void make_frame(const dpg::ViewDev &rv, const float *pos, const float *nrm, int cell,
-                                           Frame &F)
+// row k of Q applied to a point (with the 4th column) / a direction
+__device__ __forceinline__ float qpt(const float *Q, int k, const float *X)
 {
-    const double X0[3] = {(double)pos[0], (double)pos[1], (double)pos[2]};
-    const double n0[3] = {(double)nrm[0], (double)nrm[1], (double)nrm[2]};
-    double cu, cw, qu, qw;
-    dpg::project(rv.P, X0[0], X0[1], X0[2], cu, cw);
-    dpg::project(rv.P, X0[0] + rv.xr[0], X0[1] + rv.xr[1], X0[2] + rv.xr[2], qu, qw);
-    const double du = qu - cu, dv = qw - cw;
-    const double dx = sqrt(du * du + dv * dv);
-    const double nl = sqrt(dpg::dot3(n0, n0));
-    F.degenerate = !(dx > 0.0) || !(nl > 0.0) || dx != dx;
-    if (F.degenerate)
+    return __builtin_fmaf(Q[4 * k + 2], X[2],
+                          __builtin_fmaf(Q[4 * k + 1], X[1], __builtin_fmaf(Q[4 * k], X[0], Q[4 * k + 3])));
+}
+
+__device__ __forceinline__ float qdir(const float *Q, int k, const float *w)
+{
+    return __builtin_fmaf(Q[4 * k + 2], w[2], __builtin_fmaf(Q[4 * k + 1], w[1], Q[4 * k] * w[0]));
+}
+
+// projection in 1/32 px (or_fast.c fproj); false if the depth is outside the
+// reciprocal's range
+__device__ __forceinline__ bool fproj(const float *Q, const float *X, float &u, float &w)
+{
+    const float h2 = qpt(Q, 2, X);
+    if (!(h2 >= kRcpMin && h2 <= kRcpMax))
+        return false;
+    const float r = recip_rn(h2);
+    u = qpt(Q, 0, X) * r;
+    w = qpt(Q, 1, X) * r;
+    return true;
+}
+
+// the patch frame (or_fast.c fast_frame), fp32; all lanes compute the same
+// values, F is the wave's LDS copy
+__device__ __forceinline__ void make_frame(const FastCam &rc, const float *pos, const float *nrm, int cell, Frame &F)
+{
+    const float X[3] = {pos[0], pos[1], pos[2]};
+    const float n0[3] = {nrm[0], nrm[1], nrm[2]};
+    const float Xq[3] = {X[0] + rc.xr[0], X[1] + rc.xr[1], X[2] + rc.xr[2]};
+    float cu = 0.0f, cw = 0.0f, qu = 0.0f, qw = 0.0f;
+    F.degenerate = 1;
+    if (!fproj(rc.Q, X, cu, cw) || !fproj(rc.Q, Xq, qu, qw))
         return;
-    const double ps = 1.0 / dx;
-    const double inl = 1.0 / nl;
-    const double nn[3] = {n0[0] * inl, n0[1] * inl, n0[2] * inl};
-    const double xn = dpg::dot3(rv.xr, nn);
-    double e1[3] = {rv.xr[0] - xn * nn[0], rv.xr[1] - xn * nn[1], rv.xr[2] - xn * nn[2]};
-    const double el = sqrt(dpg::dot3(e1, e1));
-    if (!(el > 0.0)) {
-        F.degenerate = true;
+    const float du = qu - cu, dv = qw - cw;
+    const float dx = __builtin_sqrtf(__builtin_fmaf(dv, dv, du * du));
+    const float nl = __builtin_sqrtf(fdot(n0, n0));
+    if (!(dx > 0.0f) || !(dx <= 0x1p+100f) || !(nl > 0.0f))
         return;
-    }
-    const double iel = 1.0 / el;
+    const float ps = 32.0f / dx;
+    const float inl = 1.0f / nl;
+    const float nn[3] = {n0[0] * inl, n0[1] * inl, n0[2] * inl};
+    const float xn = fdot(rc.xr, nn);
+    float e1[3] = {__builtin_fmaf(-xn, nn[0], rc.xr[0]), __builtin_fmaf(-xn, nn[1], rc.xr[1]),
+                   __builtin_fmaf(-xn, nn[2], rc.xr[2])};
+    const float el = __builtin_sqrtf(fdot(e1, e1));
+    if (!(el > 0.0f))
+        return;
+    const float iel = 1.0f / el;
     for (int k = 0; k < 3; ++k)
         e1[k] = e1[k] * iel;
-    double e2[3];
-    dpg::cross3(nn, e1, e2);
-    const double r[3] = {X0[0] - rv.C[0], X0[1] - rv.C[1], X0[2] - rv.C[2]};
-    const double rl = sqrt(dpg::dot3(r, r));
+    const float e2[3] = {__builtin_fmaf(nn[1], e1[2], -(nn[2] * e1[1])), __builtin_fmaf(nn[2], e1[0], -(nn[0] * e1[2])),
+                         __builtin_fmaf(nn[0], e1[1], -(nn[1] * e1[0]))};
+    const float r[3] = {X[0] - rc.C[0], X[1] - rc.C[1], X[2] - rc.C[2]};
+    const float rl = __builtin_sqrtf(fdot(r, r));
+    if (!(rl > 0.0f))
+        return;
     F.sd = ps / rl;
-    F.st = 2.0 / (double)(cell - 1);
+    F.st = 2.0f / (float)(cell - 1);
     for (int k = 0; k < 3; ++k) {
-        F.X0[k] = X0[k];
+        F.X0[k] = X[k];
         F.r[k] = r[k];
         F.u1[k] = e1[k];
         F.u2[k] = e2[k];
@@ -236,86 +264,60 @@ __device__ __forceinline__ void make_frame(const dpg::ViewDev &rv, const float *
         F.e2[k] = e2[k] * ps;
         F.nn[k] = nn[k] * ps;
     }
+    F.degenerate = 0;
 }
 
-__device__ __forceinline__ double rowdot(const double *P, const double *w)
-{
-    return (P[0] * w[0] + P[1] * w[1]) + P[2] * w[2];
-}
-
-// the lane's view geometry before the budget (or_fast.c view_geo): only the
-// window box (the fp64 vectors are recomputed for the views that are kept, so
-// they are not live across the budget loop)
+// the lane's view before the budget (or_fast.c view_geo): the five homography
+// columns over the centre depth and the initial window's pixel box from its
+// first-order map
 struct Geo {
+    float g[15];
     int xa, xb, ya, yb;
     bool ok;
 };
 
-// vector i of the view (H0, Hd, He1, He2, Hn: P applied to the frame vectors),
-// in 1/32 px for rows 0-1, divided by the centre's depth H0[2] (times inv)
-__device__ __forceinline__ void geo_vec(const dpg::ViewDev &v, const Frame &F, int i, double inv, double *g)
-{
-    const double *w = i == 0 ? F.X0 : i == 1 ? F.r : i == 2 ? F.e1 : i == 3 ? F.e2 : F.nn;
-    double H[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-        H[k] = i == 0 ? rowdot(v.P + 4 * k, w) + v.P[4 * k + 3] : rowdot(v.P + 4 * k, w);
-    g[0] = (32.0 * H[0]) * inv;
-    g[1] = (32.0 * H[1]) * inv;
-    g[2] = H[2] * inv;
-}
-
-__device__ __forceinline__ double geo_inv(const dpg::ViewDev &v, const Frame &F)
-{
-    return 1.0 / (rowdot(v.P + 8, F.X0) + v.P[11]);
-}
-
-__device__ Geo view_geo(const dpg::ViewDev &v, const Frame &F, int cell)
+__device__ __forceinline__ Geo view_geo(const FastCam &c, const Frame &F, int cell)
 {
     Geo G;
     G.ok = false;
-    const double s = rowdot(v.P + 8, F.X0) + v.P[11];
-    if (!(s > 0.0))
-        return G;
-    const double inv = 1.0 / s;
-    double g0[3], g2[3], g3[3];
-    geo_vec(v, F, 0, inv, g0);
-    geo_vec(v, F, 2, inv, g2);
-    geo_vec(v, F, 3, inv, g3);
-    const double c = 0.5 * (double)(cell - 1);
-    double umin = 0, umax = 0, vmin = 0, vmax = 0;
+    float H[15];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const double ti = (q & 1) ? c : -c, tj = (q & 2) ? c : -c;
-        double h[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-            h[k] = (g0[k] + ti * g2[k]) + tj * g3[k];
-        if (!(h[2] > 0.0))
-            return G;
-        double u, ww;
-        dpg::div2(h[0], h[1], h[2], u, ww); // = h0 / h2, h1 / h2 (IEEE, one shared reciprocal)
-        if (!(u > 0.0 && u < 32.0 * v.W && ww > 0.0 && ww < 32.0 * v.H))
-            return G;
-        if (q == 0 || u < umin)
-            umin = u;
-        if (q == 0 || u > umax)
-            umax = u;
-        if (q == 0 || ww < vmin)
-            vmin = ww;
-        if (q == 0 || ww > vmax)
-            vmax = ww;
+    for (int k = 0; k < 3; ++k) {
+        H[k] = qpt(c.Q, k, F.X0);
+        H[3 + k] = qdir(c.Q, k, F.r);
+        H[6 + k] = qdir(c.Q, k, F.e1);
+        H[9 + k] = qdir(c.Q, k, F.e2);
+        H[12 + k] = qdir(c.Q, k, F.nn);
     }
-    G.xa = (int)floor(umin / 32.0);
-    G.xb = (int)floor(umax / 32.0) + 1;
-    G.ya = (int)floor(vmin / 32.0);
-    G.yb = (int)floor(vmax / 32.0) + 1;
+    const float s = H[2];
+    if (!(s >= kRcpMin && s <= kRcpMax))
+        return G;
+    const float inv = recip_rn(s);
+#pragma unroll
+    for (int i = 0; i < 15; ++i)
+        G.g[i] = H[i] * inv;
+    const float U0 = G.g[0], V0 = G.g[1];
+    const float Ui = __builtin_fmaf(-U0, G.g[8], G.g[6]), Vi = __builtin_fmaf(-V0, G.g[8], G.g[7]);
+    const float Uj = __builtin_fmaf(-U0, G.g[11], G.g[9]), Vj = __builtin_fmaf(-V0, G.g[11], G.g[10]);
+    const float cc = 0.5f * (float)(cell - 1);
+    const float eu = cc * (__builtin_fabsf(Ui) + __builtin_fabsf(Uj));
+    const float ev = cc * (__builtin_fabsf(Vi) + __builtin_fabsf(Vj));
+    const float ez = cc * (__builtin_fabsf(G.g[8]) + __builtin_fabsf(G.g[11]));
+    const float umin = U0 - eu, umax = U0 + eu, vmin = V0 - ev, vmax = V0 + ev;
+    if (!(G.g[2] - ez > 0.0f))
+        return G;
+    if (!(umin > 0.0f && umax < (float)(32 * c.W) && vmin > 0.0f && vmax < (float)(32 * c.H)))
+        return G;
+    G.xa = (int)__builtin_floorf(umin * 0.03125f);
+    G.xb = (int)__builtin_floorf(umax * 0.03125f) + 1;
+    G.ya = (int)__builtin_floorf(vmin * 0.03125f);
+    G.yb = (int)__builtin_floorf(vmax * 0.03125f) + 1;
     G.ok = G.xb - G.xa + 1 <= kFastMaxBbox && G.yb - G.ya + 1 <= kFastMaxBbox;
     return G;
 }
 
 struct Rect {
-    int x0, y0, tw, th, bytes;
+    int x0, y0, tw, th, tbytes;
 };
 
 __device__ __forceinline__ Rect tile_rect(const Geo &g, int W, int H, int M)
@@ -331,22 +333,15 @@ __device__ __forceinline__ Rect tile_rect(const Geo &g, int W, int H, int M)
     t.tw = x1 - x0 + 1;
     t.th = y1 - y0 + 1;
     // (tw + 1) columns (right tap) as words of two pixels, th + 1 rows (lower tap)
-    t.bytes = 4 * ((t.tw + 2) / 2) * (t.th + 1);
+    t.tbytes = 4 * ((t.tw + 2) / 2) * (t.th + 1);
     return t;
 }
 
-// per-lane staged view (lanes 0 .. m-1 hold ranks 0 .. m-1)
-struct Staged {
-    float v[15];
-    float umax, vmax;
-    uint32_t info;
-    int view;
-};
-
-// Stage the wave's patch: frame, usable views, margin, tiles into LDS.
-// Returns m (uniform); the lane of rank r holds that view's vectors in S.
-template <int kBudget>
-__device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged &S, unsigned long long &staged_bytes,
+// Stage the wave's patch (or_fast.c fast_stage after the frame): usable
+// views, margin, the views' records and tiles into the arena.  Returns m
+// (uniform); record r describes the view of rank r.
+template <int kArena>
+__device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned long long &staged_bytes,
                      unsigned long long &clipped)
 {
     const int lane = lane_id();
@@ -366,7 +361,7 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     const int nconsider = nvis < 64 ? nvis : 64;
     const int maxv = a.fo.max_views < kFastMaxV ? a.fo.max_views : kFastMaxV;
     const int view = lane < nconsider ? (int)L.vlist[lane] : 0;
-    const dpg::ViewDev &vw = a.views[view];
+    const FastCam &cam = a.cams[view];
     // the view's gray plane descriptor, loaded now so that its latency
     // overlaps the window geometry
     GrayPlane gpl{};
@@ -375,31 +370,33 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     Geo g;
     g.ok = false;
     if (lane < nconsider)
-        g = view_geo(vw, L.F, cell);
+        g = view_geo(cam, L.F, cell);
     const uint64_t usable = __ballot(g.ok);
     const int rank = __popcll(usable & ((1ull << lane) - 1ull));
     const bool staged = g.ok && rank < maxv;
     int M = margin;
     Rect t;
     for (;;) {
-        t = tile_rect(g, vw.W, vw.H, M);
-        const int tot = uni(wave_sum_i32(staged ? t.bytes : 0));
+        t = tile_rect(g, cam.W, cam.H, M);
+        const int tot = uni(wave_sum_i32(staged ? t.tbytes + kFastRec : 0));
         if (tot <= a.fo.tile_budget || M == 0)
             break;
         --M;
     }
-    const int incl = wave_incl_i32(staged ? t.bytes : 0);
+    const int incl = wave_incl_i32(staged ? t.tbytes + kFastRec : 0);
     const bool keep = staged && incl <= a.fo.tile_budget;
-    const int m = __popcll(__ballot(keep));
+    const uint64_t kept = __ballot(keep);
+    const int m = __popcll(kept);
     clipped += (M < margin || m < __popcll(__ballot(staged))) ? 1ull : 0ull;
     // bytes the tiles copy from the gray planes (whole 32-bit pixel pairs)
-    staged_bytes += (unsigned long long)uni(wave_sum_i32(keep ? t.bytes : 0));
+    staged_bytes += (unsigned long long)uni(wave_sum_i32(keep ? t.tbytes : 0));
+    // the tile's arena offset: after the m records, the tiles of lower rank
+    const uint32_t toff = (uint32_t)(kFastRec * m + (incl - t.tbytes - kFastRec) - kFastRec * rank);
     // the tile copy's parameters stay in the view's lane (the copy loop
     // broadcasts them per view by readlane)
     uint64_t dbase = 0;
     int dpitch = 0, dW2 = 0, dnw = 0, dylim = 0;
     float dinv = 0.0f;
-    uint32_t doff = 0;
     if (keep) {
         dbase = (uint64_t)(uintptr_t)(gpl.p + (size_t)t.y0 * (size_t)gpl.pitch + t.x0);
         dpitch = gpl.pitch;
@@ -407,40 +404,24 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
         dnw = dW2 * (t.th + 1);
         dinv = 1.0f / (float)dW2;
         dylim = gpl.h - 1 - t.y0;
-        doff = (uint32_t)(incl - t.bytes);
-    }
-    const uint64_t kept = __ballot(keep);
-    if (keep) {
-        StageRec &R = L.u.st[rank];
-        const double inv = geo_inv(vw, L.F);
+        // the record: the five vectors relative to the tile origin, packed word
+        const float ox = -32.0f * (float)t.x0, oy = -32.0f * (float)t.y0;
+        float4 *R = (float4 *)((char *)L.arena + kFastRec * rank);
+        float v[16];
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            double gv[3];
-            geo_vec(vw, L.F, i, inv, gv);
-            const double ga = gv[0] - (32.0 * (double)t.x0) * gv[2];
-            const double gb = gv[1] - (32.0 * (double)t.y0) * gv[2];
-            R.v[3 * i] = (float)ga;
-            R.v[3 * i + 1] = (float)gb;
-            R.v[3 * i + 2] = (float)gv[2];
+            v[3 * i] = __builtin_fmaf(ox, g.g[3 * i + 2], g.g[3 * i]);
+            v[3 * i + 1] = __builtin_fmaf(oy, g.g[3 * i + 2], g.g[3 * i + 1]);
+            v[3 * i + 2] = g.g[3 * i + 2];
         }
-        R.umax = (float)(32 * (t.tw - 1));
-        R.vmax = (float)(32 * (t.th - 1));
-        R.info = (uint32_t)(incl - t.bytes) | ((uint32_t)(4 * ((t.tw + 2) / 2)) << 16);
-        R.view = view;
+        v[15] = __uint_as_float((uint32_t)view | (uint32_t)(t.tw - 1) << 7 | (uint32_t)(t.th - 1) << 13 |
+                                (toff >> 2) << 19);
+        R[0] = make_float4(v[0], v[1], v[2], v[3]);
+        R[1] = make_float4(v[4], v[5], v[6], v[7]);
+        R[2] = make_float4(v[8], v[9], v[10], v[11]);
+        R[3] = make_float4(v[12], v[13], v[14], v[15]);
     }
-    wave_sync();
     TMARK(L, 2);
-    // lane r takes rank r's vectors (kept in registers for the evaluations)
-    if (lane < m) {
-        const StageRec &R = L.u.st[lane];
-#pragma unroll
-        for (int i = 0; i < 15; ++i)
-            S.v[i] = R.v[i];
-        S.umax = R.umax;
-        S.vmax = R.vmax;
-        S.info = R.info;
-        S.view = R.view;
-    }
     // tiles: rows y0t .. y0t + th (clamped to the image) of biased-fp16 gray,
     // columns x0t .. x0t + 2 W2 - 1 (the plane's padding columns replicate
     // the last pixel), copied straight into LDS by global_load_lds_dword: the
@@ -449,7 +430,7 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
     // before a single wait.
     typedef __attribute__((address_space(3))) void *lds_ptr_t;
     typedef __attribute__((address_space(1))) const void *gptr_t;
-    const uint32_t tbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)L.tiles;
+    const uint32_t tbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)L.arena;
     for (uint64_t q = kept; q; q &= q - 1) {
         const int l = (int)__builtin_ctzll(q);
         const uint64_t pb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(dbase >> 32), l) << 32) |
@@ -458,7 +439,7 @@ __device__ int stage(const FastArgs &a, FastLds<kBudget> &L, int margin, Staged 
         const int pitch = __builtin_amdgcn_readlane(dpitch, l), W2 = __builtin_amdgcn_readlane(dW2, l);
         const int nw = __builtin_amdgcn_readlane(dnw, l), ylim = __builtin_amdgcn_readlane(dylim, l);
         const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dinv), l));
-        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)doff, l);
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)toff, l);
         for (int i = 0; i < nw; i += 64) {
             const int d = i + lane;
             const int y = (int)(((float)d + 0.5f) * inv);
@@ -509,7 +490,7 @@ template <int G, int S> __device__ Slots make_slots(int cell)
 
 // One view's sample in 1/16 gray levels (or_fast.c fast_sample), in three
 // phases so that a pass issues every lane's LDS reads before it consumes any:
-// tap_addr (projective map, clamp, 1/32-px split), tap_load (the two aligned
+// tap_addr (affine map, clamp, 1/32-px split), tap_load (the two aligned
 // words around each row's tap pair), tap_blend (funnel shift, bilinear).
 struct Tap {
     uint32_t a0, a1;   // aligned LDS byte addresses of rows y0, y0 + 1
@@ -579,22 +560,22 @@ __device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
     return b >> 6;
 }
 
-// Objective evaluations at up to kFastPoses scaled poses (or_fast.c
-// fast_objective), L.cg.px[0 .. K-1] -> L.cg.fr[0 .. K-1] (uniform).  The
+// Objective evaluations at up to kFastPoses poses (or_fast.c fast_objective):
+// L.cg.pf[0 .. K-1] (sampler inputs) -> L.cg.fr[0 .. K-1] (uniform).  The
 // poses' (view, pose) items share the sampling passes: item i = r K' + k
 // (view r, pose k of a chunk of K' poses) runs in pass i / G, group i % G, so
 // the K' anchors (r = 0) are the first K' groups of pass 0 and every item's
 // anchor samples come from group k of pass 0 by ds_bpermute.  A chunk holds
 // at most kFastItems items (the LDS records) and K' <= G poses.  kScore (one
-// pose): the fp64 NCC of rank r >= 1 goes to L.u.ev.score[r] instead.
-template <int G, int NS, bool kTail, bool kMask, bool kScore, int kBudget>
-__device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m, int K)
+// pose): the fp64 NCC of rank r >= 1 goes to L.e.score[r] instead.
+template <int G, int NS, bool kTail, bool kMask, bool kScore, int kArena>
+__device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slots &sl, int m, int K)
 {
     constexpr int LP = 64 / G;
     const int lane = lane_id();
     if (m < 2) {
         for (int k = 0; k < K; ++k)
-            L.cg.fr[k] = 2.0;
+            L.cg.fr[k] = 2 << 24;
         wave_sync();
         return;
     }
@@ -604,37 +585,46 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
     kc = kc < kFastPoses ? kc : kFastPoses;
     kc = kScore ? 1 : kc;
     const int j = (int)((unsigned)lane / LP), g = lane & (LP - 1);
-    const char *tiles = (const char *)L.tiles;
+    const char *tiles = (const char *)L.arena;
     const int N = a.cell * a.cell;
     const double dmin = ((a.opt.ncc_denom_min * 256.0) * (double)N) * (double)N;
+    // lane -> (pose, view) of the NCC finish, pose-major: floor(l * rm / 2^16)
+    // = floor(l / m) for l < 64 with rm = ceil(2^16 / m) (2 <= m <= 32: the
+    // quotient is an integer or at least 1/32 from one, far above rcp's error)
+    const uint32_t rm = (uint32_t)__builtin_ceilf(65536.0f * __builtin_amdgcn_rcpf((float)m));
     for (int k0 = 0; k0 < K; k0 += kc) {
         const int kn = K - k0 < kc ? K - k0 : kc;
         const int Q = kn * m;
         // 1/kn for item -> (view, pose): floor(i * ceil(2^16 / kn) / 2^16) = i / kn for i < 2^10
-        const uint32_t rk = (65536u + (uint32_t)kn - 1u) / (uint32_t)kn;
-        if (lane < m) {
-            for (int k = 0; k < kn; ++k) {
-                const float df = (float)(L.cg.px[k0 + k][0] * L.F.sd), af = (float)(L.cg.px[k0 + k][1] * L.F.st),
-                            bf = (float)(L.cg.px[k0 + k][2] * L.F.st);
-                EvalRec &E = L.u.ev.par[lane * kn + k];
-                // homography columns at the pose (or_fast.c fast_affine), then
-                // its first-order map about the window centre: A/Az and the
-                // quotient rule's (B - (A/Az) Bz) / Az, one reciprocal
-                const float ax = __builtin_fmaf(df, S.v[3], S.v[0]), ay = __builtin_fmaf(df, S.v[4], S.v[1]);
-                const float az = __builtin_fmaxf(__builtin_fmaf(df, S.v[5], S.v[2]), 0x1p-20f);
-                const float ix = __builtin_fmaf(-af, S.v[12], S.v[6]), iy = __builtin_fmaf(-af, S.v[13], S.v[7]),
-                            iz = __builtin_fmaf(-af, S.v[14], S.v[8]);
-                const float jx = __builtin_fmaf(-bf, S.v[12], S.v[9]), jy = __builtin_fmaf(-bf, S.v[13], S.v[10]),
-                            jz = __builtin_fmaf(-bf, S.v[14], S.v[11]);
-                const float rz = recip_rn(az); // == 1.0f / az (az >= 2^-20)
-                const float u0 = ax * rz, v0 = ay * rz;
-                E.q[0] = make_float4(u0, v0, 0.0f, 0x1p23f + S.umax);
-                E.q[1] = make_float4(__builtin_fmaf(-u0, iz, ix) * rz, __builtin_fmaf(-v0, iz, iy) * rz, 0.0f,
-                                     0x1p23f + S.vmax);
-                E.q[2] = make_float4(__builtin_fmaf(-u0, jz, jx) * rz, __builtin_fmaf(-v0, jz, jy) * rz, 0.0f,
-                                     __uint_as_float((S.info & 0xffffu) -
-                                                     __umul24((0x4B000000u >> 5) & 0xffffffu, S.info >> 16)));
-            }
+        const uint32_t rk = kn == 1 ? 65536u : kn == 2 ? 32768u : kn == 3 ? 21846u : 16384u;
+        // the round's items, one lane each (lane = item r kn + k): the pose's
+        // homography columns from the view's record (fast_sample), then its
+        // first-order map about the window centre: A/Az and the quotient
+        // rule's (B - (A/Az) Bz) / Az, one reciprocal
+        if (lane < Q) {
+            const int r = (int)(__umul24((uint32_t)lane, rk) >> 16);
+            const int k = lane - r * kn;
+            const float4 *R = (const float4 *)((const char *)L.arena + kFastRec * r);
+            const float4 r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3];
+            const float4 pf = L.cg.pf[k0 + k];
+            const float df = pf.x, af = pf.y, bf = pf.z;
+            const float ax = __builtin_fmaf(df, r0.w, r0.x), ay = __builtin_fmaf(df, r1.x, r0.y);
+            const float az = __builtin_fmaxf(__builtin_fmaf(df, r1.y, r0.z), kRcpMin);
+            const float ix = __builtin_fmaf(-af, r3.x, r1.z), iy = __builtin_fmaf(-af, r3.y, r1.w),
+                        iz = __builtin_fmaf(-af, r3.z, r2.x);
+            const float jx = __builtin_fmaf(-bf, r3.x, r2.y), jy = __builtin_fmaf(-bf, r3.y, r2.z),
+                        jz = __builtin_fmaf(-bf, r3.z, r2.w);
+            const float rz = recip_rn(az); // == 1.0f / az
+            const float u0 = ax * rz, v0 = ay * rz;
+            const uint32_t pk = __float_as_uint(r3.w);
+            const uint32_t tw1 = (pk >> 7) & 63u, th1 = (pk >> 13) & 63u, toff = (pk >> 19) << 2;
+            const uint32_t rowb = ((tw1 + 3u) >> 1) << 2;
+            EvalRec &E = L.e.par[lane];
+            E.q[0] = make_float4(u0, v0, 0.0f, __uint_as_float(0x4B000000u + 32u * tw1));
+            E.q[1] = make_float4(__builtin_fmaf(-u0, iz, ix) * rz, __builtin_fmaf(-v0, iz, iy) * rz, 0.0f,
+                                 __uint_as_float(0x4B000000u + 32u * th1));
+            E.q[2] = make_float4(__builtin_fmaf(-u0, jz, jx) * rz, __builtin_fmaf(-v0, jz, jy) * rz, 0.0f,
+                                 __uint_as_float(toff - __umul24((0x4B000000u >> 5) & 0xffffffu, rowb)));
         }
         wave_sync();
         TMARK(L, 10);
@@ -649,7 +639,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
             const bool tail = kTail && p == 0;
             const int r = (int)(__umul24((uint32_t)i, rk) >> 16);
             const int k = i - r * kn;
-            const EvalRec &E = *(const EvalRec *)((const char *)L.u.ev.par + (act ? (uint32_t)i * 48u : 0u));
+            const EvalRec &E = *(const EvalRec *)((const char *)L.e.par + (act ? (uint32_t)i * 48u : 0u));
             const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
             const uint32_t off = __float_as_uint(qc.w), rowb = tile_rowb(qa.w);
             Tap tp[NS], tt{};
@@ -657,7 +647,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
             for (int s2 = 0; s2 < NS; ++s2)
                 tp[s2] = tap_addr(qa, qb, qc, off, rowb, sl.ti[s2], sl.tj[s2]);
             if (tail) {
-                const EvalRec &T = L.u.ev.par[lane < Q ? lane : 0];
+                const EvalRec &T = L.e.par[lane < Q ? lane : 0];
                 const float4 ta = T.q[0], tb = T.q[1], tc = T.q[2];
                 tt = tap_addr(ta, tb, tc, __float_as_uint(tc.w), tile_rowb(ta.w), sl.tail, sl.tail);
             }
@@ -697,30 +687,32 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
             ss = group_total<G>(ss);
             sx = group_total<G>(sx);
             if (g == LP - 1 && act) {
-                L.u.ev.mom[i][0] = s;
-                L.u.ev.mom[i][1] = ss;
-                L.u.ev.mom[i][2] = sx;
+                L.mom[i][0] = s;
+                L.mom[i][1] = ss;
+                L.mom[i][2] = sx;
             }
         }
         wave_sync();
         TMARK(L, 11);
-        // NCC per item, one lane each (lane t: view t / kn, pose t % kn): the
-        // integer moment products are below 2^53, so these fp64 expressions
-        // are exactly the spec's int64 ones
-        const int rt = (int)(__umul24((uint32_t)lane, rk) >> 16);
-        const int kt = lane - rt * kn;
-        // the tail sample of the item's anchor (lane kt holds item kt's)
+        // NCC per item, one lane each, pose-major (lane l: pose kt = l / m,
+        // view rt = l % m, item rt kn + kt): the integer moment products are
+        // below 2^53, so these fp64 expressions are exactly the spec's int64 ones
+        const int kt = (int)(__umul24((uint32_t)lane, rm) >> 16);
+        const int rt = lane - kt * m;
+        const int it = rt * kn + kt;
+        // the tail samples of the item and of its pose's anchor (lane i holds item i's)
         const uint32_t a0 = kTail ? (uint32_t)__builtin_amdgcn_ds_bpermute(kt << 2, (int)bt) : 0u;
+        const uint32_t b0 = kTail ? (uint32_t)__builtin_amdgcn_ds_bpermute((it < 64 ? it : 0) << 2, (int)bt) : 0u;
         int q = 0;
         if (lane < Q && rt >= 1) {
-            uint32_t sa = L.u.ev.mom[kt][0], saa = L.u.ev.mom[kt][1];
-            uint32_t sb = L.u.ev.mom[lane][0], sbb = L.u.ev.mom[lane][1], sab = L.u.ev.mom[lane][2];
+            uint32_t sa = L.mom[kt][0], saa = L.mom[kt][1];
+            uint32_t sb = L.mom[it][0], sbb = L.mom[it][1], sab = L.mom[it][2];
             if (kTail) {
                 sa += a0;
                 saa += __umul24(a0, a0);
-                sb += bt;
-                sbb += __umul24(bt, bt);
-                sab += __umul24(a0, bt);
+                sb += b0;
+                sbb += __umul24(b0, b0);
+                sab += __umul24(a0, b0);
             }
             const double Sa = (double)sa, Saa = (double)saa, Sb = (double)sb, Sbb = (double)sbb, Sab = (double)sab;
             const double dN = (double)N;
@@ -730,21 +722,25 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
             if (kScore) {
                 // the reported score (filter, FAST_EVAL): fp64 finish
                 const double den = sqrt(va * vb);
-                L.u.ev.score[rt] = num / (den > dmin ? den : dmin);
+                L.e.score[rt] = num / (den > dmin ? den : dmin);
             } else {
                 // the refine's objective term: fp32 finish in 2^-24 steps
                 const float den = __builtin_sqrtf((float)va * (float)vb);
                 const float dminf = (float)dmin;
-                q = (int)__builtin_rintf(((float)num / (den > dminf ? den : dminf)) * 16777216.0f);
+                const float rr = recip_rn(den > dminf ? den : dminf);
+                q = (int)__builtin_rintf(((float)num * rr) * 16777216.0f);
             }
         }
         TMARK(L, 12);
         if (!kScore) {
-            // per pose: the sum over r >= 1 of 1 - NCC, NCCs in 2^-24 steps, an
-            // exact integer reduction across the wave (|q| <= 2^24, <= 31 views)
+            // per pose: (m - 1) 2^24 minus the sum of its NCCs in 2^-24 steps,
+            // an exact integer reduction: one inclusive prefix over the wave,
+            // pose kt's lanes are kt m .. kt m + m - 1
+            const int pre = (int)group_total<1>((uint32_t)q);
             for (int k = 0; k < kn; ++k) {
-                const int tot = __builtin_amdgcn_readlane((int)group_total<1>((uint32_t)(kt == k ? q : 0)), 63);
-                L.cg.fr[k0 + k] = (double)((m - 1) * 16777216 - tot) * 0x1p-24; // < 2^29
+                const int hi = __builtin_amdgcn_readlane(pre, (k + 1) * m - 1);
+                const int lo = k ? __builtin_amdgcn_readlane(pre, k * m - 1) : 0;
+                L.cg.fr[k0 + k] = (m - 1) * 16777216 - (hi - lo); // < 2^30
             }
         }
         wave_sync();
@@ -752,51 +748,58 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kBudget> &L, const Sta
     }
 }
 
-// Nonlinear CG (or_fast.c fast_cg) as a state machine around ONE evaluation
-// call site (the sampling passes are inlined once); its state lives in LDS.
-// The start evaluation and the three forward differences of each iteration
-// are independent, so they share one set of passes (evaluate_poses); the
-// results are those of one evaluation at a time.  Returns evaluations;
-// L.cg.x = the scaled pose.
-template <int G, int NS, bool kTail, bool kMask, int kBudget>
-__device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m)
+// the sampler inputs of pose k: (x0 sd, x1 st, x2 st)
+template <int kArena> __device__ __forceinline__ void set_pose(FastLds<kArena> &L, int k, float x0, float x1, float x2)
+{
+    CgState &C = L.cg;
+    C.px[k][0] = x0;
+    C.px[k][1] = x1;
+    C.px[k][2] = x2;
+    C.pf[k] = make_float4(x0 * L.F.sd, x1 * L.F.st, x2 * L.F.st, 0.0f);
+}
+
+// Nonlinear CG (or_fast.c fast_cg, fp32) as a state machine around ONE
+// evaluation call site (the sampling passes are inlined once); its state
+// lives in LDS.  The start evaluation and the three forward differences of
+// each iteration are independent, so they share one set of passes
+// (evaluate_poses); the results are those of one evaluation at a time.
+// Returns evaluations; L.cg.x = the scaled pose.
+template <int G, int NS, bool kTail, bool kMask, int kArena>
+__device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl, int m)
 {
     enum { kStart = 0, kFd = 1, kProbe1 = 2, kProbe2 = 3 };
     CgState &C = L.cg;
-    const double h = (double)a.fo.fd_step, inv_h = 1.0 / h;
+    const float h = a.fo.fd_step;
+    const float gs = (1.0f / h) * 0x1p-24f; // gradient per objective unit
     for (int k = 0; k < 3; ++k) {
-        C.x[k] = 0.0;
-        C.gp[k] = 0.0;
-        C.dp[k] = 0.0;
+        C.x[k] = 0.0f;
+        C.gp[k] = 0.0f;
+        C.dp[k] = 0.0f;
     }
-    C.alpha = (double)a.fo.ls_step;
-    C.ggp = 0.0;
+    C.alpha = a.fo.ls_step;
+    C.ggp = 0.0f;
     int E = 0, it = 0, phase = kStart;
     for (;;) {
         int K = 1;
         if (phase == kStart || phase == kFd) {
             // f(x) (start only), then f(x + h e_i), i = 0, 1, 2
             const int k0 = phase == kStart ? 1 : 0;
-            if (phase == kStart) {
-                C.px[0][0] = C.x[0];
-                C.px[0][1] = C.x[1];
-                C.px[0][2] = C.x[2];
-            }
+            if (phase == kStart)
+                set_pose(L, 0, C.x[0], C.x[1], C.x[2]);
             K = phase == kStart ? (a.fo.iters > 0 ? 4 : 1) : 3;
-            for (int i = 0; i < 3; ++i) {
-                C.px[k0 + i][0] = i == 0 ? C.x[0] + h : C.x[0];
-                C.px[k0 + i][1] = i == 1 ? C.x[1] + h : C.x[1];
-                C.px[k0 + i][2] = i == 2 ? C.x[2] + h : C.x[2];
+            if (K > 1) {
+                set_pose(L, k0 + 0, C.x[0] + h, C.x[1], C.x[2]);
+                set_pose(L, k0 + 1, C.x[0], C.x[1] + h, C.x[2]);
+                set_pose(L, k0 + 2, C.x[0], C.x[1], C.x[2] + h);
             }
         } else {
-            const double st = phase == kProbe1 ? C.alpha : (C.f1 < C.f ? 2.0 * C.alpha : 0.5 * C.alpha);
-            C.px[0][0] = C.x[0] + st * C.u[0];
-            C.px[0][1] = C.x[1] + st * C.u[1];
-            C.px[0][2] = C.x[2] + st * C.u[2];
+            const float st = phase == kProbe1 ? C.alpha : (C.f1 < C.f ? 2.0f * C.alpha : 0.5f * C.alpha);
+            set_pose(L, 0, __builtin_fmaf(st, C.u[0], C.x[0]), __builtin_fmaf(st, C.u[1], C.x[1]),
+                     __builtin_fmaf(st, C.u[2], C.x[2]));
         }
         wave_sync();
         TMARK(L, 15);
-        evaluate_poses<G, NS, kTail, kMask, false>(a, L, S, sl, m, K);
+        evaluate_poses<G, NS, kTail, kMask, false>(a, L, sl, m, K);
         if (phase == kStart || phase == kFd) {
             int k0 = 0;
             if (phase == kStart) {
@@ -806,48 +809,47 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
                     break;
                 k0 = 1;
             }
+            float g[3];
             for (int i = 0; i < 3; ++i)
-                C.g[i] = (C.fr[k0 + i] - C.f) * inv_h;
+                g[i] = (float)(C.fr[k0 + i] - C.f) * gs;
             E += 3;
-            const double g0 = C.g[0], g1 = C.g[1], g2 = C.g[2];
-            const double gg = (g0 * g0 + g1 * g1) + g2 * g2;
-            C.gg = gg;
-            if (gg == 0.0)
+            const float gg = fdot(g, g);
+            if (gg == 0.0f)
                 break;
-            double beta = 0.0;
-            if (it > 0 && C.ggp > 0.0) {
-                beta = ((g0 * (g0 - C.gp[0]) + g1 * (g1 - C.gp[1])) + g2 * (g2 - C.gp[2])) / C.ggp;
-                beta = beta > 0.0 ? beta : 0.0;
+            float beta = 0.0f;
+            if (it > 0 && C.ggp > 0.0f) {
+                const float dg[3] = {g[0] - C.gp[0], g[1] - C.gp[1], g[2] - C.gp[2]};
+                beta = fdot(g, dg) / C.ggp;
+                beta = beta > 0.0f ? beta : 0.0f;
             }
-            double d0 = beta * C.dp[0] - g0, d1 = beta * C.dp[1] - g1, d2 = beta * C.dp[2] - g2;
-            if ((d0 * g0 + d1 * g1) + d2 * g2 >= 0.0) {
-                d0 = 0.0 - g0;
-                d1 = 0.0 - g1;
-                d2 = 0.0 - g2;
+            float d[3];
+            for (int i = 0; i < 3; ++i)
+                d[i] = __builtin_fmaf(beta, C.dp[i], -g[i]);
+            if (fdot(d, g) >= 0.0f) {
+                for (int i = 0; i < 3; ++i)
+                    d[i] = -g[i];
             }
-            const double inv_nd = 1.0 / sqrt((d0 * d0 + d1 * d1) + d2 * d2);
-            C.d[0] = d0;
-            C.d[1] = d1;
-            C.d[2] = d2;
-            C.u[0] = d0 * inv_nd;
-            C.u[1] = d1 * inv_nd;
-            C.u[2] = d2 * inv_nd;
+            const float inv_nd = 1.0f / __builtin_sqrtf(fdot(d, d));
+            for (int i = 0; i < 3; ++i) {
+                C.g[i] = g[i];
+                C.d[i] = d[i];
+                C.u[i] = d[i] * inv_nd;
+            }
+            C.gg = gg;
             phase = kProbe1;
         } else if (phase == kProbe1) {
             C.f1 = C.fr[0];
-            C.x1[0] = C.px[0][0];
-            C.x1[1] = C.px[0][1];
-            C.x1[2] = C.px[0][2];
+            for (int k = 0; k < 3; ++k)
+                C.x1[k] = C.px[0][k];
             phase = kProbe2;
         } else {
-            const double f2 = C.fr[0];
+            const int32_t f2 = C.fr[0];
             if (C.f1 < C.f) {
                 if (f2 < C.f1) {
-                    C.x[0] = C.px[0][0];
-                    C.x[1] = C.px[0][1];
-                    C.x[2] = C.px[0][2];
+                    for (int k = 0; k < 3; ++k)
+                        C.x[k] = C.px[0][k];
                     C.f = f2;
-                    C.alpha = 2.0 * C.alpha;
+                    C.alpha = 2.0f * C.alpha;
                 } else {
                     for (int k = 0; k < 3; ++k)
                         C.x[k] = C.x1[k];
@@ -855,12 +857,11 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
                 }
             } else {
                 if (f2 < C.f) {
-                    C.x[0] = C.px[0][0];
-                    C.x[1] = C.px[0][1];
-                    C.x[2] = C.px[0][2];
+                    for (int k = 0; k < 3; ++k)
+                        C.x[k] = C.px[0][k];
                     C.f = f2;
                 }
-                C.alpha = 0.5 * C.alpha;
+                C.alpha = 0.5f * C.alpha;
             }
             E += 2;
             for (int k = 0; k < 3; ++k) {
@@ -879,43 +880,50 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kBudget> &L, const Staged &S
 }
 
 // one scoring evaluation at the staged pose (FAST_EVAL, the filter): the fp64
-// NCC of rank r >= 1 in L.u.ev.score[r]
-template <int G, int NS, bool kTail, bool kMask, int kBudget>
-__device__ void evaluate_score(const FastArgs &a, FastLds<kBudget> &L, const Staged &S, const Slots &sl, int m)
+// NCC of rank r >= 1 in L.e.score[r]
+template <int G, int NS, bool kTail, bool kMask, int kArena>
+__device__ void evaluate_score(const FastArgs &a, FastLds<kArena> &L, const Slots &sl, int m)
 {
-    L.cg.px[0][0] = 0.0;
-    L.cg.px[0][1] = 0.0;
-    L.cg.px[0][2] = 0.0;
+    L.cg.pf[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     wave_sync();
-    evaluate_poses<G, NS, kTail, kMask, true>(a, L, S, sl, m, 1);
+    evaluate_poses<G, NS, kTail, kMask, true>(a, L, sl, m, 1);
 }
 
-// InitRelatedImages' per-view test (patch.cpp:30-45) with the angle tests as
-// cosine tests (or_fast.c fast_init_related): 1 visible, 2 candidate, 0 none
-__device__ __forceinline__ int classify_cos(const dpg::ViewDev &v, const double *X, const double *n, double cvis,
-                                           double ccand)
+// x > c for x = dn / sqrt(dd), compared squared (or_fast.c cos_above)
+__device__ __forceinline__ bool cos_above(float dn, float dd, float c, float c2)
 {
-    double u, w;
-    dpg::project(v.P, X[0], X[1], X[2], u, w);
-    if (!dpg::inside(u, w, v.W, v.H))
+    if (c >= 0.0f)
+        return dn > 0.0f && dn * dn > c2 * dd;
+    return dn >= 0.0f || dn * dn < c2 * dd;
+}
+
+// InitRelatedImages' per-view test (patch.cpp:30-45) in fp32 with the angle
+// tests as squared cosine tests (or_fast.c fast_init_related): 1 visible,
+// 2 candidate, 0 none
+__device__ __forceinline__ int classify_f32(const FastCam &c, const float *X, const float *n, const FastArgs &a)
+{
+    float u = 0.0f, w = 0.0f;
+    if (!fproj(c.Q, X, u, w))
         return 0;
-    const double d[3] = {X[0] - v.C[0], X[1] - v.C[1], X[2] - v.C[2]};
-    const double x = dpg::dot3(n, d) / sqrt(dpg::dot3(d, d));
-    return x > cvis ? 1 : x > ccand ? 2 : 0;
+    if (!(u > 0.0f && u < (float)(32 * c.W) && w > 0.0f && w < (float)(32 * c.H)))
+        return 0;
+    const float d[3] = {X[0] - c.C[0], X[1] - c.C[1], X[2] - c.C[2]};
+    const float dn = fdot(n, d), dd = fdot(d, d);
+    return cos_above(dn, dd, a.cvis, a.cvis2) ? 1 : cos_above(dn, dd, a.ccand, a.ccand2) ? 2 : 0;
 }
 
 // Patch::InitRelatedImages (patch.cpp:19-49), one lane per view
-template <int kBudget> __device__ void init_related(const FastArgs &a, FastLds<kBudget> &L, const dp_patch &p)
+template <int kArena> __device__ void init_related(const FastArgs &a, FastLds<kArena> &L, const dp_patch &p)
 {
     const int lane = lane_id();
     const int ref = (int)p.ref;
-    const double X[3] = {p.pos[0], p.pos[1], p.pos[2]};
-    const double n[3] = {p.normal[0], p.normal[1], p.normal[2]};
+    const float X[3] = {p.pos[0], p.pos[1], p.pos[2]};
+    const float n[3] = {p.normal[0], p.normal[1], p.normal[2]};
     int c0 = 0, c1 = 0;
     if (lane < a.V && lane != ref)
-        c0 = classify_cos(a.views[lane], X, n, a.cvis, a.ccand);
+        c0 = classify_f32(a.cams[lane], X, n, a);
     if (64 + lane < a.V && 64 + lane != ref)
-        c1 = classify_cos(a.views[64 + lane], X, n, a.cvis, a.ccand);
+        c1 = classify_f32(a.cams[64 + lane], X, n, a);
     const uint64_t v0 = __ballot(c0 == 1), v1 = __ballot(c1 == 1);
     const uint64_t k0 = __ballot(c0 == 2), k1 = __ballot(c1 == 2);
     wave_sync();
@@ -926,42 +934,50 @@ template <int kBudget> __device__ void init_related(const FastArgs &a, FastLds<k
     wave_sync();
 }
 
-// Expand::ExpandPatch child centre (expand.cpp:107-125)
-__device__ void child_position(const FastArgs &a, const dp_patch &par, int dir, float *out)
+// Expand::ExpandPatch child centres (expand.cpp:107-125, the reference's fp64
+// arithmetic as in or_child_positions): lane d < 4 computes direction d
+template <int kArena> __device__ void child_positions(const FastArgs &a, FastLds<kArena> &L)
 {
-    const dpg::ViewDev &rv = a.views[par.ref];
-    const double X[3] = {par.pos[0], par.pos[1], par.pos[2]};
-    const double nrm[3] = {par.normal[0], par.normal[1], par.normal[2]};
-    double yax[3];
-    dpg::cross3(nrm, rv.xr, yax);
-    double cu, cv, qu, qv;
-    dpg::project(rv.P, X[0], X[1], X[2], cu, cv);
-    dpg::project(rv.P, X[0] + rv.xr[0], X[1] + rv.xr[1], X[2] + rv.xr[2], qu, qv);
-    const double du = qu - cu, dv = qv - cv;
-    const double dx = sqrt(du * du + dv * dv);
-    const double scale = (double)a.opt.grid_scale / dx;
-    for (int i = 0; i < 3; ++i) {
-        const double d = dir == 0 ? rv.xr[i] : dir == 1 ? -rv.xr[i] : dir == 2 ? yax[i] : -yax[i];
-        out[i] = (float)(X[i] + scale * d);
+    const int lane = lane_id();
+    const dp_patch &par = L.par;
+    if (lane < 4) {
+        const dpg::ViewDev &rv = a.views[par.ref];
+        const double X[3] = {par.pos[0], par.pos[1], par.pos[2]};
+        const double nrm[3] = {par.normal[0], par.normal[1], par.normal[2]};
+        double yax[3];
+        dpg::cross3(nrm, rv.xr, yax);
+        double cu, cv, qu, qv;
+        dpg::project(rv.P, X[0], X[1], X[2], cu, cv);
+        dpg::project(rv.P, X[0] + rv.xr[0], X[1] + rv.xr[1], X[2] + rv.xr[2], qu, qv);
+        const double du = qu - cu, dv = qv - cv;
+        const double dx = sqrt(du * du + dv * dv);
+        const double scale = (double)a.opt.grid_scale / dx;
+        for (int i = 0; i < 3; ++i) {
+            const double d = lane == 0 ? rv.xr[i] : lane == 1 ? -rv.xr[i] : lane == 2 ? yax[i] : -yax[i];
+            L.cpos[lane][i] = (float)(X[i] + scale * d);
+        }
     }
+    wave_sync();
 }
 
-// occupancy the LDS arena allows (1-wave workgroups, 160 KiB per CU): 16 KiB
-// tiles -> 2 waves/SIMD, 8 KiB -> 3, 6 KiB -> 4; the register budget follows
-template <int kBudget> struct FastOcc {
-    static constexpr int value = kBudget <= 6144 ? 4 : kBudget <= 8192 ? 3 : 2;
+// occupancy the LDS arena allows (1-wave workgroups, 160 KiB per CU): the
+// 6.5 KiB arena -> 4 waves/SIMD, 8 KiB -> 3, 16 KiB -> 2; the register budget
+// follows
+template <int kArena> struct FastOcc {
+    static constexpr int value = kArena <= 6656 ? 4 : kArena <= 8192 ? 3 : 2;
 };
 
-template <int G, int NS, bool kTail, bool kMask, int kBudget, int kMode>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBudget>::value))) void fast_kernel(FastArgs a)
+template <int G, int NS, bool kTail, bool kMask, int kArena, int kMode>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kArena>::value))) void fast_kernel(FastArgs a)
 {
-    __shared__ FastLds<kBudget> L;
+    __shared__ FastLds<kArena> L;
     const int lane = lane_id();
     const Slots sl = make_slots<G, NS>(a.cell);
     unsigned long long wave_evals = 0, wave_vev = 0, wave_bytes = 0, wave_patches = 0, wave_clip = 0;
     dp_patch &p = L.p;
     // work is dequeued in chunks of 4 (one atomic per chunk): the 4 children of
-    // one parent, whose record is read once into LDS, or 4 consecutive patches
+    // one parent, whose record is read once into LDS (with the children's
+    // centres), or 4 consecutive patches
     uint32_t chunk_idx = 0xffffffffu, q4 = 4;
     bool par_live = true;
 #ifdef DP_FAST_TIMING
@@ -986,6 +1002,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                 if (lane < (int)(sizeof(dp_patch) / 4))
                     ((uint32_t *)&L.par)[lane] = src[lane];
                 wave_sync();
+                const dp_patch &par = L.par;
+                const int pm = __popcll(par.vis[0]) + __popcll(par.vis[1]);
+                par_live = par_live && pm >= a.opt.min_expand_visible && par.ref < (uint32_t)a.V;
+                if (par_live)
+                    child_positions(a, L);
             }
         }
         TMARK(L, 0);
@@ -1001,14 +1022,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
             p.evals = 0;
             p.flags = 0;
             p.parent = idx >> 2;
-            const int pm = __popcll(par.vis[0]) + __popcll(par.vis[1]);
-            live = pm >= a.opt.min_expand_visible && par.ref < (uint32_t)a.V && par_live;
+            live = par_live;
             if (live) {
-                float cp[3];
-                child_position(a, par, (int)(idx & 3u), cp);
-                p.pos[0] = cp[0];
-                p.pos[1] = cp[1];
-                p.pos[2] = cp[2];
+                const int d = (int)(idx & 3u);
+                p.pos[0] = L.cpos[d][0];
+                p.pos[1] = L.cpos[d][1];
+                p.pos[2] = L.cpos[d][2];
             }
         } else {
             p = a.patches[idx];
@@ -1025,24 +1044,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
             L.vis[0] = p.vis[0];
             L.vis[1] = p.vis[1];
             const int ref = uni((int)p.ref);
-            const dpg::ViewDev &rv = a.views[ref];
-            make_frame(rv, p.pos, p.normal, a.cell, L.F);
+            const FastCam &rc = a.cams[ref];
+            make_frame(rc, p.pos, p.normal, a.cell, L.F);
             wave_sync();
             TMARK(L, 1);
             if (kMode == DP_MODE_FAST_EVAL) {
-                Staged S;
-                const bool degen = L.F.degenerate;
-                const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes, wave_clip);
+                const bool degen = L.F.degenerate != 0;
+                const int m = degen ? 0 : stage(a, L, 0, wave_bytes, wave_clip);
                 p.evals += 1;
                 if (degen)
                     p.flags |= DP_PATCH_DEGENERATE;
                 ok = m >= 2;
                 wave_vev += ok ? (unsigned long long)m : 0ull;
                 if (ok) {
-                    evaluate_score<G, NS, kTail, kMask>(a, L, S, sl, m);
+                    evaluate_score<G, NS, kTail, kMask>(a, L, sl, m);
                     double sum = 0.0;
                     for (int k = 1; k < m; ++k)
-                        sum = sum + L.u.ev.score[k];
+                        sum = sum + L.e.score[k];
                     p.score = (float)(sum / (double)(m - 1));
                 } else {
                     p.score = -1.0f;
@@ -1054,23 +1072,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                     p.score = -1.0f;
                     rejected = true;
                 } else {
-                    Staged S;
-                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), S, wave_bytes, wave_clip);
+                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), wave_bytes, wave_clip);
                     if (m >= 2) {
-                        const int E = cg_refine<G, NS, kTail, kMask>(a, L, S, sl, m);
+                        const int E = cg_refine<G, NS, kTail, kMask>(a, L, sl, m);
                         TMARK(L, 5);
                         p.evals += (uint32_t)E;
                         wave_vev += (unsigned long long)E * (unsigned long long)m;
+                        // X' = X0 + d (X0 - C_ref); n' = normalize(n + a e1 + b e2)
                         const Frame &F = L.F;
-                        const double d = L.cg.x[0] * F.sd, aa = L.cg.x[1] * F.st, bb = L.cg.x[2] * F.st;
-                        double nrm[3];
+                        const float d = L.cg.x[0] * F.sd, aa = L.cg.x[1] * F.st, bb = L.cg.x[2] * F.st;
+                        float nrm[3];
                         for (int k = 0; k < 3; ++k)
-                            nrm[k] = (F.un[k] + aa * F.u1[k]) + bb * F.u2[k];
-                        const double ml = sqrt(dpg::dot3(nrm, nrm));
+                            nrm[k] = __builtin_fmaf(bb, F.u2[k], __builtin_fmaf(aa, F.u1[k], F.un[k]));
+                        const float il = 1.0f / __builtin_sqrtf(fdot(nrm, nrm));
                         float np[3], nn[3];
                         for (int k = 0; k < 3; ++k) {
-                            np[k] = (float)(F.X0[k] + d * F.r[k]);
-                            nn[k] = (float)(nrm[k] / ml);
+                            np[k] = __builtin_fmaf(d, F.r[k], F.X0[k]);
+                            nn[k] = nrm[k] * il;
                         }
                         wave_sync();
                         for (int k = 0; k < 3; ++k) {
@@ -1088,35 +1106,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kBud
                     p.cand[1] = L.cand[1];
                     TMARK(L, 6);
                     // fast filter: re-staged at the new pose, margin 0
-                    make_frame(rv, p.pos, p.normal, a.cell, L.F);
+                    make_frame(rc, p.pos, p.normal, a.cell, L.F);
                     wave_sync();
                     TMARK(L, 7);
-                    Staged S;
-                    const bool degen = L.F.degenerate;
-                    const int m = degen ? 0 : stage(a, L, 0, S, wave_bytes, wave_clip);
+                    const bool degen = L.F.degenerate != 0;
+                    const int m = degen ? 0 : stage(a, L, 0, wave_bytes, wave_clip);
                     p.evals += 1;
                     if (degen)
                         p.flags |= DP_PATCH_DEGENERATE;
                     wave_vev += m >= 2 ? (unsigned long long)m : 0ull;
+                    // the staged views (rank order) from their records
+                    const int sv = lane < m ? (int)(L.arena[(kFastRec / 4) * lane + 15] & 127u) : 0;
                     if (m < 2) {
                         p.score = -1.0f;
-                        const int v = uni(S.view);
+                        const int v = uni(sv);
                         p.vis[0] = (m == 1 && v < 64) ? (1ull << v) : 0ull;
                         p.vis[1] = (m == 1 && v >= 64) ? (1ull << (v - 64)) : 0ull;
                         ok = m >= a.opt.min_visible;
                     } else {
-                        evaluate_score<G, NS, kTail, kMask>(a, L, S, sl, m);
+                        evaluate_score<G, NS, kTail, kMask>(a, L, sl, m);
                         double sum = 0.0;
                         for (int k = 1; k < m; ++k)
-                            sum = sum + L.u.ev.score[k];
+                            sum = sum + L.e.score[k];
                         p.score = (float)(sum / (double)(m - 1));
-                        const bool kept = lane < m && (lane == 0 || !(L.u.ev.score[lane] < a.opt.ncc_threshold));
-                        const uint64_t k0 = __ballot(kept && S.view < 64);
-                        const uint64_t k1 = __ballot(kept && S.view >= 64);
+                        const bool kept = lane < m && (lane == 0 || !(L.e.score[lane] < a.opt.ncc_threshold));
+                        const uint64_t k0 = __ballot(kept && sv < 64);
+                        const uint64_t k1 = __ballot(kept && sv >= 64);
                         uint64_t n0 = 0, n1 = 0;
                         for (uint64_t q = k0 | k1; q; q &= q - 1) {
                             const int l = __builtin_ctzll(q);
-                            const int v = __builtin_amdgcn_readlane(S.view, l);
+                            const int v = __builtin_amdgcn_readlane(sv, l);
                             if (v < 64)
                                 n0 |= 1ull << v;
                             else
@@ -1237,6 +1256,10 @@ static hipError_t launch_fast_m(const FastArgs &a, hipStream_t s)
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int per_cu = (160 * 1024) / (int)sizeof(FastLds<kBudget>);
+#ifndef DP_FAST_TIMING
+    static_assert(kBudget != 6656 || sizeof(FastLds<kBudget>) <= 160 * 1024 / 16,
+                  "the default arena must keep 16 waves per CU");
+#endif
     const int64_t want = ((int64_t)a.n + 3) / 4;
     const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
     const int grid = (int)(want < cap ? want : cap);
@@ -1281,6 +1304,9 @@ int fast_check_options(dp_ctx *c, const dp_fast_options &f)
     return DP_OK;
 }
 
+// byte offset of the FastCam table in the d_gray allocation
+inline size_t fast_cam_offset(int V) { return (sizeof(dpk::GrayPlane) * (size_t)V + 255) & ~(size_t)255; }
+
 int ensure_gray(dp_ctx *c)
 {
     if (!c->V)
@@ -1288,6 +1314,9 @@ int ensure_gray(dp_ctx *c)
     if (c->gray_ready && c->gray_level == c->level && c->gray_V == c->V)
         return DP_OK;
     hipSetDevice(c->device);
+    // a fast kernel launched on a caller's stream may still read the old
+    // planes and tables: let the device drain before they are rewritten
+    DP_HIP(c, hipDeviceSynchronize());
     std::vector<dpk::GrayPlane> gp(c->V);
     size_t total = 0;
     std::vector<size_t> off(c->V);
@@ -1317,13 +1346,30 @@ int ensure_gray(dp_ctx *c)
         mw = c->hv[v].W > mw ? c->hv[v].W : mw;
         mh = c->hv[v].H > mh ? c->hv[v].H : mh;
     }
+    // fp32 cameras of the level (or_fast.c fcam_of): rows 0-1 of P times 32,
+    // row 2, centre and unit x-axis, each rounded once
+    std::vector<dpk::FastCam> fc(c->V);
+    for (int v = 0; v < c->V; ++v) {
+        const dpg::ViewDev &h = c->hv[v];
+        for (int k = 0; k < 12; ++k)
+            fc[v].Q[k] = (float)(k < 8 ? 32.0 * h.P[k] : h.P[k]);
+        for (int k = 0; k < 3; ++k) {
+            fc[v].C[k] = (float)h.C[k];
+            fc[v].xr[k] = (float)h.xr[k];
+        }
+        fc[v].W = h.W;
+        fc[v].H = h.H;
+    }
     if (c->d_gray)
         hipFree(c->d_gray);
     c->d_gray = nullptr;
     dpk::PyrPlane *d_src = nullptr;
-    DP_HIP(c, hipMalloc(&c->d_gray, sizeof(dpk::GrayPlane) * c->V));
+    // one table: GrayPlane[V], then FastCam[V] at fast_cam_offset(V)
+    DP_HIP(c, hipMalloc(&c->d_gray, fast_cam_offset(c->V) + sizeof(dpk::FastCam) * c->V));
     DP_HIP(c, hipMalloc(&d_src, sizeof(dpk::PyrPlane) * c->V));
     DP_HIP(c, hipMemcpy(c->d_gray, gp.data(), sizeof(dpk::GrayPlane) * c->V, hipMemcpyHostToDevice));
+    DP_HIP(c, hipMemcpy((char *)c->d_gray + fast_cam_offset(c->V), fc.data(), sizeof(dpk::FastCam) * c->V,
+                        hipMemcpyHostToDevice));
     DP_HIP(c, hipMemcpy(d_src, src.data(), sizeof(dpk::PyrPlane) * c->V, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(dpk::gray_kernel, dim3((gray_pitch(mw) + 1023) / 1024, mh, c->V), dim3(256), 0, c->stream, d_src,
                        (const dpk::GrayPlane *)c->d_gray);
@@ -1342,6 +1388,12 @@ int ensure_gray(dp_ctx *c)
 
 template <int B> static hipError_t fast_dispatch(int N, const dpk::FastArgs &a, hipStream_t s)
 {
+#ifdef DP_FAST_DEV_N7
+    // development builds: only the n = 7 instance (fast compiles for ISA study)
+    if (N != 49 || B != 6656)
+        return hipErrorNotSupported;
+    return dpk::launch_fast_t<4, 3, true, B>(a, s);
+#else
     if (N == 49)
         return dpk::launch_fast_t<4, 3, true, B>(a, s);
     if (N <= 16)
@@ -1359,6 +1411,7 @@ template <int B> static hipError_t fast_dispatch(int N, const dpk::FastArgs &a, 
     if (N <= 192)
         return dpk::launch_fast_t<1, 3, false, B>(a, s);
     return dpk::launch_fast_t<1, 4, false, B>(a, s);
+#endif
 }
 
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
@@ -1370,6 +1423,7 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     dpk::FastArgs a{};
     a.views = c->d_views;
     a.gray = (const dpk::GrayPlane *)c->d_gray;
+    a.cams = (const dpk::FastCam *)((const char *)c->d_gray + fast_cam_offset(c->V));
     a.V = c->V;
     a.cell = cell;
     a.mode = mode;
@@ -1384,9 +1438,12 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.parent0 = parent0;
     a.items = items;
     a.max_pops = max_pops;
-    // the InitRelatedImages thresholds as cosines, by the host libm (the spec's)
-    a.cvis = std::cos(c->opt.visible_angle);
-    a.ccand = std::cos(c->opt.candidate_angle);
+    // the InitRelatedImages thresholds as cosines, by the host libm (the
+    // spec's), rounded to fp32, and their fp32 squares
+    a.cvis = (float)std::cos(c->opt.visible_angle);
+    a.ccand = (float)std::cos(c->opt.candidate_angle);
+    a.cvis2 = a.cvis * a.cvis;
+    a.ccand2 = a.ccand * a.ccand;
     if (!c->d_fstats)
         DP_HIP(c, hipMalloc(&c->d_fstats, 8 * sizeof(unsigned long long)));
     a.stats = c->d_fstats;
@@ -1399,12 +1456,17 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     // views per pass G (LP = 64/G lanes each) and slots S = ceil(N / LP); for
     // N = 49 three slots plus the one-sample tail round
 #define DP_FAST_ARENA(B) fast_dispatch<B>(N, a, s)
-    if (tb <= 6144)
-        e = DP_FAST_ARENA(6144);
+#ifdef DP_FAST_DEV_N7
+    e = DP_FAST_ARENA(6656);
+    (void)tb;
+#else
+    if (tb <= 6656)
+        e = DP_FAST_ARENA(6656);
     else if (tb <= 8192)
         e = DP_FAST_ARENA(8192);
     else
         e = DP_FAST_ARENA(kFastBudget);
+#endif
 #undef DP_FAST_ARENA
     DP_HIP(c, e);
     DP_HIP(c, hipEventRecord(c->e1, s));
@@ -1419,7 +1481,7 @@ extern "C" void dp_default_fast_options(dp_fast_options *f)
     *f = dp_fast_options{};
     f->iters = 4;
     f->margin = 2;
-    f->tile_budget = 6144; // 4 waves per SIMD (the 6 KiB arena); up to kFastBudget
+    f->tile_budget = 6656; // 4 waves per SIMD (the 6.5 KiB arena); up to kFastBudget
     f->max_views = dpk::kFastMaxV;
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;

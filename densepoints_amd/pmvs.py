@@ -48,7 +48,7 @@ class FastOptions:
 
     iters: int = 4            # CG iterations: E = 1 + 5 iters (+1 filter evaluation)
     margin: int = 2           # tile margin around the initial window, pixels (<= 7)
-    tile_budget: int = 6144   # bytes of LDS tiles per patch (<= 16384; <= 6144: 4 waves/SIMD)
+    tile_budget: int = 6656   # LDS bytes per patch: tiles + 64 per view (<= 16384; <= 6656: 4 waves/SIMD)
     max_views: int = 32       # staged views per patch (<= 32)
     fd_step: float = 0.5      # forward-difference step, scaled units
     ls_step: float = 1.0      # initial line-search step, scaled units

@@ -12,10 +12,10 @@
  * from a gray plane, keeping the reference's objective (functor calc,
  * optimization_opencv.cpp:14-39: 1 - NCC against texture 0, the lowest-index
  * scored view, over the other views; summed, NCCs in 2^-24 steps) and its NCC
- * formula (error_measurements.cpp:36-60
- * with the 0.1 denominator floor).  What differs, by design:
+ * formula (error_measurements.cpp:36-60 with the 0.1 denominator floor).
+ * What differs, by design:
  *   - samples come from per-view TILES of the gray plane staged once per patch
- *     (the initial window's bounding box plus `margin` pixels, BORDER_REPLICATE
+ *     (the initial window's pixel box plus `margin` pixels, BORDER_REPLICATE
  *     at the tile edge) instead of being re-gathered every evaluation;
  *   - the window is a square of n x n samples one reference-view pixel apart on
  *     the patch plane (axes: the reference camera's x-axis projected onto the
@@ -24,13 +24,18 @@
  *     `iters` nonlinear conjugate-gradient steps (Polak-Ribiere+, forward-
  *     difference gradient, a two-probe line search); E = 1 + 5 * iters;
  *   - samples are bilinear in 1/32 px with 1/16 gray-level output, moments are
- *     exact integers; the refine's NCC finish is fp32 (quantised to 2^-24),
- *     the reported scores' is fp64;
+ *     exact integers; the refine's NCC finish is fp32 (quantised to 2^-24) and
+ *     its objective an exact integer, the reported scores' finish is fp64;
  *   - InitRelatedImages after the refine tests cos(angle) against the
- *     thresholds' cosines (host libm) instead of acos(x) against the angles.
- * Arithmetic: fp32 with explicit fmaf where written, every other line one
- * IEEE rounding (-ffp-contract=off); fp64 for the per-patch setup, the NCC
- * finish and the CG state.
+ *     thresholds' cosines (squared, no square root) instead of acos(x) against
+ *     the angles.
+ * Arithmetic (spec v3): fp32 throughout -- frame, per-view geometry, CG state
+ * -- with fmaf where written and every other operation one IEEE rounding
+ * (-ffp-contract=off); "1/x (RN)" is the correctly rounded fp32 reciprocal
+ * (the device computes it as v_rcp_f32 plus one Newton step, bitwise equal for
+ * the operand ranges the spec admits); fp64 only for the exact NCC moment
+ * products, the reported scores and the reference's child positions
+ * (expand.cpp, shared with the parity restatement).
  */
 #include "oracle.h"
 #include "or_internal.h"
@@ -44,15 +49,17 @@
 #endif
 
 #define FAST_MAX_VIEWS 32
-#define FAST_MAX_TILE 64     /* tile side cap incl. margins                  */
 #define FAST_MAX_BBOX 48     /* window bounding box side cap (grazing views) */
+#define FAST_REC_BYTES 64    /* LDS record per staged view, counted in the budget */
+#define FAST_RCP_MIN 0x1p-20f /* operands of 1/x (RN) are clamped to / tested   */
+#define FAST_RCP_MAX 0x1p+64f /* against [2^-20, 2^64]                         */
 
 void or_fast_default_options(or_fast_options *f)
 {
     memset(f, 0, sizeof(*f));
     f->iters = 4;
     f->margin = 2;
-    f->tile_budget = 6144;
+    f->tile_budget = 6656;
     f->max_views = FAST_MAX_VIEWS;
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;
@@ -78,11 +85,62 @@ int or_gray_plane(const or_scene *s, int view, uint8_t *out)
     return 0;
 }
 
+/* ------------------------------------------------------------------------ */
+/* fp32 camera of a view: rows 0-1 of P times 32 (1/32-px units), row 2, the  */
+/* centre and the unit x-axis, each rounded once from the fp64 values         */
+/* ------------------------------------------------------------------------ */
+typedef struct fcam {
+    float Q[12];
+    float C[3], xr[3];
+    int W, H;
+} fcam;
+
+static void fcam_of(const or_view *v, fcam *c)
+{
+    for (int k = 0; k < 12; ++k) c->Q[k] = (float)(k < 8 ? 32.0 * v->P[k] : v->P[k]);
+    for (int k = 0; k < 3; ++k) {
+        c->C[k] = (float)v->C[k];
+        c->xr[k] = (float)v->xr[k];
+    }
+    c->W = v->W;
+    c->H = v->H;
+}
+
+static inline float fdot(const float a[3], const float b[3])
+{
+    return fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0]));
+}
+
+/* row k of Q applied to a point (with the 4th column) / a direction */
+static inline float qpt(const float *Q, int k, const float X[3])
+{
+    return fmaf(Q[4 * k + 2], X[2], fmaf(Q[4 * k + 1], X[1], fmaf(Q[4 * k], X[0], Q[4 * k + 3])));
+}
+static inline float qdir(const float *Q, int k, const float w[3])
+{
+    return fmaf(Q[4 * k + 2], w[2], fmaf(Q[4 * k + 1], w[1], Q[4 * k] * w[0]));
+}
+
+/* 1/x (RN) for x in [2^-20, 2^64] */
+static inline float rcp_rn(float x) { return 1.0f / x; }
+
+/* projection in 1/32 px; 0 if the depth is outside the reciprocal's range */
+static inline int fproj(const fcam *c, const float X[3], float *u, float *w)
+{
+    const float h2 = qpt(c->Q, 2, X);
+    if (!(h2 >= FAST_RCP_MIN && h2 <= FAST_RCP_MAX)) return 0;
+    const float r = rcp_rn(h2);
+    *u = qpt(c->Q, 0, X) * r;
+    *w = qpt(c->Q, 1, X) * r;
+    return 1;
+}
+
 typedef struct fast_view {
     int view;
     int x0t, y0t, tw, th;  /* tile origin and size (pixels)           */
-    int bytes;             /* LDS footprint: 4 ceil((tw+1)/2) (th+1)   */
-    float vec[5][3];       /* H0, Hd, He1, He2, Hn (folded, scaled)    */
+    int bytes;             /* LDS footprint: tile + record             */
+    float g[5][3];         /* H0, Hd, He1, He2, Hn over the centre depth */
+    float vec[5][3];       /* the same, relative to the tile origin    */
     float umax, vmax;      /* 32 * (tw - 1), 32 * (th - 1)             */
     uint16_t *tile;        /* (tw + 1) x th entries: p[y][x] | p[y+1][x] << 8 */
 } fast_view;
@@ -90,74 +148,104 @@ typedef struct fast_view {
 typedef struct fast_patch {
     int m;                          /* staged views (first = anchor)            */
     fast_view fv[FAST_MAX_VIEWS];
-    double X0[3], r[3];             /* centre, reference ray X0 - C_ref         */
-    double e1[3], e2[3], nn[3];     /* plane axes and normal times pixel size   */
-    double u1[3], u2[3], un[3];     /* the same, unit length                    */
-    double sd, st;                  /* scaled-variable units                    */
+    float X0[3], r[3];              /* centre, reference ray X0 - C_ref          */
+    float e1[3], e2[3], nn[3];      /* plane axes and normal times pixel size    */
+    float u1[3], u2[3], un[3];      /* the same, unit length                     */
+    float sd, st;                   /* scaled-variable units                     */
     int degenerate;
 } fast_patch;
 
-/* per-view geometry before the budget is applied: fp64 vectors and the
- * initial window's pixel bounding box; returns 0 if the view is unusable */
+/* the patch frame (fp32) from the stored pose; 0 if degenerate */
+static int fast_frame(const or_scene *s, const or_patch *p, int cell, fast_patch *fp)
+{
+    fcam rc;
+    fcam_of(&s->v[p->ref], &rc);
+    const float X[3] = {p->pos[0], p->pos[1], p->pos[2]};
+    const float n0[3] = {p->normal[0], p->normal[1], p->normal[2]};
+    /* pixels per world unit along the reference x-axis (patch.cpp:97-103) */
+    const float Xq[3] = {X[0] + rc.xr[0], X[1] + rc.xr[1], X[2] + rc.xr[2]};
+    float cu, cw, qu, qw;
+    if (!fproj(&rc, X, &cu, &cw) || !fproj(&rc, Xq, &qu, &qw)) return 0;
+    const float du = qu - cu, dv = qw - cw;
+    const float dx = sqrtf(fmaf(dv, dv, du * du)); /* 1/32 px per world unit */
+    const float nl = sqrtf(fdot(n0, n0));
+    if (!(dx > 0.0f) || !(dx <= 0x1p+100f) || !(nl > 0.0f)) return 0;
+    const float ps = 32.0f / dx; /* world size of one reference pixel */
+    const float inl = 1.0f / nl;
+    float nn[3] = {n0[0] * inl, n0[1] * inl, n0[2] * inl};
+    const float xn = fdot(rc.xr, nn);
+    float e1[3] = {fmaf(-xn, nn[0], rc.xr[0]), fmaf(-xn, nn[1], rc.xr[1]), fmaf(-xn, nn[2], rc.xr[2])};
+    const float el = sqrtf(fdot(e1, e1));
+    if (!(el > 0.0f)) return 0;
+    const float iel = 1.0f / el;
+    for (int k = 0; k < 3; ++k) e1[k] = e1[k] * iel;
+    const float e2[3] = {fmaf(nn[1], e1[2], -(nn[2] * e1[1])), fmaf(nn[2], e1[0], -(nn[0] * e1[2])),
+                         fmaf(nn[0], e1[1], -(nn[1] * e1[0]))};
+    const float r[3] = {X[0] - rc.C[0], X[1] - rc.C[1], X[2] - rc.C[2]};
+    const float rl = sqrtf(fdot(r, r));
+    if (!(rl > 0.0f)) return 0;
+    fp->sd = ps / rl;                        /* x0 = 1: one pixel size along the ray     */
+    fp->st = 2.0f / (float)(cell - 1);       /* x1 = 1: window edge moves one pixel size */
+    for (int k = 0; k < 3; ++k) {
+        fp->X0[k] = X[k];
+        fp->r[k] = r[k];
+        fp->u1[k] = e1[k];
+        fp->u2[k] = e2[k];
+        fp->un[k] = nn[k];
+        fp->e1[k] = e1[k] * ps;
+        fp->e2[k] = e2[k] * ps;
+        fp->nn[k] = nn[k] * ps;
+    }
+    return 1;
+}
+
+/* per-view geometry before the budget: the five homography columns over the
+ * centre depth and the initial window's pixel box from its first-order map;
+ * returns 0 if the view is unusable */
 typedef struct fast_geo {
-    double vec[5][3];
+    float g[5][3];
     int xa, xb, ya, yb;
 } fast_geo;
 
-static inline double rowdot(const double *P, const double w[3])
+static int view_geo(const or_view *v, const fast_patch *fp, int cell, fast_geo *G)
 {
-    return (P[0] * w[0] + P[1] * w[1]) + P[2] * w[2];
-}
-
-static int view_geo(const or_view *v, const fast_patch *fp, int cell, fast_geo *g)
-{
-    const double *P = v->P;
-    double H[5][3];
+    fcam c;
+    fcam_of(v, &c);
+    const float *w[4] = {fp->r, fp->e1, fp->e2, fp->nn};
+    float H[5][3];
     for (int k = 0; k < 3; ++k) {
-        const double *Pr = P + 4 * k;
-        H[0][k] = rowdot(Pr, fp->X0) + Pr[3];
-        H[1][k] = rowdot(Pr, fp->r);
-        H[2][k] = rowdot(Pr, fp->e1);
-        H[3][k] = rowdot(Pr, fp->e2);
-        H[4][k] = rowdot(Pr, fp->nn);
+        H[0][k] = qpt(c.Q, k, fp->X0);
+        for (int i = 0; i < 4; ++i) H[1 + i][k] = qdir(c.Q, k, w[i]);
     }
-    const double s = H[0][2];
-    if (!(s > 0.0)) return 0;
-    const double inv = 1.0 / s; /* one reciprocal of the centre's depth */
-    for (int i = 0; i < 5; ++i) {
-        g->vec[i][0] = (32.0 * H[i][0]) * inv;
-        g->vec[i][1] = (32.0 * H[i][1]) * inv;
-        g->vec[i][2] = H[i][2] * inv;
-    }
-    /* initial window corners (x = 0): tau in {-c, +c} */
-    const double c = 0.5 * (double)(cell - 1);
-    double umin = 0, umax = 0, vmin = 0, vmax = 0;
-    for (int q = 0; q < 4; ++q) {
-        const double ti = (q & 1) ? c : -c, tj = (q & 2) ? c : -c;
-        double h[3];
-        for (int k = 0; k < 3; ++k)
-            h[k] = (g->vec[0][k] + ti * g->vec[2][k]) + tj * g->vec[3][k];
-        if (!(h[2] > 0.0)) return 0;
-        const double u = h[0] / h[2], w = h[1] / h[2]; /* 1/32 px */
-        /* View::IsPointInside semantics on the corner (types.cpp:77-84) */
-        if (!(u > 0.0 && u < 32.0 * v->W && w > 0.0 && w < 32.0 * v->H)) return 0;
-        if (q == 0 || u < umin) umin = u;
-        if (q == 0 || u > umax) umax = u;
-        if (q == 0 || w < vmin) vmin = w;
-        if (q == 0 || w > vmax) vmax = w;
-    }
-    g->xa = (int)floor(umin / 32.0);
-    g->xb = (int)floor(umax / 32.0) + 1;
-    g->ya = (int)floor(vmin / 32.0);
-    g->yb = (int)floor(vmax / 32.0) + 1;
-    if (g->xb - g->xa + 1 > FAST_MAX_BBOX || g->yb - g->ya + 1 > FAST_MAX_BBOX) return 0;
+    const float s = H[0][2];
+    if (!(s >= FAST_RCP_MIN && s <= FAST_RCP_MAX)) return 0;
+    const float inv = rcp_rn(s);
+    for (int i = 0; i < 5; ++i)
+        for (int k = 0; k < 3; ++k) G->g[i][k] = H[i][k] * inv;
+    /* the window's pose-0 footprint: the first-order map about its centre with
+     * the centre depth taken as 1, (U, V) = g0 + ti (g2 - g0 g2z) + tj (g3 - g0 g3z) */
+    const float U0 = G->g[0][0], V0 = G->g[0][1];
+    const float Ui = fmaf(-U0, G->g[2][2], G->g[2][0]), Vi = fmaf(-V0, G->g[2][2], G->g[2][1]);
+    const float Uj = fmaf(-U0, G->g[3][2], G->g[3][0]), Vj = fmaf(-V0, G->g[3][2], G->g[3][1]);
+    const float cc = 0.5f * (float)(cell - 1);
+    const float eu = cc * (fabsf(Ui) + fabsf(Uj)), ev = cc * (fabsf(Vi) + fabsf(Vj));
+    const float ez = cc * (fabsf(G->g[2][2]) + fabsf(G->g[3][2]));
+    const float umin = U0 - eu, umax = U0 + eu, vmin = V0 - ev, vmax = V0 + ev;
+    /* corner depths positive and View::IsPointInside on the box (types.cpp:77-84) */
+    if (!(G->g[0][2] - ez > 0.0f)) return 0;
+    if (!(umin > 0.0f && umax < (float)(32 * v->W) && vmin > 0.0f && vmax < (float)(32 * v->H))) return 0;
+    G->xa = (int)floorf(umin * 0.03125f);
+    G->xb = (int)floorf(umax * 0.03125f) + 1;
+    G->ya = (int)floorf(vmin * 0.03125f);
+    G->yb = (int)floorf(vmax * 0.03125f) + 1;
+    if (G->xb - G->xa + 1 > FAST_MAX_BBOX || G->yb - G->ya + 1 > FAST_MAX_BBOX) return 0;
     return 1;
 }
 
 /* tile rectangle: the window's pixel box grown by M, clipped to the image,
  * left edge rounded down to an even column (the device copies the rows as
  * 32-bit words of two fp16 pixels); the footprint counts tw + 1 columns
- * (right tap) and th + 1 rows (lower tap) */
+ * (right tap), th + 1 rows (lower tap) and the view's 64-byte LDS record */
 static void tile_rect(const or_view *v, const fast_geo *g, int M, fast_view *t)
 {
     int x0 = g->xa - M, x1 = g->xb + M, y0 = g->ya - M, y1 = g->yb + M;
@@ -169,62 +257,22 @@ static void tile_rect(const or_view *v, const fast_geo *g, int M, fast_view *t)
     t->y0t = y0;
     t->tw = x1 - x0 + 1;
     t->th = y1 - y0 + 1;
-    t->bytes = 4 * ((t->tw + 2) / 2) * (t->th + 1);
+    t->bytes = 4 * ((t->tw + 2) / 2) * (t->th + 1) + FAST_REC_BYTES;
 }
 
 /*
  * Stage a patch: frame, scaled-variable units, the usable views (ascending
- * visible order, at most max_views), the margin that fits the tile budget,
- * folded fp32 vectors and the tiles.  Returns the staged view count.
+ * visible order, at most max_views), the margin that fits the budget, fp32
+ * vectors relative to the tile origins and the tiles.  Returns the staged
+ * view count.
  */
 static int fast_stage(const or_scene *s, const or_patch *p, int cell, const or_fast_options *fo, int margin,
                       fast_patch *fp)
 {
     memset(fp, 0, sizeof(*fp));
-    const or_view *rv = &s->v[p->ref];
-    double X0[3], n0[3];
-    get_pos(p, X0);
-    get_nrm(p, n0);
-    memcpy(fp->X0, X0, sizeof(X0));
-    /* pixels per world unit along the reference x-axis (patch.cpp:97-103) */
-    double cu, cw, qu, qw;
-    double Xq[3] = {X0[0] + rv->xr[0], X0[1] + rv->xr[1], X0[2] + rv->xr[2]};
-    proj(rv, X0, &cu, &cw);
-    proj(rv, Xq, &qu, &qw);
-    const double du = qu - cu, dv = qw - cw;
-    const double dx = sqrt(du * du + dv * dv);
-    const double nl = sqrt(dot3(n0, n0));
-    if (!(dx > 0.0) || !(nl > 0.0) || dx != dx) {
+    if (!fast_frame(s, p, cell, fp)) {
         fp->degenerate = 1;
         return 0;
-    }
-    const double ps = 1.0 / dx; /* world size of one reference pixel */
-    /* unit vectors by one reciprocal and three products each */
-    const double inl = 1.0 / nl;
-    double nn[3] = {n0[0] * inl, n0[1] * inl, n0[2] * inl};
-    const double xn = dot3(rv->xr, nn);
-    double e1[3] = {rv->xr[0] - xn * nn[0], rv->xr[1] - xn * nn[1], rv->xr[2] - xn * nn[2]};
-    const double el = sqrt(dot3(e1, e1));
-    if (!(el > 0.0)) {
-        fp->degenerate = 1;
-        return 0;
-    }
-    const double iel = 1.0 / el;
-    for (int k = 0; k < 3; ++k) e1[k] = e1[k] * iel;
-    double e2[3];
-    cross3(nn, e1, e2);
-    const double r[3] = {X0[0] - rv->C[0], X0[1] - rv->C[1], X0[2] - rv->C[2]};
-    const double rl = sqrt(dot3(r, r));
-    fp->sd = ps / rl;                  /* x0 = 1: one pixel size along the ray      */
-    fp->st = 2.0 / (double)(cell - 1); /* x1 = 1: window edge moves one pixel size  */
-    for (int k = 0; k < 3; ++k) {
-        fp->r[k] = r[k];
-        fp->u1[k] = e1[k];
-        fp->u2[k] = e2[k];
-        fp->un[k] = nn[k];
-        fp->e1[k] = e1[k] * ps;
-        fp->e2[k] = e2[k] * ps;
-        fp->nn[k] = nn[k] * ps;
     }
     /* usable views */
     int vis[OR_MAX_VIEWS];
@@ -241,8 +289,8 @@ static int fast_stage(const or_scene *s, const or_patch *p, int cell, const or_f
             ++m;
         }
     }
-    /* the largest margin <= `margin` whose tiles fit the budget; at margin 0
-     * the longest fitting prefix of views */
+    /* the largest margin <= `margin` whose footprints fit the budget; at
+     * margin 0 the longest fitting prefix of views */
     int M = margin;
     for (;;) {
         int tot = 0;
@@ -259,12 +307,11 @@ static int fast_stage(const or_scene *s, const or_patch *p, int cell, const or_f
     for (int k = 0; k < m; ++k) {
         fast_view *t = &fp->fv[k];
         const or_view *v = &s->v[t->view];
+        const float ox = -32.0f * (float)t->x0t, oy = -32.0f * (float)t->y0t;
         for (int i = 0; i < 5; ++i) {
-            const double a = geo[k].vec[i][0] - (32.0 * (double)t->x0t) * geo[k].vec[i][2];
-            const double b = geo[k].vec[i][1] - (32.0 * (double)t->y0t) * geo[k].vec[i][2];
-            t->vec[i][0] = (float)a;
-            t->vec[i][1] = (float)b;
-            t->vec[i][2] = (float)geo[k].vec[i][2];
+            t->vec[i][0] = fmaf(ox, geo[k].g[i][2], geo[k].g[i][0]);
+            t->vec[i][1] = fmaf(oy, geo[k].g[i][2], geo[k].g[i][1]);
+            t->vec[i][2] = geo[k].g[i][2];
         }
         t->umax = (float)(32 * (t->tw - 1));
         t->vmax = (float)(32 * (t->th - 1));
@@ -284,21 +331,32 @@ static void fast_free(fast_patch *fp)
     fp->m = 0;
 }
 
-/* one view's n x n samples at scaled pose x: 1/16 gray levels, row-major */
-static void fast_sample(const fast_view *t, int cell, float df, float af, float bf, int32_t *out)
+/* the scaled pose's sampler inputs: df = x0 sd, af = x1 st, bf = x2 st */
+typedef struct fast_pose {
+    float df, af, bf;
+} fast_pose;
+
+static inline fast_pose pose_of(const fast_patch *fp, const float x[3])
+{
+    fast_pose q = {x[0] * fp->sd, x[1] * fp->st, x[2] * fp->st};
+    return q;
+}
+
+/* one view's n x n samples at a pose: 1/16 gray levels, row-major */
+static void fast_sample(const fast_view *t, int cell, fast_pose q, int32_t *out)
 {
     /* homography columns at the pose: centre A, window axes B1, B2 */
     float A[3], B1[3], B2[3];
     for (int k = 0; k < 3; ++k) {
-        A[k] = fmaf(df, t->vec[1][k], t->vec[0][k]);
-        B1[k] = fmaf(-af, t->vec[4][k], t->vec[2][k]);
-        B2[k] = fmaf(-bf, t->vec[4][k], t->vec[3][k]);
+        A[k] = fmaf(q.df, t->vec[1][k], t->vec[0][k]);
+        B1[k] = fmaf(-q.af, t->vec[4][k], t->vec[2][k]);
+        B2[k] = fmaf(-q.bf, t->vec[4][k], t->vec[3][k]);
     }
     /* its first-order (affine) map about the window centre: (U0, V0) = A / Az
-     * and the quotient rule's axes (B - U0 Bz) / Az, one division per view and
-     * pose; over an n <= 16 window the dropped second-order term is below
+     * and the quotient rule's axes (B - U0 Bz) / Az, one reciprocal per view
+     * and pose; over an n <= 16 window the dropped second-order term is below
      * |tau| |dhz| ~ 1e-3 of the offset, far under the 1/32-px quantisation */
-    const float rz = 1.0f / fmaxf(A[2], 0x1p-20f);
+    const float rz = rcp_rn(fmaxf(A[2], FAST_RCP_MIN));
     const float U0 = A[0] * rz, V0 = A[1] * rz;
     const float Ui = fmaf(-U0, B1[2], B1[0]) * rz, Vi = fmaf(-V0, B1[2], B1[1]) * rz;
     const float Uj = fmaf(-U0, B2[2], B2[0]) * rz, Vj = fmaf(-V0, B2[2], B2[1]) * rz;
@@ -327,7 +385,7 @@ static void fast_sample(const fast_view *t, int cell, float df, float af, float 
 }
 
 /* NCC of integer-moment windows (values in 1/16 gray levels): the reference
- * NCCScore with max(0.1, sigma_a sigma_b) scaled to these units */
+ * NCCScore with max(0.1, sigma_a sigma_b) scaled to these units; fp64 finish */
 static double fast_ncc(int64_t N, int64_t Sa, int64_t Saa, int64_t Sb, int64_t Sbb, int64_t Sab, double dmin)
 {
     const int64_t num = N * Sab - Sa * Sb;
@@ -339,30 +397,28 @@ static double fast_ncc(int64_t N, int64_t Sa, int64_t Saa, int64_t Sb, int64_t S
 }
 
 /* the refine's NCC in 2^-24 steps: the exact moments rounded to fp32, IEEE
- * fp32 square root and quotient, the 0.1 floor as fp32 */
+ * fp32 square root, the 0.1 floor as fp32, times its reciprocal (RN) */
 static int32_t fast_ncc_q(int64_t N, int64_t Sa, int64_t Saa, int64_t Sb, int64_t Sbb, int64_t Sab, float dminf)
 {
     const int64_t num = N * Sab - Sa * Sb;
     const int64_t va = N * Saa - Sa * Sa;
     const int64_t vb = N * Sbb - Sb * Sb;
     const float den = sqrtf((float)va * (float)vb);
-    const float d = den > dminf ? den : dminf;
-    return (int32_t)rintf(((float)num / d) * 16777216.0f);
+    const float r = rcp_rn(den > dminf ? den : dminf);
+    return (int32_t)rintf(((float)num * r) * 16777216.0f);
 }
 
-/* objective at scaled pose x: the functor calc's sum of (1 - NCC) over the
- * views scored against texture 0 (without its division by m - 1, a constant
- * of the refine), NCCs in 2^-24 steps; scores[k-1] = the fp64 NCC of staged
- * view k (the scores the filter and FAST_EVAL report) */
-static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_min, const double x[3],
-                             double *scores)
+/* objective at a pose, an exact integer: (m - 1) 2^24 minus the sum over the
+ * views scored against texture 0 of their NCCs in 2^-24 steps (the functor
+ * calc's sum of 1 - NCC, without its constant 1/(m - 1)); scores[k-1] = the
+ * fp64 NCC of staged view k (the scores the filter and FAST_EVAL report) */
+static int32_t fast_objective(const fast_patch *fp, int cell, double ncc_denom_min, fast_pose q, double *scores)
 {
     const int m = fp->m;
-    if (m < 2) return 2.0;
-    const float df = (float)(x[0] * fp->sd), af = (float)(x[1] * fp->st), bf = (float)(x[2] * fp->st);
+    if (m < 2) return 2 << 24;
     const int N = cell * cell;
     int32_t a[16 * 16], b[16 * 16];
-    fast_sample(&fp->fv[0], cell, df, af, bf, a);
+    fast_sample(&fp->fv[0], cell, q, a);
     int64_t Sa = 0, Saa = 0;
     for (int i = 0; i < N; ++i) {
         Sa += a[i];
@@ -372,7 +428,7 @@ static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_mi
     const float dminf = (float)dmin;
     int64_t qsum = 0;
     for (int k = 1; k < m; ++k) {
-        fast_sample(&fp->fv[k], cell, df, af, bf, b);
+        fast_sample(&fp->fv[k], cell, q, b);
         int64_t Sb = 0, Sbb = 0, Sab = 0;
         for (int i = 0; i < N; ++i) {
             Sb += b[i];
@@ -382,50 +438,50 @@ static double fast_objective(const fast_patch *fp, int cell, double ncc_denom_mi
         if (scores) scores[k - 1] = fast_ncc(N, Sa, Saa, Sb, Sbb, Sab, dmin);
         qsum += fast_ncc_q(N, Sa, Saa, Sb, Sbb, Sab, dminf);
     }
-    /* sum over the views of (1 - NCC), each NCC (fp32) rounded to a multiple
-     * of 2^-24 and summed exactly (so the value does not depend on the order) */
-    return (double)((int64_t)(m - 1) * 16777216 - qsum) * 0x1p-24;
+    return (int32_t)((int64_t)(m - 1) * 16777216 - qsum); /* < 2^29 */
 }
 
 /* nonlinear CG (Polak-Ribiere+) with forward differences and a two-probe
- * line search; returns evaluations, x holds the scaled pose */
-static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_options *fo, double x[3])
+ * line search, fp32; returns evaluations, x holds the scaled pose */
+static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_options *fo, float x[3])
 {
-    x[0] = x[1] = x[2] = 0.0;
-    double f = fast_objective(fp, cell, dmin0, x, NULL);
+    x[0] = x[1] = x[2] = 0.0f;
+    int32_t f = fast_objective(fp, cell, dmin0, pose_of(fp, x), NULL);
     int E = 1;
-    const double h = (double)fo->fd_step, inv_h = 1.0 / h;
-    double alpha = (double)fo->ls_step;
-    double gp[3] = {0, 0, 0}, dp[3] = {0, 0, 0}, ggp = 0.0;
+    const float h = fo->fd_step;
+    const float gs = (1.0f / h) * 0x1p-24f; /* gradient per objective unit */
+    float alpha = fo->ls_step;
+    float gp[3] = {0, 0, 0}, dp[3] = {0, 0, 0}, ggp = 0.0f;
     for (int it = 0; it < fo->iters; ++it) {
-        double g[3];
+        float g[3];
         for (int i = 0; i < 3; ++i) {
-            double xt[3] = {x[0], x[1], x[2]};
+            float xt[3] = {x[0], x[1], x[2]};
             xt[i] = x[i] + h;
-            g[i] = (fast_objective(fp, cell, dmin0, xt, NULL) - f) * inv_h;
+            g[i] = (float)(fast_objective(fp, cell, dmin0, pose_of(fp, xt), NULL) - f) * gs;
         }
         E += 3;
-        const double gg = (g[0] * g[0] + g[1] * g[1]) + g[2] * g[2];
-        if (gg == 0.0) break;
-        double beta = 0.0;
-        if (it > 0 && ggp > 0.0) {
-            beta = ((g[0] * (g[0] - gp[0]) + g[1] * (g[1] - gp[1])) + g[2] * (g[2] - gp[2])) / ggp;
-            beta = beta > 0.0 ? beta : 0.0;
+        const float gg = fdot(g, g);
+        if (gg == 0.0f) break;
+        float beta = 0.0f;
+        if (it > 0 && ggp > 0.0f) {
+            const float dg[3] = {g[0] - gp[0], g[1] - gp[1], g[2] - gp[2]};
+            beta = fdot(g, dg) / ggp;
+            beta = beta > 0.0f ? beta : 0.0f;
         }
-        double d[3];
-        for (int i = 0; i < 3; ++i) d[i] = beta * dp[i] - g[i];
-        if ((d[0] * g[0] + d[1] * g[1]) + d[2] * g[2] >= 0.0)
-            for (int i = 0; i < 3; ++i) d[i] = 0.0 - g[i];
-        const double inv_nd = 1.0 / sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
-        double u[3];
+        float d[3];
+        for (int i = 0; i < 3; ++i) d[i] = fmaf(beta, dp[i], -g[i]);
+        if (fdot(d, g) >= 0.0f)
+            for (int i = 0; i < 3; ++i) d[i] = -g[i];
+        const float inv_nd = 1.0f / sqrtf(fdot(d, d));
+        float u[3];
         for (int i = 0; i < 3; ++i) u[i] = d[i] * inv_nd;
-        double x1[3], x2[3];
-        for (int i = 0; i < 3; ++i) x1[i] = x[i] + alpha * u[i];
-        const double f1 = fast_objective(fp, cell, dmin0, x1, NULL);
+        float x1[3], x2[3];
+        for (int i = 0; i < 3; ++i) x1[i] = fmaf(alpha, u[i], x[i]);
+        const int32_t f1 = fast_objective(fp, cell, dmin0, pose_of(fp, x1), NULL);
         if (f1 < f) {
-            const double a2 = 2.0 * alpha;
-            for (int i = 0; i < 3; ++i) x2[i] = x[i] + a2 * u[i];
-            const double f2 = fast_objective(fp, cell, dmin0, x2, NULL);
+            const float a2 = 2.0f * alpha;
+            for (int i = 0; i < 3; ++i) x2[i] = fmaf(a2, u[i], x[i]);
+            const int32_t f2 = fast_objective(fp, cell, dmin0, pose_of(fp, x2), NULL);
             if (f2 < f1) {
                 memcpy(x, x2, sizeof(x2));
                 f = f2;
@@ -435,9 +491,9 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
                 f = f1;
             }
         } else {
-            const double a2 = 0.5 * alpha;
-            for (int i = 0; i < 3; ++i) x2[i] = x[i] + a2 * u[i];
-            const double f2 = fast_objective(fp, cell, dmin0, x2, NULL);
+            const float a2 = 0.5f * alpha;
+            for (int i = 0; i < 3; ++i) x2[i] = fmaf(a2, u[i], x[i]);
+            const int32_t f2 = fast_objective(fp, cell, dmin0, pose_of(fp, x2), NULL);
             if (f2 < f) {
                 memcpy(x, x2, sizeof(x2));
                 f = f2;
@@ -472,8 +528,8 @@ static int fast_filter(const or_scene *s, or_patch *p, int cell, const or_fast_o
         return m >= s->opt.min_visible;
     }
     double sc[FAST_MAX_VIEWS];
-    const double x[3] = {0.0, 0.0, 0.0};
-    fast_objective(&fp, cell, s->opt.ncc_denom_min, x, sc);
+    const fast_pose q0 = {0.0f, 0.0f, 0.0f};
+    fast_objective(&fp, cell, s->opt.ncc_denom_min, q0, sc);
     double sum = 0.0;
     for (int k = 1; k < fp.m; ++k) sum = sum + sc[k - 1];
     p->score = (float)(sum / (double)(fp.m - 1));
@@ -486,26 +542,38 @@ static int fast_filter(const or_scene *s, or_patch *p, int cell, const or_fast_o
     return nk >= s->opt.min_visible;
 }
 
-/* Patch::InitRelatedImages (patch.cpp:19-49) with its angle tests as cosine
- * tests, acos(x) < a <=> x > cos(a): the thresholds' cosines come from the
- * host libm once (the product passes the same doubles to the device), so
- * no acos is evaluated per view */
+/* x > c for x = dn / sqrt(dd) (dd > 0), without the root: compared squared
+ * (c2 = c c in fp32) with the signs handled */
+static inline int cos_above(float dn, float dd, float c, float c2)
+{
+    if (c >= 0.0f) return dn > 0.0f && dn * dn > c2 * dd;
+    return dn >= 0.0f || dn * dn < c2 * dd;
+}
+
+/* Patch::InitRelatedImages (patch.cpp:19-49) in fp32 with its angle tests as
+ * cosine tests, acos(x) < a <=> x > cos(a): the thresholds' cosines come from
+ * the host libm once (the product passes the same values to the device), so
+ * no acos or square root is evaluated per view */
 static void fast_init_related(const or_scene *s, or_patch *p)
 {
-    const double cvis = cos(s->opt.visible_angle), ccand = cos(s->opt.candidate_angle);
-    double X[3], n[3];
-    get_pos(p, X);
-    get_nrm(p, n);
+    const float cvis = (float)cos(s->opt.visible_angle), ccand = (float)cos(s->opt.candidate_angle);
+    const float cvis2 = cvis * cvis, ccand2 = ccand * ccand;
+    const float X[3] = {p->pos[0], p->pos[1], p->pos[2]};
+    const float n[3] = {p->normal[0], p->normal[1], p->normal[2]};
     int vis[OR_MAX_VIEWS], cand[OR_MAX_VIEWS], nv = 0, nc = 0;
     for (int vi = 0; vi < s->V; ++vi) {
         if ((uint32_t)vi == p->ref) continue;
-        const or_view *v = &s->v[vi];
-        if (!inside(v, X)) continue;
-        const double d[3] = {X[0] - v->C[0], X[1] - v->C[1], X[2] - v->C[2]};
-        const double x = dot3(n, d) / norm3(d);
-        if (x > cvis)
+        fcam c;
+        fcam_of(&s->v[vi], &c);
+        float u, w;
+        /* View::IsPointInside (types.cpp:77-84) in 1/32 px */
+        if (!fproj(&c, X, &u, &w)) continue;
+        if (!(u > 0.0f && u < (float)(32 * c.W) && w > 0.0f && w < (float)(32 * c.H))) continue;
+        const float d[3] = {X[0] - c.C[0], X[1] - c.C[1], X[2] - c.C[2]};
+        const float dn = fdot(n, d), dd = fdot(d, d);
+        if (cos_above(dn, dd, cvis, cvis2))
             vis[nv++] = vi;
-        else if (x > ccand)
+        else if (cos_above(dn, dd, ccand, ccand2))
             cand[nc++] = vi;
     }
     encode_mask(vis, nv, p->vis);
@@ -525,16 +593,16 @@ static int fast_refine_one(const or_scene *s, or_patch *p, int cell, const or_fa
         return 0;
     }
     if (fp.m >= 2) {
-        double x[3];
+        float x[3];
         p->evals += (uint32_t)fast_cg(&fp, cell, s->opt.ncc_denom_min, fo, x);
-        const double d = x[0] * fp.sd, a = x[1] * fp.st, b = x[2] * fp.st;
+        const float d = x[0] * fp.sd, a = x[1] * fp.st, b = x[2] * fp.st;
         /* X' = X0 + d (X0 - C_ref); n' = normalize(n + a e1 + b e2) */
-        double nrm[3];
-        for (int k = 0; k < 3; ++k) nrm[k] = (fp.un[k] + a * fp.u1[k]) + b * fp.u2[k];
-        const double ml = sqrt(dot3(nrm, nrm));
+        float nrm[3];
+        for (int k = 0; k < 3; ++k) nrm[k] = fmaf(b, fp.u2[k], fmaf(a, fp.u1[k], fp.un[k]));
+        const float il = 1.0f / sqrtf(fdot(nrm, nrm));
         for (int k = 0; k < 3; ++k) {
-            p->pos[k] = (float)(fp.X0[k] + d * fp.r[k]);
-            p->normal[k] = (float)(nrm[k] / ml);
+            p->pos[k] = fmaf(d, fp.r[k], fp.X0[k]);
+            p->normal[k] = nrm[k] * il;
         }
     }
     fast_free(&fp);
@@ -554,8 +622,8 @@ static int fast_eval_one(const or_scene *s, or_patch *p, int cell, const or_fast
     int ok = fp.m >= 2;
     if (ok) {
         double sc[FAST_MAX_VIEWS];
-        const double x[3] = {0.0, 0.0, 0.0};
-        fast_objective(&fp, cell, s->opt.ncc_denom_min, x, sc);
+        const fast_pose q0 = {0.0f, 0.0f, 0.0f};
+        fast_objective(&fp, cell, s->opt.ncc_denom_min, q0, sc);
         double sum = 0.0;
         for (int k = 1; k < fp.m; ++k) sum = sum + sc[k - 1];
         p->score = (float)(sum / (double)(fp.m - 1));

@@ -26,9 +26,34 @@ def small_scene():
 
 
 def _fmaf(a, b, c):
-    # a*b is exact in fp64 for fp32 inputs; one fp64 add then the fp32 rounding
-    # (double rounding can differ from fmaf only within 2^-29 of a tie)
-    return np.float32(np.float64(a) * np.float64(b) + np.float64(c))
+    """fmaf(a, b, c): a*b is exact in fp64 for fp32 inputs; when the fp64 sum
+    is exact too, its fp32 rounding is the single rounding of fmaf, otherwise
+    the exact value is rounded to fp32 (nearest, ties to even)."""
+    from fractions import Fraction
+
+    a, b, c = np.float32(a), np.float32(b), np.float32(c)
+    s = np.float64(a) * np.float64(b)
+    t = s + np.float64(c)
+    if not np.isfinite(t):
+        return np.float32(t)
+    ex = Fraction(float(s)) + Fraction(float(c))
+    if Fraction(float(t)) == ex:
+        return np.float32(t)
+    f = np.float32(t)
+    best = None
+    for cand in (np.nextafter(f, np.float32(-np.inf)), f, np.nextafter(f, np.float32(np.inf))):
+        d = abs(Fraction(float(cand)) - ex)
+        if best is None or d < best[0] or (d == best[0] and int(cand.view(np.uint32)) % 2 == 0):
+            best = (d, cand)
+    return np.float32(best[1])
+
+
+def _f(x):
+    return np.float32(x)
+
+
+def _fdot(a, b):
+    return _fmaf(a[2], b[2], _fmaf(a[1], b[1], _f(a[0]) * _f(b[0])))
 
 
 def _gray(img):
@@ -36,71 +61,94 @@ def _gray(img):
     return ((1868 * b + 9617 * g + 4899 * r + 8192) >> 14).astype(np.int64)
 
 
+def _fcam(orc, P, v):
+    """fp32 camera (or_fast.c fcam_of): rows 0-1 of P times 32, row 2, the
+    centre and the unit x-axis, each rounded once."""
+    Pv = np.asarray(P[v], dtype=np.float64).reshape(12)
+    Q = np.array([np.float32(32.0 * Pv[k]) if k < 8 else np.float32(Pv[k]) for k in range(12)], dtype=np.float32)
+    _, C, _, _, xa = orc.view_geometry(Pv)
+    xr = xa / np.sqrt(xa @ xa)
+    return Q, C.astype(np.float32), xr.astype(np.float32)
+
+
+def _qpt(Q, k, X):
+    return _fmaf(Q[4 * k + 2], X[2], _fmaf(Q[4 * k + 1], X[1], _fmaf(Q[4 * k], X[0], Q[4 * k + 3])))
+
+
+def _qdir(Q, k, w):
+    return _fmaf(Q[4 * k + 2], w[2], _fmaf(Q[4 * k + 1], w[1], _f(Q[4 * k]) * _f(w[0])))
+
+
 def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
     """Independent statement of DP_MODE_FAST_EVAL's score (include/densepoints.h
-    dp_fast_options, margin 0): returns the mean NCC or -1."""
+    dp_fast_options, spec v3: fp32 frame and view geometry, margin 0): returns
+    the mean NCC or -1."""
     V = len(imgs)
-    C = np.zeros((V, 3))
-    xr = np.zeros((V, 3))
-    for v in range(V):
-        _, C[v], _, _, xa = orc.view_geometry(P[v])
-        xr[v] = xa / np.sqrt(xa @ xa)
-    Pm = P.reshape(V, 3, 4)
+    cams = [_fcam(orc, P, v) for v in range(V)]
+    lo, hi = _f(2.0 ** -20), _f(2.0 ** 64)
 
     def proj(v, X):
-        h = Pm[v] @ np.append(X, 1.0)
-        return h[0] / h[2], h[1] / h[2]
+        Q = cams[v][0]
+        h2 = _qpt(Q, 2, X)
+        if not (lo <= h2 <= hi):
+            return None
+        r = _f(1.0) / h2
+        return _qpt(Q, 0, X) * r, _qpt(Q, 1, X) * r
 
     ref = int(p["ref"])
-    X0 = p["pos"].astype(np.float64)
-    n0 = p["normal"].astype(np.float64)
-    cu, cw = proj(ref, X0)
-    qu, qw = proj(ref, X0 + xr[ref])
-    dx = np.sqrt((qu - cu) ** 2 + (qw - cw) ** 2)
-    nl = np.sqrt(n0 @ n0)
-    if not (dx > 0 and nl > 0):
+    Qr, Cr, xr = cams[ref]
+    X = p["pos"].astype(np.float32)
+    n0 = p["normal"].astype(np.float32)
+    a, b = proj(ref, X), proj(ref, (X + xr).astype(np.float32))
+    if a is None or b is None:
         return -1.0
-    ps = 1.0 / dx
-    nn = n0 / nl
-    e1 = xr[ref] - (xr[ref] @ nn) * nn
-    e1 = e1 / np.sqrt(e1 @ e1)
-    e2 = np.cross(nn, e1)
-    r = X0 - C[ref]
-    c = 0.5 * (cell - 1)
+    du, dv = b[0] - a[0], b[1] - a[1]
+    dx = np.sqrt(_fmaf(dv, dv, du * du))
+    nl = np.sqrt(_fdot(n0, n0))
+    if not (dx > 0 and dx <= 2.0 ** 100 and nl > 0):
+        return -1.0
+    ps = _f(32.0) / dx
+    inl = _f(1.0) / nl
+    nn = (n0 * inl).astype(np.float32)
+    xn = _fdot(xr, nn)
+    e1 = np.array([_fmaf(-xn, nn[k], xr[k]) for k in range(3)], dtype=np.float32)
+    el = np.sqrt(_fdot(e1, e1))
+    if not el > 0:
+        return -1.0
+    e1 = (e1 * (_f(1.0) / el)).astype(np.float32)
+    e2 = np.array([_fmaf(nn[1], e1[2], -(nn[2] * e1[1])), _fmaf(nn[2], e1[0], -(nn[0] * e1[2])),
+                   _fmaf(nn[0], e1[1], -(nn[1] * e1[0]))], dtype=np.float32)
+    r = (X - Cr).astype(np.float32)
+    ws = [r, (e1 * ps).astype(np.float32), (e2 * ps).astype(np.float32), (nn * ps).astype(np.float32)]
+    c = _f(0.5) * _f(cell - 1)
     vis = [v for v in range(V) if (int(p["vis"][v >> 6]) >> (v & 63)) & 1][:64]
     staged = []
     for v in vis:
-        H = [Pm[v] @ np.append(X0, 1.0)] + [Pm[v][:, :3] @ w for w in (r, e1 * ps, e2 * ps, nn * ps)]
+        Q = cams[v][0]
+        H = [[_qpt(Q, k, X) for k in range(3)]] + [[_qdir(Q, k, w) for k in range(3)] for w in ws]
         s = H[0][2]
-        if not s > 0:
+        if not (lo <= s <= hi):
             continue
-        inv = 1.0 / s
-        g = [np.array([(32.0 * h[0]) * inv, (32.0 * h[1]) * inv, h[2] * inv]) for h in H]
-        us, ws, ok = [], [], True
-        for ti in (-c, c):
-            for tj in (-c, c):
-                h = g[0] + ti * g[2] + tj * g[3]
-                if not h[2] > 0:
-                    ok = False
-                    break
-                u, w = h[0] / h[2], h[1] / h[2]
-                if not (0 < u < 32.0 * imgs[v].shape[1] and 0 < w < 32.0 * imgs[v].shape[0]):
-                    ok = False
-                    break
-                us.append(u)
-                ws.append(w)
-            if not ok:
-                break
-        if not ok:
+        inv = _f(1.0) / s
+        g = [np.array([h[0] * inv, h[1] * inv, h[2] * inv], dtype=np.float32) for h in H]
+        U0, V0 = g[0][0], g[0][1]
+        Ui, Vi = _fmaf(-U0, g[2][2], g[2][0]), _fmaf(-V0, g[2][2], g[2][1])
+        Uj, Vj = _fmaf(-U0, g[3][2], g[3][0]), _fmaf(-V0, g[3][2], g[3][1])
+        eu, ev = c * (abs(Ui) + abs(Uj)), c * (abs(Vi) + abs(Vj))
+        ez = c * (abs(g[2][2]) + abs(g[3][2]))
+        umin, umax, vmin, vmax = U0 - eu, U0 + eu, V0 - ev, V0 + ev
+        Hh, Ww = imgs[v].shape[:2]
+        if not (g[0][2] - ez > 0):
             continue
-        xa, xb = int(np.floor(min(us) / 32)), int(np.floor(max(us) / 32)) + 1
-        ya, yb = int(np.floor(min(ws) / 32)), int(np.floor(max(ws) / 32)) + 1
+        if not (umin > 0 and umax < _f(32 * Ww) and vmin > 0 and vmax < _f(32 * Hh)):
+            continue
+        xa, xb = int(np.floor(umin * _f(0.03125))), int(np.floor(umax * _f(0.03125))) + 1
+        ya, yb = int(np.floor(vmin * _f(0.03125))), int(np.floor(vmax * _f(0.03125))) + 1
         if xb - xa + 1 > 48 or yb - ya + 1 > 48:
             continue
-        Hh, Ww = imgs[v].shape[:2]
         x0, y0 = max(xa, 0) & ~1, max(ya, 0)  # even left edge (32-bit fp16 pairs on the device)
         tw, th = min(xb, Ww - 1) - x0 + 1, min(yb, Hh - 1) - y0 + 1
-        staged.append((v, g, x0, y0, tw, th, 4 * ((tw + 2) // 2) * (th + 1)))
+        staged.append((v, g, x0, y0, tw, th, 4 * ((tw + 2) // 2) * (th + 1) + 64))
         if len(staged) == fo.max_views:
             break
     tot, keep = 0, []
@@ -114,8 +162,8 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
     N = cell * cell
     samples = []
     for v, g, x0, y0, tw, th, _ in keep:
-        vec = [np.array([np.float32(gg[0] - 32.0 * x0 * gg[2]), np.float32(gg[1] - 32.0 * y0 * gg[2]),
-                         np.float32(gg[2])], dtype=np.float32) for gg in g]
+        ox, oy = _f(-32.0 * x0), _f(-32.0 * y0)
+        vec = [np.array([_fmaf(ox, gg[2], gg[0]), _fmaf(oy, gg[2], gg[1]), gg[2]], dtype=np.float32) for gg in g]
         gray = _gray(imgs[v])
         Hh, Ww = gray.shape
         A, B1, B2 = vec[0], vec[2], vec[3]
@@ -125,11 +173,10 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
         Ui, Vi = _fmaf(-U0, B1[2], B1[0]) * rz, _fmaf(-V0, B1[2], B1[1]) * rz
         Uj, Vj = _fmaf(-U0, B2[2], B2[0]) * rz, _fmaf(-V0, B2[2], B2[1]) * rz
         out = np.zeros(N, dtype=np.int64)
-        cf = np.float32(0.5) * np.float32(cell - 1)
         for j in range(cell):
-            tj = np.float32(j) - cf
+            tj = np.float32(j) - c
             for i in range(cell):
-                ti = np.float32(i) - cf
+                ti = np.float32(i) - c
                 b23 = np.float32(2.0 ** 23)
                 U = min(max(_fmaf(tj, Uj, _fmaf(ti, Ui, U0)) + b23, b23), b23 + np.float32(32 * (tw - 1)))
                 W = min(max(_fmaf(tj, Vj, _fmaf(ti, Vi, V0)) + b23, b23), b23 + np.float32(32 * (th - 1)))
@@ -215,8 +262,9 @@ def test_fast_refine_quality_vs_ground_truth(orc):
 
 
 def test_fast_init_related_cosine_tests(orc, small_scene):
-    """After the refine, InitRelatedImages runs with its angle tests as cosine
-    tests (x > cos(angle), the cosines from the host libm): the candidate mask
+    """After the refine, InitRelatedImages runs in fp32 with its angle tests as
+    squared cosine tests (x > cos(angle) <=> dn > 0 and dn^2 > cos^2 |d|^2 for
+    a positive cosine, the cosines from the host libm): the candidate mask
     equals an independent numpy classification at the refined pose, and the
     filtered visible mask is a subset of the views that test visible."""
     import math
@@ -226,10 +274,10 @@ def test_fast_init_related_cosine_tests(orc, small_scene):
     p = S.seeds_to_patches(seeds[:60])
     S.fast_refine(p, 7, orc.MODE_FAST_REFINE)
     V = len(imgs)
-    Pm = np.asarray(P, dtype=np.float64).reshape(V, 3, 4)
-    C = [orc.view_geometry(P[v])[1] for v in range(V)]
+    cams = [_fcam(orc, P, v) for v in range(V)]
     opts = dp_options()
-    cvis, ccand = math.cos(opts.visible_angle), math.cos(opts.candidate_angle)
+    cvis, ccand = _f(math.cos(opts.visible_angle)), _f(math.cos(opts.candidate_angle))
+    assert cvis > 0 and ccand > 0
 
     def bits(m):
         return {v for v in range(128) if (int(m[v >> 6]) >> (v & 63)) & 1}
@@ -238,23 +286,26 @@ def test_fast_init_related_cosine_tests(orc, small_scene):
     for q in p:
         if q["flags"] & 2:  # degenerate
             continue
-        X = [float(t) for t in q["pos"]]
-        n = [float(t) for t in q["normal"]]
+        X = q["pos"].astype(np.float32)
+        n = q["normal"].astype(np.float32)
         vis, cand = set(), set()
         for v in range(V):
             if v == int(q["ref"]):
                 continue
-            r = Pm[v]
-            h = [((r[k, 0] * X[0] + r[k, 1] * X[1]) + r[k, 2] * X[2]) + r[k, 3] for k in range(3)]
-            u, w = h[0] / h[2], h[1] / h[2]
-            H, W = imgs[v].shape[:2]
-            if not (u > 0.0 and u < W and w > 0.0 and w < H):
+            Q, C, _ = cams[v]
+            h2 = _qpt(Q, 2, X)
+            if not (_f(2.0 ** -20) <= h2 <= _f(2.0 ** 64)):
                 continue
-            d = [X[k] - C[v][k] for k in range(3)]
-            x = ((n[0] * d[0] + n[1] * d[1]) + n[2] * d[2]) / math.sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2])
-            if x > cvis:
+            rr = _f(1.0) / h2
+            u, w = _qpt(Q, 0, X) * rr, _qpt(Q, 1, X) * rr
+            H, W = imgs[v].shape[:2]
+            if not (u > 0 and u < _f(32 * W) and w > 0 and w < _f(32 * H)):
+                continue
+            d = (X - C).astype(np.float32)
+            dn, dd = _fdot(n, d), _fdot(d, d)
+            if dn > 0 and dn * dn > (cvis * cvis) * dd:
                 vis.add(v)
-            elif x > ccand:
+            elif dn > 0 and dn * dn > (ccand * ccand) * dd:
                 cand.add(v)
         assert bits(q["cand"]) == cand
         assert bits(q["vis"]) <= vis | {int(q["ref"])}
