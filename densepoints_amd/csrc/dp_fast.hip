@@ -33,6 +33,8 @@ constexpr int kFastMaxBbox = 48;  // window bounding-box side cap (grazing views
 constexpr int kFastMaxMargin = 7; // keeps a tile row <= 64 entries (one lane each)
 constexpr int kFastSlots = 4;     // at most this many samples per lane per view pass
 constexpr int kFastRec = 64;      // LDS record per staged view (bytes), counted in the budget
+constexpr int kFastPoses = 4;     // poses per batched evaluation (start + 3 differences)
+constexpr int kFastItems = 44;    // (view, pose) records per pass set
 constexpr float kRcpMin = 0x1p-20f, kRcpMax = 0x1p+64f; // operand range of recip_rn
 
 struct GrayPlane {
@@ -76,11 +78,16 @@ struct EvalRec {
 };
 static_assert(sizeof(EvalRec) == 48, "EvalRec is indexed by byte offset i * 48");
 
-// row bytes of a tile from its biased umax = 2^23 + 32 (tw - 1): 4 ((tw + 2) / 2)
-__device__ __forceinline__ uint32_t tile_rowb(float umax_b)
-{
-    return (((__float_as_uint(umax_b) & 0x7fffffu) >> 5) + 3u) >> 1 << 2;
-}
+// a staged view's tile copy (written per rank while staging, in the round
+// records' space)
+struct DmaDesc {
+    const __half *base; // tile origin in the gray plane
+    int32_t pitch, W2;  // plane pitch (pixels), tile row in 32-bit words
+    int32_t nw, ylim;   // words to copy, last image row relative to the tile
+    float inv;          // 1 / W2
+    uint32_t off;       // tile byte offset in the arena
+};
+static_assert(sizeof(DmaDesc) * kFastMaxV <= 48 * kFastItems, "descriptors fit the round records' space");
 
 // patch frame (uniform, fp32): or_fast.c fast_frame
 struct Frame {
@@ -93,8 +100,6 @@ struct Frame {
 
 // conjugate-gradient state between evaluations (uniform, kept in LDS so the
 // sampling passes have the registers)
-constexpr int kFastPoses = 4;  // poses per batched evaluation (start + 3 differences)
-constexpr int kFastItems = 44; // (view, pose) records per pass set
 
 struct CgState {
     float4 pf[kFastPoses]; // sampler inputs (df, af, bf, 0) of the poses to evaluate
@@ -392,18 +397,20 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
     staged_bytes += (unsigned long long)uni(wave_sum_i32(keep ? t.tbytes : 0));
     // the tile's arena offset: after the m records, the tiles of lower rank
     const uint32_t toff = (uint32_t)(kFastRec * m + (incl - t.tbytes - kFastRec) - kFastRec * rank);
-    // the tile copy's parameters stay in the view's lane (the copy loop
-    // broadcasts them per view by readlane)
-    uint64_t dbase = 0;
-    int dpitch = 0, dW2 = 0, dnw = 0, dylim = 0;
-    float dinv = 0.0f;
+    // the tile copy's parameters go to a per-rank descriptor in the round
+    // records' space (free while staging); the copy loop reads them back with
+    // uniform LDS loads (broadcast) instead of eight readlanes per view
+    DmaDesc *dd = (DmaDesc *)L.e.par;
     if (keep) {
-        dbase = (uint64_t)(uintptr_t)(gpl.p + (size_t)t.y0 * (size_t)gpl.pitch + t.x0);
-        dpitch = gpl.pitch;
-        dW2 = (t.tw + 2) / 2;
-        dnw = dW2 * (t.th + 1);
-        dinv = 1.0f / (float)dW2;
-        dylim = gpl.h - 1 - t.y0;
+        DmaDesc D;
+        D.base = gpl.p + (size_t)t.y0 * (size_t)gpl.pitch + t.x0;
+        D.pitch = gpl.pitch;
+        D.W2 = (t.tw + 2) / 2;
+        D.nw = D.W2 * (t.th + 1);
+        D.ylim = gpl.h - 1 - t.y0;
+        D.inv = 1.0f / (float)D.W2;
+        D.off = toff;
+        dd[rank] = D;
         // the record: the five vectors relative to the tile origin, packed word
         const float ox = -32.0f * (float)t.x0, oy = -32.0f * (float)t.y0;
         float4 *R = (float4 *)((char *)L.arena + kFastRec * rank);
@@ -431,23 +438,19 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
     typedef __attribute__((address_space(3))) void *lds_ptr_t;
     typedef __attribute__((address_space(1))) const void *gptr_t;
     const uint32_t tbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)L.arena;
-    for (uint64_t q = kept; q; q &= q - 1) {
-        const int l = (int)__builtin_ctzll(q);
-        const uint64_t pb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(dbase >> 32), l) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dbase, l);
-        const __half *base = (const __half *)(uintptr_t)pb;
-        const int pitch = __builtin_amdgcn_readlane(dpitch, l), W2 = __builtin_amdgcn_readlane(dW2, l);
-        const int nw = __builtin_amdgcn_readlane(dnw, l), ylim = __builtin_amdgcn_readlane(dylim, l);
-        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dinv), l));
-        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)toff, l);
+    wave_sync();
+    for (int r = 0; r < m; ++r) {
+        const DmaDesc D = dd[r];
+        const int nw = uni(D.nw);
         for (int i = 0; i < nw; i += 64) {
             const int d = i + lane;
-            const int y = (int)(((float)d + 0.5f) * inv);
-            const int c = d - y * W2;
-            const int Y = y < ylim ? y : ylim;
-            const __half *src = base + (__umul24((uint32_t)Y, (uint32_t)pitch) + 2u * (uint32_t)c);
+            const int y = (int)(((float)d + 0.5f) * D.inv);
+            const int c = d - y * D.W2;
+            const int Y = y < D.ylim ? y : D.ylim;
+            const __half *src = D.base + (__umul24((uint32_t)Y, (uint32_t)D.pitch) + 2u * (uint32_t)c);
             if (d < nw)
-                __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)(uintptr_t)(tbase + off + 4u * (uint32_t)i), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)(uintptr_t)(tbase + D.off + 4u * (uint32_t)i), 4,
+                                                 0, 0);
         }
     }
     TMARK(L, 3);
@@ -620,9 +623,11 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             const uint32_t tw1 = (pk >> 7) & 63u, th1 = (pk >> 13) & 63u, toff = (pk >> 19) << 2;
             const uint32_t rowb = ((tw1 + 3u) >> 1) << 2;
             EvalRec &E = L.e.par[lane];
-            E.q[0] = make_float4(u0, v0, 0.0f, __uint_as_float(0x4B000000u + 32u * tw1));
-            E.q[1] = make_float4(__builtin_fmaf(-u0, iz, ix) * rz, __builtin_fmaf(-v0, iz, iy) * rz, 0.0f,
-                                 __uint_as_float(0x4B000000u + 32u * th1));
+            // .z fields: the tile's row bytes, and the byte offset of the
+            // lanes that hold the item's anchor samples (group k of pass 0)
+            E.q[0] = make_float4(u0, v0, __uint_as_float(rowb), __uint_as_float(0x4B000000u + 32u * tw1));
+            E.q[1] = make_float4(__builtin_fmaf(-u0, iz, ix) * rz, __builtin_fmaf(-v0, iz, iy) * rz,
+                                 __uint_as_float((uint32_t)(k * LP) << 2), __uint_as_float(0x4B000000u + 32u * th1));
             E.q[2] = make_float4(__builtin_fmaf(-u0, jz, jx) * rz, __builtin_fmaf(-v0, jz, jy) * rz, 0.0f,
                                  __uint_as_float(toff - __umul24((0x4B000000u >> 5) & 0xffffffu, rowb)));
         }
@@ -637,11 +642,9 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             const int i = p * G + j;
             const bool act = i < Q;
             const bool tail = kTail && p == 0;
-            const int r = (int)(__umul24((uint32_t)i, rk) >> 16);
-            const int k = i - r * kn;
             const EvalRec &E = *(const EvalRec *)((const char *)L.e.par + (act ? (uint32_t)i * 48u : 0u));
             const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
-            const uint32_t off = __float_as_uint(qc.w), rowb = tile_rowb(qa.w);
+            const uint32_t off = __float_as_uint(qc.w), rowb = __float_as_uint(qa.z);
             Tap tp[NS], tt{};
 #pragma unroll
             for (int s2 = 0; s2 < NS; ++s2)
@@ -649,7 +652,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             if (tail) {
                 const EvalRec &T = L.e.par[lane < Q ? lane : 0];
                 const float4 ta = T.q[0], tb = T.q[1], tc = T.q[2];
-                tt = tap_addr(ta, tb, tc, __float_as_uint(tc.w), tile_rowb(ta.w), sl.tail, sl.tail);
+                tt = tap_addr(ta, tb, tc, __float_as_uint(tc.w), __float_as_uint(ta.z), sl.tail, sl.tail);
             }
             __builtin_amdgcn_sched_barrier(0);
             TapWords tw[NS], twt{};
@@ -671,7 +674,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
                     a0s[s2] = b[s2];
             }
             // the anchor samples of this item's pose through the LDS crossbar
-            const int src = (k * LP + g) << 2;
+            const int src = (int)__float_as_uint(qb.z) + (g << 2);
             uint32_t av[NS];
 #pragma unroll
             for (int s2 = 0; s2 < NS; ++s2)
