@@ -46,8 +46,20 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def _stamp_text() -> str:
+    return " ".join(FLAGS)
+
+
 def _stale() -> bool:
     if not os.path.exists(OUT):
+        return True
+    # the default library records the flags it was built with: a variant build
+    # copied over it (or a flag change here) makes it stale even when newer
+    try:
+        with open(OUT + ".flags") as f:
+            if f.read() != _stamp_text():
+                return True
+    except OSError:
         return True
     t = os.path.getmtime(OUT)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
@@ -90,11 +102,19 @@ def build(force: bool = False, verbose: bool = False) -> str:
             os.replace(obj + ".tmp", obj)
     if failed:
         raise RuntimeError("hipcc failed")
-    # DP_LIB_NAME: a variant's file name under lib/ (loaded by DP_LIB_VARIANT)
-    out = os.path.join(os.path.dirname(OUT), os.environ.get("DP_LIB_NAME") or os.path.basename(OUT))
+    # DP_LIB_NAME: a variant's file name under lib/ (loaded by DP_LIB_VARIANT);
+    # a variant (DP_EXTRA_FLAGS) never takes the default name: without
+    # DP_LIB_NAME it is named after its flags' hash
+    name = os.environ.get("DP_LIB_NAME") or ("libdensepoints_%s.so" % tag[4:] if extra else os.path.basename(OUT))
+    out = os.path.join(os.path.dirname(OUT), name)
+    if extra and os.path.abspath(out) == os.path.abspath(OUT):
+        raise RuntimeError("DP_EXTRA_FLAGS builds must not overwrite %s (set DP_LIB_NAME)" % OUT)
     tmp = out + ".tmp"
     subprocess.run([hipcc(), *FLAGS, *extra, "-o", tmp, *objs], check=True, cwd=CSRC)
     os.replace(tmp, out)
+    if not extra:
+        with open(OUT + ".flags", "w") as f:
+            f.write(_stamp_text())
     return out
 
 
