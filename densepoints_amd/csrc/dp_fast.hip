@@ -68,6 +68,9 @@ struct FastArgs {
     int64_t max_pops;        // ... and expands only below this index (the pop cap)
     float cvis, ccand;       // cos(visible_angle), cos(candidate_angle) from the host libm, rounded
     float cvis2, ccand2;     // their squares (fp32)
+    double dmin;             // NCC denominator floor in moment units, ((ncc_denom_min 256) N) N
+    float dminf;             // the same, rounded to fp32 (the refine objective's floor)
+    float gs;                // gradient per objective unit: (1 / fd_step) 2^-24
     unsigned long long *stats; // dp_fast_stats: patches, evals, view_evals, staged_bytes
 };
 
@@ -84,7 +87,7 @@ struct DmaDesc {
     const __half *base; // tile origin in the gray plane
     int32_t pitch, W2;  // plane pitch (pixels), tile row in 32-bit words
     int32_t nw, ylim;   // words to copy, last image row relative to the tile
-    float inv;          // 1 / W2
+    uint32_t m20;       // ceil(2^20 / W2): word d's row = (d m20) >> 20 for d < 2^11
     uint32_t off;       // tile byte offset in the arena
 };
 static_assert(sizeof(DmaDesc) * kFastMaxV <= 48 * kFastItems, "descriptors fit the round records' space");
@@ -408,7 +411,7 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
         D.W2 = (t.tw + 2) / 2;
         D.nw = D.W2 * (t.th + 1);
         D.ylim = gpl.h - 1 - t.y0;
-        D.inv = 1.0f / (float)D.W2;
+        D.m20 = ((1u << 20) + (uint32_t)D.W2 - 1u) / (uint32_t)D.W2;
         D.off = toff;
         dd[rank] = D;
         // the record: the five vectors relative to the tile origin, packed word
@@ -444,10 +447,12 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
         const int nw = uni(D.nw);
         for (int i = 0; i < nw; i += 64) {
             const int d = i + lane;
-            const int y = (int)(((float)d + 0.5f) * D.inv);
+            // row y = floor(d / W2): d < 2^11 words per tile (<= 33 x 63), so
+            // the error d (m20 - 2^20 / W2) / 2^20 < 2^-9 stays below 1 / W2
+            const int y = (int)(__umul24((uint32_t)d, D.m20) >> 20);
             const int c = d - y * D.W2;
             const int Y = y < D.ylim ? y : D.ylim;
-            const __half *src = D.base + (__umul24((uint32_t)Y, (uint32_t)D.pitch) + 2u * (uint32_t)c);
+            const __half *src = D.base + 2u * (uint32_t)c + __umul24((uint32_t)Y, (uint32_t)D.pitch);
             if (d < nw)
                 __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)(uintptr_t)(tbase + D.off + 4u * (uint32_t)i), 4,
                                                  0, 0);
@@ -590,7 +595,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
     const int j = (int)((unsigned)lane / LP), g = lane & (LP - 1);
     const char *tiles = (const char *)L.arena;
     const int N = a.cell * a.cell;
-    const double dmin = ((a.opt.ncc_denom_min * 256.0) * (double)N) * (double)N;
+    const double dmin = a.dmin;
     // lane -> (pose, view) of the NCC finish, pose-major: floor(l * rm / 2^16)
     // = floor(l / m) for l < 64 with rm = ceil(2^16 / m) (2 <= m <= 32: the
     // quotient is an integer or at least 1/32 from one, far above rcp's error)
@@ -729,8 +734,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             } else {
                 // the refine's objective term: fp32 finish in 2^-24 steps
                 const float den = __builtin_sqrtf((float)va * (float)vb);
-                const float dminf = (float)dmin;
-                const float rr = recip_rn(den > dminf ? den : dminf);
+                const float rr = recip_rn(den > a.dminf ? den : a.dminf);
                 q = (int)__builtin_rintf(((float)num * rr) * 16777216.0f);
             }
         }
@@ -773,7 +777,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
     enum { kStart = 0, kFd = 1, kProbe1 = 2, kProbe2 = 3 };
     CgState &C = L.cg;
     const float h = a.fo.fd_step;
-    const float gs = (1.0f / h) * 0x1p-24f; // gradient per objective unit
+    const float gs = a.gs; // gradient per objective unit
     for (int k = 0; k < 3; ++k) {
         C.x[k] = 0.0f;
         C.gp[k] = 0.0f;
@@ -822,7 +826,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
             float beta = 0.0f;
             if (it > 0 && C.ggp > 0.0f) {
                 const float dg[3] = {g[0] - C.gp[0], g[1] - C.gp[1], g[2] - C.gp[2]};
-                beta = fdot(g, dg) / C.ggp;
+                beta = fdot(g, dg) * recip_rn(C.ggp); // ggp in [2^-88, 2^56]
                 beta = beta > 0.0f ? beta : 0.0f;
             }
             float d[3];
@@ -1087,7 +1091,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
                         float nrm[3];
                         for (int k = 0; k < 3; ++k)
                             nrm[k] = __builtin_fmaf(bb, F.u2[k], __builtin_fmaf(aa, F.u1[k], F.un[k]));
-                        const float il = 1.0f / __builtin_sqrtf(fdot(nrm, nrm));
+                        // |nrm| >= 1 (orthonormal frame): in recip_rn's range, = 1.0f / sqrtf
+                        const float il = recip_rn(__builtin_sqrtf(fdot(nrm, nrm)));
                         float np[3], nn[3];
                         for (int k = 0; k < 3; ++k) {
                             np[k] = __builtin_fmaf(d, F.r[k], F.X0[k]);
@@ -1301,9 +1306,11 @@ inline int gray_pitch(int W) { return (W + 2 + 63) & ~63; }
 int fast_check_options(dp_ctx *c, const dp_fast_options &f)
 {
     if (f.iters < 0 || f.iters > 64 || f.margin < 0 || f.margin > dpk::kFastMaxMargin || f.tile_budget < 64 ||
-        f.tile_budget > kFastBudget || f.max_views < 2 || f.max_views > dpk::kFastMaxV || !(f.fd_step > 0.0f) ||
-        !(f.ls_step > 0.0f) || (f.densify != 0 && f.densify != 1))
-        return fail(c, DP_E_ARG, "dp_fast_options out of range (margin <= 7, tile_budget <= 16384, 2 <= max_views <= 32)");
+        f.tile_budget > kFastBudget || f.max_views < 2 || f.max_views > dpk::kFastMaxV ||
+        !(f.fd_step >= 0x1p-20f && f.fd_step <= 0x1p+20f) || !(f.ls_step > 0.0f && f.ls_step <= 0x1p+20f) ||
+        (f.densify != 0 && f.densify != 1))
+        return fail(c, DP_E_ARG, "dp_fast_options out of range (margin <= 7, tile_budget <= 16384, 2 <= max_views "
+                                 "<= 32, fd_step in [2^-20, 2^20], 0 < ls_step <= 2^20)");
     return DP_OK;
 }
 
@@ -1447,6 +1454,12 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.ccand = (float)std::cos(c->opt.candidate_angle);
     a.cvis2 = a.cvis * a.cvis;
     a.ccand2 = a.ccand * a.ccand;
+    {
+        const int N = cell * cell;
+        a.dmin = ((c->opt.ncc_denom_min * 256.0) * (double)N) * (double)N;
+        a.dminf = (float)a.dmin;
+        a.gs = (1.0f / c->fopt.fd_step) * 0x1p-24f;
+    }
     if (!c->d_fstats)
         DP_HIP(c, hipMalloc(&c->d_fstats, 8 * sizeof(unsigned long long)));
     a.stats = c->d_fstats;

@@ -121,7 +121,7 @@ static inline float qdir(const float *Q, int k, const float w[3])
     return fmaf(Q[4 * k + 2], w[2], fmaf(Q[4 * k + 1], w[1], Q[4 * k] * w[0]));
 }
 
-/* 1/x (RN) for x in [2^-20, 2^64] */
+/* 1/x (RN); the spec uses it where x lies in [2^-125, 2^125] */
 static inline float rcp_rn(float x) { return 1.0f / x; }
 
 /* projection in 1/32 px; 0 if the depth is outside the reciprocal's range */
@@ -465,7 +465,7 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
         float beta = 0.0f;
         if (it > 0 && ggp > 0.0f) {
             const float dg[3] = {g[0] - gp[0], g[1] - gp[1], g[2] - gp[2]};
-            beta = fdot(g, dg) / ggp;
+            beta = fdot(g, dg) * rcp_rn(ggp); /* ggp in [2^-88, 2^56] (fd_step in [2^-20, 2^20]) */
             beta = beta > 0.0f ? beta : 0.0f;
         }
         float d[3];

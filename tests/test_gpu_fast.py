@@ -34,6 +34,27 @@ def test_recip_newton_equals_ieee_division():
     assert bad.size == 0, f"{bad.size} mismatches, e.g. {x[bad[:5]]}"
 
 
+def test_recip_newton_exhaustive_binade():
+    """v_rcp_f32 + one Newton step is IEEE 1.0f/x for EVERY fp32 significand
+    (the binade [1, 2), all 2^23 values) and, being exponent-independent while
+    input and result are normal, for every operand in [2^-125, 2^125]: the
+    spec's reciprocals (view depths, the NCC denominator, the CG's 1/|d| and
+    1/ggp) all lie there.  Spot checks of the scaling at every exponent."""
+    x = (np.arange(1 << 23, dtype=np.uint32) | np.uint32(0x3F800000)).view(np.float32)
+    out = np.zeros_like(x)
+    N.check(N.lib.dp_probe_recip_f32_device(N.ptr(x), len(x), N.ptr(out)))
+    want = np.float32(1.0) / x
+    bad = np.flatnonzero(out.view(np.uint32) != want.view(np.uint32))
+    assert bad.size == 0, f"{bad.size} mismatches in [1, 2), e.g. {x[bad[:5]]}"
+    rng = np.random.default_rng(5)
+    sig = x[rng.integers(0, len(x), 4096)]
+    y = np.concatenate([np.ldexp(sig, e).astype(np.float32) for e in range(-125, 125)])
+    out = np.zeros_like(y)
+    N.check(N.lib.dp_probe_recip_f32_device(N.ptr(y), len(y), N.ptr(out)))
+    want = np.float32(1.0) / y
+    assert np.array_equal(out.view(np.uint32), want.view(np.uint32))
+
+
 @pytest.fixture(scope="module")
 def engine():
     with dp.Engine(device=0) as eng:
