@@ -109,6 +109,7 @@ def main():
     seeds = synth.seeds(cfg, P)
     # seed stage once (untimed): FilterPatches + OptimizePatches at n = 16
     seed_p = eng.seeds_to_patches(seeds)
+    raw_seed_p = seed_p.copy()
     d_seed = torch.from_numpy(seed_p.view(np.uint8).copy()).to("cuda")
     d_ok = torch.empty(len(seed_p), dtype=torch.uint8, device="cuda")
     eng.refine_device(d_seed.data_ptr(), len(seed_p), 16, N.MODE_SEED, d_ok.data_ptr(), stream.cuda_stream)
@@ -235,7 +236,7 @@ def main():
         result["quality"] = quality(cfg, out, acc)
     if rank == 0 and not fast and not args.no_fast:
         result["perf_mode"] = perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, out, acc, parents, P,
-                                        planes)
+                                        planes, raw_seed_p)
     if rank == 0 and not args.no_densify and not fast:
         # informational: the full PMVS::Run minus matching (dp_densify) on the same scene, untimed by the contract
         t0 = time.perf_counter()
@@ -387,24 +388,56 @@ def quality(cfg, kids, acc):
             "median_normal_err_deg": round(float(np.median(ang)), 3)}
 
 
-def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, parity_acc, parents, P, planes):
+def quality_all(cfg, p):
+    """quality() of every patch in p (unrefined parents, seed patches)."""
+    return quality(cfg, p, np.ones(len(p), dtype=np.uint8))
+
+
+def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, parity_acc, parents, P, planes,
+              raw_seed_p):
     """Informational: the performance mode (DP_MODE_FAST_REFINE, dp_fast.hip --
-    LDS-staged fp16 gray tiles, fused CG, one wavefront per candidate) on the
-    same parents, per window size: Mpatches/s from HIP events on the launch
-    stream, E, the roofline on the algorithmic (every evaluation re-reads its
-    windows) and compulsory (tiles staged once) byte models, geometry against
-    the ground truth next to the parity mode's, and a CPU baseline of its spec
-    (oracle/or_fast.c) with a bit-exact check on that sample."""
+    LDS-staged fp16 gray tiles, fused CG, one wavefront per candidate) per
+    window size, on two parent sets: the headline's (the parity seed stage's
+    survivors; keys n7, n11) and the performance pipeline's own (the seed
+    stage refined in performance mode at n = 16, as dp_densify runs it with
+    dp_fast_options.densify; keys n7_fast_seeds, n11_fast_seeds).  Per run:
+    Mpatches/s from HIP events on the launch stream, E, the roofline on the
+    algorithmic (every evaluation re-reads its windows) and compulsory (tiles
+    staged once) byte models, geometry against the ground truth next to the
+    parity mode's and the unrefined parents', and (headline parents) a CPU
+    baseline of its spec (oracle/or_fast.c) with a bit-exact check."""
     import densepoints_amd as dp
+    from densepoints_amd import _native as N
     from oracle import pyoracle as orc
 
     B = 4 * NP
     res = {"parity_quality_n%d" % args.cell: quality(cfg, parity_out, parity_acc)}
+    # the performance pipeline's parents: raw seed patches -> fast refine at n = 16
+    d_raw = torch.from_numpy(raw_seed_p.view(np.uint8).copy()).to("cuda")
+    d_ok = torch.empty(len(raw_seed_p), dtype=torch.uint8, device="cuda")
+    eng.set_fast_options(dp.FastOptions())
+    eng.refine_device(d_raw.data_ptr(), len(raw_seed_p), 16, N.MODE_FAST_REFINE, d_ok.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    fseed = np.frombuffer(d_raw.cpu().numpy().tobytes(), dtype=N.PATCH_DTYPE)
+    fpar_all = fseed[d_ok.cpu().numpy() == 1]
+    fparents = np.ascontiguousarray(fpar_all[np.arange(NP) % len(fpar_all)])
+    d_fparents = torch.from_numpy(fparents.view(np.uint8).copy()).to("cuda")
+    res["parents_quality"] = {"raw_seed_patches": quality_all(cfg, raw_seed_p),
+                              "parity_seed_stage": quality_all(cfg, parents),
+                              "fast_seed_stage": quality_all(cfg, fparents)}
+    # the parity mode's children of the performance pipeline's parents
+    eng.set_options(dp.Options(expand_cell_size=args.cell))
+    eng.expand_device(d_fparents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    res["parity_quality_n%d_fast_seeds" % args.cell] = quality(
+        cfg, np.frombuffer(work.cpu().numpy().tobytes(), dtype=dp.PATCH_DTYPE), accept.cpu().numpy())
     imgs = None
     budgets = [int(b) for b in args.fast_budgets.split(",") if b] or [None]
     margins = [int(b) for b in args.fast_margins.split(",") if b] or [None]
-    combos = [(int(c), b, mg) for c in args.fast_cells.split(",") if c for b in budgets for mg in margins]
-    for cell, tb, mg in combos:
+    combos = [(int(c), b, mg, ps) for ps in ("", "_fast_seeds") for c in args.fast_cells.split(",") if c
+              for b in budgets for mg in margins]
+    for cell, tb, mg, pset in combos:
+        d_par = d_fparents if pset else d_parents
         fo = dp.FastOptions()
         if tb:
             fo.tile_budget = tb
@@ -414,13 +447,15 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
             fo.iters = args.fast_iters
         eng.set_fast_options(fo)
         eng.set_options(dp.Options(expand_cell_size=cell))
-        eng.fast_expand_device(d_parents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
+        # untimed warm-up launches (the clocks settle over the first ~15 ms of a new launch shape)
+        for _ in range(max(3, args.warmup)):
+            eng.fast_expand_device(d_par.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
         torch.cuda.synchronize()
         ms = []
         for _ in range(max(3, args.steps)):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            eng.fast_expand_device(d_parents.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
+            eng.fast_expand_device(d_par.data_ptr(), NP, work.data_ptr(), accept.data_ptr(), stream.cuda_stream)
             e1.record(stream)
             ms.append((e0, e1))
         torch.cuda.synchronize()
@@ -447,7 +482,7 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
         ft = fast_traffic(cell, fo, B)
         if ft:
             r["roofline"].update(ft)
-        if not args.no_cpu:
+        if not args.no_cpu and not pset:
             if imgs is None:
                 imgs = []
                 for pl in planes:
@@ -467,7 +502,7 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                                                                         for f in fields) and
                                                                     np.array_equal(kacc, acc[: 4 * n]))}
         res["n%d" % cell + ("_b%d" % tb if tb and len(budgets) > 1 else "") +
-            ("_m%d" % mg if mg is not None and len(margins) > 1 else "")] = r
+            ("_m%d" % mg if mg is not None and len(margins) > 1 else "") + pset] = r
     eng.set_options(dp.Options(expand_cell_size=args.cell))
     eng.set_fast_options(dp.FastOptions())
     return res

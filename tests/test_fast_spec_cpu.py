@@ -238,27 +238,73 @@ def test_fast_evaluation_count(orc, small_scene, iters):
     assert np.mean(ev == 2 + 5 * iters) > 0.5
 
 
-def test_fast_refine_quality_vs_ground_truth(orc):
+def _geom_err(cfg, k, a=None):
+    """median |z - z_true| and median normal error (degrees) of patches k
+    (the accepted ones when a is given) against synth.surface."""
+    if a is not None:
+        k = k[a == 1]
+    z, nrm = synth.surface(cfg, k["pos"][:, :2].astype(np.float64))
+    nn = k["normal"].astype(np.float64)
+    nn /= np.linalg.norm(nn, axis=1, keepdims=True)
+    ang = np.degrees(np.arccos(np.clip(np.abs((nn * nrm).sum(1)), 0.0, 1.0)))
+    return float(np.median(np.abs(k["pos"][:, 2] - z))), float(np.median(ang))
+
+
+@pytest.fixture(scope="module")
+def quality_scene():
+    cfg = synth.config(8, 640, 360, 1)
+    P, imgs, seeds = synth.scene_host(cfg)
+    return cfg, P, imgs, seeds
+
+
+def test_fast_refine_quality_vs_ground_truth(orc, quality_scene):
     """Median |z - z_true| of accepted expansion children: performance mode
     below the unrefined children and below the parity mode's Nelder-Mead,
     improving with the iteration count (synth.surface is the ground truth)."""
-    cfg = synth.config(8, 640, 360, 1)
-    P, imgs, seeds = synth.scene_host(cfg)
+    cfg, P, imgs, seeds = quality_scene
     S = orc.Scene(P, imgs)
     par = S.seeds_to_patches(seeds[::2][:400])
     acc = S.refine(par, 16, orc.MODE_SEED)
     par = par[acc == 1]
-
-    def err(k, a):
-        k = k[a == 1]
-        z, _ = synth.surface(cfg, k["pos"][:, :2].astype(np.float64))
-        return float(np.median(np.abs(k["pos"][:, 2] - z)))
-
     nk, na = S.expand(par)
-    e_nm = err(nk, na)
-    e = [err(*S.fast_expand(par, orc.fast_options(iters=it))) for it in (0, 2, 4)]
+    e_nm = _geom_err(cfg, nk, na)[0]
+    e = [_geom_err(cfg, *S.fast_expand(par, orc.fast_options(iters=it)))[0] for it in (0, 2, 4)]
     assert e[2] < e[1] < e[0]
     assert e[2] < 0.5 * e_nm
+
+
+def test_fast_pipeline_improves_normals(orc, quality_scene):
+    """Normals (and depths) against the ground truth, along the performance
+    mode's own pipeline (dp_densify with dp_fast_options.densify):
+      - the seed stage (CG refine at n = 16) takes the raw seed patches'
+        camera-facing normals to well under half their error, where the parity
+        mode's Nelder-Mead seed stage (initial simplex 0.02 of the depth, 0.2
+        rad tilts) makes them worse;
+      - expansion children refined at n = 11 from those parents have lower
+        normal and far lower depth errors than the parity mode's children of
+        the same parents, and more CG iterations lower the normal error."""
+    cfg, P, imgs, seeds = quality_scene
+    S = orc.Scene(P, imgs, _options(expand_cell_size=11))
+    raw = S.seeds_to_patches(seeds[::2][:600])
+    _, ang_raw = _geom_err(cfg, raw)
+    nm = raw.copy()
+    _, ang_nm_seed = _geom_err(cfg, nm[S.refine(nm, 16, orc.MODE_SEED) == 1])
+    par = raw.copy()
+    par = par[S.fast_refine(par, 16, orc.MODE_FAST_REFINE) == 1]
+    assert len(par) > 150
+    _, ang_seed = _geom_err(cfg, par)
+    assert ang_seed < 0.5 * ang_raw and ang_seed < ang_nm_seed, (ang_seed, ang_raw, ang_nm_seed)
+    dz_nm, ang_nm = _geom_err(cfg, *S.expand(par))
+    dz4, ang4 = _geom_err(cfg, *S.fast_expand(par, orc.fast_options(iters=4)))
+    dz8, ang8 = _geom_err(cfg, *S.fast_expand(par, orc.fast_options(iters=8)))
+    assert ang4 < ang_nm and dz4 < 0.2 * dz_nm, (ang4, ang_nm, dz4, dz_nm)
+    assert ang8 < ang4
+
+
+def _options(**kw):
+    import densepoints_amd as dp
+
+    return dp.Options(**kw)
 
 
 def test_fast_init_related_cosine_tests(orc, small_scene):

@@ -8,11 +8,4 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_fast.py -x -q --timeout 300
 rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/t_fast.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu --no-densify --no-seeds ${BENCH_EXTRA:-} > gpurun_out/b1.log 2>&1
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/b1.log; exit $rc; }
-python3 - <<'PY'
-import json
-d = json.loads(open("gpurun_out/b1.log").read().strip().splitlines()[-1])
-print("parity", d["value"])
-for k, v in d.get("perf_mode", {}).items():
-    if "Mpatches_per_s" in v:
-        print(k, v["Mpatches_per_s"], v["kernel_ms_events"], v["quality"])
-PY
+python3 tools/bench_summary.py gpurun_out/b1.log
