@@ -144,8 +144,8 @@ static int check_options(dp_ctx *c, const dp_options &o)
         return fail(c, DP_E_ARG, "cell sizes must be in [2, 16]");
     if (o.grid_scale <= 0)
         return fail(c, DP_E_ARG, "grid_scale must be > 0");
-    if (o.max_patches_per_cell != 1)
-        return fail(c, DP_E_ARG, "max_patches_per_cell != 1 is not supported");
+    if (o.max_patches_per_cell < 1 || o.max_patches_per_cell > 64)
+        return fail(c, DP_E_ARG, "max_patches_per_cell must be in [1, 64]");
     if (o.nm_max_evals < 1)
         return fail(c, DP_E_ARG, "nm_max_evals must be >= 1");
     return DP_OK;
@@ -232,6 +232,9 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     dp_seedgen_free(c->seeds);
     c->seeds = nullptr;
     c->grid.release();
+    c->cellmin.release();
+    c->pend.release();
+    c->granted.release();
     c->lpt.release();
     c->front.release();
     c->f_alive.release();
@@ -848,6 +851,30 @@ struct U8ToU32 {
     __host__ __device__ uint32_t operator()(uint8_t v) const { return v; }
 };
 
+// organizer grid of an empty store: capacity 1 keeps the owner seq per cell
+// (UINT32_MAX = free), capacity k > 1 the claims made (0) plus the per-round
+// minima (UINT32_MAX)
+static int reset_grid(dp_ctx *c, hipStream_t s)
+{
+    const size_t cells = (size_t)c->grid_cells + 1;
+    DP_HIP(c, c->grid.reserve(cells));
+    if (c->opt.max_patches_per_cell == 1) {
+        DP_HIP(c, hipMemsetAsync(c->grid.p, 0xFF, sizeof(uint32_t) * cells, s));
+    } else {
+        DP_HIP(c, hipMemsetAsync(c->grid.p, 0, sizeof(uint32_t) * cells, s));
+        DP_HIP(c, c->cellmin.reserve(cells));
+        DP_HIP(c, hipMemsetAsync(c->cellmin.p, 0xFF, sizeof(uint32_t) * cells, s));
+    }
+    return DP_OK;
+}
+
+// patch store capacity: every accepted patch holds >= 2 claims and a cell
+// takes at most max_patches_per_cell of them
+static int64_t store_capacity(const dp_ctx *c)
+{
+    return (int64_t)c->opt.max_patches_per_cell * c->grid_cells / 2 + 16;
+}
+
 static int organize(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int32_t n, uint32_t seq0,
                     int64_t base, int64_t parent0, int is_seed, int64_t *accepted_total)
 {
@@ -861,8 +888,18 @@ static int organize(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int32_t
     ca.grid = c->grid.p;
     ca.grid_scale = (double)c->opt.grid_scale;
     DP_HIP(c, c->acc.reserve((size_t)n + 1));
-    DP_HIP(c, dpk::launch_claims(ca, s));
-    DP_HIP(c, dpk::launch_resolve(ca, c->acc.p, s));
+    if (c->opt.max_patches_per_cell == 1) {
+        DP_HIP(c, dpk::launch_claims(ca, s));
+        DP_HIP(c, dpk::launch_resolve(ca, c->acc.p, s));
+    } else {
+        DP_HIP(c, c->pend.reserve(2 * (size_t)n + 2));
+        DP_HIP(c, c->granted.reserve((size_t)n + 1));
+        ca.cellmin = c->cellmin.p;
+        ca.pend = c->pend.p;
+        ca.granted = c->granted.p;
+        ca.k = c->opt.max_patches_per_cell;
+        DP_HIP(c, dpk::launch_claims_k(ca, c->acc.p, s));
+    }
     DP_HIP(c, c->prefix.reserve((size_t)n + 1));
     size_t tmp_bytes = 0;
     hipcub::TransformInputIterator<uint32_t, U8ToU32, const uint8_t *> it(c->acc.p, U8ToU32());
@@ -900,11 +937,11 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
     *out = nullptr;
     *n_out = 0;
 
-    // organizer grid: every cell free (owner seq = UINT32_MAX)
-    DP_HIP(c, c->grid.reserve((size_t)c->grid_cells + 1));
-    DP_HIP(c, hipMemsetAsync(c->grid.p, 0xFF, sizeof(uint32_t) * ((size_t)c->grid_cells + 1), s));
-    // each accepted patch owns >= 2 cells exclusively: np <= cells / 2
-    const int64_t store_cap = c->grid_cells / 2 + 16;
+    // organizer grid: every cell free
+    int rg = reset_grid(c, s);
+    if (rg != DP_OK)
+        return rg;
+    const int64_t store_cap = store_capacity(c);
     DP_HIP(c, c->store.reserve((size_t)store_cap));
     DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
 
@@ -1029,9 +1066,10 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
     c->g_np = 0;
     c->g_nseeds = n;
     c->result.clear();
-    DP_HIP(c, c->grid.reserve((size_t)c->grid_cells + 1));
-    DP_HIP(c, hipMemsetAsync(c->grid.p, 0xFF, sizeof(uint32_t) * ((size_t)c->grid_cells + 1), s));
-    DP_HIP(c, c->store.reserve((size_t)(c->grid_cells / 2 + 16)));
+    int rg = reset_grid(c, s);
+    if (rg != DP_OK)
+        return rg;
+    DP_HIP(c, c->store.reserve((size_t)store_capacity(c)));
     DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
     if (n > 0) {
         std::vector<dp_patch> sp(n);

@@ -87,6 +87,9 @@ struct dp_ctx {
     bool timed = false;
     int64_t grid_cells = 0;
     DevBuf<uint32_t> grid;
+    DevBuf<uint32_t> cellmin; // organizer with cell capacity > 1: per-round minima
+    DevBuf<uint64_t> pend;    // ... and per-candidate undecided claims
+    DevBuf<uint8_t> granted;
     DevBuf<uint32_t> lpt;    // refine dequeue order + its counters
     bool lpt_off = false;    // DP_NO_LPT=1 at dp_ctx_create: index-order dequeue
     DevBuf<dp_patch> pat, store, cand;

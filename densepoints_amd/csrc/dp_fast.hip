@@ -122,7 +122,6 @@ template <int kArena> struct FastLds {
         EvalRec par[kFastItems]; // a round's (view, pose) items
         double score[kFastMaxV]; // a scoring evaluation's fp64 NCCs (after its passes)
     } e;
-    uint32_t mom[kFastItems][4];
     uint64_t vis[2], cand[2];
     Frame F;
     CgState cg;
@@ -180,6 +179,19 @@ template <int G> __device__ __forceinline__ uint32_t group_total(uint32_t v)
     return v;
 }
 
+// sums over aligned groups of P lanes (P = 4, 8 or 16, within rows of 16);
+// the total of a group lands in its last lane
+template <int P> __device__ __forceinline__ uint32_t partial_total(uint32_t v)
+{
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true); // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true); // row_shr:2
+    if (P >= 8)
+        v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true); // row_shr:4
+    if (P >= 16)
+        v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true); // row_shr:8
+    return v;
+}
+
 // inclusive prefix sum over the wave in lane order: group_total<1> leaves
 // every lane's inclusive prefix (Hillis-Steele within rows of 16, then the
 // row broadcasts), all in DPP -- no LDS crossbar round trips
@@ -194,6 +206,17 @@ __device__ __forceinline__ float recip_rn(float b)
     const float r = __builtin_amdgcn_rcpf(b);
     const float e = __builtin_fmaf(-b, r, 1.0f);
     return __builtin_fmaf(r, e, r);
+}
+
+// IEEE sqrt (RN) for x = 0 or x >= 2^-96: v_sqrt_f32 (1 ulp) and the
+// residual correction of the compiler's own sequence, without its scaling of
+// denormal-range inputs; 0 -> a value below 2^-48 (the NCC floor replaces it)
+__device__ __forceinline__ float sqrt_rn_big(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float r = __builtin_fmaf(-sd, s, x) <= 0.0f ? sd : s;
+    return __builtin_fmaf(-su, s, x) > 0.0f ? su : r;
 }
 
 __device__ __forceinline__ float fdot(const float *a, const float *b)
@@ -577,7 +600,7 @@ __device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
 // at most kFastItems items (the LDS records) and K' <= G poses.  kScore (one
 // pose): the fp64 NCC of rank r >= 1 goes to L.e.score[r] instead.
 template <int G, int NS, bool kTail, bool kMask, bool kScore, int kArena>
-__device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slots &sl, int m, int K)
+__device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slots &sl, int m, int K, uint32_t rm)
 {
     constexpr int LP = 64 / G;
     const int lane = lane_id();
@@ -587,8 +610,10 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
         wave_sync();
         return;
     }
-    // poses per chunk: K' <= G (anchors in pass 0), K' m <= kFastItems
-    int kc = kFastItems / m;
+    // poses per chunk: K' <= G (anchors in pass 0), K' m <= kFastItems (= 44:
+    // uniform compares instead of a division)
+    static_assert(kFastItems == 44, "the pose-chunk thresholds below assume 44 items");
+    int kc = m <= 11 ? 4 : m <= 14 ? 3 : m <= 22 ? 2 : 1;
     kc = kc < G ? kc : G;
     kc = kc < kFastPoses ? kc : kFastPoses;
     kc = kScore ? 1 : kc;
@@ -596,10 +621,6 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
     const char *tiles = (const char *)L.arena;
     const int N = a.cell * a.cell;
     const double dmin = a.dmin;
-    // lane -> (pose, view) of the NCC finish, pose-major: floor(l * rm / 2^16)
-    // = floor(l / m) for l < 64 with rm = ceil(2^16 / m) (2 <= m <= 32: the
-    // quotient is an integer or at least 1/32 from one, far above rcp's error)
-    const uint32_t rm = (uint32_t)__builtin_ceilf(65536.0f * __builtin_amdgcn_rcpf((float)m));
     for (int k0 = 0; k0 < K; k0 += kc) {
         const int kn = K - k0 < kc ? K - k0 : kc;
         const int Q = kn * m;
@@ -691,13 +712,19 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
                 ss = __umul24(b[s2], b[s2]) + ss;
                 sx = __umul24(av[s2], b[s2]) + sx;
             }
-            s = group_total<G>(s);
-            ss = group_total<G>(ss);
-            sx = group_total<G>(sx);
-            if (g == LP - 1 && act) {
-                L.mom[i][0] = s;
-                L.mom[i][1] = ss;
-                L.mom[i][2] = sx;
+            // four partial sums per moment (DPP within rows of 16 down to
+            // groups of LP/4 lanes), stored in the item's own record, which
+            // this pass has read (pass 0's tail read every record first);
+            // the NCC finish adds the partials
+            s = partial_total<LP / 4>(s);
+            ss = partial_total<LP / 4>(ss);
+            sx = partial_total<LP / 4>(sx);
+            if (act && (g & (LP / 4 - 1)) == LP / 4 - 1) {
+                uint32_t *M = (uint32_t *)&L.e.par[i];
+                const int pi = g / (LP / 4);
+                M[pi] = s;
+                M[4 + pi] = ss;
+                M[8 + pi] = sx;
             }
         }
         wave_sync();
@@ -713,8 +740,11 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
         const uint32_t b0 = kTail ? (uint32_t)__builtin_amdgcn_ds_bpermute((it < 64 ? it : 0) << 2, (int)bt) : 0u;
         int q = 0;
         if (lane < Q && rt >= 1) {
-            uint32_t sa = L.mom[kt][0], saa = L.mom[kt][1];
-            uint32_t sb = L.mom[it][0], sbb = L.mom[it][1], sab = L.mom[it][2];
+            const uint4 *Ma = (const uint4 *)&L.e.par[kt], *Mb = (const uint4 *)&L.e.par[it];
+            const uint4 as = Ma[0], aas = Ma[1], bs = Mb[0], bbs = Mb[1], abs4 = Mb[2];
+            uint32_t sa = (as.x + as.y) + (as.z + as.w), saa = (aas.x + aas.y) + (aas.z + aas.w);
+            uint32_t sb = (bs.x + bs.y) + (bs.z + bs.w), sbb = (bbs.x + bbs.y) + (bbs.z + bbs.w);
+            uint32_t sab = (abs4.x + abs4.y) + (abs4.z + abs4.w);
             if (kTail) {
                 sa += a0;
                 saa += __umul24(a0, a0);
@@ -733,7 +763,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
                 L.e.score[rt] = num / (den > dmin ? den : dmin);
             } else {
                 // the refine's objective term: fp32 finish in 2^-24 steps
-                const float den = __builtin_sqrtf((float)va * (float)vb);
+                const float den = sqrt_rn_big((float)va * (float)vb);
                 const float rr = recip_rn(den > a.dminf ? den : a.dminf);
                 q = (int)__builtin_rintf(((float)num * rr) * 16777216.0f);
             }
@@ -753,6 +783,14 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
         wave_sync();
         TMARK(L, 14);
     }
+}
+
+// lane -> (pose, view) of the NCC finish, pose-major: floor(l * rm / 2^16)
+// = floor(l / m) for l < 64 with rm = ceil(2^16 / m) (2 <= m <= 32: the
+// quotient is an integer or at least 1/32 from one, far above rcp's error)
+__device__ __forceinline__ uint32_t pose_major_rm(int m)
+{
+    return (uint32_t)__builtin_ceilf(65536.0f * __builtin_amdgcn_rcpf((float)m));
 }
 
 // the sampler inputs of pose k: (x0 sd, x1 st, x2 st)
@@ -786,6 +824,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
     C.alpha = a.fo.ls_step;
     C.ggp = 0.0f;
     int E = 0, it = 0, phase = kStart;
+    const uint32_t rm = pose_major_rm(m);
     for (;;) {
         int K = 1;
         if (phase == kStart || phase == kFd) {
@@ -806,7 +845,7 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
         }
         wave_sync();
         TMARK(L, 15);
-        evaluate_poses<G, NS, kTail, kMask, false>(a, L, sl, m, K);
+        evaluate_poses<G, NS, kTail, kMask, false>(a, L, sl, m, K, rm);
         if (phase == kStart || phase == kFd) {
             int k0 = 0;
             if (phase == kStart) {
@@ -893,7 +932,7 @@ __device__ void evaluate_score(const FastArgs &a, FastLds<kArena> &L, const Slot
 {
     L.cg.pf[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     wave_sync();
-    evaluate_poses<G, NS, kTail, kMask, true>(a, L, sl, m, 1);
+    evaluate_poses<G, NS, kTail, kMask, true>(a, L, sl, m, 1, pose_major_rm(m));
 }
 
 // x > c for x = dn / sqrt(dd), compared squared (or_fast.c cos_above)

@@ -55,8 +55,13 @@ struct ClaimArgs {
     const uint8_t *ok;       // filter passed
     int32_t n;
     uint32_t seq0;           // seq of cand[0]; seq grows by one per candidate
-    uint32_t *grid;          // cell owner = min seq
+    uint32_t *grid;          // cell owner = min seq (capacity 1) / claims made (capacity k > 1)
     double grid_scale;
+    // capacity k > 1 (PatchGrid::TryInsert's size() < max_patches_per_cell)
+    uint32_t *cellmin;       // per cell, the round's smallest pending seq (UINT32_MAX between rounds)
+    uint64_t *pend;          // per candidate, its visible views whose claim is undecided (2 words)
+    uint8_t *granted;        // per candidate, claims granted so far
+    int32_t k;
 };
 
 // one image plane of a pyramid level (BGRA8, B in the low byte)
@@ -85,6 +90,9 @@ hipError_t launch_filter_visibility(const FilterArgs &a, uint8_t *keep, hipStrea
 hipError_t launch_filter_neighbors(const FilterArgs &a, uint8_t *keep, hipStream_t s);
 
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s);
+// the organizer step with cell capacity a.k > 1 (k rounds of claims in
+// sequence order); accepted[i] = more than one claim granted
+hipError_t launch_claims_k(const ClaimArgs &a, uint8_t *accepted, hipStream_t s);
 hipError_t launch_pyr_down(const PyrPlane *d_src, const PyrPlane *d_dst, int V, int max_dw, int max_dh,
                            hipStream_t s);
 int read_stamps(unsigned long long *out);

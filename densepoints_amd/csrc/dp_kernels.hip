@@ -1316,6 +1316,95 @@ __global__ void resolve_kernel(ClaimArgs a, uint8_t *accepted)
     accepted[i] = claims > 1 ? 1 : 0;
 }
 
+// ---- organizer with cell capacity k > 1 --------------------------------------
+// PatchGrid::TryInsert (patch_organizer.cpp:15-30) admits a claim while the
+// cell holds fewer than max_patches_per_cell patches, and claims persist
+// (rejected patches keep theirs), so a cell's claims are its first k attempts
+// in sequence order.  Every earlier generation's attempt has a lower seq than
+// this generation's, so grid[cell] (claims so far) plus k rounds over this
+// generation -- each round every cell with room grants its smallest pending
+// seq -- reproduces the sequential order exactly.
+
+__global__ void claimk_init_kernel(ClaimArgs a)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n)
+        return;
+    uint64_t pend[2] = {0, 0};
+    if (a.ok[i]) {
+        const dp_patch &p = a.cand[i];
+        for (int w = 0; w < 2; ++w) {
+            uint64_t bits = p.vis[w];
+            while (bits) {
+                const int b = __builtin_ctzll(bits);
+                bits &= bits - 1;
+                int64_t cell;
+                if (cell_of(a.views[w * 64 + b], p.pos, a.grid_scale, cell))
+                    pend[w] |= 1ull << b;
+            }
+        }
+    }
+    a.pend[2 * i] = pend[0];
+    a.pend[2 * i + 1] = pend[1];
+    a.granted[i] = 0;
+}
+
+__global__ void claimk_round_kernel(ClaimArgs a)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n)
+        return;
+    const dp_patch &p = a.cand[i];
+    const uint32_t seq = a.seq0 + (uint32_t)i;
+    for (int w = 0; w < 2; ++w) {
+        uint64_t bits = a.pend[2 * i + w];
+        while (bits) {
+            const int b = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            int64_t cell;
+            if (cell_of(a.views[w * 64 + b], p.pos, a.grid_scale, cell) && a.grid[cell] < (uint32_t)a.k)
+                atomicMin(&a.cellmin[cell], seq);
+        }
+    }
+}
+
+__global__ void claimk_grant_kernel(ClaimArgs a)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n)
+        return;
+    const dp_patch &p = a.cand[i];
+    const uint32_t seq = a.seq0 + (uint32_t)i;
+    int granted = a.granted[i];
+    for (int w = 0; w < 2; ++w) {
+        uint64_t bits = a.pend[2 * i + w], left = bits;
+        while (bits) {
+            const int b = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            int64_t cell;
+            cell_of(a.views[w * 64 + b], p.pos, a.grid_scale, cell);
+            if (a.cellmin[cell] == seq) {
+                // the round's winner: one per cell, so plain updates
+                a.grid[cell] += 1u;
+                a.cellmin[cell] = 0xffffffffu;
+                ++granted;
+                left &= ~(1ull << b);
+            } else if (a.grid[cell] >= (uint32_t)a.k) {
+                left &= ~(1ull << b); // full: denied for good
+            }
+        }
+        a.pend[2 * i + w] = left;
+    }
+    a.granted[i] = (uint8_t)(granted < 255 ? granted : 255);
+}
+
+__global__ void claimk_resolve_kernel(ClaimArgs a, uint8_t *accepted)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.n)
+        accepted[i] = a.granted[i] > 1 ? 1 : 0;
+}
+
 // append accepted candidates in sequence order + Patch::ComputeColor
 // (patch.cpp:51-73)
 __global__ void append_kernel(const dpg::ViewDev *views, int V, const dp_patch *cand,
@@ -1664,6 +1753,20 @@ hipError_t launch_resolve(const ClaimArgs &a, uint8_t *accepted, hipStream_t s)
     if (a.n <= 0)
         return hipSuccess;
     hipLaunchKernelGGL(resolve_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a, accepted);
+    return hipGetLastError();
+}
+
+hipError_t launch_claims_k(const ClaimArgs &a, uint8_t *accepted, hipStream_t s)
+{
+    if (a.n <= 0)
+        return hipSuccess;
+    const dim3 g((a.n + 255) / 256), b(256);
+    hipLaunchKernelGGL(claimk_init_kernel, g, b, 0, s, a);
+    for (int r = 0; r < a.k; ++r) {
+        hipLaunchKernelGGL(claimk_round_kernel, g, b, 0, s, a);
+        hipLaunchKernelGGL(claimk_grant_kernel, g, b, 0, s, a);
+    }
+    hipLaunchKernelGGL(claimk_resolve_kernel, g, b, 0, s, a, accepted);
     return hipGetLastError();
 }
 

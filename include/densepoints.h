@@ -47,7 +47,7 @@ typedef struct dp_options {
     int32_t seed_cell_size;       /* 16  matcher.h:25, used at seed.cpp:117,135       */
     int32_t expand_cell_size;     /* 11  expand.h:12, used at expand.cpp:129          */
     int32_t grid_scale;           /* 8   patch_organizer.h:43                          */
-    int32_t max_patches_per_cell; /* 1   patch_organizer.h:42 (only 1 is supported)    */
+    int32_t max_patches_per_cell; /* 1   patch_organizer.h:42 (1..64; a cell keeps its first k claims) */
     int32_t min_visible;          /* 3   optimization.h:17                             */
     int32_t min_expand_visible;   /* 2   expand.cpp:67                                 */
     int32_t nm_max_evals;         /* 500 optimization_opencv.cpp:60                    */

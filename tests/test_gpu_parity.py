@@ -186,6 +186,28 @@ def test_densify_bit_exact(orc, name):
     assert_same(gp, op, FIELDS + ("seq", "parent", "rgb"))
 
 
+@pytest.mark.parametrize("k", [2, 3])
+def test_densify_cell_capacity_bit_exact(orc, k):
+    """PatchOrganizerOptions::max_patches_per_cell > 1 (patch_organizer.h:42-46,
+    the capacity test of PatchGrid::TryInsert, patch_organizer.cpp:21): a
+    cell admits its first k claims in sequence order, claims of rejected
+    patches included.  dp_densify equals the oracle's sequential organizer,
+    and holds more patches than with capacity 1."""
+    sc = scene("hf6")
+    o = dp.Options(max_patches_per_cell=k)
+    S = orc.Scene(sc.P, sc.imgs, o)
+    op, ost = S.densify(sc.seeds)
+    with dp.Engine(o, device=0) as eng:
+        eng.set_views(sc.views)
+        gp, gst = eng.densify(sc.seeds)
+        eng.set_options(dp.Options())
+        _, g1 = eng.densify(sc.seeds)
+    assert gst["patches"] == ost["patches"] and gst["seed_patches"] == ost["seed_patches"]
+    assert gst["pops"] == ost["pops"]
+    assert gst["patches"] > g1["patches"] > 20
+    assert_same(gp, op, FIELDS + ("seq", "parent", "rgb"))
+
+
 def test_densify_two_views_is_empty(orc):
     """BASELINE config 1 (2 views): a patch needs >=3 visible non-reference
     views, so the reference yields no patches."""
