@@ -305,7 +305,11 @@ def main():
         result["stamps_share"] = {k: round(float(st[i]) / tot, 4) for i, k in
                                   enumerate(["corners_maps", "view_passes", "sync", "ncc_finish"])}
         result["stamps_share"]["rest_nm_geometry"] = round(1.0 - sum(result["stamps_share"].values()), 4)
-    tj = args.traffic_json or latest_traffic_json()
+    prof = profiled("parity" if not fast else "fast%d" % args.cell,
+                    "refine_kernel<4, 2>" if not fast else fast_kernel_tag(args.cell), B)
+    if prof and not args.traffic_json:
+        attach_profile(result["roofline"], prof, B, launch_ms)
+    tj = args.traffic_json or (None if prof else latest_traffic_json())
     if tj and os.path.exists(tj):
         with open(tj) as f:
             t = json.load(f)
@@ -479,9 +483,10 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                           "compulsory_GBps": round(comp / kms / 1e6, 2)},
              "quality": quality(cfg, out, acc), "stats": {k: int(v) for k, v in st.items()},
              "fast_options": {k: getattr(fo, k) for k in ("iters", "margin", "tile_budget", "max_views")}}
-        ft = fast_traffic(cell, fo, B)
-        if ft:
-            r["roofline"].update(ft)
+        fprof = profiled("fast%d" % cell, fast_kernel_tag(cell), B) if not pset and fo.tile_budget == 6656 \
+            and fo.iters == 4 else None
+        if fprof:
+            attach_profile(r["roofline"], fprof, B, kms)
         if not args.no_cpu and not pset:
             if imgs is None:
                 imgs = []
@@ -508,27 +513,52 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
     return res
 
 
-def fast_traffic(cell, fo, B):
-    """rocprofv3 PMC bytes per launch of the performance-mode kernel for this
-    window (profiles/<latest round>/traffic_all_kernels.json, tools/gpu_profile.sh),
-    when the recorded launch used the same arena and batch: raw = (FETCH_SIZE +
-    WRITE_SIZE) KiB, traffic = the guide's 2x FETCH correction (uncalibrated for
-    these short tile-row reads; WRITE_SIZE is mostly register-spill scratch)."""
+def fast_kernel_tag(cell):
+    """the performance kernel instance bench runs at this window (dp_fast.hip fast_dispatch)"""
+    return {7: "fast_kernel<4, 3, true, false, 6656, 6>", 11: "fast_kernel<2, 4, false, true, 6656, 6>"}.get(cell, "?")
+
+
+def profiled(workload, kernel, B):
+    """The rocprofv3 record of `kernel` under bench workload `workload`
+    (parity | fast7 | fast11) from the latest profiles/rNN/kernel_counters.json
+    (tools/r03_profile.sh + tools/profile_json.py), when it was taken on this
+    batch size (262,144 candidates): per-launch PMC counters and durations."""
     import glob
 
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_all_kernels.json")))
-    if not found or B != 4 * 65536 or fo.tile_budget > 6656:
-        return None
-    tag = {7: "fast_kernel<4, 3, true, false, 6656", 11: "fast_kernel<2, 4, false, true, 6656"}.get(cell)
-    if tag is None:
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_counters.json")))
+    if not found or B != 4 * 65536:
         return None
     with open(found[-1]) as f:
         t = json.load(f)
-    for k, v in t.items():
-        if tag in k:
-            return {"traffic": v["corrected_bytes"], "traffic_raw": v["raw_bytes"],
-                    "traffic_source": os.path.relpath(found[-1], ROOT)}
+    for k, v in t.get(workload, {}).items():
+        if kernel in k:
+            return dict(v, kernel=k, source=os.path.relpath(found[-1], ROOT))
     return None
+
+
+def attach_profile(roof, prof, B, launch_ms):
+    """roofline.traffic (HBM bytes per launch, 2 FETCH_SIZE + WRITE_SIZE per
+    MI355X_MICROARCH.md; raw beside it) and roofline.valu: the kernel is VALU-
+    issue-bound, so its second roofline is wave-instructions/s against the
+    issue peak 1024 SIMDs x clock / 2 (a wave64 VALU instruction takes two
+    cycles of a SIMD-32), with the profiled instructions per candidate (the
+    instruction stream is deterministic for this workload) over the live launch
+    time, and the profile's VALU-busy fraction and effective clock."""
+    if "hbm_bytes_corrected" in prof:
+        roof["traffic"] = prof["hbm_bytes_corrected"]
+        roof["traffic_raw"] = prof["hbm_bytes_raw"]
+    v = prof.get("valu")
+    if v:
+        per = v["insts_per_launch"] / B
+        ach = per * B / (launch_ms * 1e-3) / 1e9
+        roof["valu"] = {"insts_per_candidate": round(per, 1), "achieved_Ginst_per_s": round(ach, 1),
+                        "peak_Ginst_per_s": v["issue_peak_at_2.4GHz_Ginst_s"],
+                        "frac": round(ach / v["issue_peak_at_2.4GHz_Ginst_s"], 4),
+                        "effective_clock_GHz": round(v["effective_clock_GHz"], 3),
+                        "frac_at_effective_clock": round(ach / v["issue_peak_at_effective_clock_Ginst_s"], 4),
+                        "busy_frac": round(v["busy_frac"], 4),
+                        "profiled_launch_ms": round(prof["trace_avg_ns"] * 1e-6, 3)}
+    roof["profile_source"] = prof["source"] + " [" + prof["kernel"] + "]"
 
 
 def latest_traffic_json():
