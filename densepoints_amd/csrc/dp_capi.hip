@@ -235,6 +235,13 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->cellmin.release();
     c->pend.release();
     c->granted.release();
+    c->okeys.release();
+    c->oiota.release();
+    c->porder.release();
+    c->ocount.release();
+    c->owners.release();
+    c->items.release();
+    c->seedp.release();
     c->lpt.release();
     c->front.release();
     c->f_alive.release();
@@ -1361,6 +1368,128 @@ extern "C" int dp_densify_commit_items_device(dp_ctx *c, dp_generation *gen, con
                                             c->stream));
     }
     return densify_commit_impl(c, gen, c->cand.p, c->ok.p, (int64_t)nc, true, c->stream);
+}
+
+
+// round robin when the largest share exceeds 1.1x the mean (dp_densify_owners)
+static bool partition_falls_back(const std::vector<int64_t> &cnt, int64_t n, int world)
+{
+    int64_t mx = 0;
+    for (int64_t v : cnt)
+        mx = v > mx ? v : mx;
+    return (double)mx > 1.1 * (double)n / (double)world;
+}
+
+extern "C" int dp_densify_partition_device(dp_ctx *c, const dp_generation *gen, int world, int tile_px,
+                                           const int64_t **d_order_out, int64_t *counts_out, int32_t *fallback_out)
+{
+    if (!c || !gen || world < 1 || world > 64 || tile_px < 1 || !d_order_out || !counts_out)
+        return fail(c, DP_E_ARG, "dp_densify_partition_device: bad arguments (1 <= world <= 64)");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_partition_device: generation out of sequence");
+    const int64_t n = gen->items;
+    *d_order_out = nullptr;
+    for (int r = 0; r < world; ++r)
+        counts_out[r] = 0;
+    if (fallback_out)
+        *fallback_out = 0;
+    if (n == 0)
+        return DP_OK;
+    if (n > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_partition_device: generation too large");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const dp_patch *items = gen->index == 0 ? c->seedp.p : c->store.p + gen->head;
+    DP_HIP(c, c->owners.reserve((size_t)n));
+    DP_HIP(c, c->ocount.reserve(64));
+    DP_HIP(c, dpk::launch_owners(c->d_views, items, n, world, (double)tile_px, c->owners.p, s));
+    DP_HIP(c, dpk::launch_count_owners(c->owners.p, n, world, c->ocount.p, s));
+    std::vector<unsigned long long> h((size_t)world);
+    DP_HIP(c, hipMemcpyAsync(h.data(), c->ocount.p, sizeof(unsigned long long) * world, hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipStreamSynchronize(s));
+    std::vector<int64_t> cnt(h.begin(), h.end());
+    if (partition_falls_back(cnt, n, world)) {
+        DP_HIP(c, dpk::launch_round_robin(c->owners.p, n, world, s));
+        for (int r = 0; r < world; ++r)
+            cnt[(size_t)r] = n / world + (r < n % world ? 1 : 0);
+        if (fallback_out)
+            *fallback_out = 1;
+    }
+    // stable partition: radix sort of (owner, item index) pairs on the owner bits
+    int bits = 1;
+    while ((1 << bits) < world)
+        ++bits;
+    DP_HIP(c, c->okeys.reserve((size_t)n));
+    DP_HIP(c, c->oiota.reserve((size_t)n));
+    DP_HIP(c, c->porder.reserve((size_t)n));
+    DP_HIP(c, dpk::launch_iota(c->oiota.p, n, s));
+    const uint32_t *kin = (const uint32_t *)c->owners.p;
+    uint32_t *kout = (uint32_t *)c->okeys.p;
+    size_t tmp = 0;
+    DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, c->oiota.p, c->porder.p, (int)n, 0, bits, s));
+    DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
+    DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->scan_tmp.p, tmp, kin, kout, c->oiota.p, c->porder.p, (int)n, 0,
+                                                 bits, s));
+    for (int r = 0; r < world; ++r)
+        counts_out[r] = cnt[(size_t)r];
+    *d_order_out = c->porder.p;
+    return DP_OK;
+}
+
+extern "C" int dp_densify_compact_accepted_device(dp_ctx *c, const dp_generation *gen, const int64_t *d_items,
+                                                  int64_t n, const dp_patch *d_cand, const uint8_t *d_accept,
+                                                  dp_patch *d_out, int64_t *n_out, void *stream)
+{
+    if (!c || !gen || n < 0 || !n_out || (n > 0 && (!d_items || !d_cand || !d_accept || !d_out)))
+        return fail(c, DP_E_ARG, "dp_densify_compact_accepted_device: bad arguments");
+    *n_out = 0;
+    const int64_t m = n * gen->per_item;
+    if (m == 0)
+        return DP_OK;
+    if (m > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_compact_accepted_device: too many candidates");
+    hipSetDevice(c->device);
+    hipStream_t us = stream ? (hipStream_t)stream : c->stream;
+    DP_HIP(c, c->prefix.reserve((size_t)m + 1));
+    DP_HIP(c, c->acc.reserve((size_t)m + 1));
+    // flags with a zeroed tail: prefix[m] = the count
+    DP_HIP(c, hipMemcpyAsync(c->acc.p, d_accept, (size_t)m, hipMemcpyDeviceToDevice, us));
+    DP_HIP(c, hipMemsetAsync(c->acc.p + m, 0, 1, us));
+    hipcub::TransformInputIterator<uint32_t, U8ToU32, const uint8_t *> it(c->acc.p, U8ToU32());
+    size_t tmp = 0;
+    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, c->prefix.p, (int)m + 1, us));
+    DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
+    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, it, c->prefix.p, (int)m + 1, us));
+    DP_HIP(c, dpk::launch_compact_accepted(d_cand, c->acc.p, c->prefix.p, d_items, n, gen->per_item, d_out, us));
+    uint32_t total = 0;
+    DP_HIP(c, hipMemcpyAsync(&total, c->prefix.p + m, sizeof(uint32_t), hipMemcpyDeviceToHost, us));
+    DP_HIP(c, hipStreamSynchronize(us));
+    *n_out = total;
+    return DP_OK;
+}
+
+extern "C" int dp_densify_commit_accepted_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_recs,
+                                                 int64_t n_recs, void *stream)
+{
+    if (!c || !gen || n_recs < 0 || (n_recs > 0 && !d_recs))
+        return fail(c, DP_E_ARG, "dp_densify_commit_accepted_device: bad arguments");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_commit_accepted_device: generation out of sequence");
+    const int64_t nc = gen->items * gen->per_item;
+    if (n_recs > nc)
+        return fail(c, DP_E_ARG, "dp_densify_commit_accepted_device: more records than candidates");
+    hipSetDevice(c->device);
+    hipStream_t us = (hipStream_t)stream;
+    if (nc > 0) {
+        if (us != c->stream)
+            DP_HIP(c, hipStreamSynchronize(us));
+        DP_HIP(c, c->cand.reserve((size_t)nc));
+        DP_HIP(c, c->ok.reserve((size_t)nc));
+        // every other candidate of the generation failed the refine's filter
+        DP_HIP(c, hipMemsetAsync(c->ok.p, 0, (size_t)nc, c->stream));
+        DP_HIP(c, dpk::launch_scatter_accepted(d_recs, n_recs, nc, c->cand.p, c->ok.p, c->stream));
+    }
+    return densify_commit_impl(c, gen, c->cand.p, c->ok.p, nc, true, c->stream);
 }
 
 extern "C" int dp_densify_result(dp_ctx *c, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats)

@@ -106,6 +106,10 @@ struct dp_ctx {
     DevBuf<dp_patch> seedp;  // seed patches of generation 0
     DevBuf<int64_t> items;   // item list of a partitioned refine / commit
     DevBuf<int32_t> owners;  // owner rank per item (dp_densify_owners)
+    // dp_densify_partition_device: sorted owners, item order, per-rank counts
+    DevBuf<int32_t> okeys;
+    DevBuf<int64_t> oiota, porder;
+    DevBuf<unsigned long long> ocount;
     int64_t g_np = 0;        // patches in the replicated store
     int64_t g_nseeds = 0;
     int64_t g_expected = -1; // generation index the next commit must carry

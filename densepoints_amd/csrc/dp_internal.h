@@ -109,6 +109,18 @@ hipError_t launch_render(const dp_synth_config &cfg, const double *P, uint32_t *
 hipError_t launch_owners(const dpg::ViewDev *views, const dp_patch *items, int64_t n, int world, double tile,
                          int32_t *owner, hipStream_t s);
 hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s);
+// device-side partition of a generation: per-rank counts of the owners (atomics
+// into counts[world], zeroed here), round-robin owners, 0..n-1
+hipError_t launch_count_owners(const int32_t *owner, int64_t n, int world, unsigned long long *counts, hipStream_t s);
+hipError_t launch_round_robin(int32_t *owner, int64_t n, int world, hipStream_t s);
+hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s);
+// accepted candidates of items[0..n) (per_item each), out[prefix[j]] = cand[j]
+// with seq = items[j / per] * per + j % per (the generation position)
+hipError_t launch_compact_accepted(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
+                                   const int64_t *items, int64_t n, int per, dp_patch *out, hipStream_t s);
+// cand[r.seq] = r, ok[r.seq] = 1 for each gathered accepted record r (seq < nc)
+hipError_t launch_scatter_accepted(const dp_patch *recs, int64_t n, int64_t nc, dp_patch *cand, uint8_t *ok,
+                                   hipStream_t s);
 hipError_t launch_scatter_items(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n, int per,
                                 dp_patch *cand_out, uint8_t *acc_out, hipStream_t s);
 

@@ -1722,6 +1722,105 @@ hipError_t launch_owners(const dpg::ViewDev *views, const dp_patch *items, int64
     return hipGetLastError();
 }
 
+__global__ void count_owners_kernel(const int32_t *owner, int64_t n, int world, unsigned long long *counts)
+{
+    // per-block histogram in LDS, one global atomic per (block, rank)
+    __shared__ unsigned long long h[64];
+    if (threadIdx.x < 64)
+        h[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[owner[i]], 1ull);
+    __syncthreads();
+    if ((int)threadIdx.x < world && h[threadIdx.x])
+        atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ void round_robin_kernel(int32_t *owner, int64_t n, int world)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        owner[i] = (int32_t)(i % world);
+}
+
+__global__ void iota_kernel(int64_t *v, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        v[i] = i;
+}
+
+__global__ void compact_accepted_kernel(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
+                                        const int64_t *items, int64_t m, int per, dp_patch *out)
+{
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m || !acc[j])
+        return;
+    dp_patch r = cand[j];
+    r.seq = (uint32_t)(items[j / per] * per + j % per);
+    out[prefix[j]] = r;
+}
+
+__global__ void scatter_accepted_kernel(const dp_patch *recs, int64_t n, int64_t nc, dp_patch *cand, uint8_t *ok)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t pos = recs[i].seq;
+    if ((int64_t)pos < nc) {
+        cand[pos] = recs[i];
+        ok[pos] = 1;
+    }
+}
+
+hipError_t launch_count_owners(const int32_t *owner, int64_t n, int world, unsigned long long *counts, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(unsigned long long) * (size_t)world, s);
+    if (e != hipSuccess || n <= 0)
+        return e;
+    const int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(count_owners_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s, owner,
+                       n, world, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_round_robin(int32_t *owner, int64_t n, int world, hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(round_robin_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, owner, n, world);
+    return hipGetLastError();
+}
+
+hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(iota_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, v, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact_accepted(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
+                                   const int64_t *items, int64_t n, int per, dp_patch *out, hipStream_t s)
+{
+    const int64_t m = n * per;
+    if (m <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(compact_accepted_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, cand, acc, prefix,
+                       items, m, per, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_accepted(const dp_patch *recs, int64_t n, int64_t nc, dp_patch *cand, uint8_t *ok,
+                                   hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(scatter_accepted_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recs, n, nc, cand,
+                       ok);
+    return hipGetLastError();
+}
+
 hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s)
 {
     if (n <= 0)

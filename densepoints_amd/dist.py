@@ -237,7 +237,97 @@ def densify_partitioned(eng, seeds_xyz, dist, device: torch.device | None = None
     return patches, stats
 
 
+class _DeviceBuffers:
+    """Device byte buffers reused across generations (grown by 25% when short)."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.bufs: dict[str, torch.Tensor] = {}
+
+    def get(self, name: str, nbytes: int) -> torch.Tensor:
+        t = self.bufs.get(name)
+        if t is None or t.numel() < nbytes:
+            n = max(int(nbytes), 1)
+            t = torch.empty(n + n // 4, dtype=torch.uint8, device=self.device)
+            self.bufs[name] = t
+        return t
+
+
 def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64):
+    """dp_densify with every generation partitioned by reference-view super-tile,
+    the records in HBM and only the ACCEPTED candidates exchanged (SURVEY 8e,
+    north star: "RCCL all-gather over xGMI of accepted patches").  Per
+    generation:
+      1. dp_densify_partition_device: owners (hash of the items' (ref, v/64,
+         u/64) super-tiles, round robin above 1.1x the mean share) and the
+         rank-major item order, on the device; the host reads `world` counts;
+      2. this rank refines its slice of that order (dp_densify_refine_items_device);
+      3. dp_densify_compact_accepted_device keeps the candidates whose filter
+         passed, each tagged with its generation position;
+      4. one all_gather_into_tensor of the accepted counts (8 B per rank) and
+         ONE of the padded accepted records (RCCL over xGMI on "nccl"; host-
+         staged on "gloo" for the one-device rehearsals);
+      5. dp_densify_commit_accepted_device scatters them to sequence order and
+         commits the replicated organizer step on every rank.
+    Device buffers are reused across generations.  Every rank's store equals
+    dp_densify bit for bit.  stats gains "partition" (items, largest share,
+    fallback), "accepted" and "gathered_bytes" per generation."""
+    rank = dist.get_rank() if dist is not None else 0
+    world = dist.get_world_size() if dist is not None else 1
+    rccl = dist is not None and dist.get_backend() == "nccl"
+    rec = PATCH_DTYPE.itemsize
+    stream = torch.cuda.current_stream(device)
+    pool = _DeviceBuffers(device)
+    gen = eng.densify_begin(seeds_xyz)
+    parts, gathered, accepted = [], [], []
+    while gen.items > 0:
+        per = gen.per_item
+        d_order, counts, fallback = eng.densify_partition_device(gen, world, tile_px)
+        offs = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+        mine = int(counts[rank])
+        d_items = d_order + 8 * int(offs[rank])
+        cap = max(mine * per, 1)
+        buf = pool.get("cand", cap * rec)
+        acc = pool.get("acc", cap)
+        comp = pool.get("comp", cap * rec)
+        nacc = 0
+        if mine:
+            eng.densify_refine_items_device(gen, d_items, mine, buf.data_ptr(), acc.data_ptr(), stream.cuda_stream)
+            nacc = eng.densify_compact_accepted_device(gen, d_items, mine, buf.data_ptr(), acc.data_ptr(),
+                                                       comp.data_ptr(), stream.cuda_stream)
+        if dist is None:
+            allr, total, gb = comp, nacc, nacc * rec
+        else:
+            cdev = device if rccl else torch.device("cpu")
+            cnt = torch.tensor([nacc], dtype=torch.int64, device=cdev)
+            all_cnt = torch.empty(world, dtype=torch.int64, device=cdev)
+            dist.all_gather_into_tensor(all_cnt, cnt)
+            ns = [int(x) for x in all_cnt.tolist()]
+            mx = max(max(ns), 1)
+            send = pool.get("send", mx * rec)[: mx * rec]
+            send[: nacc * rec].copy_(comp[: nacc * rec])
+            if rccl:
+                recv = pool.get("recv", world * mx * rec)[: world * mx * rec]
+                dist.all_gather_into_tensor(recv, send)
+            else:
+                recv = torch.empty(world * mx * rec, dtype=torch.uint8)
+                dist.all_gather_into_tensor(recv, send.cpu())
+                recv = recv.to(device)
+            allr = torch.cat([recv[r * mx * rec: r * mx * rec + ns[r] * rec] for r in range(world)])
+            total, gb = sum(ns), world * (mx * rec + 8)
+        parts.append((int(gen.items), int(counts.max()), bool(fallback)))
+        gathered.append(gb)
+        accepted.append(total)
+        gen = eng.densify_commit_accepted_device(gen, allr.data_ptr(), total, stream.cuda_stream)
+    patches, stats = eng.densify_result()
+    stats = _reduce_stats(stats, dist, device)
+    stats["partition"] = parts
+    stats["gathered_bytes"] = gathered
+    stats["accepted"] = accepted
+    return patches, stats
+
+
+def densify_partitioned_device_all(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64):
     """densify_partitioned with the records in HBM: per generation the owners
     (identical on every rank), this rank's item list to the device, one refine
     launch over it (dp_densify_refine_items_device), ONE all_gather_into_tensor

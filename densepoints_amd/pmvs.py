@@ -429,6 +429,33 @@ class Engine:
                                                        ctypes.c_void_p(stream) if stream else None))
         return gen
 
+    def densify_partition_device(self, gen: N.DpGeneration, world: int, tile_px: int = 64):
+        """(device address of the rank-major item order, items per rank (np.int64
+        array), round-robin fallback flag): dp_densify_partition_device."""
+        d_order = ctypes.c_void_p()
+        counts = np.zeros(world, dtype=np.int64)
+        fb = ctypes.c_int32()
+        self._check(lib.dp_densify_partition_device(self._ctx, ctypes.byref(gen), world, tile_px,
+                                                    ctypes.byref(d_order), ptr(counts), ctypes.byref(fb)))
+        return int(d_order.value or 0), counts, bool(fb.value)
+
+    def densify_compact_accepted_device(self, gen: N.DpGeneration, d_items: int, n: int, d_cand: int, d_accept: int,
+                                        d_out: int, stream: int | None = None) -> int:
+        """Accepted candidates of a rank's items into d_out (generation position in
+        seq); returns their count."""
+        cnt = ctypes.c_int64()
+        self._check(lib.dp_densify_compact_accepted_device(
+            self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_items), n, ctypes.c_void_p(d_cand),
+            ctypes.c_void_p(d_accept), ctypes.c_void_p(d_out), ctypes.byref(cnt),
+            ctypes.c_void_p(stream) if stream else None))
+        return int(cnt.value)
+
+    def densify_commit_accepted_device(self, gen: N.DpGeneration, d_recs: int, n: int,
+                                       stream: int | None = None) -> N.DpGeneration:
+        self._check(lib.dp_densify_commit_accepted_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_recs), n,
+                                                          ctypes.c_void_p(stream) if stream else None))
+        return gen
+
     def densify_result(self):
         out = ctypes.c_void_p()
         n = ctypes.c_int64()

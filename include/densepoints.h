@@ -262,6 +262,29 @@ int dp_densify_refine_items_device(dp_ctx *ctx, const dp_generation *gen, const 
                                    dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream);
 int dp_densify_commit_items_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_cand, const uint8_t *d_accept,
                                    const int64_t *d_items, int64_t n_items, void *stream);
+/* The same protocol with the partition on the device and only the accepted
+ * candidates exchanged (the records that can claim cells):
+ *  - dp_densify_partition_device: the owners of dp_densify_owners (same hash,
+ *    same round-robin fallback), the generation's items in rank-major order,
+ *    ascending within a rank (*d_order_out: context-owned device array, valid
+ *    until the next generation), items per rank in counts_out[world] (host);
+ *    world <= 64;
+ *  - each rank refines its slice d_order + offset with
+ *    dp_densify_refine_items_device, then dp_densify_compact_accepted_device
+ *    writes the candidates whose filter passed into d_out (capacity n *
+ *    per_item), each carrying its generation position (item * per_item +
+ *    direction) in `seq`, and the count in *n_out (host);
+ *  - after an all-gather of those records (any order),
+ *    dp_densify_commit_accepted_device commits the generation: every other
+ *    candidate counts as rejected by the filter (it claims nothing), so the
+ *    store equals dp_densify's bit for bit. */
+int dp_densify_partition_device(dp_ctx *ctx, const dp_generation *gen, int world, int tile_px,
+                                const int64_t **d_order_out, int64_t *counts_out, int32_t *fallback_out);
+int dp_densify_compact_accepted_device(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
+                                       const dp_patch *d_cand, const uint8_t *d_accept, dp_patch *d_out,
+                                       int64_t *n_out, void *stream);
+int dp_densify_commit_accepted_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_recs, int64_t n_recs,
+                                      void *stream);
 
 /* ---- patch filter ----------------------------------------
  * PMVS::FilterPatches is declared (methods/pmvs/pmvs.h:27) but never defined

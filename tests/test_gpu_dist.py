@@ -3,6 +3,7 @@ result) and its multi-rank driver (densepoints_amd.dist.densify_sharded):
 one rank equals dp_densify; two ranks (two processes sharing cuda:0, gloo
 all-gathers of host records) equal it too -- the replicated-claims design of
 SURVEY 8e, bit for bit."""
+import json
 import os
 import socket
 
@@ -94,7 +95,9 @@ def _worker_dev(rank, world, port, out_path, backend, partitioned=False):
     P, imgs, seeds = _scene("hf6")
     with dp.Engine(device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
-        if partitioned:
+        if partitioned == "all":
+            got, st = D.densify_partitioned_device_all(eng, seeds, group, torch.device("cuda", 0))
+        elif partitioned:
             got, st = D.densify_partitioned_device(eng, seeds, group, torch.device("cuda", 0))
         else:
             got, st = D.densify_sharded_device(eng, seeds, group, torch.device("cuda", 0))
@@ -124,13 +127,18 @@ def test_device_resident_sharded_densify(tmp_path, backend, world):
         assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
 
 
-@pytest.mark.parametrize("backend,world", [(None, 1), ("nccl", 1), ("gloo", 2), ("gloo", 3)])
-def test_partitioned_densify_device(tmp_path, backend, world):
-    """Reference-view super-tile partition of every generation
-    (dp_densify_owners -> dp_densify_refine_items_device -> all-gather ->
-    dp_densify_commit_items_device): every rank's store equals dp_densify."""
+@pytest.mark.parametrize("backend,world,variant", [(None, 1, "accepted"), ("nccl", 1, "accepted"),
+                                                  ("gloo", 2, "accepted"), ("gloo", 3, "accepted"),
+                                                  ("gloo", 2, "all")])
+def test_partitioned_densify_device(tmp_path, backend, world, variant):
+    """Reference-view super-tile partition of every generation: the device
+    partition, refine of the rank's items, all-gather of the ACCEPTED
+    candidates only and dp_densify_commit_accepted_device (variant
+    "accepted", dist.densify_partitioned_device), or of every candidate slot
+    with dp_densify_commit_items_device ("all"): every rank's store equals
+    dp_densify."""
     out = str(tmp_path / "dense")
-    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, True), nprocs=world, join=True)
+    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, variant), nprocs=world, join=True)
     P, imgs, seeds = _scene("hf6")
     with dp.Engine(device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
@@ -167,3 +175,55 @@ def test_owners_equal_oracle_and_host_path(orc, world):
         ref, _ = eng.densify(seeds)
         got, st = D.densify_partitioned(eng, seeds, None)
     assert got.tobytes() == ref.tobytes()
+
+
+def _worker_cfg4(rank, world, port, out_path, max_pops, nseeds):
+    import torch
+    import torch.distributed as tdist
+
+    from test_gpu_configs import DeviceScene, spread
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    with dp.Engine(dp.Options(max_pops=max_pops), device=0) as eng:
+        sc = DeviceScene("cfg4_64view_4k", eng, host_views=[])
+        seeds = spread(sc.seeds, nseeds)
+        for mode in ("parity", "fast"):
+            eng.set_fast_options(dp.FastOptions(densify=1 if mode == "fast" else 0))
+            got, st = D.densify_partitioned_device(eng, seeds, tdist, torch.device("cuda", 0))
+            np.save(out_path + f".{mode}.r{rank}.npy", got.view(np.uint8), allow_pickle=False)
+            with open(out_path + f".{mode}.r{rank}.json", "w") as f:
+                f.write(json.dumps({"evals": st["evals"], "partition": st["partition"],
+                                    "accepted": st["accepted"], "gathered": st["gathered_bytes"]}))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_partitioned_densify_cfg4_two_ranks(tmp_path):
+    """BASELINE config 4 (64 views 3840x2160) in the partitioned protocol: two
+    ranks sharing cuda:0 (gloo, spawned before any GPU call), each with the
+    scene rendered into its own HBM planes, densify 1,500 spread seeds with a
+    pop cap -- in parity and in performance mode -- and both ranks' stores
+    equal the single-process dp_densify byte for byte; the super-tile
+    partition splits the generations (not all round robin)."""
+    from test_gpu_configs import DeviceScene, spread
+
+    out = str(tmp_path / "cfg4")
+    max_pops, nseeds = 6000, 1500
+    mp.spawn(_worker_cfg4, args=(2, _free_port(), out, max_pops, nseeds), nprocs=2, join=True)
+    with dp.Engine(dp.Options(max_pops=max_pops), device=0) as eng:
+        sc = DeviceScene("cfg4_64view_4k", eng, host_views=[])
+        seeds = spread(sc.seeds, nseeds)
+        for mode in ("parity", "fast"):
+            eng.set_fast_options(dp.FastOptions(densify=1 if mode == "fast" else 0))
+            ref, rst = eng.densify(seeds)
+            assert rst["patches"] > 1000 and 0 < rst["pops"] <= max_pops
+            for r in range(2):
+                got = np.frombuffer(np.load(out + f".{mode}.r{r}.npy", allow_pickle=False).tobytes(),
+                                    dtype=PATCH_DTYPE)
+                assert got.tobytes() == ref.tobytes(), f"{mode} rank {r}"
+            st = json.loads(open(out + f".{mode}.r0.json").read())
+            assert st["evals"] == rst["evals"]
+            assert any(not fb for _, _, fb in st["partition"])
+            assert sum(st["accepted"]) >= rst["patches"]
