@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mpatches/sec through the fused NCC evaluate + refine +
-filter kernel (BASELINE.json metric) on the 32-view 4K synthetic scene
-(BASELINE config 3, the HBM-roofline run).
+filter kernel (BASELINE.json metric).
 
-One step = one batch of expansion candidates through the HIP kernel -- the
-reference's hot loop, Expand::ExpandPatch (methods/pmvs/expand.cpp:103-143):
-each parent patch spawns 4 children (+-x, +-y at 8 px in its reference view),
-each child is Nelder-Mead refined at n = 11 on the parent's visible set, then
-InitRelatedImages and the NCC filter run -- with inputs resident in HBM.
-Parents are the synthetic seeds after the reference's seed stage
-(Seed::FilterPatches + OptimizePatches at n = 16, run once untimed), so the
-children look exactly like the ones the BFS produces.
+N = 1 (the driver's plain `python bench.py`): the 32-view 4K synthetic scene
+(BASELINE config 3, the HBM-roofline run).  One step = one batch of expansion
+candidates through the HIP kernel -- the reference's hot loop,
+Expand::ExpandPatch (methods/pmvs/expand.cpp:103-143): each parent patch spawns
+4 children (+-x, +-y at 8 px in its reference view), each child is Nelder-Mead
+refined at n = 11 on the parent's visible set, then InitRelatedImages and the
+NCC filter run -- with inputs resident in HBM.  Parents are the synthetic seeds
+after the reference's seed stage (Seed::FilterPatches + OptimizePatches at
+n = 16, run once untimed), so the children look exactly like the ones the BFS
+produces.
 
-Multi-GPU (torchrun, one process per GPU): candidates are sharded by rank
-(weak scaling, per-rank batch fixed); patches are independent, so there is no
-data-path collective -- barrier + max-over-ranks timing only.
+N > 1 (torchrun, one process per GPU, RCCL over xGMI): BASELINE config 4 (64
+views 4K, "reference-cell shard across 8 x MI355X with RCCL all-gather of
+accepted patches").  One step = one whole densify (PMVS::Run minus matching,
+pmvs.cpp:22-43) with every BFS generation partitioned by reference-view
+super-tile over the ranks (dist.densify_partitioned_device: device partition,
+refine of the rank's items, ONE RCCL all-gather of the accepted candidates,
+replicated organizer commit); the value is every candidate refined (seed
+stage + expansions) over the max-over-ranks wall time -- strong scaling, the
+same densify at every N.  The weak-scaled refine batch is reported beside it.
 
 Prints ONE JSON line (rank 0).
 """
@@ -25,6 +32,7 @@ import json
 import os
 import sys
 import time
+import zlib
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -38,7 +46,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="cfg3_32view_4k")
+    ap.add_argument("--config", default=None, help="default: cfg3_32view_4k at N = 1, cfg4_64view_4k at N > 1")
+    ap.add_argument("--densify-steps", type=int, default=2,
+                    help="N = 1: partitioned-densify repetitions of the informational config-4 leg")
     ap.add_argument("--batch", type=int, default=262144, help="expansion candidates per step per GPU")
     ap.add_argument("--cell", type=int, default=11)
     ap.add_argument("--cpu-parents", type=int, default=5000,
@@ -72,6 +82,8 @@ def main():
     from densepoints_amd import synth
 
     rank, world, local = D.env()
+    if args.config is None:
+        args.config = "cfg3_32view_4k" if world == 1 else "cfg4_64view_4k"
     # rehearsal knobs for a 1-GPU box (never set by the driver): DP_BENCH_BACKEND=gloo
     # and DP_BENCH_ONE_DEVICE=1 run N ranks on cuda:0 over gloo
     if os.environ.get("DP_BENCH_ONE_DEVICE") == "1":
@@ -240,63 +252,52 @@ def main():
     if rank == 0 and not args.no_densify and not fast:
         # informational: the full PMVS::Run minus matching (dp_densify) on the same scene, untimed by the contract
         t0 = time.perf_counter()
-        _, dst = eng.densify(seeds)
+        dpat, dst = eng.densify(seeds)
         wall = time.perf_counter() - t0
         result["densify_e2e"] = {"seeds": int(dst["seeds_in"]), "seed_patches": int(dst["seed_patches"]),
-                                 "patches": int(dst["patches"]), "candidates": int(dst["candidates"]),
+                                 "patches": int(dst["patches"]), "store_crc32": f"{zlib.crc32(dpat.tobytes()):08x}", "candidates": int(dst["candidates"]),
                                  "generations": int(dst["generations"]), "evals": int(dst["evals"]),
                                  "refine_ms": round(dst["refine_ms"], 1), "wall_s": round(wall, 3)}
         # informational: the same densify with the performance-mode refine
         # (dp_fast_options.densify: seed stage at n = 16 and expansions at n = 11)
         eng.set_fast_options(dp.FastOptions(densify=1))
         t0 = time.perf_counter()
-        _, fst = eng.densify(seeds)
+        fpat, fst = eng.densify(seeds)
         wall = time.perf_counter() - t0
         eng.set_fast_options(dp.FastOptions())
         result["densify_e2e_fast"] = {"seed_patches": int(fst["seed_patches"]), "patches": int(fst["patches"]),
+                                      "store_crc32": f"{zlib.crc32(fpat.tobytes()):08x}",
                                       "candidates": int(fst["candidates"]), "generations": int(fst["generations"]),
                                       "evals": int(fst["evals"]), "refine_ms": round(fst["refine_ms"], 1),
                                       "wall_s": round(wall, 3),
                                       "Mpatches_per_s_refine": round(int(fst["candidates"]) / max(fst["refine_ms"], 1e-9)
                                                                      / 1e3, 3)}
-    if world > 1 and not args.no_densify and not fast:
-        # informational: the same densify with every generation partitioned by
-        # reference-view super-tile over the ranks (north star): each
-        # rank refines its tiles' items into HBM, the candidate shards are
-        # all-gathered over RCCL (all_gather_into_tensor), every rank commits
-        # the replicated organizer step in sequence order
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        _, sst = D.densify_partitioned_device(eng, seeds, dist, torch.device("cuda", local))
-        torch.cuda.synchronize()
-        wall = D.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
-        parts = sst["partition"]
-        result["densify_partitioned"] = {
-            "ranks": world, "patches": int(sst["patches"]), "generations": int(sst["generations"]),
-            "evals": int(sst["evals"]), "refine_ms_max_rank": round(sst["refine_ms"], 1), "wall_s": round(wall, 3),
-            "Mpatches_per_s": round(int(sst["candidates"]) / wall / 1e6, 3),
-            "gathered_MB_total": round(sum(sst["gathered_bytes"]) / 1e6, 2),
-            "gathered_MB_max_generation": round(max(sst["gathered_bytes"]) / 1e6, 2),
-            "tile_partitioned_generations": sum(1 for _, _, fb in parts if not fb),
-            "round_robin_generations": sum(1 for _, _, fb in parts if fb),
-            "max_share_vs_mean": round(max((mx * world / it) for it, mx, _ in parts if it > 0), 3),
-            "collective": f"all_gather_into_tensor ({'RCCL' if backend == 'nccl' else backend}) of 80-B candidate "
-                          "records + accept flags"}
-        # the same partitioned densify with the performance-mode refine (dp_fast_options.densify)
-        eng.set_fast_options(dp.FastOptions(densify=1))
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        _, fst = D.densify_partitioned_device(eng, seeds, dist, torch.device("cuda", local))
-        torch.cuda.synchronize()
-        wall = D.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
+    if world > 1:
+        # the N > 1 headline: the whole densify on this scene partitioned over the
+        # ranks (strong scaling); the refine batch above becomes the weak-scaled
+        # informational leg
+        dev = torch.device("cuda", local)
+        legs = {m: partitioned_leg(eng, seeds, dist, coll_dev, dev, args.steps, args.warmup, m == "fast")
+                for m in ("parity", "fast")}
+        result["refine_weak_scaled"] = {k: result[k] for k in ("value", "ms_per_step", "kernel_ms_per_launch",
+                                                               "kernel_ms_events", "E_mean_evals_per_patch")}
+        result["refine_weak_scaled"]["note"] = ("per-rank batch of %d expansion candidates, no data-path collective"
+                                                % B)
+        head = legs["parity"]
+        result["value"] = head["Mpatches_per_s"]
+        result["ms_per_step"] = head["ms_per_densify"]
+        result["scaling"] = "strong"
+        result["config"]["workload"] = (
+            f"{args.config}: {V} views {W}x{H}, one step = the whole densify (PMVS::Run minus matching) of "
+            f"{len(seeds)} seed points, every BFS generation partitioned by reference-view super-tile over "
+            f"{world} ranks (RCCL all-gather of the accepted candidates), parity-mode refine (Nelder-Mead, "
+            f"n = 16 seed stage / n = {args.cell} expansions)")
+        result["config"]["parallelism"] = f"dp{world} (reference-view super-tiles, all-gather of accepted patches)"
+        result["densify_partitioned"] = head
+        result["densify_partitioned_fast"] = legs["fast"]
         eng.set_fast_options(dp.FastOptions())
-        result["densify_partitioned_fast"] = {
-            "ranks": world, "patches": int(fst["patches"]), "generations": int(fst["generations"]),
-            "refine_ms_max_rank": round(fst["refine_ms"], 1), "wall_s": round(wall, 3),
-            "Mpatches_per_s": round(int(fst["candidates"]) / wall / 1e6, 3),
-            "gathered_MB_total": round(sum(fst["gathered_bytes"]) / 1e6, 2)}
+    if world == 1 and not args.no_densify and not fast:
+        result["densify_partitioned_cfg4_1gpu"] = cfg4_densify_1gpu(args, stream)
     if rank == 0 and not args.no_seeds:
         result["seed_generation"] = seed_generation(eng, args)
     st = np.zeros(8, dtype=np.uint64)
@@ -325,13 +326,96 @@ def main():
                 result["roofline"]["traffic_calibration"] = t["calibration"]
 
     if rank == 0 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out, fast)
+        result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out, fo if fast else None)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
     eng.close()
+
+
+def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
+    """`steps` whole densifies with every generation partitioned over the ranks
+    (dist.densify_partitioned_device), after `warmup` untimed ones, bracketed by
+    barrier + synchronize; rate = candidates refined (seed stage + expansions)
+    per max-over-ranks second."""
+    import densepoints_amd as dp
+    from densepoints_amd import dist as D
+
+    eng.set_fast_options(dp.FastOptions(densify=1 if fast else 0))
+    for _ in range(warmup):
+        D.densify_partitioned_device(eng, seeds, dist, dev)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        got, st = D.densify_partitioned_device(eng, seeds, dist, dev)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = D.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
+    eng.set_fast_options(dp.FastOptions())
+    world = dist.get_world_size() if dist else 1
+    # every rank's replicated store must be the same bytes (checked after the timed region)
+    crc = zlib.crc32(got.tobytes())
+    crcs = [crc]
+    if dist:
+        t = torch.tensor([crc], dtype=torch.int64, device=coll_dev)
+        allt = torch.empty(world, dtype=torch.int64, device=coll_dev)
+        dist.all_gather_into_tensor(allt, t)
+        crcs = [int(x) for x in allt.tolist()]
+    cands = int(st["seeds_in"]) + int(st["candidates"])
+    parts = st["partition"]
+    gb = st["gathered_bytes"]
+    return {"ranks": world, "mode": "performance" if fast else "parity", "steps": steps,
+            "Mpatches_per_s": round(steps * cands / wall / 1e6, 4), "ms_per_densify": round(wall / steps * 1e3, 3),
+            "candidates_per_densify": cands, "patches": int(st["patches"]), "seed_patches": int(st["seed_patches"]),
+            "store_crc32": f"{crc:08x}", "ranks_store_equal": len(set(crcs)) == 1,
+            "generations": int(st["generations"]), "evals": int(st["evals"]),
+            "refine_ms_max_rank": round(st["refine_ms"], 1),
+            "accepted_exchanged": int(sum(st["accepted"])),
+            "gathered_MB_total": round(sum(gb) / 1e6, 3), "gathered_MB_max_generation": round(max(gb) / 1e6, 3),
+            "gathered_MB_per_generation_mean": round(sum(gb) / len(gb) / 1e6, 4),
+            "tile_partitioned_generations": sum(1 for _, _, fb in parts if not fb),
+            "round_robin_generations": sum(1 for _, _, fb in parts if fb),
+            "max_share_vs_mean": round(max((mx * world / it) for it, mx, _ in parts if it > 0), 3),
+            "collective": "all_gather_into_tensor of the accepted candidates' 80-B records (+ 8-B counts), " +
+                          ("RCCL over xGMI" if dist is not None and dist.get_backend() == "nccl" else
+                           "none (one rank)" if dist is None else dist.get_backend())}
+
+
+def cfg4_densify_1gpu(args, stream):
+    """Informational at N = 1: the N > 1 headline's workload (BASELINE config 4,
+    whole partitioned densify, both refine modes) on one rank, so the 1-GPU
+    point of that curve is in the 1-GPU line."""
+    import ctypes
+
+    import densepoints_amd as dp
+    from densepoints_amd import _native as N
+    from densepoints_amd import synth
+
+    cfg = synth.named("cfg4_64view_4k")
+    P = synth.cameras(cfg)
+    V, W, H = cfg.n_views, cfg.width, cfg.height
+    with dp.Engine(dp.Options(expand_cell_size=args.cell), device=torch.cuda.current_device()) as eng:
+        planes = torch.empty((V, H, W), dtype=torch.int32, device="cuda")
+        for v in range(V):
+            N.check(N.lib.dp_synth_render_device(eng.handle, ctypes.byref(cfg), N.ptr(P), v, planes[v].data_ptr(),
+                                                 stream.cuda_stream), eng.handle)
+        torch.cuda.synchronize()
+        eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
+        seeds = synth.seeds(cfg, P)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        out = {m: partitioned_leg(eng, seeds, None, None, dev, args.densify_steps, 1, m == "fast")
+               for m in ("parity", "fast")}
+        out["workload"] = (f"cfg4_64view_4k: {V} views {W}x{H}, whole densify of {len(seeds)} seed points, "
+                           "one rank (the N > 1 headline's workload)")
+        del planes
+    return out
 
 
 def seed_generation(eng, args):
@@ -585,7 +669,7 @@ def host_cores():
     return n
 
 
-def cpu_baseline(args, cfg, P, planes, parents, gpu_out, fast=False):
+def cpu_baseline(args, cfg, P, planes, parents, gpu_out, fo=None):
     """The oracle (CPU restatement, test infrastructure) on a FIXED sample --
     the first --cpu-parents parents (4x as many candidates) of the same batch --
     timed on all of this host's usable cores and on one thread (SURVEY 8d CPU
@@ -601,7 +685,9 @@ def cpu_baseline(args, cfg, P, planes, parents, gpu_out, fast=False):
     S = orc.Scene(P, imgs, dp.Options(expand_cell_size=args.cell))
     cores = args.cpu_threads or host_cores()
     n = min(args.cpu_parents, len(parents))
-    expand = (lambda par, th: S.fast_expand(par, None, th)) if fast else S.expand
+    fast = fo is not None
+    # the performance mode's spec with the SAME options as the GPU run
+    expand = (lambda par, th: S.fast_expand(par, fo, th)) if fast else S.expand
     t0 = time.perf_counter()
     kids, acc = expand(parents[:n], cores)
     t = time.perf_counter() - t0

@@ -1430,6 +1430,9 @@ extern "C" int dp_densify_partition_device(dp_ctx *c, const dp_generation *gen, 
     DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
     DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->scan_tmp.p, tmp, kin, kout, c->oiota.p, c->porder.p, (int)n, 0,
                                                  bits, s));
+    // the order is read on the caller's stream (refine, compaction): complete it
+    // before returning, like the counts
+    DP_HIP(c, hipStreamSynchronize(s));
     for (int r = 0; r < world; ++r)
         counts_out[r] = cnt[(size_t)r];
     *d_order_out = c->porder.p;

@@ -267,8 +267,8 @@ int dp_densify_commit_items_device(dp_ctx *ctx, dp_generation *gen, const dp_pat
  *  - dp_densify_partition_device: the owners of dp_densify_owners (same hash,
  *    same round-robin fallback), the generation's items in rank-major order,
  *    ascending within a rank (*d_order_out: context-owned device array, valid
- *    until the next generation), items per rank in counts_out[world] (host);
- *    world <= 64;
+ *    until the next generation, complete on return so any stream may read
+ *    it), items per rank in counts_out[world] (host); world <= 64;
  *  - each rank refines its slice d_order + offset with
  *    dp_densify_refine_items_device, then dp_densify_compact_accepted_device
  *    writes the candidates whose filter passed into d_out (capacity n *

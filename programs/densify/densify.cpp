@@ -357,15 +357,28 @@ int main(int argc, char **argv)
             // contexts 1..N-1 on the next devices (wrapping: several ranks may share a GPU)
             const int ndev = dp_device_count();
             std::vector<dp_ctx *> ctxs{ctx};
+            // a failure on a secondary context reports THAT context's error and
+            // releases every context created so far before exiting
+            auto check_g = [&](int rc, dp_ctx *cg, const char *what) {
+                if (rc == DP_OK)
+                    return;
+                std::fprintf(stderr, "densify: %s failed on context %zu (%d): %s\n", what, ctxs.size(), rc,
+                             cg ? dp_last_error(cg) : "context not created");
+                if (cg && (ctxs.empty() || ctxs.back() != cg))
+                    dp_ctx_destroy(cg);
+                for (dp_ctx *x : ctxs)
+                    dp_ctx_destroy(x);
+                std::exit(1);
+            };
             for (int g = 1; g < gpus; ++g) {
                 dp_ctx *cg = nullptr;
-                check(dp_ctx_create(&opt, (device + g) % (ndev > 0 ? ndev : 1), &cg), "dp_ctx_create");
+                check_g(dp_ctx_create(&opt, (device + g) % (ndev > 0 ? ndev : 1), &cg), cg, "dp_ctx_create");
                 ctxs.push_back(cg);
-                check(dp_set_views(cg, (int)imgs.size(), P.data(), dimg.data()), "dp_set_views");
-                check(dp_set_fast_options(cg, &fo), "dp_set_fast_options");
+                check_g(dp_set_views(cg, (int)imgs.size(), P.data(), dimg.data()), cg, "dp_set_views");
+                check_g(dp_set_fast_options(cg, &fo), cg, "dp_set_fast_options");
                 if (level > 0) {
-                    check(dp_build_pyramid(cg, level + 1), "dp_build_pyramid");
-                    check(dp_set_level(cg, level), "dp_set_level");
+                    check_g(dp_build_pyramid(cg, level + 1), cg, "dp_build_pyramid");
+                    check_g(dp_set_level(cg, level), cg, "dp_set_level");
                 }
             }
             std::string err;

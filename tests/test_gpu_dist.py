@@ -185,6 +185,9 @@ def _worker_cfg4(rank, world, port, out_path, max_pops, nseeds):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
+    # a real (non-NULL) caller stream like bench.py's: the library's own stream and
+    # the caller's must be ordered by the ABI, not by sharing the legacy stream
+    torch.cuda.set_stream(torch.cuda.Stream())
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     with dp.Engine(dp.Options(max_pops=max_pops), device=0) as eng:
         sc = DeviceScene("cfg4_64view_4k", eng, host_views=[])
