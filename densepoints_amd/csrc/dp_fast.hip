@@ -129,6 +129,7 @@ template <int kArena> struct FastLds {
     dp_patch par;      // parent of the current chunk (expansion)
     float cpos[4][3];  // its four children's centres
     uint8_t vlist[64];
+    float2 slast[64];  // each lane's last sample slot (i, j): Slots
 #ifdef DP_FAST_TIMING
     unsigned long long tm[16], tlast;
 #endif
@@ -150,6 +151,11 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p)
+{
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char *)p;
 }
 
 __device__ __forceinline__ int lane_id()
@@ -492,16 +498,24 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
 // gives each view LP = 64/G lanes x S slots; with kTail the last sample of
 // every view (N = S LP + 1, e.g. 7 x 7 = 3 x 16 + 1) is taken by one extra
 // round over the views instead of a fourth, nearly empty slot per pass.
+// A lane's sample positions (i, j) per slot, in registers -- except, in the
+// masked instances (kMask: the last slot has dead lanes), the last slot's, which
+// lives in the wave's LDS block (FastLds::slast) and is re-read by every pass:
+// two fewer VGPRs live across the refine kept the n = 11 instance out of scratch
+// (the unmasked n = 7 instance is 2.5% faster with them in registers).  The
+// last slot's lane mask is a wave-uniform 64-bit SGPR mask (fast_dispatch picks
+// the smallest S, so only the last slot can have dead lanes).
 struct Slots {
     float ti[kFastSlots], tj[kFastSlots];
-    uint32_t live[kFastSlots];
+    uint64_t live_last;
     float tail;  // (i, j) of the tail sample: n - 1 - c on both axes
 };
 
-template <int G, int S> __device__ Slots make_slots(int cell)
+template <int G, int S, bool kMask, int kArena> __device__ Slots make_slots(FastLds<kArena> &L, int cell)
 {
     constexpr int LP = 64 / G;
-    const int g = lane_id() & (LP - 1);
+    const int lane = lane_id();
+    const int g = lane & (LP - 1);
     const int N = cell * cell;
     const float c = 0.5f * (float)(cell - 1);
     Slots s;
@@ -511,12 +525,25 @@ template <int G, int S> __device__ Slots make_slots(int cell)
         const bool live = t < N;
         const int te = live ? t : N - 1;
         const int jj = te / cell, ii = te - jj * cell;
-        s.ti[k] = (float)ii - c;
-        s.tj[k] = (float)jj - c;
-        s.live[k] = live ? 0xffffffffu : 0u;
+        if (kMask && k == S - 1) {
+            L.slast[lane] = make_float2((float)ii - c, (float)jj - c);
+            s.live_last = __ballot(live);
+        } else {
+            s.ti[k] = (float)ii - c;
+            s.tj[k] = (float)jj - c;
+        }
     }
     s.tail = (float)(cell - 1) - c;
+    wave_sync();
     return s;
+}
+
+// v ? x : 0 per lane of a wave-uniform lane mask (one v_cndmask on the SGPR pair)
+__device__ __forceinline__ uint32_t lane_select(uint64_t mask, uint32_t x)
+{
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(mask));
+    return r;
 }
 
 // One view's sample in 1/16 gray levels (or_fast.c fast_sample), in three
@@ -671,10 +698,22 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             const EvalRec &E = *(const EvalRec *)((const char *)L.e.par + (act ? (uint32_t)i * 48u : 0u));
             const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
             const uint32_t off = __float_as_uint(qc.w), rowb = __float_as_uint(qa.z);
+            // kMask: the last slot's (i, j) by an LDS read per pass through an
+            // opaque address, so that it is not hoisted into registers again
+            float tl_i = 0.0f, tl_j = 0.0f;
+            if (kMask) {
+                uint32_t slot_a = lds_addr(&L.slast[0]) + ((uint32_t)lane << 3);
+                asm volatile("" : "+v"(slot_a));
+                const __attribute__((address_space(3))) float *slp =
+                    (const __attribute__((address_space(3))) float *)(uintptr_t)slot_a;
+                tl_i = slp[0];
+                tl_j = slp[1];
+            }
             Tap tp[NS], tt{};
 #pragma unroll
             for (int s2 = 0; s2 < NS; ++s2)
-                tp[s2] = tap_addr(qa, qb, qc, off, rowb, sl.ti[s2], sl.tj[s2]);
+                tp[s2] = (kMask && s2 == NS - 1) ? tap_addr(qa, qb, qc, off, rowb, tl_i, tl_j)
+                                                 : tap_addr(qa, qb, qc, off, rowb, sl.ti[s2], sl.tj[s2]);
             if (tail) {
                 const EvalRec &T = L.e.par[lane < Q ? lane : 0];
                 const float4 ta = T.q[0], tb = T.q[1], tc = T.q[2];
@@ -691,7 +730,8 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             uint32_t b[NS];
 #pragma unroll
             for (int s2 = 0; s2 < NS; ++s2)
-                b[s2] = kMask ? (tap_blend(tp[s2], tw[s2]) & sl.live[s2]) : tap_blend(tp[s2], tw[s2]);
+                b[s2] = (kMask && s2 == NS - 1) ? lane_select(sl.live_last, tap_blend(tp[s2], tw[s2]))
+                                                : tap_blend(tp[s2], tw[s2]);
             if (tail)
                 bt = tap_blend(tt, twt);
             if (p == 0) {
@@ -1018,7 +1058,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
 {
     __shared__ FastLds<kArena> L;
     const int lane = lane_id();
-    const Slots sl = make_slots<G, NS>(a.cell);
+    const Slots sl = make_slots<G, NS, kMask>(L, a.cell);
     unsigned long long wave_evals = 0, wave_vev = 0, wave_bytes = 0, wave_patches = 0, wave_clip = 0;
     dp_patch &p = L.p;
     // work is dequeued in chunks of 4 (one atomic per chunk): the 4 children of

@@ -454,7 +454,10 @@ typedef struct dp_fast_options {
 void dp_default_fast_options(dp_fast_options *fo);
 int dp_set_fast_options(dp_ctx *ctx, const dp_fast_options *fo);
 /* fp16 gray planes of the current level for every view (built on demand by
- * the first fast call; explicit here so callers can time it). */
+ * the first fast call; explicit here so callers can time it).  The cached
+ * planes follow dp_set_views*, dp_build_pyramid and dp_set_level only: a
+ * caller that rewrites its dp_set_views_device planes in place must call
+ * dp_build_gray again (it always rebuilds, after draining the device). */
 int dp_build_gray(dp_ctx *ctx);
 /* host copy (width*height fp16 values) of view `view`'s gray plane; the
  * planes hold 1024 + gray (biased fp16: the bits are 0x6400 | gray, so the
