@@ -230,3 +230,52 @@ def test_partitioned_densify_cfg4_two_ranks(tmp_path):
             assert st["evals"] == rst["evals"]
             assert any(not fb for _, _, fb in st["partition"])
             assert sum(st["accepted"]) >= rst["patches"]
+
+
+def _worker_cfg5(rank, world, port, out_path, max_pops, nseeds):
+    import torch
+    import torch.distributed as tdist
+
+    from test_gpu_configs import DeviceScene, spread
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    with dp.Engine(dp.Options(max_pops=max_pops, expand_cell_size=11), device=0) as eng:
+        sc = DeviceScene("cfg5_128view_8k", eng, host_views=[])
+        seeds = spread(sc.seeds, nseeds)
+        eng.set_fast_options(dp.FastOptions(densify=1))
+        got, st = D.densify_partitioned_device(eng, seeds, tdist, torch.device("cuda", 0))
+        np.save(out_path + f".r{rank}.npy", got.view(np.uint8), allow_pickle=False)
+        with open(out_path + f".r{rank}.json", "w") as f:
+            f.write(json.dumps({"evals": st["evals"], "partition": st["partition"], "accepted": st["accepted"]}))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_partitioned_densify_cfg5_two_ranks(tmp_path):
+    """BASELINE config 5 (128 views 7680x4320, fp16 gray planes, 11x11 window)
+    in the partitioned protocol: two ranks sharing cuda:0 (gloo, spawned before
+    any GPU call), each holding the whole scene in its own HBM (17 GB of BGRA8
+    levels + 8.5 GB of gray planes per rank), densify 1,200 spread seeds in
+    performance mode with a pop cap; both ranks' stores equal the
+    single-process dp_densify byte for byte and the super-tile partition splits
+    the generations."""
+    from test_gpu_configs import DeviceScene, spread
+
+    out = str(tmp_path / "cfg5")
+    max_pops, nseeds = 5000, 1200
+    mp.spawn(_worker_cfg5, args=(2, _free_port(), out, max_pops, nseeds), nprocs=2, join=True)
+    with dp.Engine(dp.Options(max_pops=max_pops, expand_cell_size=11), device=0) as eng:
+        sc = DeviceScene("cfg5_128view_8k", eng, host_views=[])
+        seeds = spread(sc.seeds, nseeds)
+        eng.set_fast_options(dp.FastOptions(densify=1))
+        ref, rst = eng.densify(seeds)
+    assert rst["patches"] > 1000 and 0 < rst["pops"] <= max_pops
+    for r in range(2):
+        got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
+        assert got.tobytes() == ref.tobytes(), f"rank {r}"
+    st = json.loads(open(out + ".r0.json").read())
+    assert st["evals"] == rst["evals"]
+    assert any(not fb for _, _, fb in st["partition"])
