@@ -246,10 +246,13 @@ def main():
         result["fast_stats"] = {k: int(v) for k, v in fst.items()}
         result["roofline"]["bytes_per_launch_compulsory"] = float(fst["staged_bytes"] + 128 * B)
         result["quality"] = quality(cfg, out, acc)
-    if rank == 0 and not fast and not args.no_fast:
+    # the informational legs and the CPU baseline run at N = 1 only (at N > 1 the
+    # partitioned densify legs below are the report)
+    solo = world == 1
+    if solo and not fast and not args.no_fast:
         result["perf_mode"] = perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, out, acc, parents, P,
                                         planes, raw_seed_p)
-    if rank == 0 and not args.no_densify and not fast:
+    if solo and not args.no_densify and not fast:
         # informational: the full PMVS::Run minus matching (dp_densify) on the same scene, untimed by the contract
         t0 = time.perf_counter()
         dpat, dst = eng.densify(seeds)
@@ -298,7 +301,7 @@ def main():
         eng.set_fast_options(dp.FastOptions())
     if world == 1 and not args.no_densify and not fast:
         result["densify_partitioned_cfg4_1gpu"] = cfg4_densify_1gpu(args, stream)
-    if rank == 0 and not args.no_seeds:
+    if solo and not args.no_seeds:
         result["seed_generation"] = seed_generation(eng, args)
     st = np.zeros(8, dtype=np.uint64)
     if N.lib.dp_debug_stamps(N.ptr(st)) == 0:  # -DDP_STAMPS diagnostic builds only
@@ -325,7 +328,7 @@ def main():
             if t.get("calibration"):
                 result["roofline"]["traffic_calibration"] = t["calibration"]
 
-    if rank == 0 and not args.no_cpu:
+    if solo and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out, fo if fast else None)
     if rank == 0:
         print(json.dumps(result), flush=True)
