@@ -41,11 +41,13 @@ DP_HD void cross3(const double *a, const double *b, double *o)
 }
 
 // a / b and sqrt(a) of the per-evaluation uniform math (NCC finish, window
-// scale).  DP_FAST_DIV=1 routes them through the fp32-seeded dp_devmath.h
-// div_rn / sqrt_rn (no slow f64 transcendental); measured neutral within
-// noise, so the default keeps the library's IEEE sequences.
+// scale, means).  DP_FAST_DIV=1 (the default since r03: +0.9% on the parity
+// headline, 3.493 vs 3.462 Mpatches/s over three alternations on one box)
+// routes them through the fp32-seeded dp_devmath.h div_rn / sqrt_rn (no slow
+// f64 transcendental; the exactness caveat of DESIGN.md, checked bitwise on
+// the GPU); DP_FAST_DIV=0 keeps the library's IEEE sequences.
 #ifndef DP_FAST_DIV
-#define DP_FAST_DIV 0
+#define DP_FAST_DIV 1
 #endif
 DP_HD double dvdiv(double a, double b)
 {

@@ -699,6 +699,10 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
 #if DP_PRELOAD_VIEWS
     const MapView mv0 = load_map_view(a, L, 0, m, 0);
 #endif
+#ifdef DP_DIAG_CORNER_REPEAT
+    // diagnostic build (timing only): the idempotent corner block runs twice
+    for (int rep = 0; rep < 2; ++rep)
+#endif
     {
         double c12[12];
         const double Xs[3] = {L.X[0], L.X[1], L.X[2]};
@@ -728,6 +732,10 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
     for (int base = 0; base < m; base += kMapChunk) {
         // window maps of this chunk, 16 views per round (4 lanes per view)
         uint64_t okmask = 0;
+#ifdef DP_DIAG_MAP_REPEAT
+        // diagnostic build (timing only): the idempotent map build runs twice
+        for (int rep = 0; rep < 2; ++rep, okmask = rep < 2 ? 0 : okmask)
+#endif
         for (int r0 = 0; r0 < kMapChunk && base + r0 < m; r0 += 16)
 #if DP_PRELOAD_VIEWS
             okmask |= build_maps_quad((base == 0 && r0 == 0) ? mv0 : load_map_view(a, L, base, m, r0), L, base, m,
@@ -748,10 +756,28 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
                                        ~((1ull << (kb - base)) - 1ull));
         const bool anc = base == 0 && va;
         views_all<G>(a, L, td, base, todo, anc, Sa, Saa);
+#ifdef DP_DIAG_PASS_REPEAT
+        // diagnostic build (timing only): the idempotent view passes run twice
+        views_all<G>(a, L, td, base, todo, anc, Sa, Saa);
+#endif
         STAMP(L, 1);
         wave_sync();
         STAMP(L, 2);
         // NCC finish, one lane per view of the chunk (error_measurements.cpp:47-59)
+#ifdef DP_DIAG_NCC_REPEAT
+        // diagnostic build (timing only): the idempotent NCC finish runs twice
+        for (int rep = 0; rep < 2; ++rep) {
+            const int kr = base + lane;
+            if (kr >= kb && kr < ke) {
+                double sc = -1.0;
+                if ((valid >> lane) & 1ull)
+                    sc = dpg::ncc_finish(N, Sa, Saa, L.mom[lane][0], L.mom[lane][1], L.mom[lane][2],
+                                         a.opt.ncc_denom_min);
+                L.score[kr - 1] = sc;
+            }
+            wave_sync();
+        }
+#endif
         const int k = base + lane;
         if (k >= kb && k < ke) {
             double sc = -1.0;
