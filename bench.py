@@ -371,6 +371,16 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
         allt = torch.empty(world, dtype=torch.int64, device=coll_dev)
         dist.all_gather_into_tensor(allt, t)
         crcs = [int(x) for x in allt.tolist()]
+    # the visibility filter after the last generation (PMVS::FilterPatches,
+    # pmvs.h:27, spec in densepoints.h): the store is replicated, so rank 0
+    # filters it (informational, outside the timed region)
+    vf = None
+    if not dist or dist.get_rank() == 0:
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
+        keep = eng.filter_patches(np.ascontiguousarray(got))
+        vf = {"patches_in": int(len(got)), "kept": int(keep.sum()),
+              "ms_wall_host_arrays": round((time.perf_counter() - tf) * 1e3, 2)}
     cands = int(st["seeds_in"]) + int(st["candidates"])
     parts = st["partition"]
     gb = st["gathered_bytes"]
@@ -388,7 +398,8 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
             "max_share_vs_mean": round(max((mx * world / it) for it, mx, _ in parts if it > 0), 3),
             "collective": "all_gather_into_tensor of the accepted candidates' 80-B records (+ 8-B counts), " +
                           ("RCCL over xGMI" if dist is not None and dist.get_backend() == "nccl" else
-                           "none (one rank)" if dist is None else dist.get_backend())}
+                           "none (one rank)" if dist is None else dist.get_backend()),
+            "visibility_filter": vf}
 
 
 def cfg4_densify_1gpu(args, stream):
