@@ -864,41 +864,51 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
     C.alpha = a.fo.ls_step;
     C.ggp = 0.0f;
     int E = 0, it = 0, phase = kStart;
+    bool reuse_g = false; // both probes failed: x and f(x) unchanged, so the
+                          // forward differences would repeat the last gradient
     const uint32_t rm = pose_major_rm(m);
     for (;;) {
-        int K = 1;
-        if (phase == kStart || phase == kFd) {
-            // f(x) (start only), then f(x + h e_i), i = 0, 1, 2
-            const int k0 = phase == kStart ? 1 : 0;
-            if (phase == kStart)
-                set_pose(L, 0, C.x[0], C.x[1], C.x[2]);
-            K = phase == kStart ? (a.fo.iters > 0 ? 4 : 1) : 3;
-            if (K > 1) {
-                set_pose(L, k0 + 0, C.x[0] + h, C.x[1], C.x[2]);
-                set_pose(L, k0 + 1, C.x[0], C.x[1] + h, C.x[2]);
-                set_pose(L, k0 + 2, C.x[0], C.x[1], C.x[2] + h);
+        const bool fd_round = phase == kStart || phase == kFd;
+        if (!(fd_round && reuse_g)) {
+            int K = 1;
+            if (fd_round) {
+                // f(x) (start only), then f(x + h e_i), i = 0, 1, 2
+                const int k0 = phase == kStart ? 1 : 0;
+                if (phase == kStart)
+                    set_pose(L, 0, C.x[0], C.x[1], C.x[2]);
+                K = phase == kStart ? (a.fo.iters > 0 ? 4 : 1) : 3;
+                if (K > 1) {
+                    set_pose(L, k0 + 0, C.x[0] + h, C.x[1], C.x[2]);
+                    set_pose(L, k0 + 1, C.x[0], C.x[1] + h, C.x[2]);
+                    set_pose(L, k0 + 2, C.x[0], C.x[1], C.x[2] + h);
+                }
+            } else {
+                const float st = phase == kProbe1 ? C.alpha : (C.f1 < C.f ? 2.0f * C.alpha : 0.5f * C.alpha);
+                set_pose(L, 0, __builtin_fmaf(st, C.u[0], C.x[0]), __builtin_fmaf(st, C.u[1], C.x[1]),
+                         __builtin_fmaf(st, C.u[2], C.x[2]));
             }
-        } else {
-            const float st = phase == kProbe1 ? C.alpha : (C.f1 < C.f ? 2.0f * C.alpha : 0.5f * C.alpha);
-            set_pose(L, 0, __builtin_fmaf(st, C.u[0], C.x[0]), __builtin_fmaf(st, C.u[1], C.x[1]),
-                     __builtin_fmaf(st, C.u[2], C.x[2]));
+            wave_sync();
+            TMARK(L, 15);
+            evaluate_poses<G, NS, kTail, kMask, false>(a, L, sl, m, K, rm);
+            if (fd_round) {
+                int k0 = 0;
+                if (phase == kStart) {
+                    C.f = C.fr[0];
+                    E = 1;
+                    if (a.fo.iters <= 0)
+                        break;
+                    k0 = 1;
+                }
+                for (int i = 0; i < 3; ++i)
+                    C.g[i] = (float)(C.fr[k0 + i] - C.f) * gs;
+                E += 3;
+            }
         }
-        wave_sync();
-        TMARK(L, 15);
-        evaluate_poses<G, NS, kTail, kMask, false>(a, L, sl, m, K, rm);
-        if (phase == kStart || phase == kFd) {
-            int k0 = 0;
-            if (phase == kStart) {
-                C.f = C.fr[0];
-                E = 1;
-                if (a.fo.iters <= 0)
-                    break;
-                k0 = 1;
-            }
-            float g[3];
-            for (int i = 0; i < 3; ++i)
-                g[i] = (float)(C.fr[k0 + i] - C.f) * gs;
-            E += 3;
+        if (fd_round) {
+            // the CG direction from the gradient in C.g (just measured, or the
+            // last one when the line search left x unchanged: or_fast.c fast_cg)
+            reuse_g = false;
+            float g[3] = {C.g[0], C.g[1], C.g[2]};
             const float gg = fdot(g, g);
             if (gg == 0.0f)
                 break;
@@ -946,6 +956,8 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
                     for (int k = 0; k < 3; ++k)
                         C.x[k] = C.px[0][k];
                     C.f = f2;
+                } else {
+                    reuse_g = true;
                 }
                 C.alpha = 0.5f * C.alpha;
             }

@@ -46,7 +46,7 @@ class FastOptions:
     mode replaces OptimizationOpenCV::Optimize, optimization_opencv.cpp:44-78,
     with a conjugate-gradient refine on LDS-staged gray tiles)."""
 
-    iters: int = 4            # CG iterations: E = 1 + 5 iters (+1 filter evaluation)
+    iters: int = 4            # CG iterations: E <= 1 + 5 iters (+1 filter evaluation)
     margin: int = 2           # tile margin around the initial window, pixels (<= 7)
     tile_budget: int = 6656   # LDS bytes per patch: tiles + 64 per view (<= 16384; <= 6656: 4 waves/SIMD)
     max_views: int = 32       # staged views per patch (<= 32)

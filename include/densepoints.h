@@ -428,7 +428,9 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  *    (FAST_EVAL, filter) use an fp64 finish;
  *  - refine: `iters` Polak-Ribiere+ conjugate-gradient steps with a forward-
  *    difference gradient (step fd_step) and a two-probe line search (initial
- *    step ls_step, doubled on success, halved on failure): E = 1 + 5 iters;
+ *    step ls_step, doubled on success, halved on failure): E = 1 + 5 iters,
+ *    less 3 per iteration after a line search that left x unchanged (the
+ *    last gradient is reused: the forward differences would repeat it);
  *  - then Patch::InitRelatedImages (patch.cpp:19-49) at the new pose (its
  *    angle tests as cosine tests, x > cos(angle) with the cosines from the
  *    host libm; frame unit vectors by one reciprocal and products) and the

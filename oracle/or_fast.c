@@ -22,7 +22,9 @@
  *     plane and normal x that), fixed in size for the refine;
  *   - the pose is (depth along the reference ray, two plane tilts), refined by
  *     `iters` nonlinear conjugate-gradient steps (Polak-Ribiere+, forward-
- *     difference gradient, a two-probe line search); E = 1 + 5 * iters;
+ *     difference gradient, a two-probe line search); E = 1 + 5 * iters, less 3
+ *     per iteration after a line search that left x unchanged (its forward
+ *     differences would repeat the last gradient, which is reused);
  *   - samples are bilinear in 1/32 px with 1/16 gray-level output, moments are
  *     exact integers; the refine's NCC finish is fp32 (quantised to 2^-24) and
  *     its objective an exact integer, the reported scores' finish is fp64;
@@ -452,14 +454,21 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
     const float gs = (1.0f / h) * 0x1p-24f; /* gradient per objective unit */
     float alpha = fo->ls_step;
     float gp[3] = {0, 0, 0}, dp[3] = {0, 0, 0}, ggp = 0.0f;
+    int moved = 1; /* x changed since the last gradient */
     for (int it = 0; it < fo->iters; ++it) {
         float g[3];
-        for (int i = 0; i < 3; ++i) {
-            float xt[3] = {x[0], x[1], x[2]};
-            xt[i] = x[i] + h;
-            g[i] = (float)(fast_objective(fp, cell, dmin0, pose_of(fp, xt), NULL) - f) * gs;
+        if (moved) {
+            for (int i = 0; i < 3; ++i) {
+                float xt[3] = {x[0], x[1], x[2]};
+                xt[i] = x[i] + h;
+                g[i] = (float)(fast_objective(fp, cell, dmin0, pose_of(fp, xt), NULL) - f) * gs;
+            }
+            E += 3;
+        } else {
+            /* both probes failed, x and f(x) are unchanged: the forward
+             * differences would repeat the last ones bit for bit */
+            for (int i = 0; i < 3; ++i) g[i] = gp[i];
         }
-        E += 3;
         const float gg = fdot(g, g);
         if (gg == 0.0f) break;
         float beta = 0.0f;
@@ -478,6 +487,7 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
         float x1[3], x2[3];
         for (int i = 0; i < 3; ++i) x1[i] = fmaf(alpha, u[i], x[i]);
         const int32_t f1 = fast_objective(fp, cell, dmin0, pose_of(fp, x1), NULL);
+        moved = 1;
         if (f1 < f) {
             const float a2 = 2.0f * alpha;
             for (int i = 0; i < 3; ++i) x2[i] = fmaf(a2, u[i], x[i]);
@@ -497,6 +507,8 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
             if (f2 < f) {
                 memcpy(x, x2, sizeof(x2));
                 f = f2;
+            } else {
+                moved = 0;
             }
             alpha = a2;
         }
