@@ -79,7 +79,7 @@ def test_two_ranks_sharded_densify_equals_dp_densify(tmp_path):
         assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
 
 
-def _worker_dev(rank, world, port, out_path, backend, partitioned=False):
+def _worker_dev(rank, world, port, out_path, backend, partitioned=False, cap=1):
     import torch
     import torch.distributed as tdist
 
@@ -93,7 +93,7 @@ def _worker_dev(rank, world, port, out_path, backend, partitioned=False):
         tdist.init_process_group(backend, rank=rank, world_size=world, **kw)
         group = tdist
     P, imgs, seeds = _scene("hf6")
-    with dp.Engine(device=0) as eng:
+    with dp.Engine(dp.Options(max_patches_per_cell=cap), device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
         if partitioned == "all":
             got, st = D.densify_partitioned_device_all(eng, seeds, group, torch.device("cuda", 0))
@@ -127,20 +127,21 @@ def test_device_resident_sharded_densify(tmp_path, backend, world):
         assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
 
 
-@pytest.mark.parametrize("backend,world,variant", [(None, 1, "accepted"), ("nccl", 1, "accepted"),
-                                                  ("gloo", 2, "accepted"), ("gloo", 3, "accepted"),
-                                                  ("gloo", 2, "all")])
-def test_partitioned_densify_device(tmp_path, backend, world, variant):
+@pytest.mark.parametrize("backend,world,variant,cap", [(None, 1, "accepted", 1), ("nccl", 1, "accepted", 1),
+                                                      ("gloo", 2, "accepted", 1), ("gloo", 3, "accepted", 1),
+                                                      ("gloo", 2, "all", 1), ("gloo", 2, "accepted", 2)])
+def test_partitioned_densify_device(tmp_path, backend, world, variant, cap):
     """Reference-view super-tile partition of every generation: the device
     partition, refine of the rank's items, all-gather of the ACCEPTED
     candidates only and dp_densify_commit_accepted_device (variant
     "accepted", dist.densify_partitioned_device), or of every candidate slot
     with dp_densify_commit_items_device ("all"): every rank's store equals
-    dp_densify."""
+    dp_densify -- also with organizer cell capacity 2
+    (max_patches_per_cell, patch_organizer.h:42-46)."""
     out = str(tmp_path / "dense")
-    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, variant), nprocs=world, join=True)
+    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, variant, cap), nprocs=world, join=True)
     P, imgs, seeds = _scene("hf6")
-    with dp.Engine(device=0) as eng:
+    with dp.Engine(dp.Options(max_patches_per_cell=cap), device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
         ref, rst = eng.densify(seeds)
     for r in range(world):
