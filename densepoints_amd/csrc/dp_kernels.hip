@@ -170,12 +170,17 @@ __device__ __forceinline__ void texel_coord(const WaveLds &L, int rb, int px, in
     iy = rint_i32(Y);
 }
 
-// Taps (x0, x0+1) of rows y0, y1 by two 8-byte loads -- the right neighbour
-// is always inside the image because the ROI ends at floor(max u) <= W-1 --
-// then BORDER_REPLICATE select, bilinear and BGR2GRAY.
+// Taps (x0, x0+1) of rows y0, y0+1 by two 8-byte loads, then bilinear and
+// BGR2GRAY.  BORDER_REPLICATE on the ROI is a clamp of the 1/32-px coordinate
+// to [0, 32*(w-1)] x [0, 32*(h-1)]: past either edge the clamped fraction is
+// 0, so the right tap / lower row carries weight 0 -- the same integer sums as
+// replicating the edge texel (equal rows or columns blend to the edge value
+// exactly) -- and only has to be readable: x0 + 1 <= tlx + w = floor(max u)
+// <= W-1 and y0 + 1 <= tly + h <= H-1, because every window corner lies
+// inside the image.
 struct TexelLoad {
     unsigned long long a, b;
-    uint32_t fx, fy; // fractions (fx = 0 where the right tap replicates the left)
+    uint32_t fx, fy; // fractions of the clamped coordinate (1/32 px)
 };
 
 __device__ __forceinline__ int32_t med3_i32(int32_t v, int32_t lo, int32_t hi)
@@ -185,56 +190,50 @@ __device__ __forceinline__ int32_t med3_i32(int32_t v, int32_t lo, int32_t hi)
     return r;
 }
 
-__device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm, int hm, int32_t ix, int32_t iy)
+// wm32 = 32*(w-1), hm32 = 32*(h-1) of the ROI; roi = its origin, pitch in pixels
+__device__ __forceinline__ TexelLoad texel_fetch(gpix_t roi, int pitch, int wm32, int hm32, int32_t ix, int32_t iy)
 {
-    const int32_t sx = ix >> 5, sy = iy >> 5;
-    const int32_t x0 = med3_i32(sx, 0, wm);
-    const int32_t y0 = med3_i32(sy, 0, hm);
-    const int32_t y1 = med3_i32(sy + 1, 0, hm);
-    TexelLoad t;
-    // sx < 0 or sx >= w-1: x1 == x0 (BORDER_REPLICATE), i.e. weight 0 on the
-    // right tap -- the same integers as fx = 0; the right tap loaded at x0+1
-    // is still inside the image (x0 + 1 <= tlx + w <= W - 1)
-    const bool same = (uint32_t)sx >= (uint32_t)wm;
+    const int32_t cx = med3_i32(ix, 0, wm32), cy = med3_i32(iy, 0, hm32);
     // pixel offsets inside one image plane: pitch < 2^24, y < 2^24
-    const uint32_t o0 = __umul24((uint32_t)y0, (uint32_t)pitch) + (uint32_t)x0;
-    const uint32_t o1 = __umul24((uint32_t)y1, (uint32_t)pitch) + (uint32_t)x0;
+    const uint32_t o0 = __umul24((uint32_t)cy >> 5, (uint32_t)pitch) + ((uint32_t)cx >> 5);
+    TexelLoad t;
 #ifdef DP_DIAG_HOTIMG
     // diagnostic build: every gather hits one 1 KiB block (timing only)
-    t.a = *(gpair_t)(roi + ((uint32_t)(y0 * 16 + x0) & 127u));
-    t.b = *(gpair_t)(roi + ((uint32_t)(y1 * 16 + x0) & 127u));
-    (void)o0;
-    (void)o1;
+    t.a = *(gpair_t)(roi + (o0 & 127u));
+    t.b = *(gpair_t)(roi + ((o0 + 16u) & 127u));
 #else
     t.a = *(gpair_t)(roi + o0);
-    t.b = *(gpair_t)(roi + o1);
+    t.b = *(gpair_t)(roi + o0 + pitch);
 #endif
-    t.fx = same ? 0u : (uint32_t)(ix & 31);
-    t.fy = (uint32_t)(iy & 31);
+    t.fx = (uint32_t)cx & 31u;
+    t.fy = (uint32_t)cy & 31u;
     return t;
 }
 
 typedef const __attribute__((address_space(1))) char *gbyte_t;
 
 // texel_fetch with narrow addressing: the taps are base (uniform, SGPR) + a
-// 32-bit byte offset, so each gather is one v_mad_u32_u24 from the shared
-// column offset (global_load saddr form, no 64-bit address arithmetic)
-__device__ __forceinline__ TexelLoad texel_fetch_n(gbyte_t base, uint32_t roi, int pitch4, int wm, int hm, int32_t ix,
-                                                   int32_t iy)
+// 32-bit byte offset (global_load saddr form, no 64-bit address arithmetic).
+// base1 = base + 4*pitch when every slot of the pass has that pitch (kUniPitch):
+// the lower row is then the same offset from a second SGPR base (no add).
+template <bool kUniPitch>
+__device__ __forceinline__ TexelLoad texel_fetch_n(gbyte_t base, gbyte_t base1, uint32_t roi, int pitch4, int wm32,
+                                                   int hm32, int32_t ix, int32_t iy)
 {
-    const int32_t sx = ix >> 5, sy = iy >> 5;
-    const int32_t x0 = med3_i32(sx, 0, wm);
-    const int32_t y0 = med3_i32(sy, 0, hm);
-    const int32_t y1 = med3_i32(sy + 1, 0, hm);
+    const int32_t cx = med3_i32(ix, 0, wm32), cy = med3_i32(iy, 0, hm32);
+    // o0 = y0 * pitch4 + (x0 * 4 + roi) as v_lshl_add + v_mad_u32_u24 (the
+    // compiler's own form is shift, mask, multiply and a 3-way add)
+    uint32_t xo, o0;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(xo) : "v"((uint32_t)cx >> 5), "v"(roi));
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(o0) : "v"((uint32_t)cy >> 5), "v"(pitch4), "v"(xo));
     TexelLoad t;
-    const bool same = (uint32_t)sx >= (uint32_t)wm; // as texel_fetch
-    const uint32_t xo = ((uint32_t)x0 << 2) + roi;
-    const uint32_t o0 = __umul24((uint32_t)y0, (uint32_t)pitch4) + xo;
-    const uint32_t o1 = __umul24((uint32_t)y1, (uint32_t)pitch4) + xo;
     t.a = *(gpair_t)(base + o0);
-    t.b = *(gpair_t)(base + o1);
-    t.fx = same ? 0u : (uint32_t)(ix & 31);
-    t.fy = (uint32_t)(iy & 31);
+    if (kUniPitch)
+        t.b = *(gpair_t)(base1 + o0);
+    else
+        t.b = *(gpair_t)(base + (o0 + (uint32_t)pitch4));
+    t.fx = (uint32_t)cx & 31u;
+    t.fy = (uint32_t)cy & 31u;
     return t;
 }
 
@@ -243,6 +242,14 @@ __device__ __forceinline__ uint32_t pk_mul_u16_sat(uint32_t a, uint32_t b)
 {
     uint32_t r;
     asm("v_pk_mad_u16 %0, %1, %2, 0 op_sel_hi:[1,0,0] clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// v_pk_mul_lo_u16 (a.lo * b.lo, a.hi * b.lo), low 16 bits of each
+__device__ __forceinline__ uint32_t pk_mul_u16(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_mul_lo_u16 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
 
@@ -267,10 +274,9 @@ __device__ __forceinline__ uint32_t texel_gray_hi(const TexelLoad &t)
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
     const uint32_t a0 = (uint32_t)t.a, b0 = (uint32_t)t.b;
     const uint32_t a1 = (uint32_t)(t.a >> 32), b1 = (uint32_t)(t.b >> 32);
-    const uint32_t wx = 32u + t.fx * 65535u; // (32 - fx) | fx << 16
-    const uint32_t fy64 = t.fy << 6;
-    const us2 w0 = __builtin_bit_cast(us2, pk_mul_u16_sat(wx, 2048u - fy64));
-    const us2 w1 = __builtin_bit_cast(us2, wx * fy64);
+    const uint32_t wx64 = 2048u + t.fx * 4194240u; // 64 (32 - fx) | 64 fx << 16
+    const us2 w0 = __builtin_bit_cast(us2, pk_mul_u16_sat(wx64, 32u - t.fy));
+    const us2 w1 = __builtin_bit_cast(us2, pk_mul_u16(wx64, t.fy));
     uint32_t ch[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -413,20 +419,25 @@ __device__ __forceinline__ void texel_coord_d(uint32_t ra, uint32_t ca, int32_t 
 // trip per pass.  kAnchor: slot 0 is texture 0, whose gray values go to LDS
 // before the other slots form their cross moments.  Lanes of an inactive slot
 // (odd view count) sample a valid view too; their group totals are dropped.
-template <int G, bool kAnchor, bool kNarrow>
+// kNarrow: 32-bit byte offsets from a.img_base; kUniPitch (narrow only): every
+// slot's view has the row pitch upitch (pixels), so the lower-row taps use the
+// SGPR base a.img_base + 4*upitch.
+template <int G, bool kAnchor, bool kNarrow, bool kUniPitch>
 __device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &L, const TexDesc &td, int j,
-                                                  uint64_t roi, int pitch, int wm, int hm, int &s, int &ss, int &sx)
+                                                  uint64_t roi, int pitch, int upitch, int wm32, int hm32, int &s,
+                                                  int &ss, int &sx)
 {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
     TexelLoad tl[kTexPerLane];
+    const gbyte_t base1 = (gbyte_t)a.img_base + (uint32_t)(upitch * 4);
 #pragma unroll
     for (int i = 0; i < kTexPerLane; ++i) {
         int32_t ix, iy;
         texel_coord_d(td.ra[i], td.ca[i], ix, iy);
         if (kNarrow)
-            tl[i] = texel_fetch_n((gbyte_t)a.img_base, (uint32_t)roi, pitch * 4, wm, hm, ix, iy);
+            tl[i] = texel_fetch_n<kUniPitch>((gbyte_t)a.img_base, base1, (uint32_t)roi, pitch * 4, wm32, hm32, ix, iy);
         else
-            tl[i] = texel_fetch((gpix_t)roi, pitch, wm, hm, ix, iy);
+            tl[i] = texel_fetch((gpix_t)roi, pitch, wm32, hm32, ix, iy);
         // one texel's fp64 coordinate math at a time: only the issued loads
         // stay live across the pass
         __builtin_amdgcn_sched_barrier(0);
@@ -473,7 +484,7 @@ struct Moments {
 // copy of them.
 template <int G, bool kAnchor>
 __device__ __attribute__((noinline)) Moments group_sample_clamped(WaveLds &L, int cell, int j, bool act, gpix_t roi,
-                                                                  int pitch, int wm, int hm)
+                                                                  int pitch, int wm32, int hm32)
 {
     constexpr int LP = kWave / G;
     const int g = lane_id() & (LP - 1);
@@ -488,7 +499,7 @@ __device__ __attribute__((noinline)) Moments group_sample_clamped(WaveLds &L, in
                 const int px = t - py * cell;
                 int32_t ix, iy;
                 texel_coord<false>(L, j * (64 / G), px, py, ix, iy);
-                const int gv = texel_gray(texel_fetch(roi, pitch, wm, hm, ix, iy));
+                const int gv = texel_gray(texel_fetch(roi, pitch, wm32, hm32, ix, iy));
                 m.s += gv;
                 m.ss += gv * gv;
                 // u16 half (i & 1) of anchor pair word anchor_slot(i / 2, g)
@@ -524,20 +535,25 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
     const int slot = pick8(j, q);
     const bool act = slot >= 0;
     const int sl = act ? slot : pick8(0, q);
-    const int wm = L.map[sl].w - 1, hm = L.map[sl].h - 1;
+    // BORDER_REPLICATE clamp bounds of the ROI in 1/32 px (texel_fetch)
+    const int wm32 = (L.map[sl].w - 1) * 32, hm32 = (L.map[sl].h - 1) * 32;
     const bool all_safe = __ballot(act && !L.map[sl].safe) == 0ull;
     const int pitch = L.pitch[sl];
+    const int upitch = uni(pitch);
+    const bool uni_pitch = __ballot(pitch != upitch) == 0ull;
     const uint64_t roi = L.roi[sl]; // narrow: byte offset from a.img_base
     wave_sync();
     int s = 0, ss = 0, sx = 0;
     if (all_safe) {
-        if (a.narrow)
-            group_sample_safe<G, kAnchor, true>(a, L, td, j, roi, pitch, wm, hm, s, ss, sx);
+        if (a.narrow && uni_pitch)
+            group_sample_safe<G, kAnchor, true, true>(a, L, td, j, roi, pitch, upitch, wm32, hm32, s, ss, sx);
+        else if (a.narrow)
+            group_sample_safe<G, kAnchor, true, false>(a, L, td, j, roi, pitch, upitch, wm32, hm32, s, ss, sx);
         else
-            group_sample_safe<G, kAnchor, false>(a, L, td, j, roi, pitch, wm, hm, s, ss, sx);
+            group_sample_safe<G, kAnchor, false, false>(a, L, td, j, roi, pitch, upitch, wm32, hm32, s, ss, sx);
     } else {
         const gpix_t roip = a.narrow ? (gpix_t)(a.img_base + (uint32_t)roi) : (gpix_t)roi;
-        const Moments mm = group_sample_clamped<G, kAnchor>(L, a.cell, j, act, roip, pitch, wm, hm);
+        const Moments mm = group_sample_clamped<G, kAnchor>(L, a.cell, j, act, roip, pitch, wm32, hm32);
         s = mm.s;
         ss = mm.ss;
         sx = mm.sx;
@@ -676,6 +692,37 @@ __device__ __forceinline__ uint64_t build_maps_quad(const MapView &vw, WaveLds &
     return bits << round0;
 }
 
+// dpg::ncc_finish for the views of lanes with `scored` (moments in
+// L.mom[lane]), with the texture-0 deviation sqrt(Saa n - Sa^2 / n^2) -- the
+// same for every view -- evaluated once on lane 63 (never a view lane: a chunk
+// has <= kMapChunk views) by the same instructions that give each view lane
+// its own, then broadcast.  Same roundings as dpg::ncc_finish.
+__device__ __forceinline__ double wave_ncc_finish(int N, int Sa, int Saa, const WaveLds &L, bool scored,
+                                                  double denom_min)
+{
+    static_assert(kMapChunk < kWave, "lane 63 is not a view lane");
+    const int lane = lane_id();
+    const bool anc = lane == kWave - 1;
+    const int64_t n = N;
+    const double dn = (double)n, dn2 = (double)(n * n);
+    double sig = 0.0;
+    int32_t Sb = 0;
+    if (scored || anc) {
+        Sb = anc ? Sa : L.mom[lane][0];
+        const int32_t Sbb = anc ? Saa : L.mom[lane][1];
+        sig = dpg::dvsqrt(dpg::dvdiv((double)(n * (int64_t)Sbb - (int64_t)Sb * Sb), dn2));
+    }
+    const double sa = readlane_f64(sig, kWave - 1);
+    double r = -1.0;
+    if (scored) {
+        double den = sa * sig;
+        den = (denom_min < den) ? den : denom_min;
+        const double num = dpg::dvdiv((double)(n * (int64_t)L.mom[lane][2] - (int64_t)Sa * Sb), dn);
+        r = dpg::dvdiv(dpg::dvdiv(num, den), dn);
+    }
+    return r;
+}
+
 // One evaluation's NCC scores against texture 0 -> L.score[0..nv-1]
 // (GetProjectedTextures + NCCScore) at candidate pose (nn, pp).  Per chunk of
 // up to 64 visible views, lane k builds view k's window map (projective map +
@@ -779,13 +826,10 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
         }
 #endif
         const int k = base + lane;
-        if (k >= kb && k < ke) {
-            double sc = -1.0;
-            if ((valid >> lane) & 1ull)
-                sc = dpg::ncc_finish(N, Sa, Saa, L.mom[lane][0], L.mom[lane][1], L.mom[lane][2],
-                                     a.opt.ncc_denom_min);
-            L.score[k - 1] = sc;
-        }
+        const bool scored = k >= kb && k < ke && ((valid >> lane) & 1ull);
+        const double sc = wave_ncc_finish(N, Sa, Saa, L, scored, a.opt.ncc_denom_min);
+        if (k >= kb && k < ke)
+            L.score[k - 1] = scored ? sc : -1.0;
         wave_sync();
         STAMP(L, 3);
     }
