@@ -368,6 +368,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p)
 struct TexDesc {
     uint32_t ra[kTexPerLane], ca[kTexPerLane];
     uint32_t sel[kTexPerLane / 2];
+    uint32_t anc; // LDS byte address of the lane's first texture-0 pair (L.anchor[anchor_slot(0, g)])
 };
 
 template <int G>
@@ -395,6 +396,8 @@ __device__ __forceinline__ TexDesc make_texdesc(const WaveLds &L, int cell)
         const bool l0 = g + LP * (2 * p) < N, l1 = g + LP * (2 * p + 1) < N;
         td.sel[p] = 0x0c000c00u | (l0 ? 0x02u : 0x0cu) | ((l1 ? 0x06u : 0x0cu) << 16);
     }
+    td.anc = lds_addr(&L.anchor[g]);
+    asm volatile("" : "+v"(td.anc));
     return td;
 }
 
@@ -456,12 +459,14 @@ __device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &
         const uint32_t r1 = texel_gray_hi(tl[2 * p + 1]);
         const uint32_t gg = __builtin_amdgcn_perm(r1, r0, td.sel[p]);
         uint32_t aa;
+        // anchor_slot<LP>(p, g) = p * LP + g: td.anc + 4 LP p
+        const lds_u32_t ap = (lds_u32_t)(uintptr_t)(td.anc + 4u * (uint32_t)(p * LP));
         if (kAnchor) {
             aa = (G == 1) ? gg : (uint32_t)__builtin_amdgcn_ds_bpermute(g << 2, (int)gg);
             if (j == 0)
-                L.anchor[anchor_slot<LP>(p, g)] = gg;
+                *ap = gg;
         } else {
-            aa = L.anchor[anchor_slot<LP>(p, g)];
+            aa = *ap;
         }
         const us2 vg = __builtin_bit_cast(us2, gg);
         us = __builtin_amdgcn_udot2(vg, ones, us, false);
@@ -524,17 +529,18 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
     constexpr int LP = kWave / G;
     const int lane = lane_id();
     const int cell = a.cell;
-    // row/column tables: G slots x 16 lanes, lane r of a slot fills row r and column r
-    for (int e = lane; e < 16 * G; e += kWave) {
-        const int je = e >> 4, r = e & 15;
-        const int ke = pick8(je, q);
-        if (ke >= 0 && r < cell)
-            fill_tables(L, je * (64 / G), L.map[ke], r);
-    }
-    const int j = lane / LP;
+    // pass_width: cell^2 <= LP * kTexPerLane <= LP^2, so a slot's LP lanes cover the window's rows
+    static_assert(LP >= kTexPerLane, "cell <= LP");
+    const int j = (int)((uint32_t)lane / (uint32_t)LP);
     const int slot = pick8(j, q);
     const bool act = slot >= 0;
     const int sl = act ? slot : pick8(0, q);
+    // row/column tables: lane r of pass slot j fills row r and column r
+    {
+        const int r = lane & (LP - 1);
+        if (act && r < cell)
+            fill_tables(L, j * LP, L.map[slot], r);
+    }
     // BORDER_REPLICATE clamp bounds of the ROI in 1/32 px (texel_fetch)
     const int wm32 = (L.map[sl].w - 1) * 32, hm32 = (L.map[sl].h - 1) * 32;
     const bool all_safe = __ballot(act && !L.map[sl].safe) == 0ull;
@@ -908,7 +914,8 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
             q2 = L.sp[vi][2];
         } else {
             const double fac = phase == kReflect ? -1.0 : (phase == kExpand ? 2.0 : 0.5);
-            const double alpha = dpg::dvdiv(1.0 - fac, 3.0);
+            // (1 - fac) / 3 of the three phases, IEEE-rounded at compile time
+            const double alpha = phase == kReflect ? 2.0 / 3.0 : (phase == kExpand ? -1.0 / 3.0 : 0.5 / 3.0);
             const double beta = alpha - fac;
             q0 = L.cs[0] * alpha - L.sp[ihi][0] * beta;
             q1 = L.cs[1] * alpha - L.sp[ihi][1] * beta;
