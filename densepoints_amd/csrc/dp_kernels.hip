@@ -333,6 +333,37 @@ __device__ __forceinline__ int group_total(int v)
     return v;
 }
 
+// group_total of three values at once.  The cross-row steps (row_bcast:15 /
+// :31, which write only some rows) are done as in-place v_add_u32_dpp in
+// inline asm: written through builtins they become a zeroed copy, a DPP move
+// and an add per value.  s_nop 1 covers the VALU-write -> DPP-read hazard of
+// the row_shr results.
+template <int G>
+__device__ __forceinline__ void group_total3(int &a, int &b, int &c)
+{
+    constexpr int LP = kWave / G;
+    if (LP < 32) {
+        a = group_total<G>(a);
+        b = group_total<G>(b);
+        c = group_total<G>(c);
+        return;
+    }
+    a = group_total<4>(a); // row_shr:1,2,4,8: row sums in lane 15 of each row
+    b = group_total<4>(b);
+    c = group_total<4>(c);
+    asm volatile("s_nop 1\n\t"
+                 "v_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                 "v_add_u32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                 "v_add_u32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf"
+                 : "+v"(a), "+v"(b), "+v"(c));
+    if (LP == 64)
+        asm volatile("s_nop 1\n\t"
+                     "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+                     "v_add_u32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+                     "v_add_u32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf"
+                     : "+v"(a), "+v"(b), "+v"(c));
+}
+
 // texels per lane per view pass: a pass of G views needs N <= 64 * K / G
 constexpr int kTexPerLane = DP_TEX_PER_LANE;
 
@@ -543,7 +574,10 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
     }
     // BORDER_REPLICATE clamp bounds of the ROI in 1/32 px (texel_fetch)
     const int wm32 = (L.map[sl].w - 1) * 32, hm32 = (L.map[sl].h - 1) * 32;
-    const bool all_safe = __ballot(act && !L.map[sl].safe) == 0ull;
+    // sl is a valid slot on every lane: the flag is read unconditionally and
+    // both conditions go straight into lane masks
+    const int safe = L.map[sl].safe;
+    const bool all_safe = (__ballot(safe == 0) & __ballot(act)) == 0ull;
     const int pitch = L.pitch[sl];
     const int upitch = uni(pitch);
     const bool uni_pitch = __ballot(pitch != upitch) == 0ull;
@@ -564,9 +598,7 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
         ss = mm.ss;
         sx = mm.sx;
     }
-    s = group_total<G>(s);
-    ss = group_total<G>(ss);
-    sx = group_total<G>(sx);
+    group_total3<G>(s, ss, sx);
     if (kAnchor) {
         sa = __builtin_amdgcn_readlane(s, LP - 1);
         saa = __builtin_amdgcn_readlane(ss, LP - 1);
@@ -608,12 +640,14 @@ __device__ __forceinline__ void views_all(const RefineArgs &a, WaveLds &L, const
 }
 
 // DPP within lane quads: xor 1, xor 2 and broadcast of quad lane i
-__device__ __forceinline__ int quad_xor1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false); }
-__device__ __forceinline__ int quad_xor2(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false); }
+// (quad permutations read only lanes of the same quad, so no lane is out of
+// bounds: mov_dpp with bound_ctrl needs no initialised destination)
+__device__ __forceinline__ int quad_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true); }
+__device__ __forceinline__ int quad_xor2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true); }
 template <int I>
 __device__ __forceinline__ float quad_bcast(float v)
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), I * 0x55, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), I * 0x55, 0xf, 0xf, true));
 }
 
 // Window maps of up to 16 views (chunk slots round0 .. round0+15) with four
@@ -658,8 +692,9 @@ __device__ __forceinline__ uint64_t build_maps_quad(const MapView &vw, WaveLds &
     const bool act = slot < kMapChunk && kk < m;
     double u, w;
     dpg::project(vw.P, L.c12[3 * ci], L.c12[3 * ci + 1], L.c12[3 * ci + 2], u, w);
-    const bool ins = act && dpg::inside(u, w, vw.W, vw.H);
-    const uint64_t insm = __ballot(ins);
+    // dpg::inside as four compares straight into lane masks
+    const uint64_t insm = __ballot(act) & __ballot(u > 0.0) & __ballot(u < (double)vw.W) & __ballot(w > 0.0) &
+                          __ballot(w < (double)vw.H);
     const bool all_in = ((insm >> (lane & ~3)) & 0xFull) == 0xFull;
     // texture_map: tl = min(W|H, ceil of the corners), br = max(0, floor of the corners)
     int cx = (int)ceil(u), cy = (int)ceil(w), lx = (int)floor(u), ly = (int)floor(w);
