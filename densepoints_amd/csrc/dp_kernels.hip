@@ -291,21 +291,27 @@ __device__ __forceinline__ uint32_t texel_gray_hi(const TexelLoad &t)
 __device__ __forceinline__ int texel_gray(const TexelLoad &t) { return (int)(texel_gray_hi(t) >> 16); }
 
 // row r and column r terms of map `tm` into the table rows from rb (one lane
-// per r: all nine coefficients are read before anything is written)
+// per r: all nine coefficients are read before anything is written).  The
+// maps in LDS hold m6, m7, m8 already scaled by 2^-5 (build_maps_quad; exact),
+// so W' = W0' + cW' = W/32 and 32/W = 1/W'.  32-bit LDS addressing (a generic
+// reference into WaveLds costs a 64-bit multiply-add per lane).
 __device__ __forceinline__ void fill_tables(WaveLds &L, int rb, const dpg::TexMap &tm, int r)
 {
+    typedef __attribute__((address_space(3))) double *lds_f64w_t;
     const double m0 = tm.m0, m1 = tm.m1, m2 = tm.m2, m3 = tm.m3, m4 = tm.m4, m5 = tm.m5;
     const double m6 = tm.m6, m7 = tm.m7, m8 = tm.m8;
     const double v = (double)r;
-    // W terms scaled by 2^-5 (exact): W' = W0' + cW' = W/32, and 32/W = 1/W'
-    const double r0 = m1 * v + m2, r1 = m4 * v + m5, r2 = (m7 * v + m8) * 0.03125;
-    const double c0 = m0 * v, c1 = m3 * v, c2 = (m6 * v) * 0.03125;
-    L.rowt[rb + r][0] = r0;
-    L.rowt[rb + r][1] = r1;
-    L.rowt[rb + r][2] = r2;
-    L.colt[rb + r][0] = c0;
-    L.colt[rb + r][1] = c1;
-    L.colt[rb + r][2] = c2;
+    const double r0 = m1 * v + m2, r1 = m4 * v + m5, r2 = m7 * v + m8;
+    const double c0 = m0 * v, c1 = m3 * v, c2 = m6 * v;
+    const uint32_t off = __umul24((uint32_t)(rb + r), (uint32_t)sizeof(double[3]));
+    const lds_f64w_t R = (lds_f64w_t)(uintptr_t)((uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)&L.rowt[0][0] + off);
+    const lds_f64w_t C = (lds_f64w_t)(uintptr_t)((uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)&L.colt[0][0] + off);
+    R[0] = r0;
+    R[1] = r1;
+    R[2] = r2;
+    C[0] = c0;
+    C[1] = c1;
+    C[2] = c2;
 }
 
 // slot list of a pass: byte j = chunk slot of pass slot j, 0xff = none
@@ -719,6 +725,10 @@ __device__ __forceinline__ uint64_t build_maps_quad(const MapView &vw, WaveLds &
         dpg::TexMap tm;
         ok = dpg::quad_map(x, y, tlx, tly, rw, rh, cell, tm);
         if (ok) {
+            // the W coefficients pre-scaled by 2^-5 for fill_tables (exact)
+            tm.m6 *= 0.03125;
+            tm.m7 *= 0.03125;
+            tm.m8 *= 0.03125;
             L.map[slot] = tm;
             // narrow: byte offset of the ROI origin from img_base (< 4 GiB, host-checked)
             L.roi[slot] = narrow ? (uint64_t)(vw.img_off + ((uint32_t)tm.tly * (uint32_t)vw.pitch + (uint32_t)tm.tlx) * 4u)
