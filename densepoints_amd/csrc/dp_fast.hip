@@ -198,6 +198,34 @@ template <int P> __device__ __forceinline__ uint32_t partial_total(uint32_t v)
     return v;
 }
 
+// partial_total of three values in inline asm: through the builtins the
+// compiler sinks the last step's add into the (masked) store block, which
+// leaves an unfused DPP move + add per value.  Consecutive DPP reads of one
+// register are two instructions apart (the VALU-write -> DPP-read hazard);
+// s_nop 1 covers the values' producers.
+template <int P> __device__ __forceinline__ void partial_total3(uint32_t &a, uint32_t &b, uint32_t &c)
+{
+    static_assert(P == 4 || P == 8 || P == 16, "groups within rows of 16");
+    asm volatile("s_nop 1\n\t"
+                 "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                 "v_add_u32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                 "v_add_u32_dpp %2, %2, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                 "v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                 "v_add_u32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                 "v_add_u32_dpp %2, %2, %2 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                 : "+v"(a), "+v"(b), "+v"(c));
+    if (P >= 8)
+        asm volatile("v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_u32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_u32_dpp %2, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                     : "+v"(a), "+v"(b), "+v"(c));
+    if (P >= 16)
+        asm volatile("v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_u32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+                     "v_add_u32_dpp %2, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                     : "+v"(a), "+v"(b), "+v"(c));
+}
+
 // inclusive prefix sum over the wave in lane order: group_total<1> leaves
 // every lane's inclusive prefix (Hillis-Steele within rows of 16, then the
 // row broadcasts), all in DPP -- no LDS crossbar round trips
@@ -756,9 +784,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             // groups of LP/4 lanes), stored in the item's own record, which
             // this pass has read (pass 0's tail read every record first);
             // the NCC finish adds the partials
-            s = partial_total<LP / 4>(s);
-            ss = partial_total<LP / 4>(ss);
-            sx = partial_total<LP / 4>(sx);
+            partial_total3<LP / 4>(s, ss, sx);
             if (act && (g & (LP / 4 - 1)) == LP / 4 - 1) {
                 uint32_t *M = (uint32_t *)&L.e.par[i];
                 const int pi = g / (LP / 4);
