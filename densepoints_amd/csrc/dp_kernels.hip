@@ -109,6 +109,15 @@ __device__ __forceinline__ int lane_id()
     return l;
 }
 
+// A dp_options field read afresh from the kernel-argument segment at its use
+// (a volatile scalar load) instead of an SGPR kept live across the kernel:
+// the kernel runs out of SGPRs, and the compiler's spills of the option block
+// came back through v_readlane (VALU) in the per-evaluation loops.
+#define DP_KARG(T, field)                                                                             \
+    (*(const volatile __attribute__((address_space(4))) T *)((const __attribute__((address_space(4))) char *) \
+                                                                  __builtin_amdgcn_kernarg_segment_ptr() +   \
+                                                              offsetof(RefineArgs, field)))
+
 // visible mask -> ascending list + count (Patch::GetTrullyVisibleImages)
 __device__ __forceinline__ void decode_vis(WaveLds &L, uint64_t v0, uint64_t v1)
 {
@@ -878,7 +887,7 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
 #endif
         const int k = base + lane;
         const bool scored = k >= kb && k < ke && ((valid >> lane) & 1ull);
-        const double sc = wave_ncc_finish(N, Sa, Saa, L, scored, a.opt.ncc_denom_min);
+        const double sc = wave_ncc_finish(N, Sa, Saa, L, scored, DP_KARG(double, opt.ncc_denom_min));
         if (k >= kb && k < ke)
             L.score[k - 1] = scored ? sc : -1.0;
         wave_sync();
@@ -940,7 +949,8 @@ __device__ __forceinline__ double pick_y(const double *yy, int i)
 template <int G>
 __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L, const TexDesc &td, bool &degen)
 {
-    const double *step = a.opt.nm_step;
+    const double step[3] = {DP_KARG(double, opt.nm_step[0]), DP_KARG(double, opt.nm_step[1]),
+                            DP_KARG(double, opt.nm_step[2])};
     for (int i = 1; i <= 3; ++i) {
         for (int jj = 0; jj < 3; ++jj)
             L.sp[i][jj] = 0.0;
@@ -1071,7 +1081,8 @@ __device__ __forceinline__ int wave_nelder_mead(const RefineArgs &a, WaveLds &L,
             const double rr = fabs(mx - mn);
             range = (range < rr) ? rr : range;
         }
-        if (range <= a.opt.nm_eps || err <= a.opt.nm_eps || fcount >= a.opt.nm_max_evals)
+        if (range <= DP_KARG(double, opt.nm_eps) || err <= DP_KARG(double, opt.nm_eps) ||
+            fcount >= DP_KARG(int32_t, opt.nm_max_evals))
             break;
         fcount += 2;
         L.ylo = L.y[ilo];
@@ -1115,7 +1126,7 @@ __device__ __forceinline__ bool wave_filter(const RefineArgs &a, WaveLds &L, con
     score = (float)(sum / (double)nv);
     const uint64_t v0 = L.vis[0], v1 = L.vis[1];
     const uint64_t below = (1ull << lane) - 1ull;
-    const double thr = a.opt.ncc_threshold;
+    const double thr = DP_KARG(double, opt.ncc_threshold);
     const int c0 = __popcll(v0);
     const bool in0 = (v0 >> lane) & 1ull;
     const int r0 = __popcll(v0 & below);
@@ -1127,7 +1138,7 @@ __device__ __forceinline__ bool wave_filter(const RefineArgs &a, WaveLds &L, con
     const uint64_t n1 = __ballot(in1 && !drop1);
     wave_sync();
     decode_vis(L, n0, n1);
-    return uni(L.m) >= a.opt.min_visible;
+    return uni(L.m) >= DP_KARG(int32_t, opt.min_visible);
 }
 
 // Patch::InitRelatedImages (patch.cpp:19-49), one lane per view
@@ -1139,9 +1150,11 @@ __device__ void wave_init_related(const RefineArgs &a, WaveLds &L)
     const double n[3] = {L.n[0], L.n[1], L.n[2]};
     int cls0 = 0, cls1 = 0;
     if (lane < a.V && lane != ref)
-        cls0 = dpg::classify_view(a.views[lane], X, n, a.opt.visible_angle, a.opt.candidate_angle);
+        cls0 = dpg::classify_view(a.views[lane], X, n, DP_KARG(double, opt.visible_angle),
+                                  DP_KARG(double, opt.candidate_angle));
     if (64 + lane < a.V && 64 + lane != ref)
-        cls1 = dpg::classify_view(a.views[64 + lane], X, n, a.opt.visible_angle, a.opt.candidate_angle);
+        cls1 = dpg::classify_view(a.views[64 + lane], X, n, DP_KARG(double, opt.visible_angle),
+                                  DP_KARG(double, opt.candidate_angle));
     const uint64_t v0 = __ballot(cls0 == 1), v1 = __ballot(cls1 == 1);
     const uint64_t c0 = __ballot(cls0 == 2), c1 = __ballot(cls1 == 2);
     wave_sync();
@@ -1163,7 +1176,7 @@ __device__ void child_position(const RefineArgs &a, const dp_patch &par, int dir
     dpg::project(rv.P, X[0] + rv.xr[0], X[1] + rv.xr[1], X[2] + rv.xr[2], qu, qv);
     const double du = qu - cu, dv = qv - cv;
     const double dx = sqrt(du * du + dv * dv);
-    const double scale = (double)a.opt.grid_scale / dx;
+    const double scale = (double)DP_KARG(int32_t, opt.grid_scale) / dx;
     for (int i = 0; i < 3; ++i) {
         const double d = dir == 0 ? rv.xr[i] : dir == 1 ? -rv.xr[i] : dir == 2 ? yax[i] : -yax[i];
         out[i] = (float)(X[i] + scale * d);
