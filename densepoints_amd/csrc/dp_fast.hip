@@ -158,6 +158,15 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p)
     return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char *)p;
 }
 
+// A FastArgs field read afresh from the kernel-argument segment at its use (a
+// volatile scalar load) instead of an SGPR kept live across the kernel: the
+// kernel runs out of SGPRs, and spilled arguments come back through v_readlane
+// (VALU) inside the refine loops.
+#define DP_FKARG(T, field)                                                                            \
+    (*(const volatile __attribute__((address_space(4))) T *)((const __attribute__((address_space(4))) char *) \
+                                                                  __builtin_amdgcn_kernarg_segment_ptr() +   \
+                                                              offsetof(FastArgs, field)))
+
 __device__ __forceinline__ int lane_id()
 {
     int l;
@@ -424,7 +433,8 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
     }
     wave_sync();
     const int nconsider = nvis < 64 ? nvis : 64;
-    const int maxv = a.fo.max_views < kFastMaxV ? a.fo.max_views : kFastMaxV;
+    const int fmv = DP_FKARG(int32_t, fo.max_views);
+    const int maxv = fmv < kFastMaxV ? fmv : kFastMaxV;
     const int view = lane < nconsider ? (int)L.vlist[lane] : 0;
     const FastCam &cam = a.cams[view];
     // the view's gray plane descriptor, loaded now so that its latency
@@ -444,12 +454,12 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
     for (;;) {
         t = tile_rect(g, cam.W, cam.H, M);
         const int tot = uni(wave_sum_i32(staged ? t.tbytes + kFastRec : 0));
-        if (tot <= a.fo.tile_budget || M == 0)
+        if (tot <= DP_FKARG(int32_t, fo.tile_budget) || M == 0)
             break;
         --M;
     }
     const int incl = wave_incl_i32(staged ? t.tbytes + kFastRec : 0);
-    const bool keep = staged && incl <= a.fo.tile_budget;
+    const bool keep = staged && incl <= DP_FKARG(int32_t, fo.tile_budget);
     const uint64_t kept = __ballot(keep);
     const int m = __popcll(kept);
     clipped += (M < margin || m < __popcll(__ballot(staged))) ? 1ull : 0ull;
@@ -675,7 +685,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
     const int j = (int)((unsigned)lane / LP), g = lane & (LP - 1);
     const char *tiles = (const char *)L.arena;
     const int N = a.cell * a.cell;
-    const double dmin = a.dmin;
+    const double dmin = DP_FKARG(double, dmin);
     for (int k0 = 0; k0 < K; k0 += kc) {
         const int kn = K - k0 < kc ? K - k0 : kc;
         const int Q = kn * m;
@@ -830,7 +840,8 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             } else {
                 // the refine's objective term: fp32 finish in 2^-24 steps
                 const float den = sqrt_rn_big((float)va * (float)vb);
-                const float rr = recip_rn(den > a.dminf ? den : a.dminf);
+                const float dminf = DP_FKARG(float, dminf);
+                const float rr = recip_rn(den > dminf ? den : dminf);
                 q = (int)__builtin_rintf(((float)num * rr) * 16777216.0f);
             }
         }
@@ -880,14 +891,14 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
 {
     enum { kStart = 0, kFd = 1, kProbe1 = 2, kProbe2 = 3 };
     CgState &C = L.cg;
-    const float h = a.fo.fd_step;
-    const float gs = a.gs; // gradient per objective unit
+    const float h = DP_FKARG(float, fo.fd_step);
+    const float gs = DP_FKARG(float, gs); // gradient per objective unit
     for (int k = 0; k < 3; ++k) {
         C.x[k] = 0.0f;
         C.gp[k] = 0.0f;
         C.dp[k] = 0.0f;
     }
-    C.alpha = a.fo.ls_step;
+    C.alpha = DP_FKARG(float, fo.ls_step);
     C.ggp = 0.0f;
     int E = 0, it = 0, phase = kStart;
     bool reuse_g = false; // both probes failed: x and f(x) unchanged, so the
@@ -1033,7 +1044,9 @@ __device__ __forceinline__ int classify_f32(const FastCam &c, const float *X, co
         return 0;
     const float d[3] = {X[0] - c.C[0], X[1] - c.C[1], X[2] - c.C[2]};
     const float dn = fdot(n, d), dd = fdot(d, d);
-    return cos_above(dn, dd, a.cvis, a.cvis2) ? 1 : cos_above(dn, dd, a.ccand, a.ccand2) ? 2 : 0;
+    return cos_above(dn, dd, DP_FKARG(float, cvis), DP_FKARG(float, cvis2))    ? 1
+           : cos_above(dn, dd, DP_FKARG(float, ccand), DP_FKARG(float, ccand2)) ? 2
+                                                                                   : 0;
 }
 
 // Patch::InitRelatedImages (patch.cpp:19-49), one lane per view
