@@ -22,6 +22,24 @@
 
 namespace dpm {
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// An fp64 constant of the polynomial kernels materialised by two s_mov_b32 at
+// its use.  A plain literal is hoisted out of the refine loops into an SGPR
+// pair kept for the whole kernel; the parity kernel runs out of SGPRs, and the
+// spilled constants came back through v_readlane (VALU) every evaluation.
+template <uint64_t B> __device__ __forceinline__ double kconst()
+{
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3"
+                 : "=s"(lo), "=s"(hi)
+                 : "i"((uint32_t)(B & 0xffffffffu)), "i"((uint32_t)(B >> 32)));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+#define DPM_K(v) (dpm::kconst<__builtin_bit_cast(uint64_t, (double)(v))>())
+#else
+#define DPM_K(v) (v)
+#endif
+
 DP_HD double bits_hi_only(double x)
 {
     uint64_t b;
@@ -40,9 +58,9 @@ DP_HD double bits_hi_only(double x)
 // polynomial kernels on [-pi/4, pi/4]; y = tail of the reduced argument
 DP_HD double sin_kernel(double x, double y, bool tail)
 {
-    const double s1 = -1.66666666666666324348e-01, s2 = 8.33333333332248946124e-03,
-                 s3 = -1.98412698298579493134e-04, s4 = 2.75573137070700676789e-06,
-                 s5 = -2.50507602534068634195e-08, s6 = 1.58969099521155010221e-10;
+    const double s1 = DPM_K(-1.66666666666666324348e-01), s2 = DPM_K(8.33333333332248946124e-03),
+                 s3 = DPM_K(-1.98412698298579493134e-04), s4 = DPM_K(2.75573137070700676789e-06),
+                 s5 = DPM_K(-2.50507602534068634195e-08), s6 = DPM_K(1.58969099521155010221e-10);
     const double z = x * x;
     const double z2 = z * z;
     const double r = s2 + z * (s3 + z * s4) + z * z2 * (s5 + z * s6);
@@ -54,9 +72,9 @@ DP_HD double sin_kernel(double x, double y, bool tail)
 
 DP_HD double cos_kernel(double x, double y)
 {
-    const double c1 = 4.16666666666666019037e-02, c2 = -1.38888888888741095749e-03,
-                 c3 = 2.48015872894767294178e-05, c4 = -2.75573143513906633035e-07,
-                 c5 = 2.08757232129817482790e-09, c6 = -1.13596475577881948265e-11;
+    const double c1 = DPM_K(4.16666666666666019037e-02), c2 = DPM_K(-1.38888888888741095749e-03),
+                 c3 = DPM_K(2.48015872894767294178e-05), c4 = DPM_K(-2.75573143513906633035e-07),
+                 c5 = DPM_K(2.08757232129817482790e-09), c6 = DPM_K(-1.13596475577881948265e-11);
     const double z = x * x;
     const double z2 = z * z;
     const double r = z * (c1 + z * (c2 + z * c3)) + z2 * z2 * (c4 + z * (c5 + z * c6));
@@ -68,15 +86,15 @@ DP_HD double cos_kernel(double x, double y)
 // sin and cos of x (Cody-Waite reduction by pi/2, two rounds)
 DP_HD void sincos(double x, double &s, double &c)
 {
-    if (fabs(x) <= 0.78539816339744827900) {
+    if (fabs(x) <= DPM_K(0.78539816339744827900)) {
         s = sin_kernel(x, 0.0, false);
         c = cos_kernel(x, 0.0);
         return;
     }
-    const double inv_half_pi = 6.36619772367581382433e-01;
-    const double hp1 = 1.57079632673412561417e+00;
-    const double hp2 = 6.07710050630396597660e-11;
-    const double hp2t = 2.02226624879595063154e-21;
+    const double inv_half_pi = DPM_K(6.36619772367581382433e-01);
+    const double hp1 = DPM_K(1.57079632673412561417e+00);
+    const double hp2 = DPM_K(6.07710050630396597660e-11);
+    const double hp2t = DPM_K(2.02226624879595063154e-21);
     const double q = rint(x * inv_half_pi);
     const double r1 = x - q * hp1;
     double w = q * hp2;
