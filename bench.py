@@ -183,6 +183,10 @@ def main():
     evals = out["evals"].astype(np.float64)
     pvis = np.array([bin(int(m[0])).count("1") + bin(int(m[1])).count("1") for m in parents["vis"]])
     nvis = np.repeat(pvis, 4)  # children refine on the parent's visible set
+    if os.environ.get("DP_BENCH_VIS_HIST") == "1":
+        # diagnostic: objective evaluations by the parent's visible-view count
+        print("visible-view histogram (evaluations):", np.bincount(nvis, weights=evals).astype(np.int64).tolist(),
+              file=sys.stderr)
     n1 = args.cell + 1
     if fast:
         # algorithmic bytes with fp16 texels: sum over evaluations of

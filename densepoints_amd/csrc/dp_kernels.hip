@@ -679,9 +679,11 @@ struct MapView {
     const uint32_t *img;
 };
 
+// kLanesLog2: 2 (four lanes per view, build_maps_quad) or 1 (two, build_maps_pair)
+template <int kLanesLog2 = 2>
 __device__ __forceinline__ MapView load_map_view(const RefineArgs &a, const WaveLds &L, int base, int m, int round0)
 {
-    const int slot = round0 + (lane_id() >> 2);
+    const int slot = round0 + (lane_id() >> kLanesLog2);
     const int kk = base + slot;
     const bool act = slot < kMapChunk && kk < m;
     const dpg::ViewDev &vw = a.views[L.vlist[act ? kk : base]];
@@ -749,6 +751,63 @@ __device__ __forceinline__ uint64_t build_maps_quad(const MapView &vw, WaveLds &
     uint64_t bits = 0;
     for (int q = 0; q < 16; ++q)
         bits |= ((okq >> (4 * q)) & 1ull) << q;
+    return bits << round0;
+}
+
+// build_maps_quad with two lanes per view (up to 32 views per round, so a
+// chunk of kMapChunk > 16 views needs one round instead of two): lane 2k+h
+// projects window corners 2h and 2h+1 into view slot round0+k; the ROI
+// min/max and the other lane's two f32 corners come across the pair by DPP;
+// lane 2k runs dpg::quad_map.  The same operations per corner as the quad
+// form, so the same maps bit for bit.
+__device__ __forceinline__ uint64_t build_maps_pair(const MapView &vw, WaveLds &L, int base, int m, int round0,
+                                                    int cell, bool narrow)
+{
+    const int lane = lane_id();
+    const int k = lane >> 1, h = lane & 1;
+    const int slot = round0 + k;
+    const int kk = base + slot;
+    const bool act = slot < kMapChunk && kk < m;
+    double u0, w0, u1, w1;
+    dpg::project(vw.P, L.c12[6 * h], L.c12[6 * h + 1], L.c12[6 * h + 2], u0, w0);
+    dpg::project(vw.P, L.c12[6 * h + 3], L.c12[6 * h + 4], L.c12[6 * h + 5], u1, w1);
+    const double dW = (double)vw.W, dH = (double)vw.H;
+    const uint64_t insm = __ballot(act) & __ballot(u0 > 0.0) & __ballot(u0 < dW) & __ballot(w0 > 0.0) &
+                          __ballot(w0 < dH) & __ballot(u1 > 0.0) & __ballot(u1 < dW) & __ballot(w1 > 0.0) &
+                          __ballot(w1 < dH);
+    const bool all_in = ((insm >> (lane & ~1)) & 0x3ull) == 0x3ull;
+    int cx = min((int)ceil(u0), (int)ceil(u1)), cy = min((int)ceil(w0), (int)ceil(w1));
+    int lx = max((int)floor(u0), (int)floor(u1)), ly = max((int)floor(w0), (int)floor(w1));
+    cx = min(cx, quad_xor1(cx));
+    cy = min(cy, quad_xor1(cy));
+    lx = max(lx, quad_xor1(lx));
+    ly = max(ly, quad_xor1(ly));
+    const int tlx = min(vw.W, cx), tly = min(vw.H, cy), brx = max(0, lx), bry = max(0, ly);
+    const float fx0 = (float)u0, fx1 = (float)u1, fy0 = (float)w0, fy1 = (float)w1;
+    const float fx2 = __int_as_float(quad_xor1(__float_as_int(fx0))), fx3 = __int_as_float(quad_xor1(__float_as_int(fx1)));
+    const float fy2 = __int_as_float(quad_xor1(__float_as_int(fy0))), fy3 = __int_as_float(quad_xor1(__float_as_int(fy1)));
+    bool ok = false;
+    const int rw = brx - tlx, rh = bry - tly;
+    if (h == 0 && all_in && rw > 0 && rh > 0) {
+        const float ftx = (float)tlx, fty = (float)tly;
+        const double x[4] = {(double)(fx0 - ftx), (double)(fx1 - ftx), (double)(fx2 - ftx), (double)(fx3 - ftx)};
+        const double y[4] = {(double)(fy0 - fty), (double)(fy1 - fty), (double)(fy2 - fty), (double)(fy3 - fty)};
+        dpg::TexMap tm;
+        ok = dpg::quad_map(x, y, tlx, tly, rw, rh, cell, tm);
+        if (ok) {
+            tm.m6 *= 0.03125;
+            tm.m7 *= 0.03125;
+            tm.m8 *= 0.03125;
+            L.map[slot] = tm;
+            L.roi[slot] = narrow ? (uint64_t)(vw.img_off + ((uint32_t)tm.tly * (uint32_t)vw.pitch + (uint32_t)tm.tlx) * 4u)
+                                 : (uint64_t)(uintptr_t)(vw.img + ((size_t)tm.tly * (size_t)vw.pitch + (size_t)tm.tlx));
+            L.pitch[slot] = vw.pitch;
+        }
+    }
+    const uint64_t okq = __ballot(ok); // bit 2k <- view slot round0 + k
+    uint64_t bits = 0;
+    for (int q = 0; q < 32; ++q)
+        bits |= ((okq >> (2 * q)) & 1ull) << q;
     return bits << round0;
 }
 
@@ -843,13 +902,18 @@ __device__ __forceinline__ int wave_scores(const RefineArgs &a, WaveLds &L, cons
         // diagnostic build (timing only): the idempotent map build runs twice
         for (int rep = 0; rep < 2; ++rep, okmask = rep < 2 ? 0 : okmask)
 #endif
-        for (int r0 = 0; r0 < kMapChunk && base + r0 < m; r0 += 16)
+        if (m - base > 16) {
+            // more than 16 views in this chunk: one round, two lanes per view
+            static_assert(kMapChunk <= 32, "a pair round covers the chunk");
+            okmask = build_maps_pair(load_map_view<1>(a, L, base, m, 0), L, base, m, 0, cell, a.narrow != 0);
+        } else {
 #if DP_PRELOAD_VIEWS
-            okmask |= build_maps_quad((base == 0 && r0 == 0) ? mv0 : load_map_view(a, L, base, m, r0), L, base, m,
-                                      r0, cell, a.narrow != 0);
+            okmask = build_maps_quad(base == 0 ? mv0 : load_map_view(a, L, base, m, 0), L, base, m, 0, cell,
+                                     a.narrow != 0);
 #else
-            okmask |= build_maps_quad(load_map_view(a, L, base, m, r0), L, base, m, r0, cell, a.narrow != 0);
+            okmask = build_maps_quad(load_map_view(a, L, base, m, 0), L, base, m, 0, cell, a.narrow != 0);
 #endif
+        }
         wave_sync();
         STAMP(L, 0);
         // texture 0 = lowest-index visible view (optimization_opencv.cpp:24-28)
