@@ -25,7 +25,7 @@ namespace {
 #endif
 
 #ifndef DP_MAP_CHUNK
-#define DP_MAP_CHUNK 20
+#define DP_MAP_CHUNK 24
 #endif
 constexpr int kMapChunk = DP_MAP_CHUNK; // views whose window maps are built per chunk
 
