@@ -524,6 +524,39 @@ __device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &
     sx = (int)usx;
 }
 
+// The last pass of a chunk when one view is left (G = 2, narrow addressing):
+// both pass slots carry that view and slot j's lanes sample only their texel
+// pair j (texels 2j and 2j+1 of the lane's four: the descriptors of slot 1
+// point into slot 1's tables, filled with the same view), so every lane
+// samples two texels instead of four; the caller sums the moments over the
+// whole wave.  Texel pair j's texture-0 grays are the word anchor_slot(j, g).
+__device__ __forceinline__ void group_sample_split(const RefineArgs &a, const TexDesc &td, int j, uint64_t roi,
+                                                   int pitch, int upitch, int wm32, int hm32, int &s, int &ss, int &sx)
+{
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    static_assert(kTexPerLane == 4, "two texel pairs per lane");
+    constexpr int LP = kWave / 2;
+    const bool hi = j != 0;
+    const uint32_t ra0 = hi ? td.ra[2] : td.ra[0], ra1 = hi ? td.ra[3] : td.ra[1];
+    const uint32_t ca0 = hi ? td.ca[2] : td.ca[0], ca1 = hi ? td.ca[3] : td.ca[1];
+    const uint32_t sel = hi ? td.sel[1] : td.sel[0];
+    const gbyte_t base1 = (gbyte_t)a.img_base + (uint32_t)(upitch * 4);
+    int32_t ix, iy;
+    texel_coord_d(ra0, ca0, ix, iy);
+    const TexelLoad t0 = texel_fetch_n<true>((gbyte_t)a.img_base, base1, (uint32_t)roi, pitch * 4, wm32, hm32, ix, iy);
+    __builtin_amdgcn_sched_barrier(0);
+    texel_coord_d(ra1, ca1, ix, iy);
+    const TexelLoad t1 = texel_fetch_n<true>((gbyte_t)a.img_base, base1, (uint32_t)roi, pitch * 4, wm32, hm32, ix, iy);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t gg = __builtin_amdgcn_perm(texel_gray_hi(t1), texel_gray_hi(t0), sel);
+    const uint32_t aa = *(lds_u32_t)(uintptr_t)(td.anc + 4u * (uint32_t)LP * (uint32_t)j);
+    const us2 vg = __builtin_bit_cast(us2, gg);
+    const us2 ones = {1, 1};
+    s = (int)__builtin_amdgcn_udot2(vg, ones, 0u, false);
+    ss = (int)__builtin_amdgcn_udot2(vg, vg, 0u, false);
+    sx = (int)__builtin_amdgcn_udot2(vg, __builtin_bit_cast(us2, aa), 0u, false);
+}
+
 struct Moments {
     int s, ss, sx;
 };
@@ -569,9 +602,13 @@ __device__ __attribute__((noinline)) Moments group_sample_clamped(WaveLds &L, in
 
 // Integer moments of up to G views (chunk slots in q; with kAnchor, pass slot
 // 0 is texture 0 and its Sa, Saa are returned in sa/saa) into L.mom[slot].
-template <int G, bool kAnchor>
+// kSplit (G = 2, not the anchor pass, narrow addressing): q names the same
+// view in both slots -- group_sample_split's half-texel pass, moments summed
+// over the wave (the clamped fallback samples it on slot 0's lanes only).
+template <int G, bool kAnchor, bool kSplit = false>
 __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, const TexDesc &td, int base, uint64_t q, int &sa, int &saa)
 {
+    static_assert(!kSplit || (G == 2 && !kAnchor), "split passes: G = 2, no anchor");
     constexpr int LP = kWave / G;
     const int lane = lane_id();
     const int cell = a.cell;
@@ -599,7 +636,15 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
     const uint64_t roi = L.roi[sl]; // narrow: byte offset from a.img_base
     wave_sync();
     int s = 0, ss = 0, sx = 0;
-    if (all_safe) {
+    if (kSplit && all_safe) {
+        group_sample_split(a, td, j, roi, pitch, upitch, wm32, hm32, s, ss, sx);
+    } else if (kSplit) {
+        const gpix_t roip = (gpix_t)(a.img_base + (uint32_t)roi);
+        const Moments mm = group_sample_clamped<G, false>(L, a.cell, j, act && j == 0, roip, pitch, wm32, hm32);
+        s = mm.s;
+        ss = mm.ss;
+        sx = mm.sx;
+    } else if (all_safe) {
         if (a.narrow && uni_pitch)
             group_sample_safe<G, kAnchor, true, true>(a, L, td, j, roi, pitch, upitch, wm32, hm32, s, ss, sx);
         else if (a.narrow)
@@ -613,12 +658,15 @@ __device__ __forceinline__ void views_pass(const RefineArgs &a, WaveLds &L, cons
         ss = mm.ss;
         sx = mm.sx;
     }
-    group_total3<G>(s, ss, sx);
+    if (kSplit)
+        group_total3<1>(s, ss, sx); // both slots: the total lands in lane 63
+    else
+        group_total3<G>(s, ss, sx);
     if (kAnchor) {
         sa = __builtin_amdgcn_readlane(s, LP - 1);
         saa = __builtin_amdgcn_readlane(ss, LP - 1);
     }
-    if ((lane & (LP - 1)) == LP - 1 && act && !(kAnchor && j == 0)) {
+    if (kSplit ? lane == kWave - 1 : ((lane & (LP - 1)) == LP - 1 && act && !(kAnchor && j == 0))) {
         L.mom[slot][0] = s;
         L.mom[slot][1] = ss;
         L.mom[slot][2] = sx;
@@ -646,10 +694,14 @@ __device__ __forceinline__ void views_all(const RefineArgs &a, WaveLds &L, const
                 q = (q & ~(0xffull << (8 * s))) | (b << (8 * s));
             }
         }
-        if (first)
+        if (first) {
             views_pass<G, true>(a, L, td, base, q, sa, saa);
-        else
+        } else if (G == 2 && (q >> 8 & 0xffull) == 0xffull && a.narrow) {
+            // one view left: split its texels over both slots
+            views_pass<2, false, true>(a, L, td, base, (q & ~0xff00ull) | ((q & 0xffull) << 8), sa, saa);
+        } else {
             views_pass<G, false>(a, L, td, base, q, sa, saa);
+        }
         first = false;
     }
 }
