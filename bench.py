@@ -13,15 +13,24 @@ after the reference's seed stage (Seed::FilterPatches + OptimizePatches at
 n = 16, run once untimed), so the children look exactly like the ones the BFS
 produces.
 
-N > 1 (torchrun, one process per GPU, RCCL over xGMI): BASELINE config 4 (64
-views 4K, "reference-cell shard across 8 x MI355X with RCCL all-gather of
-accepted patches").  One step = one whole densify (PMVS::Run minus matching,
+N > 1 (one process per GPU, RCCL over xGMI): `value` is the SAME workload as
+at N = 1 -- every rank refines its own fixed-size batch of config-3 expansion
+candidates (candidates are independent, SURVEY 8e: no data-path collective),
+value = all ranks' candidates / max-over-ranks time, "scaling": "weak".  So the
+driver's 1/2/4/8 curve built from `value` divides like quantities.
+`python bench.py --gpus N` launches the N ranks itself (torch.distributed.run,
+started before anything touches the GPU) when it is not already under a
+launcher; every rank checks that its world size equals --gpus.
+
+`scaling_leg` (every N, N = 1 included): BASELINE config 4 (64 views 4K,
+"reference-cell shard across 8 x MI355X with RCCL all-gather of accepted
+patches").  One step = one whole densify (PMVS::Run minus matching,
 pmvs.cpp:22-43) with every BFS generation partitioned by reference-view
 super-tile over the ranks (dist.densify_partitioned_device: device partition,
 refine of the rank's items, ONE RCCL all-gather of the accepted candidates,
-replicated organizer commit); the value is every candidate refined (seed
-stage + expansions) over the max-over-ranks wall time -- strong scaling, the
-same densify at every N.  The weak-scaled refine batch is reported beside it.
+replicated organizer commit); rate = every candidate refined (seed stage +
+expansions) over the max-over-ranks wall time -- strong scaling, the same
+densify at every N, under the same key at every N.
 
 Prints ONE JSON line (rank 0).
 """
@@ -46,9 +55,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default=None, help="default: cfg3_32view_4k at N = 1, cfg4_64view_4k at N > 1")
+    ap.add_argument("--config", default=None, help="default: cfg3_32view_4k (the headline at every N)")
     ap.add_argument("--densify-steps", type=int, default=2,
-                    help="N = 1: partitioned-densify repetitions of the informational config-4 leg")
+                    help="timed whole-densify repetitions of scaling_leg (config 4, every N)")
     ap.add_argument("--batch", type=int, default=262144, help="expansion candidates per step per GPU")
     ap.add_argument("--cell", type=int, default=11)
     ap.add_argument("--cpu-parents", type=int, default=5000,
@@ -58,7 +67,6 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-densify", action="store_true", help="skip the informational end-to-end densify")
-    ap.add_argument("--traffic-json", default=None, help="measured HBM bytes/launch from profiles/")
     ap.add_argument("--no-seeds", action="store_true", help="skip the informational seed generation")
     ap.add_argument("--knn-rows", type=int, default=40000, help="descriptors per side of the kNN kernel timing")
     ap.add_argument("--mode", choices=["parity", "fast"], default="parity",
@@ -74,16 +82,47 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` outside a launcher: start N ranks of this script
+    with torch.distributed.run (127.0.0.1 rendezvous on a free port) as a child
+    process -- nothing here has touched the GPU -- and return its exit code.
+    Rank 0 prints the JSON line; a failing rank fails the launcher."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    print("bench: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
+def lib_stamp(path: str) -> str:
+    """sha256 (16 hex digits) of the loaded libdensepoints.so: profiles/ record
+    it, and bench attaches a profile's counters only to the library they were
+    measured on (the build is deterministic: same sources + flags, same bytes)."""
+    import hashlib
+
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     import densepoints_amd as dp
     from densepoints_amd import _native as N
     from densepoints_amd import dist as D
     from densepoints_amd import synth
 
     rank, world, local = D.env()
+    if world != args.gpus:
+        raise SystemExit(f"bench: world size {world} != --gpus {args.gpus}")
     if args.config is None:
-        args.config = "cfg3_32view_4k" if world == 1 else "cfg4_64view_4k"
+        args.config = "cfg3_32view_4k"
     # rehearsal knobs for a 1-GPU box (never set by the driver): DP_BENCH_BACKEND=gloo
     # and DP_BENCH_ONE_DEVICE=1 run N ranks on cuda:0 over gloo
     if os.environ.get("DP_BENCH_ONE_DEVICE") == "1":
@@ -279,32 +318,11 @@ def main():
                                       "wall_s": round(wall, 3),
                                       "Mpatches_per_s_refine": round(int(fst["candidates"]) / max(fst["refine_ms"], 1e-9)
                                                                      / 1e3, 3)}
-    if world > 1:
-        # the N > 1 headline: the whole densify on this scene partitioned over the
-        # ranks (strong scaling); the refine batch above becomes the weak-scaled
-        # informational leg
-        dev = torch.device("cuda", local)
-        legs = {m: partitioned_leg(eng, seeds, dist, coll_dev, dev, args.steps, args.warmup, m == "fast")
-                for m in ("parity", "fast")}
-        result["refine_weak_scaled"] = {k: result[k] for k in ("value", "ms_per_step", "kernel_ms_per_launch",
-                                                               "kernel_ms_events", "E_mean_evals_per_patch")}
-        result["refine_weak_scaled"]["note"] = ("per-rank batch of %d expansion candidates, no data-path collective"
-                                                % B)
-        head = legs["parity"]
-        result["value"] = head["Mpatches_per_s"]
-        result["ms_per_step"] = head["ms_per_densify"]
-        result["scaling"] = "strong"
-        result["config"]["workload"] = (
-            f"{args.config}: {V} views {W}x{H}, one step = the whole densify (PMVS::Run minus matching) of "
-            f"{len(seeds)} seed points, every BFS generation partitioned by reference-view super-tile over "
-            f"{world} ranks (RCCL all-gather of the accepted candidates), parity-mode refine (Nelder-Mead, "
-            f"n = 16 seed stage / n = {args.cell} expansions)")
-        result["config"]["parallelism"] = f"dp{world} (reference-view super-tiles, all-gather of accepted patches)"
-        result["densify_partitioned"] = head
-        result["densify_partitioned_fast"] = legs["fast"]
-        eng.set_fast_options(dp.FastOptions())
-    if world == 1 and not args.no_densify and not fast:
-        result["densify_partitioned_cfg4_1gpu"] = cfg4_densify_1gpu(args, stream)
+    result["scaling_curve"] = ("value: weak scaling of the config-3 refine batch (%d candidates per rank, no "
+                               "data-path collective); scaling_leg.<mode>.Mpatches_per_s: strong scaling of the "
+                               "config-4 partitioned densify (the same densify at every N)" % B)
+    if not args.no_densify and not fast:
+        result["scaling_leg"] = scaling_leg(args, stream, dist, coll_dev, torch.device("cuda", local))
     if solo and not args.no_seeds:
         result["seed_generation"] = seed_generation(eng, args)
     st = np.zeros(8, dtype=np.uint64)
@@ -313,24 +331,12 @@ def main():
         result["stamps_share"] = {k: round(float(st[i]) / tot, 4) for i, k in
                                   enumerate(["corners_maps", "view_passes", "sync", "ncc_finish"])}
         result["stamps_share"]["rest_nm_geometry"] = round(1.0 - sum(result["stamps_share"].values()), 4)
+    lib_sha = lib_stamp(N.LIB_PATH)
+    result["lib_sha256"] = lib_sha
     prof = profiled("parity" if not fast else "fast%d" % args.cell,
-                    "refine_kernel<4, 2>" if not fast else fast_kernel_tag(args.cell), B)
-    if prof and not args.traffic_json:
+                    "refine_kernel<4, 2>" if not fast else fast_kernel_tag(args.cell), B, lib_sha)
+    if prof:
         attach_profile(result["roofline"], prof, B, launch_ms)
-    tj = args.traffic_json or (None if prof else latest_traffic_json())
-    if tj and os.path.exists(tj):
-        with open(tj) as f:
-            t = json.load(f)
-        # PMC bytes are per launch, so they only apply to the batch they were measured on
-        if t.get("batch") == result["config"]["batch_per_gpu"] and not fast:
-            # both readings: FETCH_SIZE as counted, and doubled per the gfx950
-            # correction that MI355X_MICROARCH.md calibrates for 16-B/lane
-            # streams (these are 8-B gathers: see "traffic_calibration")
-            result["roofline"]["traffic"] = t.get("hbm_bytes_per_launch")
-            result["roofline"]["traffic_raw"] = t.get("hbm_bytes_per_launch_raw")
-            result["roofline"]["traffic_source"] = os.path.relpath(tj, ROOT)
-            if t.get("calibration"):
-                result["roofline"]["traffic_calibration"] = t["calibration"]
 
     if solo and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, cfg, P, planes, parents, out, fo if fast else None)
@@ -406,10 +412,11 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
             "visibility_filter": vf}
 
 
-def cfg4_densify_1gpu(args, stream):
-    """Informational at N = 1: the N > 1 headline's workload (BASELINE config 4,
-    whole partitioned densify, both refine modes) on one rank, so the 1-GPU
-    point of that curve is in the 1-GPU line."""
+def scaling_leg(args, stream, dist, coll_dev, dev):
+    """The strong-scaling series, under this key at every N (N = 1 included):
+    BASELINE config 4 (64 views 4K), the whole densify with every generation
+    partitioned by reference-view super-tile over the ranks and the accepted
+    candidates all-gathered (RCCL over xGMI), both refine modes."""
     import ctypes
 
     import densepoints_amd as dp
@@ -419,19 +426,22 @@ def cfg4_densify_1gpu(args, stream):
     cfg = synth.named("cfg4_64view_4k")
     P = synth.cameras(cfg)
     V, W, H = cfg.n_views, cfg.width, cfg.height
-    with dp.Engine(dp.Options(expand_cell_size=args.cell), device=torch.cuda.current_device()) as eng:
-        planes = torch.empty((V, H, W), dtype=torch.int32, device="cuda")
+    world = dist.get_world_size() if dist else 1
+    with dp.Engine(dp.Options(expand_cell_size=args.cell), device=dev.index) as eng:
+        planes = torch.empty((V, H, W), dtype=torch.int32, device=dev)
         for v in range(V):
             N.check(N.lib.dp_synth_render_device(eng.handle, ctypes.byref(cfg), N.ptr(P), v, planes[v].data_ptr(),
                                                  stream.cuda_stream), eng.handle)
         torch.cuda.synchronize()
         eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
         seeds = synth.seeds(cfg, P)
-        dev = torch.device("cuda", torch.cuda.current_device())
-        out = {m: partitioned_leg(eng, seeds, None, None, dev, args.densify_steps, 1, m == "fast")
+        out = {m: partitioned_leg(eng, seeds, dist, coll_dev, dev, args.densify_steps, 1, m == "fast")
                for m in ("parity", "fast")}
-        out["workload"] = (f"cfg4_64view_4k: {V} views {W}x{H}, whole densify of {len(seeds)} seed points, "
-                           "one rank (the N > 1 headline's workload)")
+        out["workload"] = (f"cfg4_64view_4k: {V} views {W}x{H}, one step = the whole densify (PMVS::Run minus "
+                           f"matching) of {len(seeds)} seed points, every BFS generation partitioned by "
+                           f"reference-view super-tile over {world} rank(s), accepted candidates all-gathered")
+        out["scaling"] = "strong"
+        out["n_gpus"] = world
         del planes
     return out
 
@@ -585,8 +595,8 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                           "compulsory_GBps": round(comp / kms / 1e6, 2)},
              "quality": quality(cfg, out, acc), "stats": {k: int(v) for k, v in st.items()},
              "fast_options": {k: getattr(fo, k) for k in ("iters", "margin", "tile_budget", "max_views")}}
-        fprof = profiled("fast%d" % cell, fast_kernel_tag(cell), B) if not pset and fo.tile_budget == 6656 \
-            and fo.iters == 4 else None
+        fprof = profiled("fast%d" % cell, fast_kernel_tag(cell), B, lib_stamp(N.LIB_PATH)) \
+            if not pset and fo.tile_budget == 6656 and fo.iters == 4 else None
         if fprof:
             attach_profile(r["roofline"], fprof, B, kms)
         if not args.no_cpu and not pset:
@@ -620,11 +630,13 @@ def fast_kernel_tag(cell):
     return {7: "fast_kernel<4, 3, true, false, 6656, 6>", 11: "fast_kernel<2, 4, false, true, 6656, 6>"}.get(cell, "?")
 
 
-def profiled(workload, kernel, B):
+def profiled(workload, kernel, B, lib_sha):
     """The rocprofv3 record of `kernel` under bench workload `workload`
     (parity | fast7 | fast11) from the latest profiles/rNN/kernel_counters.json
-    (tools/r03_profile.sh + tools/profile_json.py), when it was taken on this
-    batch size (262,144 candidates): per-launch PMC counters and durations."""
+    (tools/r04_profile.sh + tools/profile_json.py), when it was taken on this
+    batch size (262,144 candidates): per-launch PMC counters and durations.
+    The record carries the sha256 stamp of the library it profiled; a record
+    of another library comes back with stale=True and is not attached."""
     import glob
 
     found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_counters.json")))
@@ -634,7 +646,8 @@ def profiled(workload, kernel, B):
         t = json.load(f)
     for k, v in t.get(workload, {}).items():
         if kernel in k:
-            return dict(v, kernel=k, source=os.path.relpath(found[-1], ROOT))
+            return dict(v, kernel=k, source=os.path.relpath(found[-1], ROOT),
+                        stale=v.get("lib_sha256") != lib_sha)
     return None
 
 
@@ -645,7 +658,16 @@ def attach_profile(roof, prof, B, launch_ms):
     issue peak 1024 SIMDs x clock / 2 (a wave64 VALU instruction takes two
     cycles of a SIMD-32), with the profiled instructions per candidate (the
     instruction stream is deterministic for this workload) over the live launch
-    time, and the profile's VALU-busy fraction and effective clock."""
+    time, and the profile's VALU-busy fraction, effective clock and wave-cycle
+    split (issuing / waiting on a dependency or pipe / parked on s_waitcnt).
+    Only a profile of the loaded library is attached (roofline.profile_stale
+    says which case applies)."""
+    roof["profile_source"] = prof["source"] + " [" + prof["kernel"] + "]"
+    roof["profile_stale"] = bool(prof["stale"])
+    if prof["stale"]:
+        roof["profile_lib_sha256"] = prof.get("lib_sha256")
+        return
+    roof["profiled_launch_ms"] = round(prof["trace_avg_ns"] * 1e-6, 3)
     if "hbm_bytes_corrected" in prof:
         roof["traffic"] = prof["hbm_bytes_corrected"]
         roof["traffic_raw"] = prof["hbm_bytes_raw"]
@@ -658,18 +680,11 @@ def attach_profile(roof, prof, B, launch_ms):
                         "frac": round(ach / v["issue_peak_at_2.4GHz_Ginst_s"], 4),
                         "effective_clock_GHz": round(v["effective_clock_GHz"], 3),
                         "frac_at_effective_clock": round(ach / v["issue_peak_at_effective_clock_Ginst_s"], 4),
-                        "busy_frac": round(v["busy_frac"], 4),
-                        "profiled_launch_ms": round(prof["trace_avg_ns"] * 1e-6, 3)}
-    roof["profile_source"] = prof["source"] + " [" + prof["kernel"] + "]"
-
-
-def latest_traffic_json():
-    """profiles/<latest round>/refine_traffic.json: rocprofv3 PMC HBM bytes per
-    launch of the expansion kernel, collected by tools/gpu_profile.sh"""
-    import glob
-
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "refine_traffic.json")))
-    return found[-1] if found else None
+                        "simd_cycles_per_valu": round(v["simd_cycles_per_valu"], 3)
+                        if "simd_cycles_per_valu" in v else None,
+                        "busy_frac": round(v["busy_frac"], 4)}
+        if "wave_cycles" in v:
+            roof["valu"]["wave_cycles"] = v["wave_cycles"]
 
 
 def host_cores():

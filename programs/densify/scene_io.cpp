@@ -295,9 +295,11 @@ Image load_image(const std::string &path)
     static const uint8_t png_sig[8] = {0x89, 'P', 'N', 'G', 0x0d, 0x0a, 0x1a, 0x0a};
     if (d.size() >= 8 && std::memcmp(d.data(), png_sig, 8) == 0)
         return decode_png(d, path);
+    if (is_jpeg(d))
+        return decode_jpeg(d, path);
     if (d.size() >= 2 && d[0] == 'P' && d[1] == '6')
         return decode_ppm(d, path);
-    throw std::runtime_error(path + ": unsupported image format (PNG or binary PPM)");
+    throw std::runtime_error(path + ": unsupported image format (JPEG, PNG or binary PPM)");
 }
 
 // ---------------------------------------------------------------------------

@@ -1,5 +1,5 @@
 // scene_io.h -- host-side IO of the densify CLI: a small JSON reader (scene and
-// settings files), PNG/PPM image decoding to BGR8, seed files and the ASCII
+// settings files), JPEG/PNG/PPM image decoding to BGR8, seed files and the ASCII
 // PLY writer.  Restates the reference's modules/io surface:
 //   scene JSON  modules/io/json_reader.cpp:9-28 ({"imagesPath", "views": [{
 //               "filename", "projectionMatrix": 3x4}]})
@@ -38,9 +38,15 @@ struct Image {
     std::vector<uint8_t> bgr; // rows of 3*width bytes, B G R as cv::imread returns
 };
 
-// PNG (8-bit gray / gray+alpha / RGB / RGBA, non-interlaced) or binary PPM
-// (P6, maxval 255); chosen by the file's signature.  Throws on anything else.
+// JPEG (baseline / extended sequential / progressive Huffman, 8-bit gray or
+// YCbCr/RGB, EXIF orientation applied; jpeg.cpp), PNG (8-bit gray / gray+alpha
+// / RGB / RGBA, non-interlaced) or binary PPM (P6, maxval 255); chosen by the
+// file's signature.  Throws on anything else.
 Image load_image(const std::string &path);
+
+// the JPEG decoder behind load_image (cv::imread IMREAD_COLOR semantics)
+bool is_jpeg(const std::string &data);
+Image decode_jpeg(const std::string &data, const std::string &path);
 
 // ---- scene ------------------------------------------------------------------
 struct SceneView {

@@ -47,13 +47,29 @@ def one(d):
         for (disp, cn), v in acc.items():
             ctr[name[(disp, cn)]][cn].append(v)
     args = open(os.path.join(d, "args.txt")).read().strip() if os.path.exists(os.path.join(d, "args.txt")) else ""
+    toks = args.split()
+    steps = int(toks[toks.index("--steps") + 1]) if "--steps" in toks else 5
+    # the library the profiled bench loaded: its own JSON line in the trace log
+    lib_sha = None
+    if os.path.exists(os.path.join(d, "trace.log")):
+        for line in open(os.path.join(d, "trace.log")):
+            if line.startswith("{"):
+                try:
+                    lib_sha = json.loads(line).get("lib_sha256", lib_sha)
+                except ValueError:
+                    pass
     for k in set(durs) | set(ctr):
         if not any(s in k for s in KEEP):
             continue
-        e = {"command": "python3 bench.py " + args}
+        e = {"command": "python3 bench.py " + args, "lib_sha256": lib_sha}
         if k in durs:
-            e["trace_avg_ns"] = statistics.fmean(durs[k])
-            e["trace_launches"] = len(durs[k])
+            # the bench's timed launches are the last --steps of the kernel's
+            # dispatches (the first are its untimed warm-up, clocks settling)
+            timed = durs[k][-steps:] if len(durs[k]) > steps else durs[k]
+            e["trace_avg_ns"] = statistics.fmean(timed)
+            e["trace_launches"] = len(timed)
+            e["trace_avg_all_ns"] = statistics.fmean(durs[k])
+            e["trace_launches_all"] = len(durs[k])
         if k in stats:
             e["stats"] = stats[k]
         c = {n: statistics.fmean(v) for n, v in ctr.get(k, {}).items()}
@@ -70,7 +86,18 @@ def one(d):
                 "busy_frac": 4.0 * c.get("SQ_ACTIVE_INST_VALU", 0.0) / (SIMDS * clk * 1e9 * t),
                 "issue_peak_at_effective_clock_Ginst_s": SIMDS * clk / 2.0,
                 "issue_peak_at_2.4GHz_Ginst_s": SIMDS * CLOCK_GHZ / 2.0,
+                # SIMD cycles of wall time per wave-instruction of VALU (2 = the
+                # issue peak; a fp64 add/mul/fma takes 4, a transcendental 8)
+                "simd_cycles_per_valu": SIMDS * clk * 1e9 * t / c["SQ_INSTS_VALU"],
             }
+            wc = c.get("SQ_WAVE_CYCLES")
+            if wc and "SQ_WAIT_ANY" in c and "SQ_WAIT_INST_ANY" in c and "SQ_ACTIVE_INST_ANY" in c:
+                # disjoint split of wave lifetime (MI355X_MICROARCH.md, PMC slots)
+                e["valu"]["wave_cycles"] = {
+                    "issuing_frac": c["SQ_ACTIVE_INST_ANY"] / wc,
+                    "wait_inst_frac": c["SQ_WAIT_INST_ANY"] / wc,
+                    "wait_any_frac": c["SQ_WAIT_ANY"] / wc,
+                }
         out[k] = e
     return out
 
