@@ -357,8 +357,12 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
     from densepoints_amd import dist as D
 
     eng.set_fast_options(dp.FastOptions(densify=1 if fast else 0))
-    for _ in range(warmup):
-        D.densify_partitioned_device(eng, seeds, dist, dev)
+    probe = None
+    for i in range(warmup):
+        # the untimed warm-up also computes the partitions world sizes 2 and 8
+        # would use on the same generations (statistics only)
+        _, wst = D.densify_partitioned_device(eng, seeds, dist, dev, probe_worlds=(2, 8) if i == 0 else ())
+        probe = probe or wst.get("partition_probe")
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -403,13 +407,25 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
             "accepted_exchanged": int(sum(st["accepted"])),
             "gathered_MB_total": round(sum(gb) / 1e6, 3), "gathered_MB_max_generation": round(max(gb) / 1e6, 3),
             "gathered_MB_per_generation_mean": round(sum(gb) / len(gb) / 1e6, 4),
-            "tile_partitioned_generations": sum(1 for _, _, fb in parts if not fb),
-            "round_robin_generations": sum(1 for _, _, fb in parts if fb),
-            "max_share_vs_mean": round(max((mx * world / it) for it, mx, _ in parts if it > 0), 3),
+            "partition": partition_summary(parts, world),
+            "partition_probe": {str(w): partition_summary(p, w) for w, p in (probe or {}).items()},
             "collective": "all_gather_into_tensor of the accepted candidates' 80-B records (+ 8-B counts), " +
                           ("RCCL over xGMI" if dist is not None and dist.get_backend() == "nccl" else
                            "none (one rank)" if dist is None else dist.get_backend()),
             "visibility_filter": vf}
+
+
+def partition_summary(parts, world):
+    """Per-densify summary of the super-tile partition records (items, largest
+    share, items in tiles split between ranks, tiles) of every generation."""
+    items = sum(p[0] for p in parts)
+    big = [p for p in parts if p[0] >= 64 * world]  # generations large enough to share evenly
+    return {"world": world, "generations": len(parts), "items": items,
+            "tile_partitioned_item_frac": round(1.0 - sum(p[2] for p in parts) / max(items, 1), 5),
+            "max_share_vs_mean": round(max((p[1] * world / p[0]) for p in parts if p[0] > 0), 4) if parts else None,
+            "max_share_vs_mean_items_ge_64_per_rank": round(max(p[1] * world / p[0] for p in big), 4) if big else None,
+            "item_weighted_share_vs_mean": round(sum(p[1] * world for p in parts) / max(items, 1), 4),
+            "tiles_mean": round(sum(p[3] for p in parts) / max(len(parts), 1), 1)}
 
 
 def scaling_leg(args, stream, dist, coll_dev, dev):

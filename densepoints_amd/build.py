@@ -112,7 +112,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     tmp = out + ".tmp"
     subprocess.run([hipcc(), *FLAGS, *extra, "-o", tmp, *objs], check=True, cwd=CSRC)
     os.replace(tmp, out)
-    if not extra:
+    # only the default library's own build records the default flags (a
+    # DP_LIB_NAME link elsewhere leaves the default library -- and its stamp -- alone)
+    if not extra and os.path.abspath(out) == os.path.abspath(OUT):
         with open(OUT + ".flags", "w") as f:
             f.write(_stamp_text())
     return out

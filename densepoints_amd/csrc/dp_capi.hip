@@ -235,11 +235,12 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->cellmin.release();
     c->pend.release();
     c->granted.release();
+    c->tkeys.release();
     c->okeys.release();
     c->oiota.release();
     c->porder.release();
+    c->olo.release();
     c->ocount.release();
-    c->owners.release();
     c->items.release();
     c->seedp.release();
     c->lpt.release();
@@ -875,11 +876,17 @@ static int reset_grid(dp_ctx *c, hipStream_t s)
     return DP_OK;
 }
 
-// patch store capacity: every accepted patch holds >= 2 claims and a cell
-// takes at most max_patches_per_cell of them
-static int64_t store_capacity(const dp_ctx *c)
+// patch store capacity, the smaller of two bounds on the accepted patches:
+// every accepted patch holds >= 2 claims and a cell takes at most
+// max_patches_per_cell of them; and the store holds at most the seed patches
+// plus 4 children per pop, pops <= max_pops (expand.cpp:95).  (The first alone
+// reserved ~42 GB at config 5 with k = 16.)
+static int64_t store_capacity(const dp_ctx *c, int64_t nseeds)
 {
-    return (int64_t)c->opt.max_patches_per_cell * c->grid_cells / 2 + 16;
+    const int64_t by_cells = (int64_t)c->opt.max_patches_per_cell * c->grid_cells / 2;
+    const int64_t pops = c->opt.max_pops > 0 ? c->opt.max_pops : 0;
+    const int64_t by_pops = nseeds + 4 * pops;
+    return (by_cells < by_pops ? by_cells : by_pops) + 16;
 }
 
 static int organize(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int32_t n, uint32_t seq0,
@@ -948,7 +955,7 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
     int rg = reset_grid(c, s);
     if (rg != DP_OK)
         return rg;
-    const int64_t store_cap = store_capacity(c);
+    const int64_t store_cap = store_capacity(c, n);
     DP_HIP(c, c->store.reserve((size_t)store_cap));
     DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
 
@@ -1076,7 +1083,7 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
     int rg = reset_grid(c, s);
     if (rg != DP_OK)
         return rg;
-    DP_HIP(c, c->store.reserve((size_t)store_capacity(c)));
+    DP_HIP(c, c->store.reserve((size_t)store_capacity(c, n)));
     DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
     if (n > 0) {
         std::vector<dp_patch> sp(n);
@@ -1232,38 +1239,82 @@ extern "C" int dp_densify_commit_device(dp_ctx *c, dp_generation *gen, const dp_
 
 // ---- partitioned generations (reference-view super-tiles) -------
 
+// The partition of a generation (spec in include/densepoints.h):
+// items stable-sorted by super-tile key, the order cut into `world` contiguous
+// shares lo[r] = floor(r n / world).  Leaves the order in c->porder (complete
+// on return), the shares in counts (host) and the statistics in c->part_stats.
+static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int tile_px, int64_t *counts)
+{
+    const int64_t n = gen->items;
+    for (int r = 0; r < world; ++r)
+        counts[r] = (int64_t)(((__int128)(r + 1) * n) / world - ((__int128)r * n) / world);
+    c->part_stats[0] = n;
+    c->part_stats[1] = world;
+    c->part_stats[2] = c->part_stats[3] = 0;
+    if (n == 0)
+        return DP_OK;
+    if (n > INT32_MAX)
+        return fail(c, DP_E_OOM, "partition: generation too large");
+    hipStream_t s = c->stream;
+    const dp_patch *items = gen->index == 0 ? c->seedp.p : c->store.p + gen->head;
+    DP_HIP(c, c->tkeys.reserve((size_t)n));
+    DP_HIP(c, c->okeys.reserve((size_t)n));
+    DP_HIP(c, c->oiota.reserve((size_t)n));
+    DP_HIP(c, c->porder.reserve((size_t)n));
+    DP_HIP(c, c->olo.reserve(65));
+    DP_HIP(c, c->ocount.reserve(2));
+    DP_HIP(c, dpk::launch_tile_keys(c->d_views, items, n, (double)tile_px, c->tkeys.p, s));
+    DP_HIP(c, dpk::launch_iota(c->oiota.p, n, s));
+    size_t tmp = 0;
+    DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, c->tkeys.p, c->okeys.p, c->oiota.p, c->porder.p, (int)n,
+                                                 0, 64, s));
+    DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
+    DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->scan_tmp.p, tmp, c->tkeys.p, c->okeys.p, c->oiota.p, c->porder.p,
+                                                 (int)n, 0, 64, s));
+    std::vector<int64_t> lo((size_t)world + 1, 0);
+    for (int r = 1; r <= world; ++r)
+        lo[(size_t)r] = lo[(size_t)r - 1] + counts[r - 1];
+    DP_HIP(c, hipMemcpyAsync(c->olo.p, lo.data(), sizeof(int64_t) * (world + 1), hipMemcpyHostToDevice, s));
+    DP_HIP(c, dpk::launch_partition_stats(c->okeys.p, n, c->olo.p, world, c->ocount.p, s));
+    unsigned long long st[2] = {0, 0};
+    DP_HIP(c, hipMemcpyAsync(st, c->ocount.p, sizeof(st), hipMemcpyDeviceToHost, s));
+    // the order is read on the caller's stream (refine, compaction): complete it
+    DP_HIP(c, hipStreamSynchronize(s));
+    c->part_stats[2] = (int64_t)st[0];
+    c->part_stats[3] = (int64_t)st[1];
+    return DP_OK;
+}
+
 extern "C" int dp_densify_owners(dp_ctx *c, const dp_generation *gen, int world, int tile_px, int32_t *owner_out,
                                  int32_t *fallback_out)
 {
-    if (!c || !gen || world < 1 || tile_px < 1 || (gen->items > 0 && !owner_out))
-        return fail(c, DP_E_ARG, "dp_densify_owners: bad arguments");
+    if (!c || !gen || world < 1 || world > 64 || tile_px < 1 || (gen->items > 0 && !owner_out))
+        return fail(c, DP_E_ARG, "dp_densify_owners: bad arguments (1 <= world <= 64)");
     if (gen->index != c->g_expected)
         return fail(c, DP_E_STATE, "dp_densify_owners: generation out of sequence");
     const int64_t n = gen->items;
     if (fallback_out)
         *fallback_out = 0;
-    if (n == 0)
-        return DP_OK;
     hipSetDevice(c->device);
-    hipStream_t s = c->stream;
-    const dp_patch *items = gen->index == 0 ? c->seedp.p : c->store.p + gen->head;
-    DP_HIP(c, c->owners.reserve((size_t)n));
-    DP_HIP(c, dpk::launch_owners(c->d_views, items, n, world, (double)tile_px, c->owners.p, s));
-    DP_HIP(c, hipMemcpyAsync(owner_out, c->owners.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
-    DP_HIP(c, hipStreamSynchronize(s));
-    // round robin when the largest share exceeds 1.1x the mean
-    std::vector<int64_t> cnt((size_t)world, 0);
-    for (int64_t i = 0; i < n; ++i)
-        cnt[(size_t)owner_out[i]] += 1;
-    int64_t mx = 0;
-    for (int64_t v : cnt)
-        mx = v > mx ? v : mx;
-    if ((double)mx > 1.1 * (double)n / (double)world) {
-        for (int64_t i = 0; i < n; ++i)
-            owner_out[i] = (int32_t)(i % world);
-        if (fallback_out)
-            *fallback_out = 1;
-    }
+    std::vector<int64_t> counts((size_t)world);
+    int rc = partition_impl(c, gen, world, tile_px, counts.data());
+    if (rc != DP_OK || n == 0)
+        return rc;
+    std::vector<int64_t> order((size_t)n);
+    DP_HIP(c, hipMemcpy(order.data(), c->porder.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+    int64_t j = 0;
+    for (int r = 0; r < world; ++r)
+        for (int64_t k = 0; k < counts[r]; ++k, ++j)
+            owner_out[order[(size_t)j]] = r;
+    return DP_OK;
+}
+
+extern "C" int dp_densify_partition_stats(dp_ctx *c, int64_t *stats_out)
+{
+    if (!c || !stats_out)
+        return fail(c, DP_E_ARG, "dp_densify_partition_stats: bad arguments");
+    for (int k = 0; k < 4; ++k)
+        stats_out[k] = c->part_stats[k];
     return DP_OK;
 }
 
@@ -1371,15 +1422,6 @@ extern "C" int dp_densify_commit_items_device(dp_ctx *c, dp_generation *gen, con
 }
 
 
-// round robin when the largest share exceeds 1.1x the mean (dp_densify_owners)
-static bool partition_falls_back(const std::vector<int64_t> &cnt, int64_t n, int world)
-{
-    int64_t mx = 0;
-    for (int64_t v : cnt)
-        mx = v > mx ? v : mx;
-    return (double)mx > 1.1 * (double)n / (double)world;
-}
-
 extern "C" int dp_densify_partition_device(dp_ctx *c, const dp_generation *gen, int world, int tile_px,
                                            const int64_t **d_order_out, int64_t *counts_out, int32_t *fallback_out)
 {
@@ -1387,55 +1429,15 @@ extern "C" int dp_densify_partition_device(dp_ctx *c, const dp_generation *gen, 
         return fail(c, DP_E_ARG, "dp_densify_partition_device: bad arguments (1 <= world <= 64)");
     if (gen->index != c->g_expected)
         return fail(c, DP_E_STATE, "dp_densify_partition_device: generation out of sequence");
-    const int64_t n = gen->items;
     *d_order_out = nullptr;
-    for (int r = 0; r < world; ++r)
-        counts_out[r] = 0;
     if (fallback_out)
         *fallback_out = 0;
-    if (n == 0)
-        return DP_OK;
-    if (n > INT32_MAX)
-        return fail(c, DP_E_OOM, "dp_densify_partition_device: generation too large");
     hipSetDevice(c->device);
-    hipStream_t s = c->stream;
-    const dp_patch *items = gen->index == 0 ? c->seedp.p : c->store.p + gen->head;
-    DP_HIP(c, c->owners.reserve((size_t)n));
-    DP_HIP(c, c->ocount.reserve(64));
-    DP_HIP(c, dpk::launch_owners(c->d_views, items, n, world, (double)tile_px, c->owners.p, s));
-    DP_HIP(c, dpk::launch_count_owners(c->owners.p, n, world, c->ocount.p, s));
-    std::vector<unsigned long long> h((size_t)world);
-    DP_HIP(c, hipMemcpyAsync(h.data(), c->ocount.p, sizeof(unsigned long long) * world, hipMemcpyDeviceToHost, s));
-    DP_HIP(c, hipStreamSynchronize(s));
-    std::vector<int64_t> cnt(h.begin(), h.end());
-    if (partition_falls_back(cnt, n, world)) {
-        DP_HIP(c, dpk::launch_round_robin(c->owners.p, n, world, s));
-        for (int r = 0; r < world; ++r)
-            cnt[(size_t)r] = n / world + (r < n % world ? 1 : 0);
-        if (fallback_out)
-            *fallback_out = 1;
-    }
-    // stable partition: radix sort of (owner, item index) pairs on the owner bits
-    int bits = 1;
-    while ((1 << bits) < world)
-        ++bits;
-    DP_HIP(c, c->okeys.reserve((size_t)n));
-    DP_HIP(c, c->oiota.reserve((size_t)n));
-    DP_HIP(c, c->porder.reserve((size_t)n));
-    DP_HIP(c, dpk::launch_iota(c->oiota.p, n, s));
-    const uint32_t *kin = (const uint32_t *)c->owners.p;
-    uint32_t *kout = (uint32_t *)c->okeys.p;
-    size_t tmp = 0;
-    DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, c->oiota.p, c->porder.p, (int)n, 0, bits, s));
-    DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
-    DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->scan_tmp.p, tmp, kin, kout, c->oiota.p, c->porder.p, (int)n, 0,
-                                                 bits, s));
-    // the order is read on the caller's stream (refine, compaction): complete it
-    // before returning, like the counts
-    DP_HIP(c, hipStreamSynchronize(s));
-    for (int r = 0; r < world; ++r)
-        counts_out[r] = cnt[(size_t)r];
-    *d_order_out = c->porder.p;
+    const int rc = partition_impl(c, gen, world, tile_px, counts_out);
+    if (rc != DP_OK)
+        return rc;
+    if (gen->items > 0)
+        *d_order_out = c->porder.p;
     return DP_OK;
 }
 
@@ -1446,6 +1448,8 @@ extern "C" int dp_densify_compact_accepted_device(dp_ctx *c, const dp_generation
     if (!c || !gen || n < 0 || !n_out || (n > 0 && (!d_items || !d_cand || !d_accept || !d_out)))
         return fail(c, DP_E_ARG, "dp_densify_compact_accepted_device: bad arguments");
     *n_out = 0;
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_compact_accepted_device: generation out of sequence");
     const int64_t m = n * gen->per_item;
     if (m == 0)
         return DP_OK;

@@ -105,11 +105,12 @@ struct dp_ctx {
     // generation-at-a-time densify (dp_densify_begin/refine/commit/result)
     DevBuf<dp_patch> seedp;  // seed patches of generation 0
     DevBuf<int64_t> items;   // item list of a partitioned refine / commit
-    DevBuf<int32_t> owners;  // owner rank per item (dp_densify_owners)
-    // dp_densify_partition_device: sorted owners, item order, per-rank counts
-    DevBuf<int32_t> okeys;
-    DevBuf<int64_t> oiota, porder;
+    // partitioned generations: super-tile keys, key-sorted keys and item order
+    // (the rank-major order), the cut positions, partition statistics
+    DevBuf<uint64_t> tkeys, okeys;
+    DevBuf<int64_t> oiota, porder, olo;
     DevBuf<unsigned long long> ocount;
+    int64_t part_stats[4] = {0, 0, 0, 0}; // items, world, tiles, items in split tiles
     int64_t g_np = 0;        // patches in the replicated store
     int64_t g_nseeds = 0;
     int64_t g_expected = -1; // generation index the next commit must carry

@@ -224,12 +224,14 @@ template <int P> __device__ __forceinline__ void partial_total3(uint32_t &a, uin
                  "v_add_u32_dpp %2, %2, %2 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
                  : "+v"(a), "+v"(b), "+v"(c));
     if (P >= 8)
-        asm volatile("v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        asm volatile("s_nop 1\n\t"
+                     "v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
                      "v_add_u32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
                      "v_add_u32_dpp %2, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1"
                      : "+v"(a), "+v"(b), "+v"(c));
     if (P >= 16)
-        asm volatile("v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        asm volatile("s_nop 1\n\t"
+                     "v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
                      "v_add_u32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
                      "v_add_u32_dpp %2, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1"
                      : "+v"(a), "+v"(b), "+v"(c));

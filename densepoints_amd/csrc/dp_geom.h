@@ -41,13 +41,14 @@ DP_HD void cross3(const double *a, const double *b, double *o)
 }
 
 // a / b and sqrt(a) of the per-evaluation uniform math (NCC finish, window
-// scale, means).  DP_FAST_DIV=1 (the default since r03: +0.9% on the parity
-// headline, 3.493 vs 3.462 Mpatches/s over three alternations on one box)
-// routes them through the fp32-seeded dp_devmath.h div_rn / sqrt_rn (no slow
-// f64 transcendental; the exactness caveat of DESIGN.md, checked bitwise on
-// the GPU); DP_FAST_DIV=0 keeps the library's IEEE sequences.
+// scale, means).  These quotients feed Nelder-Mead's comparisons and the
+// stored score directly -- no later rounding absorbs a 1-ulp error -- so the
+// default (DP_FAST_DIV=0, since r04) is the IEEE-correct library sequence.
+// DP_FAST_DIV=1 routes them through the fp32-seeded dp_devmath.h div_rn /
+// sqrt_rn (r03's default, +0.9% on the parity headline, within noise), which
+// carry the exactness caveat of DESIGN.md.
 #ifndef DP_FAST_DIV
-#define DP_FAST_DIV 1
+#define DP_FAST_DIV 0
 #endif
 DP_HD double dvdiv(double a, double b)
 {

@@ -105,14 +105,14 @@ hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand,
                          int64_t parent0, int is_seed, hipStream_t s);
 hipError_t launch_render(const dp_synth_config &cfg, const double *P, uint32_t *out, int v,
                          hipStream_t s);
-// multi-GPU partition of a generation's items (dp_densify_owners)
-hipError_t launch_owners(const dpg::ViewDev *views, const dp_patch *items, int64_t n, int world, double tile,
-                         int32_t *owner, hipStream_t s);
+// multi-GPU partition of a generation's items: super-tile keys
+// (ref, tile row, tile column) of the items' centres, and the statistics of a
+// cut of the key-sorted order at lo[1..world-1] (stats[2], zeroed here)
+hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
+                            uint64_t *key, hipStream_t s);
+hipError_t launch_partition_stats(const uint64_t *key, int64_t n, const int64_t *lo, int world,
+                                  unsigned long long *stats, hipStream_t s);
 hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s);
-// device-side partition of a generation: per-rank counts of the owners (atomics
-// into counts[world], zeroed here), round-robin owners, 0..n-1
-hipError_t launch_count_owners(const int32_t *owner, int64_t n, int world, unsigned long long *counts, hipStream_t s);
-hipError_t launch_round_robin(int32_t *owner, int64_t n, int world, hipStream_t s);
 hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s);
 // accepted candidates of items[0..n) (per_item each), out[prefix[j]] = cand[j]
 // with seq = items[j / per] * per + j % per (the generation position)

@@ -24,6 +24,12 @@ namespace {
 #define DP_TEX_PER_LANE 4
 #endif
 
+// texels whose fp64 coordinate chains the scheduler may interleave in a pass
+// (a scheduling barrier after every DP_TEX_ILP texels)
+#ifndef DP_TEX_ILP
+#define DP_TEX_ILP 1
+#endif
+
 #ifndef DP_MAP_CHUNK
 #define DP_MAP_CHUNK 24
 #endif
@@ -487,9 +493,10 @@ __device__ __forceinline__ void group_sample_safe(const RefineArgs &a, WaveLds &
             tl[i] = texel_fetch_n<kUniPitch>((gbyte_t)a.img_base, base1, (uint32_t)roi, pitch * 4, wm32, hm32, ix, iy);
         else
             tl[i] = texel_fetch((gpix_t)roi, pitch, wm32, hm32, ix, iy);
-        // one texel's fp64 coordinate math at a time: only the issued loads
-        // stay live across the pass
-        __builtin_amdgcn_sched_barrier(0);
+        // DP_TEX_ILP texels' fp64 coordinate math at a time: only the issued
+        // loads stay live across the pass
+        if ((i + 1) % DP_TEX_ILP == 0)
+            __builtin_amdgcn_sched_barrier(0);
     }
     // one consume phase for all lanes (no divergence): grays packed in u16
     // pairs, moments as u16 dot products.  In the anchor pass the texture-0
@@ -1915,25 +1922,23 @@ hipError_t launch_refine(const RefineArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
-// Owner rank of each item: the centre projected into its
-// reference view, super-tile (ref, floor(v / tile), floor(u / tile)) hashed.
-__device__ __forceinline__ uint32_t owner_hash(uint32_t ref, uint32_t ty, uint32_t tx)
+// Super-tile key of each item: the centre projected into its
+// reference view, key = ref << 56 | ty' << 28 | tx' with ty = floor(v / tile),
+// tx = floor(u / tile) clamped to [-2^27, 2^27) and biased by 2^27 (NaN and
+// out-of-range coordinates count as 0).  Sorting by key orders the items by
+// (reference view, tile row, tile column); the partition cuts that order into
+// `world` contiguous equal shares.
+__device__ __forceinline__ uint64_t tile_coord(double q)
 {
-    uint32_t h = (ref * 73856093u) ^ (ty * 19349663u) ^ (tx * 83492791u);
-    h ^= h >> 16;
-    h *= 0x85ebca6bu;
-    h ^= h >> 13;
-    return h;
+    int64_t t = 0;
+    if (q > -2.0e9 && q < 2.0e9)
+        t = (int64_t)floor(q);
+    t = t < -(1ll << 27) ? -(1ll << 27) : t > (1ll << 27) - 1 ? (1ll << 27) - 1 : t;
+    return (uint64_t)(t + (1ll << 27));
 }
 
-__device__ __forceinline__ uint32_t tile_coord(double q)
-{
-    // floor to int32 (wraps through uint32); NaN and out-of-range go to 0
-    return (q > -2.0e9 && q < 2.0e9) ? (uint32_t)(int32_t)floor(q) : 0u;
-}
-
-__global__ void owners_kernel(const dpg::ViewDev *views, const dp_patch *items, int64_t n, int world, double tile,
-                              int32_t *owner)
+__global__ void tile_keys_kernel(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
+                                 uint64_t *key)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
@@ -1942,7 +1947,56 @@ __global__ void owners_kernel(const dpg::ViewDev *views, const dp_patch *items, 
     const dpg::ViewDev &v = views[p.ref];
     double u, w;
     dpg::project(v.P, (double)p.pos[0], (double)p.pos[1], (double)p.pos[2], u, w);
-    owner[i] = (int32_t)(owner_hash(p.ref, tile_coord(w / tile), tile_coord(u / tile)) % (uint32_t)world);
+    key[i] = (uint64_t)(p.ref & 0xffu) << 56 | tile_coord(w / tile) << 28 | tile_coord(u / tile);
+}
+
+// partition statistics over the key-sorted items: stats[0] = distinct tiles,
+// stats[1] = items of the tiles a cut lo[r] (0 < lo[r] < n) splits between ranks
+__global__ void partition_stats_kernel(const uint64_t *key, int64_t n, const int64_t *lo, int world,
+                                       unsigned long long *stats)
+{
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long heads = 0, split = 0;
+    if (j < n) {
+        const uint64_t k = key[j];
+        heads = (j == 0 || key[j - 1] != k) ? 1ull : 0ull;
+        for (int r = 1; r < world; ++r) {
+            const int64_t c = lo[r];
+            if (c > 0 && c < n && key[c - 1] == key[c] && key[c] == k) {
+                split = 1;
+                break;
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        heads += __shfl_xor(heads, o);
+        split += __shfl_xor(split, o);
+    }
+    if ((threadIdx.x & 63) == 0 && (heads | split)) {
+        atomicAdd(&stats[0], heads);
+        atomicAdd(&stats[1], split);
+    }
+}
+
+hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
+                            uint64_t *key, hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(tile_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, views, items, n, tile,
+                       key);
+    return hipGetLastError();
+}
+
+hipError_t launch_partition_stats(const uint64_t *key, int64_t n, const int64_t *lo, int world,
+                                  unsigned long long *stats, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(unsigned long long), s);
+    if (e != hipSuccess || n <= 0)
+        return e;
+    hipLaunchKernelGGL(partition_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, key, n, lo, world,
+                       stats);
+    return hipGetLastError();
 }
 
 __global__ void gather_patches_kernel(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst)
@@ -1961,37 +2015,6 @@ __global__ void scatter_items_kernel(const dp_patch *cand, const uint8_t *acc, c
     const int64_t dst = items[j / per] * per + j % per;
     cand_out[dst] = cand[j];
     acc_out[dst] = acc[j];
-}
-
-hipError_t launch_owners(const dpg::ViewDev *views, const dp_patch *items, int64_t n, int world, double tile,
-                         int32_t *owner, hipStream_t s)
-{
-    if (n <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(owners_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, views, items, n, world,
-                       tile, owner);
-    return hipGetLastError();
-}
-
-__global__ void count_owners_kernel(const int32_t *owner, int64_t n, int world, unsigned long long *counts)
-{
-    // per-block histogram in LDS, one global atomic per (block, rank)
-    __shared__ unsigned long long h[64];
-    if (threadIdx.x < 64)
-        h[threadIdx.x] = 0;
-    __syncthreads();
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&h[owner[i]], 1ull);
-    __syncthreads();
-    if ((int)threadIdx.x < world && h[threadIdx.x])
-        atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
-}
-
-__global__ void round_robin_kernel(int32_t *owner, int64_t n, int world)
-{
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n)
-        owner[i] = (int32_t)(i % world);
 }
 
 __global__ void iota_kernel(int64_t *v, int64_t n)
@@ -2022,25 +2045,6 @@ __global__ void scatter_accepted_kernel(const dp_patch *recs, int64_t n, int64_t
         cand[pos] = recs[i];
         ok[pos] = 1;
     }
-}
-
-hipError_t launch_count_owners(const int32_t *owner, int64_t n, int world, unsigned long long *counts, hipStream_t s)
-{
-    hipError_t e = hipMemsetAsync(counts, 0, sizeof(unsigned long long) * (size_t)world, s);
-    if (e != hipSuccess || n <= 0)
-        return e;
-    const int64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(count_owners_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s, owner,
-                       n, world, counts);
-    return hipGetLastError();
-}
-
-hipError_t launch_round_robin(int32_t *owner, int64_t n, int world, hipStream_t s)
-{
-    if (n <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(round_robin_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, owner, n, world);
-    return hipGetLastError();
 }
 
 hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s)

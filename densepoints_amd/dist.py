@@ -12,9 +12,11 @@ gathered shards in rank order restores the 1-GPU order bit for bit.
 
 The densify BFS is also sharded by REFERENCE-VIEW SUPER-TILE (north star:
 "reference-view grid cells shard across the 8 GPUs"):
-densify_partitioned[_device] hand each rank the generation items whose centre
-falls in its hashed (ref, v/64, u/64) tiles (dp_densify_owners), all-gather the
-candidates, put them back in sequence order and commit -- still bit-exact.
+densify_partitioned[_device] sort each generation's items by the (ref, v/64,
+u/64) super-tile of their centre and hand rank r the r-th of `world`
+contiguous equal shares of that order (dp_densify_owners / _partition_device),
+all-gather the candidates, put them back in sequence order and commit -- still
+bit-exact.
 """
 from __future__ import annotations
 
@@ -202,23 +204,31 @@ def partition(owners: np.ndarray, world: int):
     return order, counts, offsets
 
 
+def _part_record(eng, counts) -> tuple:
+    """(items, largest share, items in tiles split between ranks, tiles) of the
+    partition just computed"""
+    st = eng.densify_partition_stats()
+    return (st["items"], int(np.max(counts)) if len(counts) else 0, st["split_items"], st["tiles"])
+
+
 def densify_partitioned(eng, seeds_xyz, dist, device: torch.device | None = None, tile_px: int = 64):
     """dp_densify with every generation partitioned by reference-view super-tile
-    (dp_densify_owners: (ref, floor(v/tile), floor(u/tile)) hashed to a rank,
-    round robin when the largest share exceeds 1.1x the mean).  Each rank
+    (dp_densify_owners: items sorted by their (ref, floor(v/tile),
+    floor(u/tile)) key, the order cut into `world` contiguous equal shares).  Each rank
     refines its own items (dp_densify_refine_items), the candidates are
     all-gathered in rank order, scattered back to sequence order and committed
     by every rank (dp_densify_commit): the replicated store equals dp_densify's
     bit for bit.  Host arrays: `eng` is an Engine or the oracle's
     GenerationEngine (gloo tests on the CPU).  stats gains "partition": per
-    generation (items, largest share, fallback)."""
+    generation (items, largest share, items in split tiles, tiles)."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
     gen = eng.densify_begin(seeds_xyz)
     parts = []
     while gen.items > 0:
-        owners, fallback = eng.densify_owners(gen, world, tile_px)
+        owners, _ = eng.densify_owners(gen, world, tile_px)
         order, counts, offsets = partition(owners, world)
+        parts.append(_part_record(eng, counts))
         mine = order[offsets[rank]: offsets[rank] + counts[rank]]
         cand, acc = eng.densify_refine_items(gen, mine)
         all_cand = allgather_array(cand, dist, device)
@@ -229,7 +239,6 @@ def densify_partitioned(eng, seeds_xyz, dist, device: torch.device | None = None
         item_acc = np.empty_like(all_acc)
         item_cand[pos] = all_cand
         item_acc[pos] = all_acc
-        parts.append((int(gen.items), int(counts.max()), bool(fallback)))
         gen = eng.densify_commit(gen, item_cand, item_acc)
     patches, stats = eng.densify_result()
     stats = _reduce_stats(stats, dist, device)
@@ -253,14 +262,15 @@ class _DeviceBuffers:
         return t
 
 
-def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64):
+def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64,
+                               probe_worlds: tuple = ()):
     """dp_densify with every generation partitioned by reference-view super-tile,
     the records in HBM and only the ACCEPTED candidates exchanged (SURVEY 8e,
     north star: "RCCL all-gather over xGMI of accepted patches").  Per
     generation:
-      1. dp_densify_partition_device: owners (hash of the items' (ref, v/64,
-         u/64) super-tiles, round robin above 1.1x the mean share) and the
-         rank-major item order, on the device; the host reads `world` counts;
+      1. dp_densify_partition_device: the items sorted by their (ref, v/64,
+         u/64) super-tile key and cut into `world` contiguous equal shares (the
+         rank-major item order), on the device; the host reads `world` counts;
       2. this rank refines its slice of that order (dp_densify_refine_items_device);
       3. dp_densify_compact_accepted_device keeps the candidates whose filter
          passed, each tagged with its generation position;
@@ -271,7 +281,10 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
          commits the replicated organizer step on every rank.
     Device buffers are reused across generations.  Every rank's store equals
     dp_densify bit for bit.  stats gains "partition" (items, largest share,
-    fallback), "accepted" and "gathered_bytes" per generation."""
+    items in split tiles, tiles), "accepted" and "gathered_bytes" per
+    generation; with probe_worlds, "partition_probe" {world: the same records}
+    of the partitions those world sizes would use (computed on this rank before
+    the real one; statistics only)."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
     rccl = dist is not None and dist.get_backend() == "nccl"
@@ -280,9 +293,14 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
     pool = _DeviceBuffers(device)
     gen = eng.densify_begin(seeds_xyz)
     parts, gathered, accepted = [], [], []
+    probe = {int(w): [] for w in probe_worlds}
     while gen.items > 0:
         per = gen.per_item
-        d_order, counts, fallback = eng.densify_partition_device(gen, world, tile_px)
+        for w in probe:
+            _, pc, _ = eng.densify_partition_device(gen, w, tile_px)
+            probe[w].append(_part_record(eng, pc))
+        d_order, counts, _ = eng.densify_partition_device(gen, world, tile_px)
+        parts.append(_part_record(eng, counts))
         offs = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
         mine = int(counts[rank])
         d_items = d_order + 8 * int(offs[rank])
@@ -315,7 +333,6 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
                 recv = recv.to(device)
             allr = torch.cat([recv[r * mx * rec: r * mx * rec + ns[r] * rec] for r in range(world)])
             total, gb = sum(ns), world * (mx * rec + 8)
-        parts.append((int(gen.items), int(counts.max()), bool(fallback)))
         gathered.append(gb)
         accepted.append(total)
         gen = eng.densify_commit_accepted_device(gen, allr.data_ptr(), total, stream.cuda_stream)
@@ -324,6 +341,8 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
     stats["partition"] = parts
     stats["gathered_bytes"] = gathered
     stats["accepted"] = accepted
+    if probe:
+        stats["partition_probe"] = probe
     return patches, stats
 
 
@@ -334,7 +353,7 @@ def densify_partitioned_device_all(eng, seeds_xyz, dist, device: torch.device, t
     per array of the padded shards (RCCL over xGMI on "nccl"), trim to the true
     shard sizes, and one commit that scatters the gathered candidates back to
     sequence order on the device (dp_densify_commit_items_device).  stats gains
-    "partition" (items, largest share, fallback) and "gathered_bytes" per
+    "partition" (items, largest share, items in split tiles, tiles) and "gathered_bytes" per
     generation (81 B per candidate slot incl. padding)."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
@@ -345,8 +364,9 @@ def densify_partitioned_device_all(eng, seeds_xyz, dist, device: torch.device, t
     parts, gathered = [], []
     while gen.items > 0:
         per = gen.per_item
-        owners, fallback = eng.densify_owners(gen, world, tile_px)
+        owners, _ = eng.densify_owners(gen, world, tile_px)
         order, counts, offsets = partition(owners, world)
+        parts.append(_part_record(eng, counts))
         sizes = [int(c) * per for c in counts]
         cap = max(max(sizes), 1)
         mine = torch.from_numpy(order[offsets[rank]: offsets[rank] + counts[rank]].copy()).to(device)
@@ -371,7 +391,6 @@ def densify_partitioned_device_all(eng, seeds_xyz, dist, device: torch.device, t
             all_c = torch.cat([gb[r * cap * rec: r * cap * rec + sizes[r] * rec] for r in range(world)])
             all_a = torch.cat([ga[r * cap: r * cap + sizes[r]] for r in range(world)])
         d_order = torch.from_numpy(order).to(device)
-        parts.append((int(gen.items), int(counts.max()), bool(fallback)))
         gathered.append(world * cap * (rec + 1))
         gen = eng.densify_commit_items_device(gen, all_c.data_ptr(), all_a.data_ptr(), d_order.data_ptr(),
                                               len(order), stream.cuda_stream)

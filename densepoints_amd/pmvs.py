@@ -401,11 +401,20 @@ class Engine:
 
     # ---- partitioned generations (reference-view super-tiles) ----
     def densify_owners(self, gen: N.DpGeneration, world: int, tile_px: int = 64):
-        """(owner rank per item, round-robin fallback flag) of the generation."""
+        """(owner rank per item, fallback flag -- always False since the round-4
+        partition spec) of the generation: dp_densify_owners."""
         own = np.zeros(gen.items, dtype=np.int32)
         fb = ctypes.c_int32()
         self._check(lib.dp_densify_owners(self._ctx, ctypes.byref(gen), world, tile_px, ptr(own), ctypes.byref(fb)))
         return own, bool(fb.value)
+
+    def densify_partition_stats(self) -> dict:
+        """The last partition's {items, world, tiles, split_items}
+        (dp_densify_partition_stats): distinct super-tiles, and items in the
+        tiles a cut shares between two ranks."""
+        st = np.zeros(4, dtype=np.int64)
+        self._check(lib.dp_densify_partition_stats(self._ctx, ptr(st)))
+        return {"items": int(st[0]), "world": int(st[1]), "tiles": int(st[2]), "split_items": int(st[3])}
 
     def densify_refine_items(self, gen: N.DpGeneration, items: np.ndarray):
         items = np.ascontiguousarray(items, dtype=np.int64)
@@ -431,7 +440,7 @@ class Engine:
 
     def densify_partition_device(self, gen: N.DpGeneration, world: int, tile_px: int = 64):
         """(device address of the rank-major item order, items per rank (np.int64
-        array), round-robin fallback flag): dp_densify_partition_device."""
+        array), fallback flag -- always False): dp_densify_partition_device."""
         d_order = ctypes.c_void_p()
         counts = np.zeros(world, dtype=np.int64)
         fb = ctypes.c_int32()

@@ -244,18 +244,31 @@ int dp_densify_commit_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_
                              const uint8_t *d_accept, int64_t n_cand, void *stream);
 /* Partitioned generations (north star: "reference-view grid cells shard across
  * the 8 GPUs").  owner_out[i] (host, gen->items) = the rank that
- * refines item i: the item's centre (seed patch or parent) projected into its
- * reference view, super-tile (ref, floor(v/tile_px), floor(u/tile_px)) hashed to
- * [0, world); if the largest share exceeds 1.1x the mean, round robin
- * (i % world) instead and *fallback_out = 1.  Every rank computes the same
- * owners from its replicated store.  Each rank then refines its own items
- * (ascending) with dp_densify_refine_items[_device] -- candidates in list
- * order -- the caller all-gathers them in rank order, and
+ * refines item i.  Partition spec (round 4; round 3 hashed the tiles and fell
+ * back to round robin above 1.1x the mean share):
+ *  - key(i) = ref << 56 | ty' << 28 | tx', the item's centre (seed patch or
+ *    parent) projected into its reference view (fp64, ((p0 x + p1 y) + p2 z) +
+ *    p3, one division per coordinate), ty = floor(v / tile_px), tx =
+ *    floor(u / tile_px) (NaN or |q| >= 2e9 -> 0), clamped to [-2^27, 2^27) and
+ *    biased by 2^27 (ty', tx' < 2^28; ref < 256);
+ *  - the items stable-sorted by key (ties: ascending item index) -- reference
+ *    view, then super-tile row, then column -- and that order cut into `world`
+ *    contiguous shares: rank r refines sorted positions [lo_r, lo_{r+1}),
+ *    lo_r = floor(r * items / world).  Every share is spatially contiguous and
+ *    at most one item above the mean; only the <= world - 1 tiles a cut falls
+ *    in are shared by two ranks.
+ * Every rank computes the same owners from its replicated store.
+ * *fallback_out is always 0 (kept for ABI compatibility).  Each rank then
+ * refines its own items with dp_densify_refine_items[_device] -- candidates in
+ * list order -- the caller all-gathers them in rank order, and
  * dp_densify_commit_items_device scatters the gathered candidates back to item
  * order (d_items = the concatenated item lists, a permutation of the
- * generation) and commits: the store equals dp_densify's bit for bit. */
+ * generation) and commits: the store equals dp_densify's bit for bit.
+ * dp_densify_partition_stats: the last partition's {items, world, distinct
+ * super-tiles, items in tiles split between two ranks}. */
 int dp_densify_owners(dp_ctx *ctx, const dp_generation *gen, int world, int tile_px, int32_t *owner_out,
                       int32_t *fallback_out);
+int dp_densify_partition_stats(dp_ctx *ctx, int64_t *stats_out);
 int dp_densify_refine_items(dp_ctx *ctx, const dp_generation *gen, const int64_t *items, int64_t n,
                             dp_patch *cand_out, uint8_t *accept_out);
 int dp_densify_refine_items_device(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
@@ -264,9 +277,9 @@ int dp_densify_commit_items_device(dp_ctx *ctx, dp_generation *gen, const dp_pat
                                    const int64_t *d_items, int64_t n_items, void *stream);
 /* The same protocol with the partition on the device and only the accepted
  * candidates exchanged (the records that can claim cells):
- *  - dp_densify_partition_device: the owners of dp_densify_owners (same hash,
- *    same round-robin fallback), the generation's items in rank-major order,
- *    ascending within a rank (*d_order_out: context-owned device array, valid
+ *  - dp_densify_partition_device: the partition of dp_densify_owners, the
+ *    generation's items in rank-major order = the key-sorted order
+ *    (*d_order_out: context-owned device array, valid
  *    until the next generation, complete on return so any stream may read
  *    it), items per rank in counts_out[world] (host); world <= 64;
  *  - each rank refines its slice d_order + offset with
@@ -441,7 +454,7 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
 typedef struct dp_fast_options {
     int32_t iters;        /* 4     CG iterations                                    */
     int32_t margin;       /* 2     tile margin around the initial window, px       */
-    int32_t tile_budget;  /* 6144  bytes of LDS tiles per patch (<= 16384; the
+    int32_t tile_budget;  /* 6656  bytes of LDS tiles per patch (<= 16384; the
                                    kernel's arena is 6, 8 or 16 KiB by this value) */
     int32_t max_views;    /* 32    staged views per patch (<= 32)                   */
     float fd_step;        /* 0.5   forward-difference step, scaled units            */

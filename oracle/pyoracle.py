@@ -348,33 +348,47 @@ class GenerationEngine:
 
     # ---- partitioned generations (dp_densify_owners spec) ----
     def densify_owners(self, g, world, tile_px=64):
-        """Owner rank per item: centre projected into the reference view (fp64,
-        ((p0 x + p1 y) + p2 z) + p3 then one division), super-tile hash, round
-        robin when the largest share exceeds 1.1x the mean."""
+        """Owner rank per item (include/densepoints.h, partition spec): the
+        centre projected into the reference view (fp64, ((p0 x + p1 y) + p2 z)
+        + p3 then one division), key = ref << 56 | ty' << 28 | tx' (tile
+        coordinates floored, clamped to [-2^27, 2^27), biased), items stable-
+        sorted by key and cut into `world` contiguous shares lo_r = floor(r n /
+        world).  Returns (owners, False); densify_partition_stats() gives the
+        partition's statistics."""
         items = self.sp if g.index == 0 else np.array(self.store[g.head: g.head + g.items], dtype=PATCH_DTYPE)
-        P = np.stack([self._P[int(r)] for r in items["ref"]]) if len(items) else np.zeros((0, 12))
+        n = len(items)
+        P = np.stack([self._P[int(r)] for r in items["ref"]]) if n else np.zeros((0, 12))
         X = items["pos"].astype(np.float64)
         h = [((P[:, 4 * k] * X[:, 0] + P[:, 4 * k + 1] * X[:, 1]) + P[:, 4 * k + 2] * X[:, 2]) + P[:, 4 * k + 3]
              for k in range(3)]
-        u, w = h[0] / h[2], h[1] / h[2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u, w = h[0] / h[2], h[1] / h[2]
 
         def tc(q):
-            q = q / float(tile_px)
-            ok = (q > -2.0e9) & (q < 2.0e9)
-            return np.where(ok, np.floor(np.where(ok, q, 0.0)), 0.0).astype(np.int64).astype(np.int32).view(np.uint32)
+            with np.errstate(invalid="ignore"):
+                q = q / float(tile_px)
+                ok = (q > -2.0e9) & (q < 2.0e9)
+            t = np.where(ok, np.floor(np.where(ok, q, 0.0)), 0.0).astype(np.int64)
+            return (np.clip(t, -(1 << 27), (1 << 27) - 1) + (1 << 27)).astype(np.uint64)
 
-        with np.errstate(over="ignore"):
-            ref = items["ref"].astype(np.uint32)
-            hh = (ref * np.uint32(73856093)) ^ (tc(w) * np.uint32(19349663)) ^ (tc(u) * np.uint32(83492791))
-            hh ^= hh >> np.uint32(16)
-            hh *= np.uint32(0x85EBCA6B)
-            hh ^= hh >> np.uint32(13)
-        own = (hh % np.uint32(world)).astype(np.int32)
-        cnt = np.bincount(own, minlength=world)
-        fb = len(own) > 0 and cnt.max() > 1.1 * len(own) / world
-        if fb:
-            own = (np.arange(len(own)) % world).astype(np.int32)
-        return own, bool(fb)
+        key = ((items["ref"].astype(np.uint64) & np.uint64(0xFF)) << np.uint64(56)) | (tc(w) << np.uint64(28)) | tc(u)
+        order = np.argsort(key, kind="stable")
+        lo = np.array([(r * n) // world for r in range(world + 1)], dtype=np.int64)
+        own = np.empty(n, dtype=np.int32)
+        for r in range(world):
+            own[order[lo[r]:lo[r + 1]]] = r
+        sk = key[order]
+        split = np.zeros(n, dtype=bool)
+        for r in range(1, world):
+            c = int(lo[r])
+            if 0 < c < n and sk[c - 1] == sk[c]:
+                split |= sk == sk[c]
+        tiles = int(np.count_nonzero(np.diff(sk))) + 1 if n else 0
+        self._pstats = {"items": n, "world": world, "tiles": tiles, "split_items": int(split.sum())}
+        return own, False
+
+    def densify_partition_stats(self):
+        return dict(self._pstats)
 
     def densify_refine_items(self, g, items):
         items = np.asarray(items, dtype=np.int64)

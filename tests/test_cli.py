@@ -238,3 +238,64 @@ def test_cli_gpus_partitioned_equals_one_gpu(scene_dir, tmp_path, gpus):
     assert rn["gpus"] == gpus and rn["patches"] == r1["patches"] > 0
     assert rn["evals"] == r1["evals"]
     assert many.read_bytes() == one.read_bytes()
+
+
+def _jpeg_scene(scene_dir, tmp_path, quality=92, subsampling=2):
+    """The 4-view synthetic scene with its views re-encoded as JPEG (libjpeg-turbo,
+    via Pillow) and, beside it, the same scene with PNG views holding exactly the
+    pixels libjpeg-turbo decodes those JPEGs to (the decode cv::imread does)."""
+    import io
+
+    from PIL import Image
+
+    with open(os.path.join(scene_dir, "scene.json")) as f:
+        sc = json.load(f)
+    cfg = synth.config(4, 160, 120, 1)
+    P = synth.cameras(cfg)
+    decoded = []
+    jv, pv = [], []
+    for v, view in enumerate(sc["views"]):
+        bgr = synth.render_host(cfg, P, v)
+        buf = io.BytesIO()
+        Image.fromarray(np.ascontiguousarray(bgr[:, :, ::-1])).save(buf, format="JPEG", quality=quality,
+                                                                    subsampling=subsampling)
+        (tmp_path / f"view{v}.jpg").write_bytes(buf.getvalue())
+        dec = np.ascontiguousarray(np.asarray(Image.open(io.BytesIO(buf.getvalue())).convert("RGB"))[:, :, ::-1])
+        decoded.append(dec)
+        _png(tmp_path / f"view{v}.png", np.ascontiguousarray(dec[:, :, ::-1]), 2)
+        jv.append({"filename": f"view{v}.jpg", "projectionMatrix": view["projectionMatrix"]})
+        pv.append({"filename": f"view{v}.png", "projectionMatrix": view["projectionMatrix"]})
+    (tmp_path / "scene_jpg.json").write_text(json.dumps({"imagesPath": str(tmp_path), "views": jv}))
+    (tmp_path / "scene_png.json").write_text(json.dumps({"imagesPath": str(tmp_path), "views": pv}))
+    return decoded
+
+
+def test_jpeg_scene_loads_libjpeg_turbo_pixels(scene_dir, tmp_path):
+    """a scene folder of JPEG views (SURVEY 8f row 4; cv::imread, types.cpp:7-11):
+    the CLI's loaded BGR8 planes equal libjpeg-turbo's decode of the same files"""
+    decoded = _jpeg_scene(scene_dir, tmp_path)
+    chk = json.loads(run("-i", str(tmp_path / "scene_jpg.json"), "--seeds", os.path.join(scene_dir, "seeds.xyz"),
+                         "--check-only").stdout)
+    assert chk["image_fnv"] == [fnv(d) for d in decoded]
+
+
+@pytest.mark.gpu
+def test_cli_jpeg_scene_ply_equals_png_scene(scene_dir, tmp_path, orc):
+    """densify -i scene.json with .jpg views writes the same PLY as with PNG
+    views of the same pixels, and that PLY equals the oracle's densify of the
+    decoded images, byte for byte."""
+    from densepoints_amd.pmvs import write_ply
+
+    decoded = _jpeg_scene(scene_dir, tmp_path)
+    seeds = os.path.join(scene_dir, "seeds.xyz")
+    oj, op_ = tmp_path / "jpg.ply", tmp_path / "png.ply"
+    rj = json.loads(run("-i", str(tmp_path / "scene_jpg.json"), "--seeds", seeds, "-o", str(oj)).stdout)
+    rp = json.loads(run("-i", str(tmp_path / "scene_png.json"), "--seeds", seeds, "-o", str(op_)).stdout)
+    assert rj["patches"] == rp["patches"] > 0
+    assert oj.read_bytes() == op_.read_bytes()
+    cfg = synth.config(4, 160, 120, 1)
+    P = synth.cameras(cfg)
+    op, ost = orc.Scene(P, decoded).densify(synth.seeds(cfg, P))
+    ref = tmp_path / "oracle.ply"
+    write_ply(str(ref), op)
+    assert oj.read_bytes() == ref.read_bytes()

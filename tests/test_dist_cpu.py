@@ -167,9 +167,9 @@ def _part_worker(rank, world, port, out_path, max_pops):
 @pytest.mark.parametrize("world,max_pops", [(2, 0), (3, 0), (2, 23)])
 def test_gloo_partitioned_densify_equals_single_process(tmp_path, orc, world, max_pops):
     """North star / SURVEY 8e: every generation partitioned by reference-view
-    super-tile (hashed (ref, v/64, u/64), round-robin fallback), candidates
-    all-gathered and put back in sequence order -> the 1-process densify bit
-    for bit on every rank."""
+    super-tile (items sorted by their (ref, v/64, u/64) key, the order cut into
+    `world` contiguous equal shares), candidates all-gathered and put back in
+    sequence order -> the 1-process densify bit for bit on every rank."""
     import ast
 
     import densepoints_amd as dp
@@ -185,5 +185,7 @@ def test_gloo_partitioned_densify_equals_single_process(tmp_path, orc, world, ma
         got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
         assert got.tobytes() == ref.tobytes(), f"rank {r}"
     parts = ast.literal_eval(open(out + ".parts").read())
-    # the big generations really were split by tile, not by round robin
-    assert any((not fb) and items >= 100 for items, _, fb in parts)
+    # every share is within one item of the mean, and a big generation is cut
+    # at tile boundaries except at the world - 1 cuts
+    assert all(mx <= -(-items // world) for items, mx, _, _ in parts)
+    assert any(items >= 100 and tiles > world and split < items / 2 for items, _, split, tiles in parts)

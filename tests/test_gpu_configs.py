@@ -131,3 +131,22 @@ def test_cfg4_64view_4k_seed_and_expand(orc):
     kids = _seed_and_expand(orc, "cfg4_64view_4k", 400, 1000)
     nvis = np.array([bin(int(a)).count("1") + bin(int(b)).count("1") for a, b in kids["vis"]])
     print("cfg4 visible views per child: mean %.2f max %d" % (nvis.mean(), nvis.max()))
+
+
+def test_cfg4_64view_4k_whole_densify_equals_oracle(orc):
+    """cfg4 (64 views 3840x2160), the whole densify -- PMVS::Run minus matching
+    (methods/pmvs/pmvs.cpp:22-43): seed stage, organizer, FIFO expansion with
+    the pop cap -- on 400 spread seeds, max_pops 1,500, against the oracle's
+    single-thread restatement on every field and in order.  This pins, at the
+    config-4 scale, the dp_densify that the partitioned multi-rank tests
+    (test_gpu_dist.py) compare their stores with."""
+    opts = dp.Options(max_pops=1500)
+    with dp.Engine(opts, device=0) as eng:
+        sc = DeviceScene("cfg4_64view_4k", eng)
+        seeds = spread(sc.seeds, 400)
+        gp, gst = eng.densify(seeds)
+        S = orc.Scene(sc.P, sc.host_images(), opts)
+        op, ost = S.densify(seeds)
+    assert gst["patches"] == ost["patches"] and gst["pops"] == ost["pops"], (gst, ost)
+    assert 500 < gst["pops"] <= 1500 and len(gp) > 1000, gst
+    assert_same(gp, op, FIELDS + ("seq", "parent", "rgb"))

@@ -9,6 +9,7 @@ import socket
 
 import numpy as np
 import pytest
+import torch
 import torch.multiprocessing as mp
 
 import densepoints_amd as dp
@@ -152,8 +153,9 @@ def test_partitioned_densify_device(tmp_path, backend, world, variant, cap):
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_owners_equal_oracle_and_host_path(orc, world):
-    """dp_densify_owners (device projection + hash) equals the oracle's numpy
-    statement generation by generation, and the host-array partitioned driver
+    """dp_densify_owners (device projection, super-tile keys, sorted-order cut)
+    equals the oracle's numpy statement generation by generation -- owners and
+    partition statistics -- and the host-array partitioned driver
     equals dp_densify (with the pop cap)."""
     P, imgs, seeds = _scene("wide70")
     S = orc.Scene(P, imgs)
@@ -167,6 +169,7 @@ def test_owners_equal_oracle_and_host_path(orc, world):
             own, fb = eng.densify_owners(g, world)
             oown, ofb = G.densify_owners(og, world)
             assert fb == ofb and np.array_equal(own, oown), f"generation {gens}"
+            assert eng.densify_partition_stats() == G.densify_partition_stats(), f"generation {gens}"
             cand, acc = eng.densify_refine(g, 0, g.items)
             g = eng.densify_commit(g, cand, acc)
             oc, oa = G.densify_refine(og, 0, og.items)
@@ -204,13 +207,23 @@ def _worker_cfg4(rank, world, port, out_path, max_pops, nseeds):
     tdist.destroy_process_group()
 
 
+def _check_partition(parts, world):
+    """balanced contiguous shares, tiles rarely split (records: items, largest
+    share, items in split tiles, tiles)"""
+    items = sum(p[0] for p in parts)
+    assert all(mx <= -(-it // world) for it, mx, _, _ in parts)
+    assert sum(p[2] for p in parts) <= 0.1 * items, parts
+
+
 def test_partitioned_densify_cfg4_two_ranks(tmp_path):
     """BASELINE config 4 (64 views 3840x2160) in the partitioned protocol: two
     ranks sharing cuda:0 (gloo, spawned before any GPU call), each with the
     scene rendered into its own HBM planes, densify 1,500 spread seeds with a
     pop cap -- in parity and in performance mode -- and both ranks' stores
-    equal the single-process dp_densify byte for byte; the super-tile
-    partition splits the generations (not all round robin)."""
+    equal the single-process dp_densify byte for byte; every share is within
+    one item of the mean and >= 90% of the items are in tiles no cut splits,
+    at world 2 and (the partitions a world-8 run would use, computed on one
+    rank) at world 8."""
     from test_gpu_configs import DeviceScene, spread
 
     out = str(tmp_path / "cfg4")
@@ -229,8 +242,11 @@ def test_partitioned_densify_cfg4_two_ranks(tmp_path):
                 assert got.tobytes() == ref.tobytes(), f"{mode} rank {r}"
             st = json.loads(open(out + f".{mode}.r0.json").read())
             assert st["evals"] == rst["evals"]
-            assert any(not fb for _, _, fb in st["partition"])
+            _check_partition(st["partition"], 2)
             assert sum(st["accepted"]) >= rst["patches"]
+        eng.set_fast_options(dp.FastOptions())
+        _, pst = D.densify_partitioned_device(eng, seeds, None, torch.device("cuda", 0), probe_worlds=(8,))
+        _check_partition(pst["partition_probe"][8], 8)
 
 
 def _worker_cfg5(rank, world, port, out_path, max_pops, nseeds):
@@ -279,4 +295,4 @@ def test_partitioned_densify_cfg5_two_ranks(tmp_path):
         assert got.tobytes() == ref.tobytes(), f"rank {r}"
     st = json.loads(open(out + ".r0.json").read())
     assert st["evals"] == rst["evals"]
-    assert any(not fb for _, _, fb in st["partition"])
+    _check_partition(st["partition"], 2)
