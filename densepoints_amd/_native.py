@@ -142,7 +142,7 @@ class DpMatcherOptions(ctypes.Structure):
         ("epipolar_matching", ctypes.c_int32),
         ("max_epipolar_distance", ctypes.c_float),
         ("nn_match_ratio", ctypes.c_float),
-        ("reserved", ctypes.c_int32),
+        ("matcher_type", ctypes.c_int32),
     ]
 
 

@@ -241,6 +241,10 @@ __device__ __forceinline__ TexelLoad texel_fetch_n(gbyte_t base, gbyte_t base1, 
     uint32_t xo, o0;
     asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(xo) : "v"((uint32_t)cx >> 5), "v"(roi));
     asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(o0) : "v"((uint32_t)cy >> 5), "v"(pitch4), "v"(xo));
+#ifdef DP_DIAG_HOTIMG
+    // diagnostic build: every gather hits the first 4 KiB of the pool (timing only)
+    o0 &= 4095u;
+#endif
     TexelLoad t;
     t.a = *(gpair_t)(base + o0);
     if (kUniPitch)

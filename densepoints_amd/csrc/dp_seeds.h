@@ -53,6 +53,7 @@ struct MatchArgs {
     const dp_keypoint *kp;
     float ratio;
     float max_dist;
+    int32_t flann;         // DP_MATCHER_FLANN: exact 1-NN, kept iff distance < 30
     int32_t *q2t;          // per (pair, query): train index or -1
     int32_t *t2q;          // per (pair, train): smallest matching query (init INT32_MAX)
     unsigned long long *n_ratio, *n_match;

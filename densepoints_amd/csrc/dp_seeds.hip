@@ -292,15 +292,18 @@ __global__ void match_kernel(MatchArgs a)
     const SeedPair pr = a.pairs[lo];
     const int64_t q = i - job.out_off;
     int32_t t = -1;
-    if (job.nt >= 2) { // knnMatch with one train row leaves matches_groups[i][1] undefined
+    // knnMatch with one train row leaves matches_groups[i][1] undefined; the
+    // FLANN form's match() needs one
+    if (job.nt >= (a.flann ? 1 : 2)) {
         const uint32_t k0 = a.keys[2 * i], k1 = a.keys[2 * i + 1];
         // Hamming distances: (key >> 22) - 256 + popcnt(query)
         int pq = 0;
         for (int s = 0; s < 8; ++s)
             pq += __popc(a.desc[(size_t)(job.q_off + q) * 8 + s]);
         const int32_t h0 = (int32_t)(k0 >> 22) - 256 + pq, h1 = (int32_t)(k1 >> 22) - 256 + pq;
-        // DMatch::distance is float; nn_match_ratio is a float constant
-        if ((float)h0 < a.ratio * (float)h1) {
+        // DMatch::distance is float; nn_match_ratio is a float constant; FLANN
+        // keeps matches with distance < 30 (matcher.cpp:235)
+        if (a.flann ? (float)h0 < 30.0f : (float)h0 < a.ratio * (float)h1) {
             const int32_t tt = (int32_t)(k0 & ((1u << 22) - 1));
             atomicAdd(a.n_ratio, 1ull);
             const dp_keypoint &kl = a.kp[job.q_off + q];

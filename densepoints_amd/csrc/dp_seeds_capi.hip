@@ -128,6 +128,7 @@ extern "C" void dp_default_matcher_options(dp_matcher_options *mo)
     mo->epipolar_matching = 0;
     mo->max_epipolar_distance = 1.5f;
     mo->nn_match_ratio = 0.7f;
+    mo->matcher_type = DP_MATCHER_KNN;
 }
 
 // ---------------------------------------------------------------------------
@@ -369,7 +370,8 @@ static int check_matcher_options(dp_ctx *c, const dp_matcher_options &m)
     if (m.n_features < 0 || m.n_levels < 1 || m.n_levels > dpk::kOrbMaxLevels || !(m.scale_factor > 1.0) ||
         m.edge_threshold < 19 || m.fast_threshold < 0 || m.fast_threshold > 254 || m.cell_size < 1 ||
         m.max_keypoints_per_cell < 0 || (m.epipolar_matching != 0 && m.epipolar_matching != 1) ||
-        !(m.nn_match_ratio >= 0.0f) || !(m.max_epipolar_distance >= 0.0f))
+        !(m.nn_match_ratio >= 0.0f) || !(m.max_epipolar_distance >= 0.0f) ||
+        (m.matcher_type != DP_MATCHER_KNN && m.matcher_type != DP_MATCHER_FLANN))
         return fail(c, DP_E_ARG, "dp_matcher_options: value out of range (edge_threshold >= 19, 1 <= n_levels <= 16)");
     return DP_OK;
 }
@@ -643,8 +645,8 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     DP_HIP(c, hipMemsetAsync(s->t2q.p, 0x7F, (size_t)(t2q_total + 1) * 4, st)); // kNoMatch > any index
     DP_HIP(c, hipMemsetAsync(s->counters.p, 0, 2 * sizeof(unsigned long long), st));
     dpk::MatchArgs ma{s->jobs.p, s->pairs.p, np, q_total, s->keys.p, s->desc.p, s->kp_b.p,
-                      mo.nn_match_ratio, mo.max_epipolar_distance, s->q2t.p, s->t2q.p, s->counters.p,
-                      s->counters.p + 1};
+                      mo.nn_match_ratio, mo.max_epipolar_distance, mo.matcher_type == DP_MATCHER_FLANN,
+                      s->q2t.p, s->t2q.p, s->counters.p, s->counters.p + 1};
     if (mo.epipolar_matching) {
         DP_HIP(c, dpk::launch_epipolar_match(ma, st));
     } else {

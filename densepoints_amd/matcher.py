@@ -32,6 +32,9 @@ class MatcherOptions:
     epipolar_matching: bool = False
     max_epipolar_distance: float = 1.5
     nn_match_ratio: float = 0.7
+    # MatcherType (matcher.h:12): KNN (default) or FLANN -- the LSH match() kept
+    # iff distance < 30, answered exactly (include/densepoints.h DP_MATCHER_FLANN)
+    matcher_type: int = 0
 
     def to_c(self) -> N.DpMatcherOptions:
         o = N.DpMatcherOptions()
@@ -40,6 +43,9 @@ class MatcherOptions:
             v = getattr(self, f.name)
             setattr(o, f.name, int(v) if isinstance(v, bool) else v)
         return o
+
+
+MATCHER_KNN, MATCHER_FLANN = 0, 1
 
 
 class Matcher:

@@ -360,8 +360,20 @@ typedef struct dp_matcher_options {
     int32_t epipolar_matching;      /* 0     matcher.h:23 (1: DirectEpipolarMatching) */
     float max_epipolar_distance;    /* 1.5f  matcher.h:24                             */
     float nn_match_ratio;           /* 0.7f  matcher.cpp:217                          */
-    int32_t reserved;
+    int32_t matcher_type;           /* DP_MATCHER_KNN  MatcherOptions::matcher_type    */
 } dp_matcher_options;
+/* MatcherType (matcher.h:12, MatchKeypoints matcher.cpp:206-265):
+ *  DP_MATCHER_KNN    BruteForce-Hamming knnMatch k = 2, ratio test d0 < 0.7 d1
+ *  DP_MATCHER_FLANN  FlannBasedMatcher(LshIndexParams(12, 20, 2)).match, kept iff
+ *                    distance < 30 (matcher.cpp:229-240).  LSH is approximate and
+ *                    its hash tables come from FLANN's random generator, so no two
+ *                    builds agree on its misses; this build answers the same query
+ *                    exactly -- the nearest train descriptor by Hamming distance
+ *                    (ties: lowest index, as BFMatcher), kept iff distance < 30 --
+ *                    which LSH approximates (parity unpinned).  Both then go
+ *                    through the same epipolar filter (FilterMatches). */
+#define DP_MATCHER_KNN 0
+#define DP_MATCHER_FLANN 1
 
 /* the cv::KeyPoint fields the matcher reads (pt, response, angle, octave) */
 typedef struct dp_keypoint {

@@ -33,7 +33,7 @@ typedef struct or_matcher_options {
     double scale_factor;
     int32_t edge_threshold, fast_threshold, cell_size, max_keypoints_per_cell, epipolar_matching;
     float max_epipolar_distance, nn_match_ratio;
-    int32_t reserved;
+    int32_t matcher_type; /* 0 kNN ratio test, 1 FLANN (exact 1-NN, distance < 30) */
 } or_matcher_options;
 
 /* ------------------------------------------------------------------------ */
@@ -780,11 +780,17 @@ or_seeds *or_seeds_run(int V, const double *P, const int32_t *W, const int32_t *
             int32_t *i2 = (int32_t *)malloc(sizeof(int32_t) * 2 * (size_t)(nq + 1));
             int32_t *d2 = (int32_t *)malloc(sizeof(int32_t) * 2 * (size_t)(nq + 1));
             or_knn_match(r->desc + 32 * r->kp_off[i], nq, r->desc + 32 * r->kp_off[j], nt, i2, d2);
+            const int flann = mo->matcher_type == 1;
             for (int64_t q = 0; q < nq; ++q) {
                 q2t[q] = -1;
-                if (nt < 2)
+                /* knnMatch k = 2 needs two train rows; FLANN's match() one */
+                if (nt < (flann ? 1 : 2))
                     continue;
-                if ((float)d2[2 * q] < mo->nn_match_ratio * (float)d2[2 * q + 1]) {
+                /* kNN: ratio test (matcher.cpp:217-222); FLANN: LshIndexParams(12, 20,
+                 * 2) match kept iff distance < 30 (matcher.cpp:229-240), stated as
+                 * the exact nearest neighbour LSH approximates */
+                if (flann ? (float)d2[2 * q] < 30.0f
+                          : (float)d2[2 * q] < mo->nn_match_ratio * (float)d2[2 * q + 1]) {
                     r->ratio_matches++;
                     int t = i2[2 * q];
                     float dist = or_epipolar_distance(F, kq[q].x, kq[q].y, kt[t].x, kt[t].y);

@@ -484,7 +484,7 @@ class OrMatcherOptions(ctypes.Structure):
         ("epipolar_matching", ctypes.c_int32),
         ("max_epipolar_distance", ctypes.c_float),
         ("nn_match_ratio", ctypes.c_float),
-        ("reserved", ctypes.c_int32),
+        ("matcher_type", ctypes.c_int32),
     ]
 
 
@@ -496,7 +496,7 @@ KEYPOINT_DTYPE = np.dtype(
 def matcher_options(**kw) -> OrMatcherOptions:
     o = OrMatcherOptions(n_features=40000, n_levels=8, scale_factor=1.2, edge_threshold=31, fast_threshold=20,
                          cell_size=16, max_keypoints_per_cell=4, epipolar_matching=0, max_epipolar_distance=1.5,
-                         nn_match_ratio=0.7)
+                         nn_match_ratio=0.7, matcher_type=0)
     for k, v in kw.items():
         setattr(o, k, int(v) if isinstance(v, bool) else v)
     return o

@@ -237,3 +237,16 @@ def test_seeds_min_edge_threshold(orc):
     x, y = kp["x"] / s, kp["y"] / s
     w, h = np.rint(320 / s), np.rint(240 / s)
     assert np.any(np.minimum(np.minimum(x, y), np.minimum(w - 1 - x, h - 1 - y)) < 22)
+
+
+def test_generate_seeds_flann_matcher(orc):
+    """MatcherType::FLANN (matcher.cpp:229-240; DP_MATCHER_FLANN: the exact
+    nearest neighbour the LSH match approximates, kept iff distance < 30):
+    every stage bit-exact against the oracle's FLANN mode."""
+    cfg = synth.config(n_views=4, width=640, height=480, kind=1)
+    P, imgs, _ = synth.scene_host(cfg)
+    kw = dict(n_features=5000, fast_threshold=10, matcher_type=M.MATCHER_FLANN)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    with engine_with(P, imgs) as eng:
+        m = compare_run(eng, r, kw, 4)
+        assert m.stats["points"] > 100

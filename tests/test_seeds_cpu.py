@@ -183,3 +183,27 @@ def test_golden_seeds_fixture_pins_the_oracle(orc):
     assert np.array_equal(np.concatenate(r["descriptors"]), g["descriptors"])
     assert np.array_equal(np.concatenate(r["q2t"]), g["q2t"])
     assert np.array_equal(r["points"], g["points"])
+
+
+def test_oracle_flann_matcher_is_exact_nn_below_30(orc):
+    """MatcherType::FLANN (matcher.cpp:229-240: LSH match, distance < 30),
+    stated as the exact Hamming nearest neighbour it approximates: every
+    epipolar-filtered match of the oracle's FLANN mode is a query's brute-force
+    nearest train descriptor (lowest index on ties) at distance < 30."""
+    cfg = synth.config(n_views=3, width=640, height=480, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    kw = dict(n_features=3000, fast_threshold=10)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(matcher_type=1, **kw))
+    rk = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    assert r["counts"]["matches"] > 100
+    # the same keypoints and descriptors as the kNN mode; a different match rule
+    assert np.array_equal(np.concatenate(r["descriptors"]), np.concatenate(rk["descriptors"]))
+    assert r["counts"]["ratio_matches"] != rk["counts"]["ratio_matches"]
+    for p, (a, b) in enumerate(r["pairs"]):
+        da, db = r["descriptors"][a], r["descriptors"][b]
+        ham = np.unpackbits(da[:, None, :] ^ db[None, :, :], axis=2).sum(axis=2)
+        nn = ham.argmin(axis=1)
+        d0 = ham[np.arange(len(da)), nn]
+        q2t = r["q2t"][p]
+        hit = q2t >= 0
+        assert np.array_equal(q2t[hit], nn[hit]) and np.all(d0[hit] < 30)
