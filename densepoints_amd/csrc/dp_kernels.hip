@@ -242,8 +242,9 @@ __device__ __forceinline__ TexelLoad texel_fetch_n(gbyte_t base, gbyte_t base1, 
     asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(xo) : "v"((uint32_t)cx >> 5), "v"(roi));
     asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(o0) : "v"((uint32_t)cy >> 5), "v"(pitch4), "v"(xo));
 #ifdef DP_DIAG_HOTIMG
-    // diagnostic build: every gather hits the first 4 KiB of the pool (timing only)
-    o0 &= 4095u;
+    // diagnostic build: every gather hits the first DP_DIAG_HOTIMG bytes of the
+    // pool (a power of two; timing only)
+    o0 &= (uint32_t)(DP_DIAG_HOTIMG) - 1u;
 #endif
     TexelLoad t;
     t.a = *(gpair_t)(base + o0);
