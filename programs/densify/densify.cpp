@@ -9,7 +9,7 @@
 //
 //   densify -i scene.json [--seeds seeds.xyz] [-s settings.json] [-o points.ply]
 //           [--device N] [--max-pops N] [--level L] [--filter] [--check-only]
-//           [--features N] [--fast-threshold T] [--epipolar-matching]
+//           [--features N] [--fast-threshold T] [--epipolar-matching] [--matcher knn|flann]
 //   densify --synthetic V,W,H,KIND --write-scene DIR   (deterministic test scene
 //           written as scene.json + PPM images + seeds.xyz; no GPU needed)
 #include "scene_io.h"
@@ -35,6 +35,7 @@ void usage()
                  "usage: densify -i scene.json [--seeds seeds.xyz] [-s settings.json] [-o points.ply]\n"
                  "               [--device N] [--max-pops N] [--level L] [--filter] [--check-only]\n"
                  "               [--features N] [--fast-threshold T] [--epipolar-matching]\n"
+                 "               [--matcher knn|flann]  (MatcherType, matcher.h:12)\n"
                  "               [--gpus N]   (one context per GPU, generations partitioned by\n"
                  "                             reference-view super-tile; output identical to 1 GPU)\n"
                  "               [--mode parity|fast] [--fast-iters N]  (fast: the performance-mode\n"
@@ -250,6 +251,17 @@ int main(int argc, char **argv)
         else if (a == "--features") mopt.n_features = std::atoi(next().c_str());
         else if (a == "--fast-threshold") mopt.fast_threshold = std::atoi(next().c_str());
         else if (a == "--epipolar-matching") mopt.epipolar_matching = 1;
+        else if (a == "--matcher") {
+            const std::string v = next();
+            if (v == "knn")
+                mopt.matcher_type = DP_MATCHER_KNN;
+            else if (v == "flann")
+                mopt.matcher_type = DP_MATCHER_FLANN;
+            else {
+                std::fprintf(stderr, "densify: --matcher expects knn or flann\n");
+                return 2;
+            }
+        }
         else if (a == "--mode") {
             const std::string m = next();
             if (m != "parity" && m != "fast") {

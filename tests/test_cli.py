@@ -299,3 +299,28 @@ def test_cli_jpeg_scene_ply_equals_png_scene(scene_dir, tmp_path, orc):
     ref = tmp_path / "oracle.ply"
     write_ply(str(ref), op)
     assert oj.read_bytes() == ref.read_bytes()
+
+
+@pytest.mark.gpu
+def test_cli_flann_matcher_pipeline(tmp_path_factory, tmp_path, orc):
+    """densify --matcher flann (MatcherType::FLANN, matcher.cpp:229-240): seeds
+    from the FLANN-mode match rule, then the densify; the PLY equals the
+    oracle's FLANN-mode seed generation + densify byte for byte."""
+    from densepoints_amd.pmvs import write_ply
+
+    d = str(tmp_path_factory.mktemp("scene_flann"))
+    run("--synthetic", "4,320,240,0", "--write-scene", d)
+    out = tmp_path / "points.ply"
+    res = json.loads(run("-i", os.path.join(d, "scene.json"), "--features", "2000", "--fast-threshold", "8",
+                         "--matcher", "flann", "-o", str(out)).stdout)
+    cfg = synth.config(4, 320, 240, 0)
+    P = synth.cameras(cfg)
+    imgs = [synth.render_host(cfg, P, v) for v in range(4)]
+    r = orc.seeds_run(P, imgs, orc.matcher_options(n_features=2000, fast_threshold=8, matcher_type=1))
+    assert res["generated_seeds"] is True and res["seeds"] == len(r["points"]) > 0
+    op, ost = orc.Scene(P, imgs).densify(r["points"])
+    assert res["patches"] == ost["patches"] > 0
+    ref = tmp_path / "oracle.ply"
+    write_ply(str(ref), op)
+    assert out.read_bytes() == ref.read_bytes()
+    assert run("-i", os.path.join(d, "scene.json"), "--matcher", "lsh", check=False).returncode == 2
