@@ -243,6 +243,8 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->ocount.release();
     c->items.release();
     c->seedp.release();
+    c->seedx.release();
+    c->sconv.release();
     c->lpt.release();
     c->front.release();
     c->f_alive.release();
@@ -614,47 +616,17 @@ extern "C" int dp_filter_patches(dp_ctx *c, const dp_patch *patches, int64_t n, 
 }
 
 // ---------------------------------------------------------------------------
-// seeds (host; O(N*V), negligible next to the refine)
+// seeds: Seed::CreatePatchesFromPoints (seed.cpp:26-54) on the device
 // ---------------------------------------------------------------------------
 
-static void seed_patch(const std::vector<dpg::ViewDev> &hv, const dp_options &o, const double *X, dp_patch &p)
+// n host seed points -> seed patches in device memory d_out (async on s)
+static int seeds_device(dp_ctx *c, const double *xyz, int64_t n, dp_patch *d_out, hipStream_t s)
 {
-    // Seed::CreatePatchesFromPoints (seed.cpp:30-49)
-    const int V = (int)hv.size();
-    auto dist = [&](int v) {
-        const double d[3] = {X[0] - hv[v].C[0], X[1] - hv[v].C[1], X[2] - hv[v].C[2]};
-        return std::sqrt(dpg::dot3(d, d));
-    };
-    double best = dist(0);
-    int ref = 0;
-    for (int v = 1; v < V; ++v) {
-        const double d = dist(v);
-        if (d < best) {
-            best = d;
-            ref = v;
-        }
-    }
-    const double t[3] = {X[0] - hv[ref].C[0], X[1] - hv[ref].C[1], X[2] - hv[ref].C[2]};
-    const double tn = std::sqrt(dpg::dot3(t, t));
-    std::memset(&p, 0, sizeof(p));
-    p.ref = (uint32_t)ref;
-    p.parent = 0xFFFFFFFFu;
-    for (int i = 0; i < 3; ++i) {
-        p.pos[i] = (float)X[i];
-        p.normal[i] = (float)(t[i] / tn);
-    }
-    // InitRelatedImages on the stored f32 pose (patch.cpp:19-49)
-    const double Xs[3] = {p.pos[0], p.pos[1], p.pos[2]};
-    const double ns[3] = {p.normal[0], p.normal[1], p.normal[2]};
-    for (int v = 0; v < V; ++v) {
-        if (v == ref)
-            continue;
-        const int cls = dpg::classify_view(hv[v], Xs, ns, o.visible_angle, o.candidate_angle);
-        if (cls == 1)
-            p.vis[v >> 6] |= 1ull << (v & 63);
-        else if (cls == 2)
-            p.cand[v >> 6] |= 1ull << (v & 63);
-    }
+    DP_HIP(c, c->seedx.reserve((size_t)(3 * n)));
+    DP_HIP(c, hipMemcpyAsync(c->seedx.p, xyz, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice, s));
+    DP_HIP(c, dpk::launch_seed_patches(c->d_views, c->V, c->seedx.p, n, c->opt.visible_angle,
+                                       c->opt.candidate_angle, d_out, s));
+    return DP_OK;
 }
 
 extern "C" int dp_seeds_to_patches(dp_ctx *c, const double *xyz, int n, dp_patch *out)
@@ -663,7 +635,15 @@ extern "C" int dp_seeds_to_patches(dp_ctx *c, const double *xyz, int n, dp_patch
         return fail(c, DP_E_ARG, "dp_seeds_to_patches: bad arguments");
     if (!c->V)
         return fail(c, DP_E_STATE, "dp_seeds_to_patches: no views");
-    parallel_for(n, [&](int64_t i) { seed_patch(c->hv, c->opt, xyz + 3 * i, out[i]); });
+    if (n == 0)
+        return DP_OK;
+    hipSetDevice(c->device);
+    DP_HIP(c, c->sconv.reserve((size_t)n));
+    const int rc = seeds_device(c, xyz, n, c->sconv.p, c->stream);
+    if (rc != DP_OK)
+        return rc;
+    DP_HIP(c, hipMemcpyAsync(out, c->sconv.p, sizeof(dp_patch) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    DP_HIP(c, hipStreamSynchronize(c->stream));
     return DP_OK;
 }
 
@@ -962,13 +942,11 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
     double refine_ms = 0.0;
     int64_t np = 0;
     if (n > 0) {
-        std::vector<dp_patch> sp(n);
-        int rc = dp_seeds_to_patches(c, seeds, n, sp.data());
-        if (rc != DP_OK)
-            return rc;
         DP_HIP(c, c->cand.reserve(n));
         DP_HIP(c, c->ok.reserve(n));
-        DP_HIP(c, hipMemcpyAsync(c->cand.p, sp.data(), sizeof(dp_patch) * n, hipMemcpyHostToDevice, s));
+        int rc = seeds_device(c, seeds, n, c->cand.p, s);
+        if (rc != DP_OK)
+            return rc;
         // seed.cpp:110-144: FilterPatches then OptimizePatches at the seed cell
         // size (performance mode, dp_fast_options.densify: the fast refine)
         if (fast) {
@@ -1086,12 +1064,10 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
     DP_HIP(c, c->store.reserve((size_t)store_capacity(c, n)));
     DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
     if (n > 0) {
-        std::vector<dp_patch> sp(n);
-        int rc = dp_seeds_to_patches(c, seeds, n, sp.data());
+        DP_HIP(c, c->seedp.reserve(n));
+        int rc = seeds_device(c, seeds, n, c->seedp.p, s);
         if (rc != DP_OK)
             return rc;
-        DP_HIP(c, c->seedp.reserve(n));
-        DP_HIP(c, hipMemcpyAsync(c->seedp.p, sp.data(), sizeof(dp_patch) * n, hipMemcpyHostToDevice, s));
     }
     DP_HIP(c, hipStreamSynchronize(s));
     *gen = dp_generation{};

@@ -104,6 +104,8 @@ struct dp_ctx {
     std::vector<dp_patch> result;
     // generation-at-a-time densify (dp_densify_begin/refine/commit/result)
     DevBuf<dp_patch> seedp;  // seed patches of generation 0
+    DevBuf<double> seedx;    // seed points (3 f64 each) on the device
+    DevBuf<dp_patch> sconv;  // dp_seeds_to_patches output staging
     DevBuf<int64_t> items;   // item list of a partitioned refine / commit
     // partitioned generations: super-tile keys, key-sorted keys and item order
     // (the rank-major order), the cut positions, partition statistics

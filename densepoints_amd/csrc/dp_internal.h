@@ -105,6 +105,9 @@ hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand,
                          int64_t parent0, int is_seed, hipStream_t s);
 hipError_t launch_render(const dp_synth_config &cfg, const double *P, uint32_t *out, int v,
                          hipStream_t s);
+// Seed::CreatePatchesFromPoints: seed patches of n points (xyz device, 3n f64)
+hipError_t launch_seed_patches(const dpg::ViewDev *views, int V, const double *xyz, int64_t n, double vis_angle,
+                               double cand_angle, dp_patch *out, hipStream_t s);
 // multi-GPU partition of a generation's items: super-tile keys
 // (ref, tile row, tile column) of the items' centres, and the statistics of a
 // cut of the key-sorted order at lo[1..world-1] (stats[2], zeroed here)

@@ -1927,6 +1927,60 @@ hipError_t launch_refine(const RefineArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
+// Seed::CreatePatchesFromPoints (seed.cpp:26-54), one thread per seed point:
+// ref = the nearest camera centre (first minimum), normal = the unit ray from
+// it, then InitRelatedImages (patch.cpp:19-49) on the stored f32 pose.  The
+// views are read in lock-step by the wave (broadcast loads).
+__global__ void seed_patches_kernel(const dpg::ViewDev *views, int V, const double *xyz, int64_t n,
+                                    double vis_angle, double cand_angle, dp_patch *out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const double X[3] = {xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]};
+    double best = 0.0;
+    int ref = 0;
+    for (int v = 0; v < V; ++v) {
+        const double d[3] = {X[0] - views[v].C[0], X[1] - views[v].C[1], X[2] - views[v].C[2]};
+        const double dist = sqrt(dpg::dot3(d, d));
+        if (v == 0 || dist < best) {
+            best = dist;
+            ref = v;
+        }
+    }
+    const double t[3] = {X[0] - views[ref].C[0], X[1] - views[ref].C[1], X[2] - views[ref].C[2]};
+    const double tn = sqrt(dpg::dot3(t, t));
+    dp_patch p{};
+    p.ref = (uint32_t)ref;
+    p.parent = 0xFFFFFFFFu;
+    for (int k = 0; k < 3; ++k) {
+        p.pos[k] = (float)X[k];
+        p.normal[k] = (float)(t[k] / tn);
+    }
+    const double Xs[3] = {p.pos[0], p.pos[1], p.pos[2]};
+    const double ns[3] = {p.normal[0], p.normal[1], p.normal[2]};
+    for (int v = 0; v < V; ++v) {
+        if (v == ref)
+            continue;
+        const int cls = dpg::classify_view(views[v], Xs, ns, vis_angle, cand_angle);
+        if (cls == 1)
+            p.vis[v >> 6] |= 1ull << (v & 63);
+        else if (cls == 2)
+            p.cand[v >> 6] |= 1ull << (v & 63);
+    }
+    out[i] = p;
+}
+
+hipError_t launch_seed_patches(const dpg::ViewDev *views, int V, const double *xyz, int64_t n, double vis_angle,
+                               double cand_angle, dp_patch *out, hipStream_t s)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(seed_patches_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, views, V, xyz, n,
+                       vis_angle, cand_angle, out);
+    return hipGetLastError();
+}
+
 // Super-tile key of each item: the centre projected into its
 // reference view, key = ref << 56 | ty' << 28 | tx' with ty = floor(v / tile),
 // tx = floor(u / tile) clamped to [-2^27, 2^27) and biased by 2^27 (NaN and

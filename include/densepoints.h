@@ -162,7 +162,7 @@ int dp_view_geometry(const double P[12], double C[3], double K[9], double E[12],
                      double xaxis[3]);
 
 /* Seed::CreatePatchesFromPoints (seed.cpp:26-54): ref = nearest camera,
- * normal = unit ray, InitRelatedImages.  Host arrays. */
+ * normal = unit ray, InitRelatedImages.  Host arrays; computed on the device. */
 int dp_seeds_to_patches(dp_ctx *ctx, const double *xyz, int n, dp_patch *out);
 
 /* One objective evaluation per patch at its stored pose: score_out[i] = mean
