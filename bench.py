@@ -422,8 +422,13 @@ def partition_summary(parts, world):
     big = [p for p in parts if p[0] >= 64 * world]  # generations large enough to share evenly
     return {"world": world, "generations": len(parts), "items": items,
             "tile_partitioned_item_frac": round(1.0 - sum(p[2] for p in parts) / max(items, 1), 5),
-            "max_share_vs_mean": round(max((p[1] * world / p[0]) for p in parts if p[0] > 0), 4) if parts else None,
-            "max_share_vs_mean_items_ge_64_per_rank": round(max(p[1] * world / p[0] for p in big), 4) if big else None,
+            # largest rank share / mean share over the generations with >= 64 items
+            # per rank; a generation of fewer items than ranks has share `world`
+            # whatever the partition, so the all-generation maximum is reported apart
+            "max_share_vs_mean": round(max(p[1] * world / p[0] for p in big), 4) if big else None,
+            "max_share_generations": len(big),
+            "max_share_vs_mean_any_generation": round(max((p[1] * world / p[0]) for p in parts if p[0] > 0), 4)
+            if parts else None,
             "item_weighted_share_vs_mean": round(sum(p[1] * world for p in parts) / max(items, 1), 4),
             "tiles_mean": round(sum(p[3] for p in parts) / max(len(parts), 1), 1)}
 
