@@ -115,6 +115,37 @@ def test_seed_conversion_equals_oracle(engine, orc):
     assert gp.tobytes() == op.tobytes()
 
 
+def test_seed_conversion_edge_points(engine, orc):
+    """seed_patches_kernel on the points the reference's nearest-camera rule
+    and InitRelatedImages are sensitive to: exact distance ties (two cameras
+    mirrored about the seed plane: the first camera wins, seed.cpp:33-40),
+    midpoints of camera pairs, points 1e-6 from a camera centre, far points,
+    points behind the cameras and off every image."""
+    sc = scene("hf6")
+    # two extra cameras mirrored in x about x = 0 (same image): every seed with
+    # x = 0 is exactly equidistant from both
+    Pm = []
+    for s in (-1.0, 1.0):
+        C = np.array([s * 0.75, 0.1, 3.0])
+        K = np.array([[200.0, 0, 160], [0, 200.0, 120], [0, 0, 1]])
+        R = np.eye(3)
+        Pm.append(K @ np.hstack([R, -R @ C[:, None]]))
+    views = [dp.View(Pm[0], sc.imgs[0]), dp.View(Pm[1], sc.imgs[0])] + sc.views
+    engine.set_views(views)
+    Cs = np.stack([v.camera_center for v in views])
+    rng = np.random.default_rng(7)
+    pts = [np.column_stack([np.zeros(64), rng.uniform(-0.5, 0.5, 64), rng.uniform(-0.3, 0.3, 64)])]
+    pts.append(0.5 * (Cs[:, None, :] + Cs[None, :, :]).reshape(-1, 3))
+    pts.append(Cs + 1e-6 * rng.standard_normal(Cs.shape))
+    pts.append(rng.uniform(-1e6, 1e6, (32, 3)))
+    pts.append(Cs + np.array([0.0, 0.0, 5.0]))
+    seeds = np.ascontiguousarray(np.concatenate(pts))
+    gp = engine.seeds_to_patches(seeds)
+    op = orc.Scene(np.stack([v.P for v in views]), [v.image for v in views]).seeds_to_patches(seeds)
+    assert gp.tobytes() == op.tobytes()
+    assert (gp["ref"][:64] == 0).all()  # exact ties: the lowest camera index
+
+
 @pytest.mark.parametrize("mode", [N.MODE_EVAL, N.MODE_FILTER, N.MODE_NM, N.MODE_SEED, N.MODE_EXPAND])
 @pytest.mark.parametrize("cell", [16, 11, 7])
 def test_refine_modes_bit_exact(engine, orc, mode, cell):
