@@ -117,13 +117,13 @@ def test_seed_conversion_equals_oracle(engine, orc):
 
 def test_seed_conversion_edge_points(engine, orc):
     """seed_patches_kernel on the points the reference's nearest-camera rule
-    and InitRelatedImages are sensitive to: exact distance ties (two cameras
-    mirrored about the seed plane: the first camera wins, seed.cpp:33-40),
-    midpoints of camera pairs, points 1e-6 from a camera centre, far points,
+    and InitRelatedImages are sensitive to: near-ties (two extra cameras
+    mirrored about the plane x = 0 and seeds on it; strict '<', the first
+    camera wins, seed.cpp:33-40), midpoints of camera pairs, points 1e-6 from a camera centre, far points,
     points behind the cameras and off every image."""
     sc = scene("hf6")
-    # two extra cameras mirrored in x about x = 0 (same image): every seed with
-    # x = 0 is exactly equidistant from both
+    # two extra cameras mirrored in x about x = 0 (same image): seeds with x = 0
+    # are equidistant from both up to the rounding of the SVD camera centres
     Pm = []
     for s in (-1.0, 1.0):
         C = np.array([s * 0.75, 0.1, 3.0])
@@ -143,7 +143,6 @@ def test_seed_conversion_edge_points(engine, orc):
     gp = engine.seeds_to_patches(seeds)
     op = orc.Scene(np.stack([v.P for v in views]), [v.image for v in views]).seeds_to_patches(seeds)
     assert gp.tobytes() == op.tobytes()
-    assert (gp["ref"][:64] == 0).all()  # exact ties: the lowest camera index
 
 
 @pytest.mark.parametrize("mode", [N.MODE_EVAL, N.MODE_FILTER, N.MODE_NM, N.MODE_SEED, N.MODE_EXPAND])
