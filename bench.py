@@ -404,6 +404,10 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
             "store_crc32": f"{crc:08x}", "ranks_store_equal": len(set(crcs)) == 1,
             "generations": int(st["generations"]), "evals": int(st["evals"]),
             "refine_ms_max_rank": round(st["refine_ms"], 1),
+            # host time per phase of the last densify (each phase ends in a host sync;
+            # refine_compact includes this rank's refine kernels), max over ranks
+            "phase_ms_max_rank": {k: round(D.max_over_ranks(v, dist, coll_dev), 2)
+                                  for k, v in st["phase_ms"].items()},
             "accepted_exchanged": int(sum(st["accepted"])),
             "gathered_MB_total": round(sum(gb) / 1e6, 3), "gathered_MB_max_generation": round(max(gb) / 1e6, 3),
             "gathered_MB_per_generation_mean": round(sum(gb) / len(gb) / 1e6, 4),

@@ -22,6 +22,8 @@ from __future__ import annotations
 
 import os
 
+import time
+
 import numpy as np
 import torch
 
@@ -284,14 +286,20 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
     items in split tiles, tiles), "accepted" and "gathered_bytes" per
     generation; with probe_worlds, "partition_probe" {world: the same records}
     of the partitions those world sizes would use (computed on this rank before
-    the real one; statistics only)."""
+    the real one; statistics only), and "phase_ms": this rank's host time per
+    phase summed over the generations (partition; refine + compaction, which
+    ends in the accepted-count read; exchange; commit) -- each phase already
+    ends in a host sync, so the split adds none."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
     rccl = dist is not None and dist.get_backend() == "nccl"
     rec = PATCH_DTYPE.itemsize
     stream = torch.cuda.current_stream(device)
     pool = _DeviceBuffers(device)
+    ph = {"begin": 0.0, "partition": 0.0, "refine_compact": 0.0, "exchange": 0.0, "commit": 0.0}
+    t = time.perf_counter()
     gen = eng.densify_begin(seeds_xyz)
+    ph["begin"] += time.perf_counter() - t
     parts, gathered, accepted = [], [], []
     probe = {int(w): [] for w in probe_worlds}
     while gen.items > 0:
@@ -299,6 +307,7 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
         for w in probe:
             _, pc, _ = eng.densify_partition_device(gen, w, tile_px)
             probe[w].append(_part_record(eng, pc))
+        t = time.perf_counter()
         d_order, counts, _ = eng.densify_partition_device(gen, world, tile_px)
         parts.append(_part_record(eng, counts))
         offs = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
@@ -309,10 +318,14 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
         acc = pool.get("acc", cap)
         comp = pool.get("comp", cap * rec)
         nacc = 0
+        t1 = time.perf_counter()
+        ph["partition"] += t1 - t
         if mine:
             eng.densify_refine_items_device(gen, d_items, mine, buf.data_ptr(), acc.data_ptr(), stream.cuda_stream)
             nacc = eng.densify_compact_accepted_device(gen, d_items, mine, buf.data_ptr(), acc.data_ptr(),
                                                        comp.data_ptr(), stream.cuda_stream)
+        t2 = time.perf_counter()
+        ph["refine_compact"] += t2 - t1
         if dist is None:
             allr, total, gb = comp, nacc, nacc * rec
         else:
@@ -335,9 +348,13 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
             total, gb = sum(ns), world * (mx * rec + 8)
         gathered.append(gb)
         accepted.append(total)
+        t3 = time.perf_counter()
+        ph["exchange"] += t3 - t2
         gen = eng.densify_commit_accepted_device(gen, allr.data_ptr(), total, stream.cuda_stream)
+        ph["commit"] += time.perf_counter() - t3
     patches, stats = eng.densify_result()
     stats = _reduce_stats(stats, dist, device)
+    stats["phase_ms"] = {k: round(v * 1e3, 2) for k, v in ph.items()}
     stats["partition"] = parts
     stats["gathered_bytes"] = gathered
     stats["accepted"] = accepted
