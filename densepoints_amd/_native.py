@@ -172,7 +172,7 @@ class DpFastOptions(ctypes.Structure):
         ("fd_step", ctypes.c_float),
         ("ls_step", ctypes.c_float),
         ("densify", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("gradient", ctypes.c_int32),
     ]
 
 

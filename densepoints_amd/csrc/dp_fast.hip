@@ -111,6 +111,7 @@ struct CgState {
     int32_t f, f1;
     float px[kFastPoses][3]; // poses to evaluate (scaled units)
     int32_t fr[kFastPoses];  // their objectives (exact integers)
+    float ga[3];             // spec v4: the gradient of the last gradient evaluation
 };
 
 // The wave's LDS.  The arena holds the staged views' 64-byte records (rank
@@ -594,6 +595,7 @@ struct Tap {
     uint32_t a0, a1;   // aligned LDS byte addresses of rows y0, y0 + 1
     uint32_t sh;       // 16 if the pair starts at an odd pixel
     uint32_t w0, w1;   // packed bilinear weights of the two rows
+    uint32_t wx, fy;   // (32 - fx) | fx << 16 and fy (the gradient's slopes only)
 };
 
 __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, const float4 &qc, uint32_t off,
@@ -623,6 +625,8 @@ __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, cons
     const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
     t.w0 = __umul24(wx, 32u - fy);
     t.w1 = __umul24(wx, fy);
+    t.wx = wx;
+    t.fy = fy;
     return t;
 }
 
@@ -645,17 +649,86 @@ __device__ __forceinline__ TapWords tap_load(const char *tiles, const Tap &t)
 
 // (p(x0), p(x0+1)) of each row as u16 pairs, each value 0x6400 + gray (fp16 of
 // 1024 + gray): sum w (0x6400 + p) + 32 = sum w p + 32 + 0x6400 * 1024
-__device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
+__device__ __forceinline__ uint32_t tap_blend_rows(const Tap &t, uint32_t r0, uint32_t r1)
 {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const uint32_t r0 = __builtin_amdgcn_alignbit(w.d[1], w.d[0], t.sh);
-    const uint32_t r1 = __builtin_amdgcn_alignbit(w.d[3], w.d[2], t.sh);
     const uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r0), __builtin_bit_cast(us2, t.w0),
                                               __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r1),
                                                                      __builtin_bit_cast(us2, t.w1),
                                                                      32u - 0x6400u * 1024u, false),
                                               false);
     return b >> 6;
+}
+
+__device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
+{
+    const uint32_t r0 = __builtin_amdgcn_alignbit(w.d[1], w.d[0], t.sh);
+    const uint32_t r1 = __builtin_amdgcn_alignbit(w.d[3], w.d[2], t.sh);
+    return tap_blend_rows(t, r0, r1);
+}
+
+// Spec v4's per-sample derivatives (or_fast.c fast_sample_q), from the same tap
+// pairs: the bilinear slopes Gx = 32 (p01 - p00) + fy ((p11 - p01) - (p10 - p00))
+// and Gy = (32 - fx)(p10 - p00) + fx (p11 - p01) as i16 dot products (the
+// fp16 bias cancels in every difference), then the three Q's as biased fp32
+// (1.5 2^23 + Q: the low 16 bits are Q as an i16)
+struct GradCoef {
+    float cu0, cv0, cui, cvi, cuj, cvj, cku, ckv;
+};
+
+struct SampleQ {
+    uint32_t qd, qa, qb; // biased fp32 bits; low halves = Qd, Qa, Qb (i16)
+};
+
+__device__ __forceinline__ SampleQ sample_q(const Tap &t, uint32_t r0, uint32_t r1, const GradCoef &c, float ti,
+                                            float tj)
+{
+    typedef short ss2 __attribute__((ext_vector_type(2)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const ss2 d = __builtin_bit_cast(ss2, r1) - __builtin_bit_cast(ss2, r0); // (p10 - p00, p11 - p01)
+    const ss2 m1 = {-1, 1};
+    const int gy = __builtin_amdgcn_sdot2(d, __builtin_bit_cast(ss2, t.wx), 0, false);
+    const int d0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(ss2, r0), m1, 0, false); // p01 - p00
+    const int e = __builtin_amdgcn_sdot2(d, m1, 0, false);                              // (p11 - p01) - (p10 - p00)
+    const int gx = __mul24((int)t.fy, e) + (d0 << 5);
+    const float fgx = (float)gx, fgy = (float)gy;
+    const f2 uv = __builtin_elementwise_fma((f2){tj, tj}, (f2){c.cuj, c.cvj},
+                                            __builtin_elementwise_fma((f2){ti, ti}, (f2){c.cui, c.cvi},
+                                                                      (f2){c.cu0, c.cv0}));
+    SampleQ q;
+    q.qd = __float_as_uint(__builtin_fmaf(fgy, uv.y, __builtin_fmaf(fgx, uv.x, 12582912.0f)));
+    const float s = __builtin_fmaf(fgy, c.ckv, fgx * c.cku);
+    q.qa = __float_as_uint(__builtin_fmaf(ti, s, 12582912.0f));
+    q.qb = __float_as_uint(__builtin_fmaf(tj, s, 12582912.0f));
+    return q;
+}
+
+// low halves of x (-> bits 0-15) and y (-> bits 16-31)
+__device__ __forceinline__ uint32_t pack_lo(uint32_t x, uint32_t y) { return __builtin_amdgcn_perm(y, x, 0x05040100u); }
+// high half of x (-> bits 0-15), low half of y (-> bits 16-31)
+__device__ __forceinline__ uint32_t pack_hl(uint32_t x, uint32_t y) { return __builtin_amdgcn_perm(y, x, 0x05040302u); }
+
+// the gradient sums of one sample: Db += Q, Dbb += b Q, Dab += QA b + a Q per
+// variable p, with P_p = (QA_p, Q_p), BA = (b, a), ZB = (0, b), as i16 dots
+struct GradSums {
+    uint32_t db[3], dbb[3], dab[3];
+};
+
+__device__ __forceinline__ void grad_acc(GradSums &S, const SampleQ &q, uint32_t aw1, uint32_t aw2, uint32_t b,
+                                         uint32_t a)
+{
+    typedef short ss2 __attribute__((ext_vector_type(2)));
+    const uint32_t P[3] = {pack_lo(aw1, q.qd), pack_hl(aw1, q.qa), pack_lo(aw2, q.qb)};
+    const ss2 BA = __builtin_bit_cast(ss2, pack_lo(b, a));
+    const ss2 ZB = __builtin_bit_cast(ss2, b << 16);
+    const ss2 Z1 = {0, 1};
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const ss2 Pp = __builtin_bit_cast(ss2, P[p]);
+        S.dab[p] = (uint32_t)__builtin_amdgcn_sdot2(Pp, BA, (int)S.dab[p], false);
+        S.dbb[p] = (uint32_t)__builtin_amdgcn_sdot2(Pp, ZB, (int)S.dbb[p], false);
+        S.db[p] = (uint32_t)__builtin_amdgcn_sdot2(Pp, Z1, (int)S.db[p], false);
+    }
 }
 
 // Objective evaluations at up to kFastPoses poses (or_fast.c fast_objective):
@@ -666,10 +739,24 @@ __device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
 // anchor samples come from group k of pass 0 by ds_bpermute.  A chunk holds
 // at most kFastItems items (the LDS records) and K' <= G poses.  kScore (one
 // pose): the fp64 NCC of rank r >= 1 goes to L.e.score[r] instead.
-template <int G, int NS, bool kTail, bool kMask, bool kScore, int kArena>
+// bf16 of x (round to nearest even on the fp32 bits, or_fast.c bf16_rn), in
+// the high half of the result
+__device__ __forceinline__ uint32_t bf16_bits(float x)
+{
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u;
+}
+
+// kGrad (spec v4, one pose: K = 1): the evaluation also yields the objective's
+// gradient (or_fast.c fast_objective_grad) in L.cg.ga; the items' records are
+// 64 bytes (the 48 of a plain item + the eight bf16 derivative coefficients)
+// and each pass reduces twelve sums per item over its whole group.
+template <int G, int NS, bool kTail, bool kMask, bool kScore, int kArena, bool kGrad = false>
 __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slots &sl, int m, int K, uint32_t rm)
 {
     constexpr int LP = 64 / G;
+    constexpr uint32_t kRS = kGrad ? 64u : 48u; // item record stride (bytes)
+    static_assert(!kGrad || 33 * 64 <= (int)sizeof(EvalRec) * kFastItems, "32 gradient items fit the records");
     const int lane = lane_id();
     if (m < 2) {
         for (int k = 0; k < K; ++k)
@@ -683,7 +770,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
     int kc = m <= 11 ? 4 : m <= 14 ? 3 : m <= 22 ? 2 : 1;
     kc = kc < G ? kc : G;
     kc = kc < kFastPoses ? kc : kFastPoses;
-    kc = kScore ? 1 : kc;
+    kc = (kScore || kGrad) ? 1 : kc;
     const int j = (int)((unsigned)lane / LP), g = lane & (LP - 1);
     const char *tiles = (const char *)L.arena;
     const int N = a.cell * a.cell;
@@ -702,6 +789,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             const int k = lane - r * kn;
             const float4 *R = (const float4 *)((const char *)L.arena + kFastRec * r);
             const float4 r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3];
+            EvalRec &E = *(EvalRec *)((char *)L.e.par + (uint32_t)lane * kRS);
             const float4 pf = L.cg.pf[k0 + k];
             const float df = pf.x, af = pf.y, bf = pf.z;
             const float ax = __builtin_fmaf(df, r0.w, r0.x), ay = __builtin_fmaf(df, r1.x, r0.y);
@@ -715,29 +803,56 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             const uint32_t pk = __float_as_uint(r3.w);
             const uint32_t tw1 = (pk >> 7) & 63u, th1 = (pk >> 13) & 63u, toff = (pk >> 19) << 2;
             const uint32_t rowb = ((tw1 + 3u) >> 1) << 2;
-            EvalRec &E = L.e.par[lane];
             // .z fields: the tile's row bytes, and the byte offset of the
             // lanes that hold the item's anchor samples (group k of pass 0)
             E.q[0] = make_float4(u0, v0, __uint_as_float(rowb), __uint_as_float(0x4B000000u + 32u * tw1));
             E.q[1] = make_float4(__builtin_fmaf(-u0, iz, ix) * rz, __builtin_fmaf(-v0, iz, iy) * rz,
                                  __uint_as_float((uint32_t)(k * LP) << 2), __uint_as_float(0x4B000000u + 32u * th1));
-            E.q[2] = make_float4(__builtin_fmaf(-u0, jz, jx) * rz, __builtin_fmaf(-v0, jz, jy) * rz, 0.0f,
-                                 __uint_as_float(toff - __umul24((0x4B000000u >> 5) & 0xffffffu, rowb)));
+            (void)0;
+            const float ui = __builtin_fmaf(-u0, iz, ix) * rz, vi = __builtin_fmaf(-v0, iz, iy) * rz;
+            const float uj = __builtin_fmaf(-u0, jz, jx) * rz, vj = __builtin_fmaf(-v0, jz, jy) * rz;
+            E.q[2] = make_float4(uj, vj, 0.0f, __uint_as_float(toff - __umul24((0x4B000000u >> 5) & 0xffffffu, rowb)));
+            if (kGrad) {
+                // or_fast.c fast_sample_q: the affine map's derivatives, scaled by
+                // sd 2^-10 / st 2^-10, as bf16 pairs (U low, V high)
+                const float z1 = r1.y;
+                const float du0 = __builtin_fmaf(-u0, z1, r0.w) * rz, dv0 = __builtin_fmaf(-v0, z1, r1.x) * rz;
+                const float dui = __builtin_fmaf(-du0, iz, -(ui * z1)) * rz, dvi = __builtin_fmaf(-dv0, iz, -(vi * z1)) * rz;
+                const float duj = __builtin_fmaf(-du0, jz, -(uj * z1)) * rz, dvj = __builtin_fmaf(-dv0, jz, -(vj * z1)) * rz;
+                const float ku = __builtin_fmaf(u0, r3.z, -r3.x) * rz, kv = __builtin_fmaf(v0, r3.z, -r3.y) * rz;
+                const float fd = L.F.sd * 0x1p-10f, fa = L.F.st * 0x1p-10f;
+                uint4 &W = *(uint4 *)((char *)&E + 48);
+                W.x = (bf16_bits(du0 * fd) >> 16) | bf16_bits(dv0 * fd);
+                W.y = (bf16_bits(dui * fd) >> 16) | bf16_bits(dvi * fd);
+                W.z = (bf16_bits(duj * fd) >> 16) | bf16_bits(dvj * fd);
+                W.w = (bf16_bits(ku * fa) >> 16) | bf16_bits(kv * fa);
+            }
         }
         wave_sync();
         TMARK(L, 10);
         uint32_t a0s[NS]; // pass 0's samples: group k holds pose k's anchor
+        // kGrad: pass 0's anchor derivatives, (QAd, QAa) and QAb per slot
+        uint32_t aq1[NS], aq2[NS];
         // kTail: the last sample of every item (N = NS LP + 1), one lane per
         // item (Q <= kFastItems < 64), computed alongside the first pass
         uint32_t bt = 0;
+        SampleQ qt{}; // kGrad: the tail sample's derivatives
         const int passes = (Q + G - 1) / G;
         for (int p = 0; p < passes; ++p) {
             const int i = p * G + j;
             const bool act = i < Q;
             const bool tail = kTail && p == 0;
-            const EvalRec &E = *(const EvalRec *)((const char *)L.e.par + (act ? (uint32_t)i * 48u : 0u));
+            const EvalRec &E = *(const EvalRec *)((const char *)L.e.par + (act ? (uint32_t)i * kRS : 0u));
             const float4 qa = E.q[0], qb = E.q[1], qc = E.q[2];
             const uint32_t off = __float_as_uint(qc.w), rowb = __float_as_uint(qa.z);
+            GradCoef gc{};
+            if (kGrad) {
+                const uint4 W = *(const uint4 *)((const char *)&E + 48);
+                gc = GradCoef{__uint_as_float(W.x << 16), __uint_as_float(W.x & 0xFFFF0000u),
+                              __uint_as_float(W.y << 16), __uint_as_float(W.y & 0xFFFF0000u),
+                              __uint_as_float(W.z << 16), __uint_as_float(W.z & 0xFFFF0000u),
+                              __uint_as_float(W.w << 16), __uint_as_float(W.w & 0xFFFF0000u)};
+            }
             // kMask: the last slot's (i, j) by an LDS read per pass through an
             // opaque address, so that it is not hoisted into registers again
             float tl_i = 0.0f, tl_j = 0.0f;
@@ -754,10 +869,18 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             for (int s2 = 0; s2 < NS; ++s2)
                 tp[s2] = (kMask && s2 == NS - 1) ? tap_addr(qa, qb, qc, off, rowb, tl_i, tl_j)
                                                  : tap_addr(qa, qb, qc, off, rowb, sl.ti[s2], sl.tj[s2]);
+            GradCoef tgc{};
             if (tail) {
-                const EvalRec &T = L.e.par[lane < Q ? lane : 0];
+                const EvalRec &T = *(const EvalRec *)((const char *)L.e.par + (uint32_t)(lane < Q ? lane : 0) * kRS);
                 const float4 ta = T.q[0], tb = T.q[1], tc = T.q[2];
                 tt = tap_addr(ta, tb, tc, __float_as_uint(tc.w), __float_as_uint(ta.z), sl.tail, sl.tail);
+                if (kGrad) {
+                    const uint4 W = *(const uint4 *)((const char *)&T + 48);
+                    tgc = GradCoef{__uint_as_float(W.x << 16), __uint_as_float(W.x & 0xFFFF0000u),
+                                   __uint_as_float(W.y << 16), __uint_as_float(W.y & 0xFFFF0000u),
+                                   __uint_as_float(W.z << 16), __uint_as_float(W.z & 0xFFFF0000u),
+                                   __uint_as_float(W.w << 16), __uint_as_float(W.w & 0xFFFF0000u)};
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
             TapWords tw[NS], twt{};
@@ -768,16 +891,40 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
                 twt = tap_load(tiles, tt);
             __builtin_amdgcn_sched_barrier(0);
             uint32_t b[NS];
+            SampleQ sq[NS];
 #pragma unroll
-            for (int s2 = 0; s2 < NS; ++s2)
-                b[s2] = (kMask && s2 == NS - 1) ? lane_select(sl.live_last, tap_blend(tp[s2], tw[s2]))
-                                                : tap_blend(tp[s2], tw[s2]);
-            if (tail)
-                bt = tap_blend(tt, twt);
+            for (int s2 = 0; s2 < NS; ++s2) {
+                const uint32_t r0 = __builtin_amdgcn_alignbit(tw[s2].d[1], tw[s2].d[0], tp[s2].sh);
+                const uint32_t r1 = __builtin_amdgcn_alignbit(tw[s2].d[3], tw[s2].d[2], tp[s2].sh);
+                const uint32_t bb = tap_blend_rows(tp[s2], r0, r1);
+                b[s2] = (kMask && s2 == NS - 1) ? lane_select(sl.live_last, bb) : bb;
+                if (kGrad) {
+                    const bool last = kMask && s2 == NS - 1;
+                    sq[s2] = sample_q(tp[s2], r0, r1, gc, last ? tl_i : sl.ti[s2], last ? tl_j : sl.tj[s2]);
+                    if (last) {
+                        // dead lanes of the last slot: Q = 0 (their samples are not in the window)
+                        sq[s2].qd = lane_select(sl.live_last, sq[s2].qd);
+                        sq[s2].qa = lane_select(sl.live_last, sq[s2].qa);
+                        sq[s2].qb = lane_select(sl.live_last, sq[s2].qb);
+                    }
+                }
+            }
+            if (tail) {
+                const uint32_t r0 = __builtin_amdgcn_alignbit(twt.d[1], twt.d[0], tt.sh);
+                const uint32_t r1 = __builtin_amdgcn_alignbit(twt.d[3], twt.d[2], tt.sh);
+                bt = tap_blend_rows(tt, r0, r1);
+                if (kGrad)
+                    qt = sample_q(tt, r0, r1, tgc, sl.tail, sl.tail);
+            }
             if (p == 0) {
 #pragma unroll
-                for (int s2 = 0; s2 < NS; ++s2)
+                for (int s2 = 0; s2 < NS; ++s2) {
                     a0s[s2] = b[s2];
+                    if (kGrad) {
+                        aq1[s2] = pack_lo(sq[s2].qd, sq[s2].qa);
+                        aq2[s2] = sq[s2].qb;
+                    }
+                }
             }
             // the anchor samples of this item's pose through the LDS crossbar
             const int src = (int)__float_as_uint(qb.z) + (g << 2);
@@ -792,17 +939,41 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
                 ss = __umul24(b[s2], b[s2]) + ss;
                 sx = __umul24(av[s2], b[s2]) + sx;
             }
-            // four partial sums per moment (DPP within rows of 16 down to
-            // groups of LP/4 lanes), stored in the item's own record, which
-            // this pass has read (pass 0's tail read every record first);
-            // the NCC finish adds the partials
-            partial_total3<LP / 4>(s, ss, sx);
-            if (act && (g & (LP / 4 - 1)) == LP / 4 - 1) {
-                uint32_t *M = (uint32_t *)&L.e.par[i];
-                const int pi = g / (LP / 4);
-                M[pi] = s;
-                M[4 + pi] = ss;
-                M[8 + pi] = sx;
+            if (!kGrad) {
+                // four partial sums per moment (DPP within rows of 16 down to
+                // groups of LP/4 lanes), stored in the item's own record, which
+                // this pass has read (pass 0's tail read every record first);
+                // the NCC finish adds the partials
+                partial_total3<LP / 4>(s, ss, sx);
+                if (act && (g & (LP / 4 - 1)) == LP / 4 - 1) {
+                    uint32_t *M = (uint32_t *)&L.e.par[i];
+                    const int pi = g / (LP / 4);
+                    M[pi] = s;
+                    M[4 + pi] = ss;
+                    M[8 + pi] = sx;
+                }
+            } else {
+                GradSums S{};
+#pragma unroll
+                for (int s2 = 0; s2 < NS; ++s2) {
+                    const uint32_t aw1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)aq1[s2]);
+                    const uint32_t aw2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)aq2[s2]);
+                    grad_acc(S, sq[s2], aw1, aw2, b[s2], av[s2]);
+                }
+                // twelve totals per item over its whole group (lane LP - 1 of
+                // the group), stored as words 0..11 of the item's record: Sb,
+                // Sbb, Sab, Db[3], Dbb[3], Dab[3]
+                uint32_t tot[12] = {s, ss, sx, S.db[0], S.db[1], S.db[2], S.dbb[0], S.dbb[1], S.dbb[2],
+                                    S.dab[0], S.dab[1], S.dab[2]};
+#pragma unroll
+                for (int k = 0; k < 12; ++k)
+                    tot[k] = group_total<G>(tot[k]);
+                if (act && g == LP - 1) {
+                    uint32_t *M = (uint32_t *)((char *)L.e.par + (uint32_t)i * kRS);
+#pragma unroll
+                    for (int k = 0; k < 12; ++k)
+                        M[k] = tot[k];
+                }
             }
         }
         wave_sync();
@@ -817,12 +988,56 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
         const uint32_t a0 = kTail ? (uint32_t)__builtin_amdgcn_ds_bpermute(kt << 2, (int)bt) : 0u;
         const uint32_t b0 = kTail ? (uint32_t)__builtin_amdgcn_ds_bpermute((it < 64 ? it : 0) << 2, (int)bt) : 0u;
         int q = 0;
+        uint32_t gq[3] = {0u, 0u, 0u}; // kGrad: this view's dNCC_p in 2^-24 steps
+        // kGrad + kTail: the anchor's tail derivatives (item 0's, lane 0)
+        uint32_t atq[3] = {0u, 0u, 0u};
+        if (kGrad && kTail) {
+            atq[0] = (uint32_t)__builtin_amdgcn_ds_bpermute(0, (int)qt.qd);
+            atq[1] = (uint32_t)__builtin_amdgcn_ds_bpermute(0, (int)qt.qa);
+            atq[2] = (uint32_t)__builtin_amdgcn_ds_bpermute(0, (int)qt.qb);
+        }
         if (lane < Q && rt >= 1) {
-            const uint4 *Ma = (const uint4 *)&L.e.par[kt], *Mb = (const uint4 *)&L.e.par[it];
-            const uint4 as = Ma[0], aas = Ma[1], bs = Mb[0], bbs = Mb[1], abs4 = Mb[2];
-            uint32_t sa = (as.x + as.y) + (as.z + as.w), saa = (aas.x + aas.y) + (aas.z + aas.w);
-            uint32_t sb = (bs.x + bs.y) + (bs.z + bs.w), sbb = (bbs.x + bbs.y) + (bbs.z + bbs.w);
-            uint32_t sab = (abs4.x + abs4.y) + (abs4.z + abs4.w);
+            uint32_t sa, saa, sb, sbb, sab;
+            uint32_t da[3], daa[3], db[3], dbb[3], dab[3];
+            if (kGrad) {
+                // whole-item totals (words 0..11 of the 64-byte records)
+                const uint32_t *Ma = (const uint32_t *)L.e.par;
+                const uint32_t *Mb = (const uint32_t *)((const char *)L.e.par + (uint32_t)it * kRS);
+                sa = Ma[0];
+                saa = Ma[1];
+                sb = Mb[0];
+                sbb = Mb[1];
+                sab = Mb[2];
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp) {
+                    da[pp] = Ma[3 + pp];
+                    daa[pp] = Ma[6 + pp];
+                    db[pp] = Mb[3 + pp];
+                    dbb[pp] = Mb[6 + pp];
+                    dab[pp] = Mb[9 + pp];
+                }
+            } else {
+                const uint4 *Ma = (const uint4 *)&L.e.par[kt], *Mb = (const uint4 *)&L.e.par[it];
+                const uint4 as = Ma[0], aas = Ma[1], bs = Mb[0], bbs = Mb[1], abs4 = Mb[2];
+                sa = (as.x + as.y) + (as.z + as.w);
+                saa = (aas.x + aas.y) + (aas.z + aas.w);
+                sb = (bs.x + bs.y) + (bs.z + bs.w);
+                sbb = (bbs.x + bbs.y) + (bbs.z + bbs.w);
+                sab = (abs4.x + abs4.y) + (abs4.z + abs4.w);
+            }
+            if (kGrad && kTail) {
+                // the tail sample's terms (the spec sums every sample of the window)
+                const uint32_t btq[3] = {qt.qd, qt.qa, qt.qb}; // own lane = item it
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp) {
+                    const int qa_t = (int)(short)(atq[pp] & 0xFFFFu), qb_t = (int)(short)(btq[pp] & 0xFFFFu);
+                    da[pp] += (uint32_t)qa_t;
+                    daa[pp] += (uint32_t)((int)a0 * qa_t);
+                    db[pp] += (uint32_t)qb_t;
+                    dbb[pp] += (uint32_t)((int)b0 * qb_t);
+                    dab[pp] += (uint32_t)(qa_t * (int)b0 + (int)a0 * qb_t);
+                }
+            }
             if (kTail) {
                 sa += a0;
                 saa += __umul24(a0, a0);
@@ -846,8 +1061,35 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
                 const float rr = recip_rn(den > dminf ? den : dminf);
                 q = (int)__builtin_rintf(((float)num * rr) * 16777216.0f);
             }
+            if (kGrad) {
+                // or_fast.c fast_objective_grad: fp64, each operation one IEEE rounding
+                const double den = sqrt(va * vb);
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp) {
+                    const double dA = (double)(int)da[pp], dAA = (double)(int)daa[pp];
+                    const double dB = (double)(int)db[pp], dBB = (double)(int)dbb[pp], dAB = (double)(int)dab[pp];
+                    const double dnum = dN * dAB - dA * Sb - Sa * dB;
+                    double dncc;
+                    if (den > dmin) {
+                        const double dva = 2.0 * (dN * dAA - Sa * dA);
+                        const double dvb = 2.0 * (dN * dBB - Sb * dB);
+                        dncc = dnum / den - (num / den) * (0.5 * (dva / va + dvb / vb));
+                    } else {
+                        dncc = dnum / dmin;
+                    }
+                    gq[pp] = (uint32_t)(int)__builtin_rint(dncc * 16777216.0);
+                }
+            }
         }
         TMARK(L, 12);
+        if (kGrad) {
+            // the gradient: exact integer sums over the views, times -2^-20
+#pragma unroll
+            for (int pp = 0; pp < 3; ++pp) {
+                const int tot = __builtin_amdgcn_readlane((int)group_total<1>(gq[pp]), 63);
+                L.cg.ga[pp] = (float)tot * -0x1p-20f;
+            }
+        }
         if (!kScore) {
             // per pose: (m - 1) 2^24 minus the sum of its NCCs in 2^-24 steps,
             // an exact integer reduction: one inclusive prefix over the wave,
@@ -888,7 +1130,7 @@ template <int kArena> __device__ __forceinline__ void set_pose(FastLds<kArena> &
 // each iteration are independent, so they share one set of passes
 // (evaluate_poses); the results are those of one evaluation at a time.
 // Returns evaluations; L.cg.x = the scaled pose.
-template <int G, int NS, bool kTail, bool kMask, int kArena>
+template <int G, int NS, bool kTail, bool kMask, int kArena, bool kGrad>
 __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl, int m)
 {
     enum { kStart = 0, kFd = 1, kProbe1 = 2, kProbe2 = 3 };
@@ -910,7 +1152,10 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
         const bool fd_round = phase == kStart || phase == kFd;
         if (!(fd_round && reuse_g)) {
             int K = 1;
-            if (fd_round) {
+            if (fd_round && kGrad) {
+                // spec v4: one evaluation with the analytic gradient at x
+                set_pose(L, 0, C.x[0], C.x[1], C.x[2]);
+            } else if (fd_round) {
                 // f(x) (start only), then f(x + h e_i), i = 0, 1, 2
                 const int k0 = phase == kStart ? 1 : 0;
                 if (phase == kStart)
@@ -928,8 +1173,22 @@ __device__ int cg_refine(const FastArgs &a, FastLds<kArena> &L, const Slots &sl,
             }
             wave_sync();
             TMARK(L, 15);
-            evaluate_poses<G, NS, kTail, kMask, false>(a, L, sl, m, K, rm);
-            if (fd_round) {
+            if (kGrad && fd_round)
+                evaluate_poses<G, NS, kTail, kMask, false, kArena, true>(a, L, sl, m, 1, rm);
+            else
+                evaluate_poses<G, NS, kTail, kMask, false, kArena, false>(a, L, sl, m, K, rm);
+            if (fd_round && kGrad) {
+                if (phase == kStart) {
+                    C.f = C.fr[0];
+                    E = 1;
+                    if (a.fo.iters <= 0)
+                        break;
+                } else {
+                    E += 1;
+                }
+                for (int i = 0; i < 3; ++i)
+                    C.g[i] = C.ga[i];
+            } else if (fd_round) {
                 int k0 = 0;
                 if (phase == kStart) {
                     C.f = C.fr[0];
@@ -1106,6 +1365,11 @@ template <int kArena> struct FastOcc {
     static constexpr int value = kArena <= 6656 ? 4 : kArena <= 8192 ? 3 : 2;
 };
 
+// the refine with spec v4's analytic gradient (dp_fast_options.gradient = 1):
+// its own kernel instances (kMode), so the forward-difference ones keep their
+// register allocation
+constexpr int kFastRefineGrad = 100;
+
 template <int G, int NS, bool kTail, bool kMask, int kArena, int kMode>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kArena>::value))) void fast_kernel(FastArgs a)
 {
@@ -1213,7 +1477,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
                 } else {
                     const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), wave_bytes, wave_clip);
                     if (m >= 2) {
-                        const int E = cg_refine<G, NS, kTail, kMask>(a, L, sl, m);
+                        const int E = cg_refine<G, NS, kTail, kMask, kArena, kMode == kFastRefineGrad>(a, L, sl, m);
                         TMARK(L, 5);
                         p.evals += (uint32_t)E;
                         wave_vev += (unsigned long long)E * (unsigned long long)m;
@@ -1405,6 +1669,8 @@ static hipError_t launch_fast_m(const FastArgs &a, hipStream_t s)
     const int grid = (int)(want < cap ? want : cap);
     if (a.mode == DP_MODE_FAST_EVAL)
         hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, a);
+    else if (a.fo.gradient)
+        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, kFastRefineGrad>), dim3(grid), dim3(64), 0, s, a);
     else
         hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_REFINE>), dim3(grid), dim3(64), 0, s,
                            a);
@@ -1413,10 +1679,14 @@ static hipError_t launch_fast_m(const FastArgs &a, hipStream_t s)
 
 // kMask: the last slot has dead lanes (N not a multiple of the pass's lane
 // count and no tail round)
+// The gradient refine always takes the masked instance (a full last slot is a
+// lane mask of all ones): keeping the last slot's (i, j) in LDS is what holds
+// its n = 16 instance to 128 VGPRs without scratch.
 template <int G, int NS, bool kTail, int kBudget> static hipError_t launch_fast_t(const FastArgs &a, hipStream_t s)
 {
     const int N = a.cell * a.cell;
-    if (kTail || N == NS * (64 / G))
+    const bool grad = a.mode != DP_MODE_FAST_EVAL && a.fo.gradient != 0;
+    if (kTail || (N == NS * (64 / G) && !grad))
         return launch_fast_m<G, NS, kTail, false, kBudget>(a, s);
     return launch_fast_m<G, NS, kTail, true, kBudget>(a, s);
 }
@@ -1440,9 +1710,9 @@ int fast_check_options(dp_ctx *c, const dp_fast_options &f)
     if (f.iters < 0 || f.iters > 64 || f.margin < 0 || f.margin > dpk::kFastMaxMargin || f.tile_budget < 64 ||
         f.tile_budget > kFastBudget || f.max_views < 2 || f.max_views > dpk::kFastMaxV ||
         !(f.fd_step >= 0x1p-20f && f.fd_step <= 0x1p+20f) || !(f.ls_step > 0.0f && f.ls_step <= 0x1p+20f) ||
-        (f.densify != 0 && f.densify != 1))
+        (f.densify != 0 && f.densify != 1) || (f.gradient != 0 && f.gradient != 1))
         return fail(c, DP_E_ARG, "dp_fast_options out of range (margin <= 7, tile_budget <= 16384, 2 <= max_views "
-                                 "<= 32, fd_step in [2^-20, 2^20], 0 < ls_step <= 2^20)");
+                                 "<= 32, fd_step in [2^-20, 2^20], 0 < ls_step <= 2^20, gradient 0 or 1)");
     return DP_OK;
 }
 
@@ -1634,6 +1904,7 @@ extern "C" void dp_default_fast_options(dp_fast_options *f)
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;
     f->densify = 0;
+    f->gradient = 1;
 }
 
 extern "C" int dp_set_fast_options(dp_ctx *c, const dp_fast_options *f)

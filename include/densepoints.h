@@ -451,11 +451,20 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  *    finished in fp32 and rounded to a multiple of 2^-24, summed exactly (the
  *    functor calc's mean without its constant 1/(m-1)); reported scores
  *    (FAST_EVAL, filter) use an fp64 finish;
- *  - refine: `iters` Polak-Ribiere+ conjugate-gradient steps with a forward-
- *    difference gradient (step fd_step) and a two-probe line search (initial
- *    step ls_step, doubled on success, halved on failure): E = 1 + 5 iters,
- *    less 3 per iteration after a line search that left x unchanged (the
- *    last gradient is reused: the forward differences would repeat it);
+ *  - refine: `iters` Polak-Ribiere+ conjugate-gradient steps with a two-probe
+ *    line search (initial step ls_step, doubled on success, halved on
+ *    failure) and, by `gradient`:
+ *      1 (spec v4, default): the ANALYTIC gradient of the objective -- per
+ *        sample the bilinear tap slopes times the window map's derivatives
+ *        (bf16 coefficients per view and pose), as 16-bit integers Q (one unit
+ *        = one gray level per scaled pose unit); per view exact integer sums
+ *        (sum Q, sum b Q, sum (Q_anchor b + a Q)) and NCC's quotient rule in
+ *        fp64, quantised to 2^-24 and summed exactly.  One evaluation with the
+ *        gradient at the start and after every line search that moved x:
+ *        E = 1 + 2 iters + (iterations after a moving line search);
+ *      0 (spec v3): a forward-difference gradient (step fd_step): E = 1 +
+ *        5 iters, less 3 per iteration after a line search that left x
+ *        unchanged (the last gradient is reused: the differences would repeat it);
  *  - then Patch::InitRelatedImages (patch.cpp:19-49) at the new pose (its
  *    angle tests as cosine tests, x > cos(angle) with the cosines from the
  *    host libm; frame unit vectors by one reciprocal and products) and the
@@ -469,13 +478,14 @@ typedef struct dp_fast_options {
     int32_t tile_budget;  /* 6656  bytes of LDS tiles per patch (<= 16384; the
                                    kernel's arena is 6, 8 or 16 KiB by this value) */
     int32_t max_views;    /* 32    staged views per patch (<= 32)                   */
-    float fd_step;        /* 0.5   forward-difference step, scaled units            */
+    float fd_step;        /* 0.5   forward-difference step, scaled units (gradient 0) */
     float ls_step;        /* 1.0   initial line-search step, scaled units           */
     int32_t densify;      /* 0     1: dp_densify runs the seed stage (at
                                    seed_cell_size) and every expansion (at
                                    expand_cell_size) with the fast refine, and so
                                    does the generation-at-a-time (multi-GPU) API */
-    int32_t reserved;
+    int32_t gradient;     /* 1     1: analytic gradient (spec v4), 0: forward
+                                   differences (spec v3, rounds 2-4)              */
 } dp_fast_options;
 
 void dp_default_fast_options(dp_fast_options *fo);

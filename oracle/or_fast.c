@@ -65,6 +65,7 @@ void or_fast_default_options(or_fast_options *f)
     f->max_views = FAST_MAX_VIEWS;
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;
+    f->gradient = 1;
 }
 
 /* BGR2GRAY on 8U (the parity spec's 14-bit fixed point); the product stores
@@ -386,6 +387,98 @@ static void fast_sample(const fast_view *t, int cell, fast_pose q, int32_t *out)
     }
 }
 
+/*
+ * Spec v4 (gradient = 1): the samples of one view at a pose together with their
+ * derivatives with respect to the scaled pose x, as 16-bit integers Q.
+ *
+ * Per (view, pose), fp32, each operation one rounding (z1 = vec[1].z, the
+ * depth column's z):
+ *   dU0 = fmaf(-U0, z1, vec[1].x) rz            dV0 likewise with V0, vec[1].y
+ *   dUi = fmaf(-dU0, B1z, -(Ui z1)) rz          dVi, dUj (B2z), dVj likewise
+ *   ku  = fmaf(U0, vec[4].z, -vec[4].x) rz      kv likewise with V0, vec[4].y
+ * scaled by fd = sd 2^-10 (dU0 .. dVj) and fa = st 2^-10 (ku, kv): 2^-10 =
+ * 2^-6 (the bilinear slope's 1/64) times 2^-4, the derivative quantum (one Q
+ * unit = 16 sample units = one gray level per scaled pose unit), and rounded
+ * to bf16 (round to nearest even on the fp32 bits: the device keeps the eight
+ * coefficients of a (view, pose) in one 16-byte record word).
+ * Per sample, with the taps p00, p01 (row y0), p10, p11 and fx, fy of fast_sample:
+ *   Gx = (32 - fy)(p01 - p00) + fy (p11 - p10),  Gy = (32 - fx)(p10 - p00) + fx (p11 - p01)
+ *   au = fmaf(tj, cUj, fmaf(ti, cUi, cU0))        av likewise (the window map's form)
+ *   Qd = fmaf(Gy, av, fmaf(Gx, au, M)) - M        (M = 1.5 2^23: each fmaf rounds to an integer)
+ *   s  = fmaf(Gy, ckv, Gx cku),  Qa = fmaf(ti, s, M) - M,  Qb = fmaf(tj, s, M) - M
+ * each Q taken as its low 16 bits, sign-extended (the device keeps Q in i16
+ * halves); no special case at a clamped tile edge (the slope of the taps read).
+ */
+#define FAST_QMAGIC 12582912.0f /* 1.5 * 2^23 */
+static inline float bf16_rn(float x)
+{
+    union {
+        float f;
+        uint32_t u;
+    } v = {x};
+    v.u = (v.u + 0x7FFFu + ((v.u >> 16) & 1u)) & 0xFFFF0000u;
+    return v.f;
+}
+
+static inline int32_t q16_of(float biased)
+{
+    union {
+        float f;
+        uint32_t u;
+    } v = {biased};
+    return (int32_t)(int16_t)(uint16_t)(v.u - 0x4B400000u);
+}
+
+static void fast_sample_q(const fast_view *t, int cell, fast_pose q, float sd, float st, int32_t *out,
+                          int32_t (*Q)[3])
+{
+    float A[3], B1[3], B2[3];
+    for (int k = 0; k < 3; ++k) {
+        A[k] = fmaf(q.df, t->vec[1][k], t->vec[0][k]);
+        B1[k] = fmaf(-q.af, t->vec[4][k], t->vec[2][k]);
+        B2[k] = fmaf(-q.bf, t->vec[4][k], t->vec[3][k]);
+    }
+    const float rz = rcp_rn(fmaxf(A[2], FAST_RCP_MIN));
+    const float U0 = A[0] * rz, V0 = A[1] * rz;
+    const float Ui = fmaf(-U0, B1[2], B1[0]) * rz, Vi = fmaf(-V0, B1[2], B1[1]) * rz;
+    const float Uj = fmaf(-U0, B2[2], B2[0]) * rz, Vj = fmaf(-V0, B2[2], B2[1]) * rz;
+    const float z1 = t->vec[1][2];
+    const float dU0 = fmaf(-U0, z1, t->vec[1][0]) * rz, dV0 = fmaf(-V0, z1, t->vec[1][1]) * rz;
+    const float dUi = fmaf(-dU0, B1[2], -(Ui * z1)) * rz, dVi = fmaf(-dV0, B1[2], -(Vi * z1)) * rz;
+    const float dUj = fmaf(-dU0, B2[2], -(Uj * z1)) * rz, dVj = fmaf(-dV0, B2[2], -(Vj * z1)) * rz;
+    const float ku = fmaf(U0, t->vec[4][2], -t->vec[4][0]) * rz, kv = fmaf(V0, t->vec[4][2], -t->vec[4][1]) * rz;
+    const float fd = sd * 0x1p-10f, fa = st * 0x1p-10f;
+    const float cU0 = bf16_rn(dU0 * fd), cUi = bf16_rn(dUi * fd), cUj = bf16_rn(dUj * fd);
+    const float cV0 = bf16_rn(dV0 * fd), cVi = bf16_rn(dVi * fd), cVj = bf16_rn(dVj * fd);
+    const float cku = bf16_rn(ku * fa), ckv = bf16_rn(kv * fa);
+    const float c = 0.5f * (float)(cell - 1);
+    for (int j = 0; j < cell; ++j) {
+        const float tj = (float)j - c;
+        for (int i = 0; i < cell; ++i) {
+            const float ti = (float)i - c;
+            const float u = fmaf(tj, Uj, fmaf(ti, Ui, U0));
+            const float w = fmaf(tj, Vj, fmaf(ti, Vi, V0));
+            const float Ub = fminf(fmaxf(u + 0x1p23f, 0x1p23f), 0x1p23f + t->umax);
+            const float Vb = fminf(fmaxf(w + 0x1p23f, 0x1p23f), 0x1p23f + t->vmax);
+            const int iu = (int)(Ub - 0x1p23f), iv = (int)(Vb - 0x1p23f);
+            const int x0 = iu >> 5, fx = iu & 31, y0 = iv >> 5, fy = iv & 31;
+            const uint16_t e0 = t->tile[y0 * (t->tw + 1) + x0];
+            const uint16_t e1 = t->tile[y0 * (t->tw + 1) + x0 + 1];
+            const int p00 = e0 & 255, p10 = e0 >> 8, p01 = e1 & 255, p11 = e1 >> 8;
+            const int idx = j * cell + i;
+            out[idx] = ((32 - fx) * (32 - fy) * p00 + fx * (32 - fy) * p01 + (32 - fx) * fy * p10 + fx * fy * p11 +
+                        32) >> 6;
+            const float gx = (float)((32 - fy) * (p01 - p00) + fy * (p11 - p10));
+            const float gy = (float)((32 - fx) * (p10 - p00) + fx * (p11 - p01));
+            const float au = fmaf(tj, cUj, fmaf(ti, cUi, cU0)), av = fmaf(tj, cVj, fmaf(ti, cVi, cV0));
+            Q[idx][0] = q16_of(fmaf(gy, av, fmaf(gx, au, FAST_QMAGIC)));
+            const float s = fmaf(gy, ckv, gx * cku);
+            Q[idx][1] = q16_of(fmaf(ti, s, FAST_QMAGIC));
+            Q[idx][2] = q16_of(fmaf(tj, s, FAST_QMAGIC));
+        }
+    }
+}
+
 /* NCC of integer-moment windows (values in 1/16 gray levels): the reference
  * NCCScore with max(0.1, sigma_a sigma_b) scaled to these units; fp64 finish */
 static double fast_ncc(int64_t N, int64_t Sa, int64_t Saa, int64_t Sb, int64_t Sbb, int64_t Sab, double dmin)
@@ -443,12 +536,93 @@ static int32_t fast_objective(const fast_patch *fp, int cell, double ncc_denom_m
     return (int32_t)((int64_t)(m - 1) * 16777216 - qsum); /* < 2^29 */
 }
 
-/* nonlinear CG (Polak-Ribiere+) with forward differences and a two-probe
- * line search, fp32; returns evaluations, x holds the scaled pose */
+/*
+ * Spec v4: the objective (as fast_objective) and its gradient at a pose.  Per
+ * view k >= 1, exact integer sums over the samples (uint32, wrapping) of the
+ * anchor's a, QA and the view's b, Q (fast_sample_q):
+ *   Da = sum QA, Daa = sum a QA (the anchor's), Db = sum Q, Dbb = sum b Q,
+ *   Dab = sum (QA b + a Q)
+ * then fp64 (each operation one IEEE rounding) with the moments of
+ * fast_objective (num, va, vb; den = sqrt(va vb)):
+ *   dnum = N Dab - Da Sb - Sa Db,  dva = 2 (N Daa - Sa Da),  dvb = 2 (N Dbb - Sb Db)
+ *   dncc = den > dmin ? dnum / den - (num / den) (0.5 (dva / va + dvb / vb)) : dnum / dmin
+ * rounded to an integer multiple of 2^-24 (rint(dncc 2^24), int32) and summed
+ * over the views exactly; g = -(that sum) 2^-20 (fp32): the derivative of
+ * sum_k (1 - NCC_k) per scaled pose unit (Q carries 2^-4 of it).
+ */
+static int32_t fast_objective_grad(const fast_patch *fp, int cell, double ncc_denom_min, const float x[3],
+                                   float g[3])
+{
+    const int m = fp->m;
+    g[0] = g[1] = g[2] = 0.0f;
+    if (m < 2) return 2 << 24;
+    const fast_pose q = pose_of(fp, x);
+    const int N = cell * cell;
+    int32_t a[16 * 16], b[16 * 16], QA[16 * 16][3], Q[16 * 16][3];
+    fast_sample_q(&fp->fv[0], cell, q, fp->sd, fp->st, a, QA);
+    int64_t Sa = 0, Saa = 0;
+    uint32_t Da[3] = {0, 0, 0}, Daa[3] = {0, 0, 0};
+    for (int i = 0; i < N; ++i) {
+        Sa += a[i];
+        Saa += (int64_t)a[i] * a[i];
+        for (int p = 0; p < 3; ++p) {
+            Da[p] += (uint32_t)QA[i][p];
+            Daa[p] += (uint32_t)(a[i] * QA[i][p]);
+        }
+    }
+    const double dmin = ncc_denom_min * 256.0 * (double)N * (double)N;
+    const float dminf = (float)dmin;
+    int64_t qsum = 0;
+    uint32_t G[3] = {0, 0, 0};
+    for (int k = 1; k < m; ++k) {
+        fast_sample_q(&fp->fv[k], cell, q, fp->sd, fp->st, b, Q);
+        int64_t Sb = 0, Sbb = 0, Sab = 0;
+        uint32_t Db[3] = {0, 0, 0}, Dbb[3] = {0, 0, 0}, Dab[3] = {0, 0, 0};
+        for (int i = 0; i < N; ++i) {
+            Sb += b[i];
+            Sbb += (int64_t)b[i] * b[i];
+            Sab += (int64_t)a[i] * b[i];
+            for (int p = 0; p < 3; ++p) {
+                Db[p] += (uint32_t)Q[i][p];
+                Dbb[p] += (uint32_t)(b[i] * Q[i][p]);
+                Dab[p] += (uint32_t)(QA[i][p] * b[i] + a[i] * Q[i][p]);
+            }
+        }
+        qsum += fast_ncc_q(N, Sa, Saa, Sb, Sbb, Sab, dminf);
+        const double dN = (double)N;
+        const double num = dN * (double)Sab - (double)Sa * (double)Sb;
+        const double va = dN * (double)Saa - (double)Sa * (double)Sa;
+        const double vb = dN * (double)Sbb - (double)Sb * (double)Sb;
+        const double den = sqrt(va * vb);
+        for (int p = 0; p < 3; ++p) {
+            const double dA = (double)(int32_t)Da[p], dAA = (double)(int32_t)Daa[p];
+            const double dB = (double)(int32_t)Db[p], dBB = (double)(int32_t)Dbb[p], dAB = (double)(int32_t)Dab[p];
+            const double dnum = dN * dAB - dA * (double)Sb - (double)Sa * dB;
+            double dncc;
+            if (den > dmin) {
+                const double dva = 2.0 * (dN * dAA - (double)Sa * dA);
+                const double dvb = 2.0 * (dN * dBB - (double)Sb * dB);
+                dncc = dnum / den - (num / den) * (0.5 * (dva / va + dvb / vb));
+            } else {
+                dncc = dnum / dmin;
+            }
+            G[p] += (uint32_t)(int32_t)rint(dncc * 16777216.0);
+        }
+    }
+    for (int p = 0; p < 3; ++p) g[p] = (float)(int32_t)G[p] * -0x1p-20f;
+    return (int32_t)((int64_t)(m - 1) * 16777216 - qsum);
+}
+
+/* nonlinear CG (Polak-Ribiere+) with a two-probe line search, fp32; the
+ * gradient analytic (spec v4, fo->gradient = 1: one evaluation with gradient
+ * at the start and after every line search that moved x) or by forward
+ * differences (v3); returns evaluations, x holds the scaled pose */
 static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_options *fo, float x[3])
 {
     x[0] = x[1] = x[2] = 0.0f;
-    int32_t f = fast_objective(fp, cell, dmin0, pose_of(fp, x), NULL);
+    float ga[3] = {0, 0, 0};
+    int32_t f = fo->gradient ? fast_objective_grad(fp, cell, dmin0, x, ga)
+                             : fast_objective(fp, cell, dmin0, pose_of(fp, x), NULL);
     int E = 1;
     const float h = fo->fd_step;
     const float gs = (1.0f / h) * 0x1p-24f; /* gradient per objective unit */
@@ -457,7 +631,16 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
     int moved = 1; /* x changed since the last gradient */
     for (int it = 0; it < fo->iters; ++it) {
         float g[3];
-        if (moved) {
+        if (fo->gradient && moved) {
+            /* the start evaluation's gradient, or one more evaluation at x */
+            if (it > 0) {
+                fast_objective_grad(fp, cell, dmin0, x, ga);
+                E += 1;
+            }
+            for (int i = 0; i < 3; ++i) g[i] = ga[i];
+        } else if (fo->gradient) {
+            for (int i = 0; i < 3; ++i) g[i] = gp[i];
+        } else if (moved) {
             for (int i = 0; i < 3; ++i) {
                 float xt[3] = {x[0], x[1], x[2]};
                 xt[i] = x[i] + h;
@@ -644,6 +827,21 @@ static int fast_eval_one(const or_scene *s, or_patch *p, int cell, const or_fast
     }
     fast_free(&fp);
     return ok;
+}
+
+/* spec v4 probe for tests: stage the patch at margin 0 and return the staged
+ * view count m; f = the objective and g = its analytic gradient at x = 0 */
+int or_fast_grad_probe(const or_scene *s, const or_patch *p, int cell, const or_fast_options *fo, int32_t *f,
+                       float g[3])
+{
+    fast_patch fp;
+    fast_stage(s, p, cell, fo, 0, &fp);
+    const float x[3] = {0.0f, 0.0f, 0.0f};
+    g[0] = g[1] = g[2] = 0.0f;
+    *f = fp.degenerate ? 0 : fast_objective_grad(&fp, cell, s->opt.ncc_denom_min, x, g);
+    const int m = fp.degenerate ? 0 : fp.m;
+    fast_free(&fp);
+    return m;
 }
 
 int or_fast_refine_batch(const or_scene *s, or_patch *p, int n, int cell, int mode, const or_fast_options *fo,

@@ -71,14 +71,14 @@ typedef struct or_scene or_scene;
 
 /* performance-mode options (layout of include/densepoints.h dp_fast_options) */
 typedef struct or_fast_options {
-    int32_t iters;        /* conjugate-gradient iterations (E = 1 + 5 iters) */
+    int32_t iters;        /* conjugate-gradient iterations                   */
     int32_t margin;       /* tile margin around the initial window, pixels   */
     int32_t tile_budget;  /* bytes of gray tiles per patch                   */
     int32_t max_views;    /* staged views per patch (<= 32)                  */
     float fd_step;        /* forward-difference step, scaled units           */
     float ls_step;        /* initial line-search step, scaled units          */
     int32_t densify;      /* product only: fast expansions in dp_densify     */
-    int32_t reserved;
+    int32_t gradient;     /* 1: analytic gradient (spec v4), 0: forward differences (v3) */
 } or_fast_options;
 
 #ifdef __cplusplus
@@ -130,6 +130,8 @@ int or_filter_patches(const or_scene *s, const or_patch *p, int64_t n, int passe
 /* performance mode (or_fast.c) */
 void or_fast_default_options(or_fast_options *f);
 int or_gray_plane(const or_scene *s, int view, uint8_t *out);
+int or_fast_grad_probe(const or_scene *s, const or_patch *p, int cell, const or_fast_options *fo, int32_t *f,
+                       float g[3]);
 int or_fast_refine_batch(const or_scene *s, or_patch *p, int n, int cell, int mode, const or_fast_options *fo,
                          uint8_t *accept, int nthreads);
 int or_fast_expand_batch(const or_scene *s, const or_patch *parents, int n, const or_fast_options *fo,

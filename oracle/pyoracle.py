@@ -64,7 +64,7 @@ class OrFastOptions(ctypes.Structure):
         ("fd_step", ctypes.c_float),
         ("ls_step", ctypes.c_float),
         ("densify", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("gradient", ctypes.c_int32),
     ]
 
 
@@ -107,6 +107,7 @@ def _load():
         "or_gray_plane": (ctypes.c_int, [P, ctypes.c_int, P]),
         "or_fast_refine_batch": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int]),
         "or_fast_expand_batch": (ctypes.c_int, [P, P, ctypes.c_int, P, P, P, ctypes.c_int]),
+        "or_fast_grad_probe": (ctypes.c_int, [P, P, ctypes.c_int, P, P, P]),
         # seed generation (or_seeds.c)
         "or_orb_pattern": (None, [P]),
         "or_features_per_level": (None, [ctypes.c_int, ctypes.c_double, ctypes.c_int, P]),
@@ -253,6 +254,16 @@ def _scene_fast_expand(self, parents, fo=None, nthreads=0):
     return kids, acc
 
 
+def _scene_fast_grad_probe(self, patch, cell, fo=None):
+    """Spec v4 at x = 0, staged at margin 0: (staged views, objective, gradient)."""
+    fo = fast_options() if fo is None else fast_options(fo)
+    one = np.ascontiguousarray(np.asarray(patch).reshape(1))
+    f = ctypes.c_int32()
+    g = np.zeros(3, dtype=np.float32)
+    m = lib.or_fast_grad_probe(self._h, _p(one), cell, ctypes.byref(fo), ctypes.byref(f), _p(g))
+    return m, f.value, g
+
+
 def _scene_gray(self, view):
     W, H = self._keep[1][view], self._keep[2][view]
     out = np.zeros((H, W), dtype=np.uint8)
@@ -262,6 +273,7 @@ def _scene_gray(self, view):
 
 Scene.fast_refine = _scene_fast_refine
 Scene.fast_expand = _scene_fast_expand
+Scene.fast_grad_probe = _scene_fast_grad_probe
 Scene.gray = _scene_gray
 
 

@@ -80,10 +80,24 @@ def _qdir(Q, k, w):
     return _fmaf(Q[4 * k + 2], w[2], _fmaf(Q[4 * k + 1], w[1], _f(Q[4 * k]) * _f(w[0])))
 
 
-def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
+def _bf16(x):
+    u = int(np.float32(x).view(np.uint32))
+    return np.uint32((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000).view(np.float32)
+
+
+def _q16(f):
+    return int(np.int16(np.uint16((int(np.float32(f).view(np.uint32)) - 0x4B400000) & 0xFFFF)))
+
+
+def _i32(x):
+    return ((int(x) + 2 ** 31) % 2 ** 32) - 2 ** 31
+
+
+def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo, grad=False):
     """Independent statement of DP_MODE_FAST_EVAL's score (include/densepoints.h
     dp_fast_options, spec v3: fp32 frame and view geometry, margin 0): returns
-    the mean NCC or -1."""
+    the mean NCC or -1.  grad: spec v4's objective and analytic gradient at
+    the staged pose instead (or_fast.c fast_objective_grad), (m, f, g)."""
     V = len(imgs)
     cams = [_fcam(orc, P, v) for v in range(V)]
     lo, hi = _f(2.0 ** -20), _f(2.0 ** 64)
@@ -120,6 +134,8 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
     e2 = np.array([_fmaf(nn[1], e1[2], -(nn[2] * e1[1])), _fmaf(nn[2], e1[0], -(nn[0] * e1[2])),
                    _fmaf(nn[0], e1[1], -(nn[1] * e1[0]))], dtype=np.float32)
     r = (X - Cr).astype(np.float32)
+    sd = ps / np.sqrt(_fdot(r, r))
+    st = _f(2.0) / _f(cell - 1)
     ws = [r, (e1 * ps).astype(np.float32), (e2 * ps).astype(np.float32), (nn * ps).astype(np.float32)]
     c = _f(0.5) * _f(cell - 1)
     vis = [v for v in range(V) if (int(p["vis"][v >> 6]) >> (v & 63)) & 1][:64]
@@ -159,9 +175,10 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
         tot += t[6]
         keep.append(t)
     if len(keep) < 2:
-        return -1.0
+        return (len(keep), None, None) if grad else -1.0
     N = cell * cell
-    samples = []
+    samples, qs = [], []
+    M = _f(1.5 * 2.0 ** 23)
     for v, g, x0, y0, tw, th, _ in keep:
         ox, oy = _f(-32.0 * x0), _f(-32.0 * y0)
         vec = [np.array([_fmaf(ox, gg[2], gg[0]), _fmaf(oy, gg[2], gg[1]), gg[2]], dtype=np.float32) for gg in g]
@@ -173,6 +190,16 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
         U0, V0 = A[0] * rz, A[1] * rz
         Ui, Vi = _fmaf(-U0, B1[2], B1[0]) * rz, _fmaf(-V0, B1[2], B1[1]) * rz
         Uj, Vj = _fmaf(-U0, B2[2], B2[0]) * rz, _fmaf(-V0, B2[2], B2[1]) * rz
+        if grad:
+            z1, Hn = vec[1][2], vec[4]
+            dU0, dV0 = _fmaf(-U0, z1, vec[1][0]) * rz, _fmaf(-V0, z1, vec[1][1]) * rz
+            dUi, dVi = _fmaf(-dU0, B1[2], -(Ui * z1)) * rz, _fmaf(-dV0, B1[2], -(Vi * z1)) * rz
+            dUj, dVj = _fmaf(-dU0, B2[2], -(Uj * z1)) * rz, _fmaf(-dV0, B2[2], -(Vj * z1)) * rz
+            ku, kv = _fmaf(U0, Hn[2], -Hn[0]) * rz, _fmaf(V0, Hn[2], -Hn[1]) * rz
+            fd, fa = sd * _f(2.0 ** -10), st * _f(2.0 ** -10)
+            cU0, cV0, cUi, cVi, cUj, cVj = (_bf16(x * fd) for x in (dU0, dV0, dUi, dVi, dUj, dVj))
+            cku, ckv = _bf16(ku * fa), _bf16(kv * fa)
+            qv = np.zeros((N, 3), dtype=np.int64)
         out = np.zeros(N, dtype=np.int64)
         for j in range(cell):
             tj = np.float32(j) - c
@@ -189,9 +216,50 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo):
                 b = ((32 - fx) * (32 - fy) * px(xx, yy) + fx * (32 - fy) * px(xx + 1, yy) +
                      (32 - fx) * fy * px(xx, yy + 1) + fx * fy * px(xx + 1, yy + 1) + 32) >> 6
                 out[j * cell + i] = b
+                if grad:
+                    p00, p01, p10, p11 = (int(px(xx, yy)), int(px(xx + 1, yy)), int(px(xx, yy + 1)),
+                                          int(px(xx + 1, yy + 1)))
+                    gx = _f((32 - fy) * (p01 - p00) + fy * (p11 - p10))
+                    gy = _f((32 - fx) * (p10 - p00) + fx * (p11 - p01))
+                    au, av = _fmaf(tj, cUj, _fmaf(ti, cUi, cU0)), _fmaf(tj, cVj, _fmaf(ti, cVi, cV0))
+                    sl_ = _fmaf(gy, ckv, gx * cku)
+                    qv[j * cell + i] = (_q16(_fmaf(gy, av, _fmaf(gx, au, M))), _q16(_fmaf(ti, sl_, M)),
+                                        _q16(_fmaf(tj, sl_, M)))
         samples.append(out)
+        if grad:
+            qs.append(qv)
     a = samples[0]
     dmin = 0.1 * 256.0 * N * N
+    if grad:
+        import math
+        Sa, Saa = int(a.sum()), int((a * a).sum())
+        QA = qs[0]
+        Da = [_i32(QA[:, p].sum()) for p in range(3)]
+        Daa = [_i32((a * QA[:, p]).sum()) for p in range(3)]
+        G, qsum = [0, 0, 0], 0
+        for b, Q in zip(samples[1:], qs[1:]):
+            Sb, Sbb, Sab = int(b.sum()), int((b * b).sum()), int((a * b).sum())
+            num = float(N) * float(Sab) - float(Sa) * float(Sb)
+            va = float(N) * float(Saa) - float(Sa) * float(Sa)
+            vb = float(N) * float(Sbb) - float(Sb) * float(Sb)
+            den32 = np.sqrt(_f(va) * _f(vb))
+            r32 = _f(1.0) / (den32 if den32 > _f(dmin) else _f(dmin))
+            qsum += int(np.rint((_f(num) * r32) * _f(16777216.0)))
+            den = math.sqrt(va * vb)
+            for p in range(3):
+                dA, dAA = float(Da[p]), float(Daa[p])
+                dB, dBB = float(_i32(Q[:, p].sum())), float(_i32((b * Q[:, p]).sum()))
+                dAB = float(_i32((QA[:, p] * b + a * Q[:, p]).sum()))
+                dnum = float(N) * dAB - dA * float(Sb) - float(Sa) * dB
+                if den > dmin:
+                    dva = 2.0 * (float(N) * dAA - float(Sa) * dA)
+                    dvb = 2.0 * (float(N) * dBB - float(Sb) * dB)
+                    dncc = dnum / den - (num / den) * (0.5 * (dva / va + dvb / vb))
+                else:
+                    dncc = dnum / dmin
+                G[p] = _i32(G[p] + int(np.rint(dncc * 16777216.0)))
+        f = (len(samples) - 1) * 16777216 - qsum
+        return len(samples), f, np.array([_f(G[p]) * _f(-2.0 ** -20) for p in range(3)], dtype=np.float32)
     tot = 0.0
     for b in samples[1:]:
         num = N * int((a * b).sum()) - int(a.sum()) * int(b.sum())
@@ -215,6 +283,27 @@ def test_fast_eval_equals_numpy_restatement(orc, small_scene, cell):
     assert np.array_equal(q["score"].view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("cell", [7, 11])
+def test_fast_gradient_equals_numpy_restatement(orc, small_scene, cell):
+    """Spec v4's analytic gradient (bf16 window-map derivatives, 16-bit
+    per-sample Q's, exact integer sums, fp64 quotient rule) restated in numpy
+    equals the C oracle's at the staged pose, bit for bit, with the objective."""
+    cfg, P, imgs, seeds = small_scene
+    S = orc.Scene(P, imgs)
+    p = S.seeds_to_patches(seeds[::9][:14])
+    fo = orc.fast_options()
+    n = 0
+    for x in p:
+        m, f, g = S.fast_grad_probe(x, cell, fo)
+        mw, fw, gw = _fast_eval_numpy(orc, S, P, imgs, x, cell, fo, grad=True)
+        assert m == mw
+        if m >= 2:
+            n += 1
+            assert f == fw and g.view(np.uint32).tolist() == gw.view(np.uint32).tolist(), (g, gw)
+            assert np.abs(g).max() > 0
+    assert n >= 8
+
+
 def test_fast_eval_does_not_mutate_pose(orc, small_scene):
     _, P, imgs, seeds = small_scene
     S = orc.Scene(P, imgs)
@@ -227,11 +316,28 @@ def test_fast_eval_does_not_mutate_pose(orc, small_scene):
 
 
 @pytest.mark.parametrize("iters", [0, 2, 4])
+def test_fast_evaluation_count_analytic(orc, small_scene, iters):
+    """Spec v4: 1 + 2 iters + (iterations after a line search that moved x)
+    evaluations, + 1 for the filter; one fewer per reused gradient."""
+    _, P, imgs, seeds = small_scene
+    S = orc.Scene(P, imgs)
+    p = S.seeds_to_patches(seeds[:80])
+    S.fast_refine(p, 11, orc.MODE_FAST_REFINE, orc.fast_options(iters=iters, gradient=1))
+    ev = p["evals"]
+    top = 2 + 3 * iters - (1 if iters > 0 else 0)
+    assert ev.max() == top
+    assert (ev[ev > 1] <= top).all()
+    assert np.mean(ev == top) > 0.3
+    if iters >= 4:
+        assert np.mean((ev > 1) & (ev < top)) > 0.05  # gradients are reused
+
+
+@pytest.mark.parametrize("iters", [0, 2, 4])
 def test_fast_evaluation_count(orc, small_scene, iters):
     _, P, imgs, seeds = small_scene
     S = orc.Scene(P, imgs)
     p = S.seeds_to_patches(seeds[:80])
-    S.fast_refine(p, 11, orc.MODE_FAST_REFINE, orc.fast_options(iters=iters))
+    S.fast_refine(p, 11, orc.MODE_FAST_REFINE, orc.fast_options(iters=iters, gradient=0))
     ev = p["evals"]
     # 1 + 5 iters (CG) + 1 (filter), less 3 for every iteration whose forward
     # differences repeat the last ones (the previous line search left x and

@@ -80,25 +80,35 @@ def test_gray_planes_equal_spec(engine, orc):
         assert np.array_equal(g.astype(np.int32) - 1024, S.gray(v).astype(np.int32)), f"view {v}"
 
 
+@pytest.mark.parametrize("gradient", [1, 0])
 @pytest.mark.parametrize("cell", [16, 11, 7, 5])
 @pytest.mark.parametrize("mode", [N.MODE_FAST_EVAL, N.MODE_FAST_REFINE])
-def test_fast_modes_bit_exact(engine, orc, cell, mode):
+def test_fast_modes_bit_exact(engine, orc, cell, mode, gradient):
+    """Both refine specs: the analytic gradient (v4, default) and forward
+    differences (v3), at every pass shape (n = 16, 11, 7 with its tail sample, 5)."""
     sc = scene("hf6")
     engine.set_views(sc.views)
     S = orc.Scene(sc.P, sc.imgs)
     seeds = sc.seeds[:200]
     gp = engine.seeds_to_patches(seeds)
     op = S.seeds_to_patches(seeds)
-    ga = engine.fast_refine(gp, cell, mode)
-    oa = S.fast_refine(op, cell, mode)
+    fo = dp.FastOptions(gradient=gradient)
+    engine.set_fast_options(fo)
+    try:
+        ga = engine.fast_refine(gp, cell, mode)
+    finally:
+        engine.set_fast_options(dp.FastOptions())
+    oa = S.fast_refine(op, cell, mode, fo=orc.fast_options(fo))
     assert np.array_equal(ga, oa)
     assert_same(gp, op)
     if mode == N.MODE_FAST_REFINE:
         assert gp["evals"].mean() > 10 and ga.sum() > 0
 
 
-@pytest.mark.parametrize("opts", [dict(), dict(iters=0), dict(iters=7, margin=7), dict(margin=0, tile_budget=2048),
-                                  dict(max_views=3, fd_step=0.25, ls_step=2.0)])
+@pytest.mark.parametrize("opts", [dict(), dict(iters=0), dict(iters=1), dict(iters=7, margin=7),
+                                  dict(margin=0, tile_budget=2048), dict(max_views=3, ls_step=2.0),
+                                  dict(gradient=0), dict(gradient=0, iters=7, margin=7),
+                                  dict(gradient=0, max_views=3, fd_step=0.25, ls_step=2.0)])
 def test_fast_expand_bit_exact_options(orc, opts):
     sc = scene("hf6")
     S = orc.Scene(sc.P, sc.imgs)
