@@ -77,9 +77,9 @@ def parse():
                                                          "FastOptions default")
     ap.add_argument("--fast-iters", type=int, default=None, help="performance-mode CG iterations (default: FastOptions)")
     ap.add_argument("--fast-margins", default="", help="tile margins (px) to sweep in perf_mode")
-    ap.add_argument("--fast-gradients", default="1,0",
-                    help="perf_mode refine specs: 1 = analytic gradient (v4, the default), 0 = forward "
-                         "differences (v3; keys *_fd, headline parents only)")
+    ap.add_argument("--fast-gradients", default="0,1",
+                    help="perf_mode refine specs: 0 = forward differences (v3, the default), 1 = the analytic "
+                         "gradient (v4; keys *_an)")
     ap.add_argument("--no-fast", action="store_true", help="skip the perf_mode sub-object")
     ap.add_argument("--seed-stride", type=float, default=32.0, help="synthetic seed grid stride (px)")
     return ap.parse_args()
@@ -580,7 +580,7 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
     margins = [int(b) for b in args.fast_margins.split(",") if b] or [None]
     grads = [int(x) for x in args.fast_gradients.split(",") if x]
     combos = [(int(c), b, mg, ps, gr) for gr in grads for ps in ("", "_fast_seeds") for c in args.fast_cells.split(",")
-              if c for b in budgets for mg in margins if gr == grads[0] or ps == ""]
+              if c for b in budgets for mg in margins]
     for cell, tb, mg, pset, gr in combos:
         d_par = d_fparents if pset else d_parents
         fo = dp.FastOptions()
@@ -626,7 +626,7 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
              "quality": quality(cfg, out, acc), "stats": {k: int(v) for k, v in st.items()},
              "fast_options": {k: getattr(fo, k) for k in ("iters", "margin", "tile_budget", "max_views", "gradient")}}
         fprof = profiled("fast%d" % cell, fast_kernel_tag(cell, gr), B, lib_stamp(N.LIB_PATH)) \
-            if not pset and fo.tile_budget == 6656 and fo.iters == 4 and gr == 1 else None
+            if not pset and fo.tile_budget == 6656 and fo.iters == 4 and gr == 0 else None
         if fprof:
             attach_profile(r["roofline"], fprof, B, kms)
         if not args.no_cpu and not pset and gr == grads[0]:
@@ -649,13 +649,13 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                                                                         for f in fields) and
                                                                     np.array_equal(kacc, acc[: 4 * n]))}
         res["n%d" % cell + ("_b%d" % tb if tb and len(budgets) > 1 else "") +
-            ("_m%d" % mg if mg is not None and len(margins) > 1 else "") + pset + ("_fd" if gr == 0 else "")] = r
+            ("_m%d" % mg if mg is not None and len(margins) > 1 else "") + pset + ("_an" if gr == 1 else "")] = r
     eng.set_options(dp.Options(expand_cell_size=args.cell))
     eng.set_fast_options(dp.FastOptions())
     return res
 
 
-def fast_kernel_tag(cell, gradient=1):
+def fast_kernel_tag(cell, gradient=0):
     """the performance kernel instance bench runs at this window (dp_fast.hip fast_dispatch;
     kMode 100 = the analytic-gradient refine, 6 = forward differences)"""
     mode = 100 if gradient else 6

@@ -1904,7 +1904,7 @@ extern "C" void dp_default_fast_options(dp_fast_options *f)
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;
     f->densify = 0;
-    f->gradient = 1;
+    f->gradient = 0;
 }
 
 extern "C" int dp_set_fast_options(dp_ctx *c, const dp_fast_options *f)

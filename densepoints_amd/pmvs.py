@@ -53,7 +53,7 @@ class FastOptions:
     fd_step: float = 0.5      # forward-difference step, scaled units (gradient 0)
     ls_step: float = 1.0      # initial line-search step, scaled units
     densify: int = 0          # 1: dp_densify expands with the fast refine
-    gradient: int = 1         # 1: analytic gradient (spec v4); 0: forward differences (spec v3)
+    gradient: int = 0         # 0: forward differences (spec v3); 1: analytic gradient (spec v4)
 
     def to_c(self) -> N.DpFastOptions:
         o = N.DpFastOptions()

@@ -454,7 +454,7 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  *  - refine: `iters` Polak-Ribiere+ conjugate-gradient steps with a two-probe
  *    line search (initial step ls_step, doubled on success, halved on
  *    failure) and, by `gradient`:
- *      1 (spec v4, default): the ANALYTIC gradient of the objective -- per
+ *      1 (spec v4): the ANALYTIC gradient of the objective -- per
  *        sample the bilinear tap slopes times the window map's derivatives
  *        (bf16 coefficients per view and pose), as 16-bit integers Q (one unit
  *        = one gray level per scaled pose unit); per view exact integer sums
@@ -462,7 +462,7 @@ int dp_triangulate(dp_ctx *ctx, int64_t n_points, const int32_t *offsets, const 
  *        fp64, quantised to 2^-24 and summed exactly.  One evaluation with the
  *        gradient at the start and after every line search that moved x:
  *        E = 1 + 2 iters + (iterations after a moving line search);
- *      0 (spec v3): a forward-difference gradient (step fd_step): E = 1 +
+ *      0 (spec v3, default): a forward-difference gradient (step fd_step): E = 1 +
  *        5 iters, less 3 per iteration after a line search that left x
  *        unchanged (the last gradient is reused: the differences would repeat it);
  *  - then Patch::InitRelatedImages (patch.cpp:19-49) at the new pose (its
@@ -484,8 +484,9 @@ typedef struct dp_fast_options {
                                    seed_cell_size) and every expansion (at
                                    expand_cell_size) with the fast refine, and so
                                    does the generation-at-a-time (multi-GPU) API */
-    int32_t gradient;     /* 1     1: analytic gradient (spec v4), 0: forward
-                                   differences (spec v3, rounds 2-4)              */
+    int32_t gradient;     /* 0     0: forward differences (spec v3), 1: analytic
+                                   gradient (spec v4: better children from
+                                   refined parents, worse from raw ones)          */
 } dp_fast_options;
 
 void dp_default_fast_options(dp_fast_options *fo);

@@ -65,7 +65,7 @@ void or_fast_default_options(or_fast_options *f)
     f->max_views = FAST_MAX_VIEWS;
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;
-    f->gradient = 1;
+    f->gradient = 0;
 }
 
 /* BGR2GRAY on 8U (the parity spec's 14-bit fixed point); the product stores
@@ -631,14 +631,15 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
     int moved = 1; /* x changed since the last gradient */
     for (int it = 0; it < fo->iters; ++it) {
         float g[3];
-        if (fo->gradient && moved) {
+        const int an = fo->gradient != 0;
+        if (an && moved) {
             /* the start evaluation's gradient, or one more evaluation at x */
             if (it > 0) {
                 fast_objective_grad(fp, cell, dmin0, x, ga);
                 E += 1;
             }
             for (int i = 0; i < 3; ++i) g[i] = ga[i];
-        } else if (fo->gradient) {
+        } else if (an) {
             for (int i = 0; i < 3; ++i) g[i] = gp[i];
         } else if (moved) {
             for (int i = 0; i < 3; ++i) {

@@ -78,7 +78,7 @@ typedef struct or_fast_options {
     float fd_step;        /* forward-difference step, scaled units           */
     float ls_step;        /* initial line-search step, scaled units          */
     int32_t densify;      /* product only: fast expansions in dp_densify     */
-    int32_t gradient;     /* 1: analytic gradient (spec v4), 0: forward differences (v3) */
+    int32_t gradient;     /* 0: forward differences (spec v3), 1: analytic gradient (v4) */
 } or_fast_options;
 
 #ifdef __cplusplus

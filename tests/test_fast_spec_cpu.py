@@ -559,3 +559,21 @@ def test_generation_engine_densify_all(orc):
     assert len(fp) > 20
     assert (fp["seq"] == np.arange(len(fp))).all()
     assert (fp["flags"] & 1).all()
+
+
+def test_fast_analytic_gradient_quality(orc, quality_scene):
+    """Spec v4 (analytic gradient) against v3 (forward differences) on the
+    performance pipeline's own parents (the seed stage refined in performance
+    mode, as dp_densify runs it), same iterations: lower depth and normal
+    errors of the accepted children with fewer evaluations."""
+    cfg, P, imgs, seeds = quality_scene
+    S = orc.Scene(P, imgs, _options(expand_cell_size=11))
+    out = {}
+    for gr in (0, 1):
+        fo = orc.fast_options(gradient=gr)
+        par = S.seeds_to_patches(seeds[::2][:600])
+        par = par[S.fast_refine(par, 16, orc.MODE_FAST_REFINE, fo) == 1]
+        kids, acc = S.fast_expand(par, fo)
+        out[gr] = _geom_err(cfg, kids, acc) + (float(kids["evals"][kids["evals"] > 0].mean()),)
+    (dz0, ang0, e0), (dz1, ang1, e1) = out[0], out[1]
+    assert dz1 < dz0 and ang1 < ang0 and e1 < 0.75 * e0, out

@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--parents", type=int, default=2000)
     ap.add_argument("--cell", type=int, default=11)
     ap.add_argument("--variants", default="0:4,1:2,1:3,1:4", help="gradient:iters,...")
+    ap.add_argument("--parents-from", default="fast", choices=["fast", "parity"],
+                    help="parents: the variant's own seed stage (fast) or the parity Nelder-Mead seed stage "
+                         "(bench.py's headline parents)")
     a = ap.parse_args()
     cfg = synth.named(a.config)
     P, imgs, seeds = synth.scene_host(cfg)
@@ -54,7 +57,7 @@ def main():
         gr, it = (int(x) for x in v.split(":"))
         fo = orc.fast_options(iters=it, gradient=gr)
         par = raw.copy()
-        ok = S.fast_refine(par, 16, fo=fo)
+        ok = S.fast_refine(par, 16, fo=fo) if a.parents_from == "fast" else S.refine(par, 16, orc.MODE_SEED)
         parents = np.ascontiguousarray(par[ok == 1][: a.parents])
         kids, acc = S.fast_expand(parents, fo)
         E = kids["evals"].astype(np.float64)
