@@ -208,16 +208,17 @@ def test_fast_expand_cfg5_full_scene(orc):
           % (len(k), len(gk), float(np.median(np.abs(k["pos"][:, 2] - z))), st["view_evals"] / st["evals"]))
 
 
-@pytest.mark.parametrize("name,max_pops", [("hf6", None), ("plane4", None), ("hf6", 37)])
-def test_fast_densify_bit_exact(orc, name, max_pops):
+@pytest.mark.parametrize("name,max_pops,gradient", [("hf6", None, 0), ("plane4", None, 0), ("hf6", 37, 0),
+                                                    ("hf6", None, 1), ("hf6", 37, 1)])
+def test_fast_densify_bit_exact(orc, name, max_pops, gradient):
     """dp_densify with dp_fast_options.densify = 1: the seed stage and every
-    expansion generation refined in performance mode, the organizer claims as
-    in the parity densify (PatchOrganizer::TryInsert in sequence order), the
-    pop cap (expand.cpp:95); equal to the oracle's generation-at-a-time
-    restatement on every stored field."""
+    expansion generation refined in performance mode (forward differences or
+    the analytic gradient), the organizer claims as in the parity densify
+    (PatchOrganizer::TryInsert in sequence order), the pop cap (expand.cpp:95);
+    equal to the oracle's generation-at-a-time restatement on every stored field."""
     sc = scene(name)
     opts = dp.Options() if max_pops is None else dp.Options(max_pops=max_pops)
-    fo = dp.FastOptions(densify=1)
+    fo = dp.FastOptions(densify=1, gradient=gradient)
     S = orc.Scene(sc.P, sc.imgs, opts)
     op = orc.GenerationEngine(S, threads=8, fast=fo).densify_all(sc.seeds)
     with dp.Engine(opts, device=0) as eng:
