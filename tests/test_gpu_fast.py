@@ -147,10 +147,12 @@ def test_fast_edge_cases(engine, orc):
         engine.set_fast_options(dp.FastOptions(tile_budget=32768))
 
 
-def test_fast_expand_cfg3_full_scene(orc):
+@pytest.mark.parametrize("gradient", [0, 1])
+def test_fast_expand_cfg3_full_scene(orc, gradient):
     """BASELINE config 3 (32 views 3840x2160): performance-mode expansion of
-    2,000 refined parents equals the spec bit for bit, and its geometry beats
-    the parity mode's against the synthetic ground truth."""
+    2,000 refined parents equals the spec bit for bit (forward differences and
+    the analytic gradient), and its geometry beats the parity mode's against
+    the synthetic ground truth."""
     from test_gpu_configs import DeviceScene, spread
 
     with dp.Engine(device=0) as eng:
@@ -160,12 +162,14 @@ def test_fast_expand_cfg3_full_scene(orc):
         par = eng.seeds_to_patches(seeds)
         acc = eng.refine(par, 16, N.MODE_SEED)
         par = np.ascontiguousarray(np.resize(par[acc == 1], 2000))
+        fo = dp.FastOptions(gradient=gradient)
+        eng.set_fast_options(fo)
         for cell in (11, 7):
             o = dp.Options(expand_cell_size=cell)
             eng.set_options(o)
             gk, ga = eng.fast_expand(par)
             S2 = orc.Scene(sc.P, sc.host_images(), o)
-            ok, oa = S2.fast_expand(par)
+            ok, oa = S2.fast_expand(par, orc.fast_options(fo))
             assert np.array_equal(ga, oa)
             assert_same(gk, ok, FIELDS + ("parent",))
             assert 0.1 < ga.mean() < 0.95
