@@ -38,9 +38,10 @@ void usage()
                  "               [--matcher knn|flann]  (MatcherType, matcher.h:12)\n"
                  "               [--gpus N]   (one context per GPU, generations partitioned by\n"
                  "                             reference-view super-tile; output identical to 1 GPU)\n"
-                 "               [--mode parity|fast] [--fast-iters N]  (fast: the performance-mode\n"
-                 "                             refine -- LDS-staged gray tiles, fused CG -- for the seed\n"
-                 "                             stage and every expansion)\n"
+                 "               [--mode parity|fast] [--fast-iters N] [--fast-gradient 0|1]\n"
+                 "                            (fast: the performance-mode refine -- LDS-staged gray\n"
+                 "                             tiles, fused CG -- for the seed stage and every expansion;\n"
+                 "                             gradient 1: analytic, 0: forward differences)\n"
                  "       densify --synthetic V,W,H,KIND --write-scene DIR\n");
 }
 
@@ -226,7 +227,7 @@ int main(int argc, char **argv)
     long long max_pops = -1;
     int level = 0;
     bool check_only = false, do_filter = false, fast = false;
-    int fast_iters = -1;
+    int fast_iters = -1, fast_gradient = -1;
     dp_matcher_options mopt; // MatcherOptions defaults (matcher.h:21-32), ORB::create(40000)
     dp_default_matcher_options(&mopt);
     for (int i = 1; i < argc; ++i) {
@@ -270,6 +271,7 @@ int main(int argc, char **argv)
             }
             fast = m == "fast";
         } else if (a == "--fast-iters") fast_iters = std::atoi(next().c_str());
+        else if (a == "--fast-gradient") fast_gradient = std::atoi(next().c_str());
         else if (a == "--synthetic") synth = next();
         else if (a == "--write-scene") scene_dir = next();
         else if (a == "-h" || a == "--help") {
@@ -342,6 +344,8 @@ int main(int argc, char **argv)
         fo.densify = fast ? 1 : 0;
         if (fast_iters >= 0)
             fo.iters = fast_iters;
+        if (fast_gradient >= 0)
+            fo.gradient = fast_gradient;
         check(dp_set_fast_options(ctx, &fo), "dp_set_fast_options");
         if (level > 0) {
             // run on pyramid level L (cv::pyrDown^L on the device, P rows 0-1 / 2^L)

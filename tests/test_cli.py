@@ -171,6 +171,13 @@ def test_cli_fast_mode_ply_equals_oracle(scene_dir, tmp_path, orc):
     res2 = json.loads(run(*args, "--mode", "fast", "--gpus", "2", "-o", str(out2)).stdout)
     assert res2["gpus"] == 2 and out2.read_bytes() == ref.read_bytes()
     assert run(*args, "--mode", "turbo", check=False).returncode == 2
+    # --fast-gradient 1: the analytic-gradient refine (spec v4)
+    out3 = tmp_path / "points3.ply"
+    run(*args, "--mode", "fast", "--fast-gradient", "1", "-o", str(out3))
+    op3 = orc.GenerationEngine(S, threads=8, fast=FastOptions(densify=1, gradient=1)).densify_all(synth.seeds(cfg, P))
+    ref3 = tmp_path / "oracle3.ply"
+    write_ply(str(ref3), op3)
+    assert out3.read_bytes() == ref3.read_bytes() != ref.read_bytes()
 
 
 @pytest.mark.gpu
