@@ -124,7 +124,8 @@ def test_fast_expand_bit_exact_options(orc, opts):
     assert_same(gk, ok, FIELDS + ("parent",))
 
 
-def test_fast_edge_cases(engine, orc):
+@pytest.mark.parametrize("gradient", [0, 1])
+def test_fast_edge_cases(engine, orc, gradient):
     sc = scene("wide70")
     engine.set_views(sc.views)
     S = orc.Scene(sc.P, sc.imgs)
@@ -133,13 +134,18 @@ def test_fast_edge_cases(engine, orc):
     p["vis"][1] = dp.mask_from_list(dp.visible_list(p["vis"][1])[:1])
     p["pos"][2] = [50.0, 50.0, 50.0]         # off every image
     p["normal"][3] = [0.0, 0.0, 0.0]         # degenerate normal
-    for mode in (N.MODE_FAST_EVAL, N.MODE_FAST_REFINE):
-        for cell in (5, 9):
-            gp, op = p.copy(), p.copy()
-            ga = engine.fast_refine(gp, cell, mode)
-            oa = S.fast_refine(op, cell, mode)
-            assert np.array_equal(ga, oa)
-            assert_same(gp, op)
+    fo = dp.FastOptions(gradient=gradient)
+    engine.set_fast_options(fo)
+    try:
+        for mode in (N.MODE_FAST_EVAL, N.MODE_FAST_REFINE):
+            for cell in (5, 9):
+                gp, op = p.copy(), p.copy()
+                ga = engine.fast_refine(gp, cell, mode)
+                oa = S.fast_refine(op, cell, mode, fo=orc.fast_options(fo))
+                assert np.array_equal(ga, oa)
+                assert_same(gp, op)
+    finally:
+        engine.set_fast_options(dp.FastOptions())
     assert len(engine.fast_refine(dp.empty_patches(0), 11)) == 0
     with pytest.raises(dp.DensePointsError):
         engine.set_fast_options(dp.FastOptions(margin=8))
