@@ -1670,43 +1670,64 @@ __global__ void claimk_resolve_kernel(ClaimArgs a, uint8_t *accepted)
 
 // append accepted candidates in sequence order + Patch::ComputeColor
 // (patch.cpp:51-73)
-__global__ void append_kernel(const dpg::ViewDev *views, int V, const dp_patch *cand,
-                              const uint8_t *accepted, const uint32_t *prefix, int32_t n,
-                              dp_patch *store, int64_t base, int64_t parent0, int is_seed)
+// The organizer's append (PatchOrganizer::TryInsert's push_back + ComputeColor), one
+// WAVE per candidate (4 per block): lane v projects
+// the centre into views v and v + 64 (Patch::ComputeColor, patch.cpp:51-73),
+// the BGR sums are exact integers in any order, so the wave reduction gives
+// the reference's fp64 sums; lanes 0..19 copy the 80-byte record
+__global__ __launch_bounds__(256) void append_wave_kernel(const dpg::ViewDev *views, int V, const dp_patch *cand,
+                                                          const uint8_t *accepted, const uint32_t *prefix, int32_t n,
+                                                          dp_patch *store, int64_t base, int64_t parent0, int is_seed)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = (int)(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63u);
     if (i >= n || !accepted[i])
         return;
     const int64_t pos = base + (int64_t)prefix[i];
-    dp_patch *r = store + pos;
-    *r = cand[i];
-    r->seq = (uint32_t)pos;
-    r->parent = is_seed ? 0xFFFFFFFFu : (uint32_t)(parent0 + (i >> 2));
-    r->flags |= DP_PATCH_ACCEPTED;
-    const float p0 = r->pos[0], p1 = r->pos[1], p2 = r->pos[2];
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    int cnt = 0;
-    for (int v = 0; v < V; ++v) {
+    const float p0 = cand[i].pos[0], p1 = cand[i].pos[1], p2 = cand[i].pos[2];
+    uint32_t s0 = 0, s1 = 0, s2 = 0, cnt = 0;
+    for (int v = lane; v < V; v += 64) {
         const dpg::ViewDev &vw = views[v];
         double u, w;
         dpg::project(vw.P, p0, p1, p2, u, w);
-        if (!dpg::inside(u, w, vw.W, vw.H))
-            continue;
-        const uint32_t px = vw.img[(size_t)(int)w * (size_t)vw.pitch + (size_t)(int)u];
-        s0 = s0 + (double)(px & 255u);
-        s1 = s1 + (double)((px >> 8) & 255u);
-        s2 = s2 + (double)((px >> 16) & 255u);
-        ++cnt;
+        if (dpg::inside(u, w, vw.W, vw.H)) {
+            const uint32_t px = vw.img[(size_t)(int)w * (size_t)vw.pitch + (size_t)(int)u];
+            s0 += px & 255u;
+            s1 += (px >> 8) & 255u;
+            s2 += (px >> 16) & 255u;
+            ++cnt;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_xor(s0, o);
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+        cnt += __shfl_xor(cnt, o);
     }
     uint8_t c0 = 0, c1 = 0, c2 = 0;
     if (cnt) {
-        c0 = (uint8_t)(s2 / (double)cnt);
-        c1 = (uint8_t)(s1 / (double)cnt);
-        c2 = (uint8_t)(s0 / (double)cnt);
+        c0 = (uint8_t)((double)s2 / (double)cnt);
+        c1 = (uint8_t)((double)s1 / (double)cnt);
+        c2 = (uint8_t)((double)s0 / (double)cnt);
     }
-    r->rgb[0] = c0;
-    r->rgb[1] = c1;
-    r->rgb[2] = c2;
+    // the record, one 32-bit word per lane, with seq, parent, rgb and the
+    // accepted flag patched into their words (one store per word)
+    constexpr int kWords = (int)(sizeof(dp_patch) / 4);
+    constexpr int kSeq = (int)(offsetof(dp_patch, seq) / 4), kPar = (int)(offsetof(dp_patch, parent) / 4);
+    constexpr int kRgb = (int)(offsetof(dp_patch, rgb) / 4);
+    static_assert(sizeof(dp_patch) % 4 == 0 && kWords <= 64, "record copy by lanes");
+    static_assert(offsetof(dp_patch, rgb) % 4 == 0 && offsetof(dp_patch, flags) == offsetof(dp_patch, rgb) + 3,
+                  "rgb[3] and flags share one word");
+    if (lane < kWords) {
+        uint32_t w = ((const uint32_t *)(cand + i))[lane];
+        if (lane == kSeq)
+            w = (uint32_t)pos;
+        else if (lane == kPar)
+            w = is_seed ? 0xFFFFFFFFu : (uint32_t)(parent0 + (i >> 2));
+        else if (lane == kRgb)
+            w = (uint32_t)c0 | (uint32_t)c1 << 8 | (uint32_t)c2 << 16 | ((w >> 24) | DP_PATCH_ACCEPTED) << 24;
+        ((uint32_t *)(store + pos))[lane] = w;
+    }
 }
 
 // probe: the texel loop's bilinear + BGR2GRAY on explicit taps (fxy = fx |
@@ -2189,8 +2210,8 @@ hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand,
 {
     if (n <= 0)
         return hipSuccess;
-    hipLaunchKernelGGL(append_kernel, dim3((n + 255) / 256), dim3(256), 0, s, views, V, cand, accepted,
-                       prefix, n, store, base, parent0, is_seed);
+    hipLaunchKernelGGL(append_wave_kernel, dim3((n + 3) / 4), dim3(256), 0, s, views, V, cand, accepted, prefix, n,
+                       store, base, parent0, is_seed);
     return hipGetLastError();
 }
 
