@@ -3,7 +3,7 @@
 #   tools/r04_profile.sh parity|fast7|fast11
 # a --kernel-trace --stats run, then separate --pmc passes (SQ issue counters
 # with GRBM_GUI_ACTIVE; wave-cycle split; VALU mix; FETCH_SIZE; WRITE_SIZE: MI355X_MICROARCH.md's per-pass
-# limits) of the same bench command; lines starting with "?" are optional passes.  Output: gpurun_out/prof_r04c/<workload>/.
+# limits) of the same bench command; lines starting with "?" are optional passes.  Output: gpurun_out/prof_r04d/<workload>/.
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -15,7 +15,7 @@ case $W in
   fast11) ARGS="--mode fast --cell 11 $BASE" ;;
   *) echo "unknown workload $W"; exit 2 ;;
 esac
-D=gpurun_out/prof_r04c/$W
+D=gpurun_out/prof_r04d/$W
 mkdir -p $D
 echo "$ARGS" > $D/args.txt
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 bench.py $ARGS > $D/trace.log 2>&1
