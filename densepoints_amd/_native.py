@@ -233,6 +233,7 @@ SIGNATURES = [
     ("dp_filter_patches_device", _I, [_P, _P, ctypes.c_int64, _P, _P, _P]),
     ("dp_last_kernel_ms", _I, [_P, _P]),
     ("dp_default_matcher_options", None, [_P]),
+    ("dp_orb_pattern", _I, [_P]),
     ("dp_generate_seeds", _I, [_P, _P, _P, _P, _P]),
     ("dp_seed_keypoints", _I, [_P, _I, _P, _P, _P]),
     ("dp_seed_matches", _I, [_P, _I, _P, _P, _P, _P]),

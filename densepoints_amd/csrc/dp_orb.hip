@@ -8,8 +8,10 @@
 // processed by each launch (blockIdx.z = view); one launch per pyramid level.
 #include "dp_orb.h"
 #include "dp_detmath.h"
+#include "dp_orb_pattern.h"
 
 #include <cmath>
+#include <cstring>
 
 namespace dpk {
 
@@ -696,30 +698,13 @@ hipError_t launch_iota(int32_t *out, int64_t n, hipStream_t s)
 // host helpers
 // ---------------------------------------------------------------------------
 
-// rBRIEF sampling pattern: OpenCV's learned bit_pattern_31_ table is not
-// available offline, so the pattern is BRIEF's isotropic Gaussian G II
-// (sigma = 31/5), drawn with integer arithmetic only: splitmix64, 12-term
-// Irwin-Hall sums of 16-bit uniforms, rounded half away from zero, clipped to
-// [-13, 13].  oracle/or_seeds.c generates the same table independently.
+// rBRIEF sampling pattern: OpenCV's learned bit_pattern_31_ (the table
+// cv::ORB::create()->compute samples, matcher.cpp:171-173), generated into
+// dp_orb_pattern.h from the plain-data copy scikit-image ships
+// (tests/golden/make_orb_pattern.py).
 void orb_pattern(int8_t *xy)
 {
-    uint64_t st = 0x0DE25E7017ULL;
-    for (int i = 0; i < 4 * kOrbPatternPairs; ++i) {
-        int64_t v = 0;
-        for (int k = 0; k < 12; ++k) {
-            st += 0x9E3779B97F4A7C15ULL;
-            uint64_t z = st;
-            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-            z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-            z = z ^ (z >> 31);
-            v += (int64_t)(z & 0xFFFF);
-        }
-        v -= 6 * 65536;
-        const int64_t num = v * 31, den = 5 * 65536;
-        int64_t c = num >= 0 ? (num + den / 2) / den : -((-num + den / 2) / den);
-        c = c < -13 ? -13 : (c > 13 ? 13 : c);
-        xy[i] = (int8_t)c;
-    }
+    std::memcpy(xy, kOrbBitPattern31, sizeof(kOrbBitPattern31));
 }
 
 // ORB constructor's u_max table for half patch 15

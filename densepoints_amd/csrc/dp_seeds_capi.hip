@@ -131,6 +131,14 @@ extern "C" void dp_default_matcher_options(dp_matcher_options *mo)
     mo->matcher_type = DP_MATCHER_KNN;
 }
 
+extern "C" int dp_orb_pattern(int8_t *xy_out)
+{
+    if (!xy_out)
+        return DP_E_ARG;
+    dpk::orb_pattern(xy_out);
+    return DP_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Geometry::ComputeFundamentalMatrix (fundamental_matrix.cpp:6-34):
 // F = [P' C]_x P' P^+,  P^+ = P^T (P P^T)^-1,  C = cofactor null vector of P

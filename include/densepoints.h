@@ -345,7 +345,8 @@ int dp_filter_patches_device(dp_ctx *ctx, const dp_patch *d_patches, int64_t n, 
  *   TriangulateMatches matcher.cpp:374-450 DLT, geometry/triangulation.cpp:15-34
  * OpenCV's ORB is restated, not reproduced bit-for-bit (OpenCV is absent from
  * the image; DESIGN.md "Seed generation" lists the restated semantics and the
- * points that are parity-unpinned, e.g. the rBRIEF sampling pattern).  The
+ * points that are parity-unpinned; the rBRIEF sampling pattern is OpenCV's own
+ * bit_pattern_31_, see dp_orb_pattern).  The
  * reference's unspecified orders (nth_element, omp critical push_back) are
  * fixed here: keypoints in (level, y, x) order, per-cell picks by (response
  * desc, index), seed points in (view, keypoint) order. */
@@ -395,6 +396,11 @@ typedef struct dp_seed_stats {
 } dp_seed_stats;
 
 void dp_default_matcher_options(dp_matcher_options *mo);
+/* The rBRIEF sampling pattern ComputeDescriptors uses: OpenCV 3.4's learned
+ * bit_pattern_31_ (ORB::create()->compute, matcher.cpp:171-173), 512 points as
+ * (x, y) int8 pairs; test i compares points 2i and 2i+1.  xy_out: 1024 bytes.
+ * Host-only (no device needed). */
+int dp_orb_pattern(int8_t *xy_out);
 /* GenerateSeeds over the context's level-0 views.  *xyz_out (n x 3 doubles)
  * is context-owned, valid until the next dp_generate_seeds or destroy. */
 int dp_generate_seeds(dp_ctx *ctx, const dp_matcher_options *mo, const double **xyz_out, int64_t *n_out,

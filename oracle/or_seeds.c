@@ -13,8 +13,10 @@
  * DirectLinearTriangulation is pinned by the reference's own property tests
  * (tests/core/test_triangulation.cpp:11-52, reproduced in
  * tests/test_seeds_cpu.py).  OpenCV's ORB internals (pyramid resize, FAST,
- * Harris, IC angle, the learned rBRIEF pattern) are absent from the image:
- * parity unpinned against OpenCV itself.
+ * Harris, IC angle) are absent from the image: parity unpinned against
+ * OpenCV itself.  The learned rBRIEF pattern bit_pattern_31_ is
+ * OpenCV's own table (or_orb_pattern.h, from the plain-data copy scikit-image
+ * ships; tests/golden/make_orb_pattern.py).
  */
 #include <math.h>
 #include <stdint.h>
@@ -22,6 +24,7 @@
 #include <string.h>
 
 #include "or_detmath.h"
+#include "or_orb_pattern.h"
 
 typedef struct or_keypoint {
     float x, y, response, angle;
@@ -39,31 +42,14 @@ typedef struct or_matcher_options {
 /* ------------------------------------------------------------------------ */
 /* pattern, umax, features per level                                         */
 /* ------------------------------------------------------------------------ */
+/* OpenCV 3.4 bit_pattern_31_ (or_orb_pattern.h), flattened to the (x, y) per
+ * point layout the descriptor loop below reads: point 2i = (x0, y0) and point
+ * 2i + 1 = (x1, y1) of row i. */
 void or_orb_pattern(int8_t *xy)
 {
-    uint64_t st = 0x0DE25E7017ULL;
-    for (int i = 0; i < 1024; ++i) {
-        int64_t v = 0;
-        for (int k = 0; k < 12; ++k) {
-            st += 0x9E3779B97F4A7C15ULL;
-            uint64_t z = st;
-            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-            z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-            z = z ^ (z >> 31);
-            v += (int64_t)(z & 0xFFFF);
-        }
-        v -= 6 * 65536;
-        int64_t num = v * 31, den = 5 * 65536, c;
-        if (num >= 0)
-            c = (num + den / 2) / den;
-        else
-            c = -((-num + den / 2) / den);
-        if (c < -13)
-            c = -13;
-        if (c > 13)
-            c = 13;
-        xy[i] = (int8_t)c;
-    }
+    for (int i = 0; i < 256; ++i)
+        for (int k = 0; k < 4; ++k)
+            xy[4 * i + k] = (int8_t)or_bit_pattern_31[i][k];
 }
 
 static void orb_umax(int *umax)

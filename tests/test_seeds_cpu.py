@@ -145,10 +145,42 @@ def test_fundamental_matrix_product_equals_oracle_and_is_epipolar(orc):
         assert d < 1e-3 + 4 * float(np.spacing(np.float32(ys))) * (1.0 + abs(x2[0]))
 
 
+def _load_make_orb_pattern():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("mop", os.path.join(ROOT, "tests", "golden", "make_orb_pattern.py"))
+    mop = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mop)
+    return mop
+
+
+def test_orb_pattern_is_opencv_bit_pattern_31(orc):
+    """The oracle's and the product's rBRIEF tables are OpenCV's bit_pattern_31_
+    (ORB::create()->compute, matcher.cpp:171-173), read from the plain-data copy
+    scikit-image ships, and the committed headers are what the script emits."""
+    import ctypes
+
+    from densepoints_amd import _native as N
+
+    mop = _load_make_orb_pattern()
+    if not os.path.exists(mop.SOURCE):
+        pytest.skip("scikit-image's orb_descriptor_positions.txt is absent")
+    rows = mop.read_table()
+    want = np.array(rows, dtype=np.int8).reshape(512, 2)
+    # OpenCV's first pairs (orb.cpp bit_pattern_31_): 8,-3, 9,5 / 4,2, 7,-12 / -11,9, -8,2
+    assert want[:6].ravel().tolist() == [8, -3, 9, 5, 4, 2, 7, -12, -11, 9, -8, 2]
+    assert np.array_equal(orc.orb_pattern(), want)
+    prod = np.zeros(1024, dtype=np.int8)
+    assert N.lib.dp_orb_pattern(prod.ctypes.data_as(ctypes.c_void_p)) == N.DP_OK
+    assert np.array_equal(prod.reshape(512, 2), want)
+    for path, text in ((mop.PRODUCT_H, mop.product_header(rows)), (mop.ORACLE_H, mop.oracle_header(rows))):
+        assert open(path).read() == text, f"{path} is stale: rerun tests/golden/make_orb_pattern.py"
+
+
 def test_orb_constants(orc):
     pat = orc.orb_pattern()
     assert pat.shape == (512, 2) and pat.min() >= -13 and pat.max() <= 13
-    assert len({tuple(r) for r in pat.reshape(256, 4)}) > 250  # pairs are distinct tests
+    assert len({tuple(r) for r in pat.reshape(256, 4)}) == 256  # pairs are distinct tests
     for n, L in ((40000, 8), (3000, 4), (500, 1)):
         f = orc.features_per_level(n, 1.2, L)
         assert f.sum() == n and np.all(np.diff(f[:-1]) <= 0)
