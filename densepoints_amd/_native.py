@@ -260,6 +260,7 @@ SIGNATURES = [
     ("dp_probe_math_device", _I, [_P, _I, _P]),
     ("dp_probe_texel_device", _I, [_P, _P, _P, _I, _P]),
     ("dp_probe_recip_f32_device", _I, [_P, _I, _P]),
+    ("dp_probe_grad_q24_device", _I, [_P, _I, _P]),
     ("dp_probe_lds_unaligned_device", _I, [_P]),
     ("dp_debug_stamps", _I, [_P]),
 ]

@@ -254,6 +254,17 @@ __device__ __forceinline__ float recip_rn(float b)
     return __builtin_fmaf(r, e, r);
 }
 
+// spec v4: one view's NCC derivative as an integer multiple of 2^-24,
+// rint(dncc 2^24) clamped to the int32 range by IEEE maxNum / minNum (NaN ->
+// INT32_MIN; or_fast.c sat_rint_i32).  A near-flat window (den just above the
+// floor, or the dnum / dmin branch) can give |dncc| >= 128, where a plain
+// conversion would be undefined in C and saturate here.
+__device__ __forceinline__ int32_t grad_q24(double dncc)
+{
+    const double r = __builtin_fmin(__builtin_fmax(__builtin_rint(dncc * 16777216.0), -2147483648.0), 2147483647.0);
+    return (int32_t)r;
+}
+
 // IEEE sqrt (RN) for x = 0 or x >= 2^-96: v_sqrt_f32 (1 ulp) and the
 // residual correction of the compiler's own sequence, without its scaling of
 // denormal-range inputs; 0 -> a value below 2^-48 (the NCC floor replaces it)
@@ -1077,7 +1088,7 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
                     } else {
                         dncc = dnum / dmin;
                     }
-                    gq[pp] = (uint32_t)(int)__builtin_rint(dncc * 16777216.0);
+                    gq[pp] = (uint32_t)grad_q24(dncc);
                 }
             }
         }
@@ -1632,6 +1643,13 @@ __global__ void lds_unaligned_probe_kernel(uint32_t *out)
     }
 }
 
+__global__ void grad_q24_probe_kernel(const double *x, int n, int32_t *out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        out[i] = grad_q24(x[i]);
+}
+
 __global__ void recip_probe_kernel(const float *x, int n, float *out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1644,6 +1662,12 @@ __global__ void recip_probe_kernel(const float *x, int n, float *out)
 hipError_t launch_lds_probe(uint32_t *out)
 {
     hipLaunchKernelGGL(lds_unaligned_probe_kernel, dim3(1), dim3(64), 0, 0, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_grad_q24_probe(const double *x, int n, int32_t *out)
+{
+    hipLaunchKernelGGL(grad_q24_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, x, n, out);
     return hipGetLastError();
 }
 
@@ -2007,6 +2031,30 @@ extern "C" int dp_probe_recip_f32_device(const float *x, int n, float *out)
         e = dpk::launch_recip_probe(dx, n, dy);
     if (e == hipSuccess)
         e = hipMemcpy(out, dy, sizeof(float) * n, hipMemcpyDeviceToHost);
+    hipFree(dx);
+    hipFree(dy);
+    return e == hipSuccess ? DP_OK : DP_E_HIP;
+}
+
+extern "C" int dp_probe_grad_q24_device(const double *dncc, int n, int32_t *out)
+{
+    if (n < 0 || (n > 0 && (!dncc || !out)))
+        return DP_E_ARG;
+    if (n == 0)
+        return DP_OK;
+    double *dx = nullptr;
+    int32_t *dy = nullptr;
+    if (hipMalloc(&dx, sizeof(double) * n) != hipSuccess)
+        return DP_E_OOM;
+    if (hipMalloc(&dy, sizeof(int32_t) * n) != hipSuccess) {
+        hipFree(dx);
+        return DP_E_OOM;
+    }
+    hipError_t e = hipMemcpy(dx, dncc, sizeof(double) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = dpk::launch_grad_q24_probe(dx, n, dy);
+    if (e == hipSuccess)
+        e = hipMemcpy(out, dy, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
     hipFree(dx);
     hipFree(dy);
     return e == hipSuccess ? DP_OK : DP_E_HIP;

@@ -32,6 +32,9 @@ int dp_probe_texel_device(const uint64_t *taps_a, const uint64_t *taps_b, const 
 /* device run of the performance mode's fp32 reciprocal (v_rcp_f32 + one
  * Newton step) on n inputs >= 2^-20; the kernel's spec is IEEE 1.0f / x */
 int dp_probe_recip_f32_device(const float *x, int n, float *out);
+/* device run of the performance mode's spec-v4 gradient quantiser:
+ * rint(dncc 2^24) clamped to int32 (maxNum / minNum, NaN -> INT32_MIN) */
+int dp_probe_grad_q24_device(const double *dncc, int n, int32_t *out);
 /* 32-bit LDS reads at 2-byte alignment on the device (out: 4 x 64 words) */
 int dp_probe_lds_unaligned_device(uint32_t *out256);
 /* diagnostic builds (-DDP_STAMPS) only: per-phase s_memtime cycle sums of the

@@ -546,10 +546,22 @@ static int32_t fast_objective(const fast_patch *fp, int cell, double ncc_denom_m
  * fast_objective (num, va, vb; den = sqrt(va vb)):
  *   dnum = N Dab - Da Sb - Sa Db,  dva = 2 (N Daa - Sa Da),  dvb = 2 (N Dbb - Sb Db)
  *   dncc = den > dmin ? dnum / den - (num / den) (0.5 (dva / va + dvb / vb)) : dnum / dmin
- * rounded to an integer multiple of 2^-24 (rint(dncc 2^24), int32) and summed
+ * rounded to an integer multiple of 2^-24 (rint(dncc 2^24), saturated to int32
+ * by sat_rint_i32) and summed
  * over the views exactly; g = -(that sum) 2^-20 (fp32): the derivative of
  * sum_k (1 - NCC_k) per scaled pose unit (Q carries 2^-4 of it).
  */
+/* rint(x) clamped to the int32 range by IEEE maxNum / minNum (so NaN ->
+ * INT32_MIN), a defined conversion where a plain cast would be UB: near-flat
+ * windows (den just above dmin, or the dnum / dmin branch) can give
+ * |dncc| >= 128, i.e. |dncc 2^24| >= 2^31. */
+static int32_t sat_rint_i32(double x)
+{
+    return (int32_t)fmin(fmax(rint(x), -2147483648.0), 2147483647.0);
+}
+
+int32_t or_fast_grad_q24(double dncc) { return sat_rint_i32(dncc * 16777216.0); }
+
 static int32_t fast_objective_grad(const fast_patch *fp, int cell, double ncc_denom_min, const float x[3],
                                    float g[3])
 {
@@ -606,7 +618,7 @@ static int32_t fast_objective_grad(const fast_patch *fp, int cell, double ncc_de
             } else {
                 dncc = dnum / dmin;
             }
-            G[p] += (uint32_t)(int32_t)rint(dncc * 16777216.0);
+            G[p] += (uint32_t)sat_rint_i32(dncc * 16777216.0);
         }
     }
     for (int p = 0; p < 3; ++p) g[p] = (float)(int32_t)G[p] * -0x1p-20f;

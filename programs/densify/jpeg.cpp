@@ -41,11 +41,15 @@ struct Huffman {
     uint8_t vals[256] = {};
     int mincode[17] = {}, maxcode[18] = {}, valoff[17] = {};
     uint16_t look[512] = {}; // 9-bit lookahead: (length << 8) | value, 0 = longer code
+    int max_sym = 0;         // largest symbol (a DC table's must be <= 15)
 
     void build(const uint8_t counts[16], const uint8_t *v, int nv)
     {
         std::memcpy(vals, v, (size_t)nv);
         std::memset(look, 0, sizeof(look));
+        max_sym = 0;
+        for (int i = 0; i < nv; ++i)
+            max_sym = std::max(max_sym, (int)v[i]);
         int code = 0, k = 0;
         for (int l = 1; l <= 16; ++l) {
             valoff[l] = k;
@@ -650,6 +654,12 @@ private:
             if (ss > se || se > 63 || (ss == 0 && se != 0) || (ss > 0 && ns != 1) || al > 13)
                 throw JpegError("bad progressive scan parameters");
         }
+        // jdhuff.c jpeg_make_d_derived_tbl: a table used for DC may only hold
+        // magnitude categories 0..15 (a larger one would shift by >= 32 below)
+        if (!progressive_ || (ss == 0 && ah == 0))
+            for (Component *c : sc)
+                if (dc_[c->td].present && dc_[c->td].max_sym > 15)
+                    throw JpegError("bad Huffman table (DC symbol > 15)");
         for (Component *c : sc)
             c->pred = 0;
         eobrun_ = 0;

@@ -257,7 +257,7 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo, grad=False):
                     dncc = dnum / den - (num / den) * (0.5 * (dva / va + dvb / vb))
                 else:
                     dncc = dnum / dmin
-                G[p] = _i32(G[p] + int(np.rint(dncc * 16777216.0)))
+                G[p] = _i32(G[p] + _sat_q24(dncc))
         f = (len(samples) - 1) * 16777216 - qsum
         return len(samples), f, np.array([_f(G[p]) * _f(-2.0 ** -20) for p in range(3)], dtype=np.float32)
     tot = 0.0
@@ -268,6 +268,26 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo, grad=False):
         den = np.sqrt(float(va) * float(vb))
         tot = tot + num / max(den, dmin)
     return float(np.float32(tot / (len(samples) - 1)))
+
+
+def _sat_q24(dncc):
+    """spec v4's quantiser: rint(dncc 2^24) clamped to int32 by maxNum/minNum"""
+    if dncc != dncc:
+        return -(2 ** 31)
+    return int(min(max(np.rint(dncc * 16777216.0), -(2.0 ** 31)), 2.0 ** 31 - 1))
+
+
+def test_fast_gradient_quantiser_saturates(orc):
+    """a near-flat window (den just above the NCC floor, or the
+    dnum / dmin branch) can give |dncc| >= 128; the spec saturates the 2^-24
+    quantisation to int32 (the device's v_cvt semantics made explicit) instead
+    of the C cast's undefined behaviour."""
+    f = orc.lib.or_fast_grad_q24
+    cases = [0.0, -0.0, 0.5 / 16777216, 1.5 / 16777216, -2.5 / 16777216, 0.3, -0.7, 127.99999994, 128.0,
+             -128.0, -128.00000006, 200.0, -1e9, 1e300, float("inf"), float("-inf"), float("nan")]
+    for x in cases:
+        assert f(x) == _sat_q24(x), x
+    assert f(1e6) == 2 ** 31 - 1 and f(-1e6) == -(2 ** 31) and f(float("nan")) == -(2 ** 31)
 
 
 @pytest.mark.parametrize("cell", [7, 11])

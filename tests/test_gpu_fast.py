@@ -55,6 +55,26 @@ def test_recip_newton_exhaustive_binade():
     assert np.array_equal(out.view(np.uint32), want.view(np.uint32))
 
 
+def test_gradient_quantiser_saturates_like_the_spec(orc):
+    """Spec v4's rint(dncc 2^24) with the int32 saturation: the
+    kernel's grad_q24 equals or_fast.c's sat_rint_i32 on the range edges, the
+    non-finite values and 1M random doubles spanning |dncc| up to 2^40."""
+    rng = np.random.default_rng(23)
+    edge = np.array([0.0, -0.0, 0.5 / 2 ** 24, 1.5 / 2 ** 24, -2.5 / 2 ** 24, 127.99999994, 128.0, -128.0,
+                     -128.00000006, 200.0, -1e9, 1e300, np.inf, -np.inf, np.nan])
+    x = np.concatenate([edge, rng.standard_normal(500_000) * np.exp2(rng.uniform(-30, 40, 500_000)),
+                        rng.uniform(-129, 129, 500_000)])
+    out = np.zeros(len(x), dtype=np.int32)
+    N.check(N.lib.dp_probe_grad_q24_device(N.ptr(x), len(x), N.ptr(out)))
+    want = np.array([orc.lib.or_fast_grad_q24(float(v)) for v in x[:20_000]], dtype=np.int32)
+    assert np.array_equal(out[:20_000], want)
+    # the rest against the same definition in numpy (maxNum/minNum clamp)
+    r = np.clip(np.rint(x * 2.0 ** 24), -2.0 ** 31, 2.0 ** 31 - 1)
+    r[np.isnan(x)] = -2.0 ** 31
+    assert np.array_equal(out, r.astype(np.int64).astype(np.int32))
+    assert (out == 2 ** 31 - 1).sum() > 1000 and (out == -(2 ** 31)).sum() > 1000
+
+
 @pytest.fixture(scope="module")
 def engine():
     with dp.Engine(device=0) as eng:

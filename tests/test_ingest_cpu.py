@@ -95,3 +95,15 @@ def test_unsupported_and_corrupt_jpegs_fail_loudly(tool, tmp_path):
     tw.write_bytes(bytes(data))
     r, _ = decode(tool, tw, tmp_path)
     assert r.returncode != 0 and "8-bit" in r.stderr
+    # a DC Huffman table with a magnitude category above 15 (libjpeg
+    # rejects it when it builds the table): the first DHT of class 0 gets
+    # symbol 200 in place of its last symbol
+    data = bytearray(GOLD["q90_444__jpg"].tobytes())
+    i = data.index(b"\xff\xc4")
+    assert data[i + 4] >> 4 == 0  # class 0 (DC)
+    nv = sum(data[i + 5:i + 21])
+    data[i + 21 + nv - 1] = 200
+    bd = tmp_path / "baddc.jpg"
+    bd.write_bytes(bytes(data))
+    r, _ = decode(tool, bd, tmp_path)
+    assert r.returncode != 0 and "DC symbol" in r.stderr, r.stderr
