@@ -228,6 +228,9 @@ SIGNATURES = [
     ("dp_densify_partition_device", _I, [_P, _P, _I, _I, _P, _P, _P]),
     ("dp_densify_compact_accepted_device", _I, [_P, _P, _P, ctypes.c_int64, _P, _P, _P, _P, _P]),
     ("dp_densify_commit_accepted_device", _I, [_P, _P, _P, ctypes.c_int64, _P]),
+    ("dp_densify_partition_async", _I, [_P, _P, _I, _I, _P, _P, _P]),
+    ("dp_densify_compact_accepted_async", _I, [_P, _P, _P, ctypes.c_int64, _P, _P, _P, _P, _P]),
+    ("dp_densify_commit_gathered_device", _I, [_P, _P, _P, ctypes.c_int64, _P, _I, _P, _P]),
     ("dp_default_filter_options", None, [_P]),
     ("dp_filter_patches", _I, [_P, _P, ctypes.c_int64, _P, _P]),
     ("dp_filter_patches_device", _I, [_P, _P, ctypes.c_int64, _P, _P, _P]),

@@ -188,7 +188,9 @@ extern "C" int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out)
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_work, dpk::kWorkCounters * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_evals, sizeof(unsigned long long)) != hipSuccess ||
-        hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess) {
+        hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ej, hipEventDisableTiming) != hipSuccess || c->mbox.reserve(8) != hipSuccess ||
+        hipMemset(c->mbox.p, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
         dp_ctx_destroy(c);
         return DP_E_HIP;
     }
@@ -241,6 +243,7 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->porder.release();
     c->olo.release();
     c->ocount.release();
+    c->mbox.release();
     c->items.release();
     c->seedp.release();
     c->seedx.release();
@@ -272,6 +275,8 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
         hipEventDestroy(c->e0);
     if (c->e1)
         hipEventDestroy(c->e1);
+    if (c->ej)
+        hipEventDestroy(c->ej);
     if (c->stream)
         hipStreamDestroy(c->stream);
     delete c;
@@ -869,10 +874,15 @@ static int64_t store_capacity(const dp_ctx *c, int64_t nseeds)
     return (by_cells < by_pops ? by_cells : by_pops) + 16;
 }
 
-static int organize(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int32_t n, uint32_t seq0,
-                    int64_t base, int64_t parent0, int is_seed, int64_t *accepted_total)
+// PatchOrganizer::TryInsert over n candidates in sequence order, then the
+// append of the accepted ones at store[base ..], asynchronously on s: the
+// accepted count is read with the generation's status (read_status) -- one
+// host sync per generation, not one before the append (r05).  The append
+// guards the store capacity on the device (store_capacity bounds the accepts,
+// so the guard never fires with a correct organizer).
+static int organize_async(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int32_t n, uint32_t seq0,
+                          int64_t base, int64_t parent0, int is_seed, hipStream_t s)
 {
-    hipStream_t s = c->stream;
     dpk::ClaimArgs ca{};
     ca.views = c->d_views;
     ca.cand = cand;
@@ -902,14 +912,56 @@ static int organize(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int32_t
     // acc[n] must read as 0: scan n+1 items with a zeroed tail
     DP_HIP(c, hipMemsetAsync(c->acc.p + n, 0, 1, s));
     DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp_bytes, it, c->prefix.p, n + 1, s));
-    uint32_t total = 0;
-    DP_HIP(c, hipMemcpyAsync(&total, c->prefix.p + n, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    DP_HIP(c, dpk::launch_append(c->d_views, c->V, cand, c->acc.p, c->prefix.p, n, c->store.p, base, parent0, is_seed,
+                                 (int64_t)c->store.cap, c->mbox.p + 7, s));
+    return DP_OK;
+}
+
+// The generation's one host sync: status_kernel gathers the organizer's
+// accepts (prefix[n] of the last organize_async, n > 0), the store-overflow
+// flag, the pending partition statistics and the exchanged record total into
+// c->mbox, one copy brings them back.  st[5]: accepts, overflow, tiles, split
+// items, records exchanged.
+static int read_status(dp_ctx *c, hipStream_t s, int32_t n, const int64_t *d_counts, int world, uint64_t st[5])
+{
+    DP_HIP(c, dpk::launch_status(n > 0 ? c->prefix.p + n : nullptr, c->part_pending ? c->ocount.p : nullptr, d_counts,
+                                 world, c->mbox.p, s));
+    unsigned long long h[5] = {0, 0, 0, 0, 0};
+    DP_HIP(c, hipMemcpyAsync(h, c->mbox.p, sizeof(h), hipMemcpyDeviceToHost, s));
     DP_HIP(c, hipStreamSynchronize(s));
-    if (base + (int64_t)total > (int64_t)c->store.cap)
+    for (int k = 0; k < 5; ++k)
+        st[k] = h[k];
+    if (c->part_pending) {
+        c->part_stats[2] = (int64_t)h[2];
+        c->part_stats[3] = (int64_t)h[3];
+        c->part_pending = false;
+    }
+    if (h[1])
         return fail(c, DP_E_OOM, "patch store overflow");
-    DP_HIP(c, dpk::launch_append(c->d_views, c->V, cand, c->acc.p, c->prefix.p, n, c->store.p, base,
-                                 parent0, is_seed, s));
-    *accepted_total = total;
+    return DP_OK;
+}
+
+// the refine events of the generation (recorded by launch_timed /
+// dp_fast_launch), read after the generation's sync: no extra wait
+static int take_refine_ms(dp_ctx *c, double *acc_ms)
+{
+    if (!c->g_time_pending)
+        return DP_OK;
+    c->g_time_pending = false;
+    DP_HIP(c, hipEventSynchronize(c->e1));
+    float f = 0.f;
+    DP_HIP(c, hipEventElapsedTime(&f, c->e0, c->e1));
+    *acc_ms += f;
+    return DP_OK;
+}
+
+// make `to` wait for the work queued on `from` so far (device-side, no host wait)
+static int join_streams(dp_ctx *c, hipStream_t from, hipStream_t to)
+{
+    if (from == to)
+        return DP_OK;
+    DP_HIP(c, hipEventRecord(c->ej, from));
+    DP_HIP(c, hipStreamWaitEvent(to, c->ej, 0));
     return DP_OK;
 }
 
@@ -957,14 +1009,14 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         }
         if (rc != DP_OK)
             return rc;
-        double ms = 0.0;
-        if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
-            return rc;
-        refine_ms += ms;
+        c->g_time_pending = true;
         // PatchOrganizer::SetSeeds: TryInsert in seed order (seq = seed index)
-        rc = organize(c, c->cand.p, c->ok.p, n, 0u, 0, 0, 1, &np);
-        if (rc != DP_OK)
+        rc = organize_async(c, c->cand.p, c->ok.p, n, 0u, 0, 0, 1, s);
+        uint64_t gs[5];
+        if (rc != DP_OK || (rc = read_status(c, s, n, nullptr, 0, gs)) != DP_OK ||
+            (rc = take_refine_ms(c, &refine_ms)) != DP_OK)
             return rc;
+        np = (int64_t)gs[0];
     }
     st.seed_patches = np;
     const uint32_t seq_base = (uint32_t)n;
@@ -978,7 +1030,7 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         const int32_t nc = (int32_t)nc64;
         if ((uint64_t)seq_base + 4ull * (uint64_t)np > 0xFFFFFFF0ull)
             return fail(c, DP_E_OOM, "sequence space exhausted");
-        DP_HIP(c, hipStreamSynchronize(s)); // previous append may still read cand
+        // (the previous generation's append finished at its status read)
         DP_HIP(c, c->cand.reserve(nc));
         DP_HIP(c, c->ok.reserve(nc));
         int rc;
@@ -994,18 +1046,17 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         }
         if (rc != DP_OK)
             return rc;
-        double ms = 0.0;
-        if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
-            return rc;
-        refine_ms += ms;
+        c->g_time_pending = true;
         const int64_t expandable = std::min<int64_t>(np, o.max_pops) - head;
         st.candidates += 4 * expandable;
-        int64_t acc = 0;
-        rc = organize(c, c->cand.p, c->ok.p, nc, seq_base + 4u * (uint32_t)head, np, head, 0, &acc);
-        if (rc != DP_OK)
+        // one host sync per generation: the accepts come back with the status
+        rc = organize_async(c, c->cand.p, c->ok.p, nc, seq_base + 4u * (uint32_t)head, np, head, 0, s);
+        uint64_t gs[5];
+        if (rc != DP_OK || (rc = read_status(c, s, nc, nullptr, 0, gs)) != DP_OK ||
+            (rc = take_refine_ms(c, &refine_ms)) != DP_OK)
             return rc;
         head = np;
-        np += acc;
+        np += (int64_t)gs[0];
         ++gens;
     }
     st.pops = std::min<int64_t>(np, o.max_pops);
@@ -1057,6 +1108,8 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
     c->g_st.seeds_in = n;
     c->g_np = 0;
     c->g_nseeds = n;
+    c->g_time_pending = false;
+    c->part_pending = false;
     c->result.clear();
     int rg = reset_grid(c, s);
     if (rg != DP_OK)
@@ -1107,7 +1160,9 @@ static int densify_refine_impl(dp_ctx *c, const dp_generation *gen, int64_t lo, 
     }
     dpk::RefineArgs a{};
     const bool fast = c->fopt.densify != 0;
-    int rc;
+    int rc = take_refine_ms(c, &c->g_st.refine_ms); // an earlier refine's events, before they are re-recorded
+    if (rc != DP_OK)
+        return rc;
     if (gen->index == 0) {
         // seed.cpp:110-144 on this shard of the seed patches
         DP_HIP(c, hipMemcpyAsync(work, c->seedp.p + lo, sizeof(dp_patch) * nc, hipMemcpyDeviceToDevice, s));
@@ -1124,10 +1179,7 @@ static int densify_refine_impl(dp_ctx *c, const dp_generation *gen, int64_t lo, 
     }
     if (rc != DP_OK)
         return rc;
-    double ms = 0.0;
-    if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
-        return rc;
-    c->g_st.refine_ms += ms;
+    c->g_time_pending = true; // read at the commit's status sync
     if (!dev) {
         DP_HIP(c, hipMemcpyAsync(cand_out, work, sizeof(dp_patch) * nc, hipMemcpyDeviceToHost, s));
         DP_HIP(c, hipMemcpyAsync(accept_out, okp, (size_t)nc, hipMemcpyDeviceToHost, s));
@@ -1149,43 +1201,27 @@ extern "C" int dp_densify_refine_device(dp_ctx *c, const dp_generation *gen, int
                                stream ? (hipStream_t)stream : (c ? c->stream : nullptr));
 }
 
-static int densify_commit_impl(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
-                               int64_t n_cand, bool dev, hipStream_t user)
+// The organizer step of a whole generation on stream s (every input already
+// ordered before it on s), ending in the generation's one status read.
+// d_counts/world: the exchanged per-rank record counts (statistics only).
+static int commit_on_stream(dp_ctx *c, dp_generation *gen, const dp_patch *cp, const uint8_t *op, int32_t nc,
+                            hipStream_t s, const int64_t *d_counts = nullptr, int world = 0, int64_t *exchanged = nullptr)
 {
-    if (!c || !gen || n_cand != gen->items * gen->per_item || (n_cand > 0 && (!cand || !accept)))
-        return fail(c, DP_E_ARG, "dp_densify_commit: need all candidates of the generation");
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_commit: generation out of sequence");
-    if (n_cand > INT32_MAX)
-        return fail(c, DP_E_OOM, "dp_densify_commit: generation too large");
-    hipSetDevice(c->device);
-    hipStream_t s = c->stream;
-    const int32_t nc = (int32_t)n_cand;
-    int64_t acc = 0;
+    uint64_t gs[5] = {0, 0, 0, 0, 0};
     if (nc > 0) {
         if ((uint64_t)gen->seq0 + (uint64_t)nc > 0xFFFFFFF0ull)
             return fail(c, DP_E_OOM, "sequence space exhausted");
-        const dp_patch *cp = cand;
-        const uint8_t *op = accept;
-        if (dev) {
-            // the gathered records are produced on the caller's stream (RCCL,
-            // torch ops); NULL = the legacy default stream, which is synced too
-            if (user != s)
-                DP_HIP(c, hipStreamSynchronize(user));
-        } else {
-            DP_HIP(c, c->cand.reserve(nc));
-            DP_HIP(c, c->ok.reserve(nc));
-            DP_HIP(c, hipMemcpyAsync(c->cand.p, cand, sizeof(dp_patch) * nc, hipMemcpyHostToDevice, s));
-            DP_HIP(c, hipMemcpyAsync(c->ok.p, accept, (size_t)nc, hipMemcpyHostToDevice, s));
-            cp = c->cand.p;
-            op = c->ok.p;
-        }
         const int is_seed = gen->index == 0;
-        int rc = organize(c, cp, op, nc, gen->seq0, c->g_np, is_seed ? 0 : gen->head, is_seed, &acc);
+        int rc = organize_async(c, cp, op, nc, gen->seq0, c->g_np, is_seed ? 0 : gen->head, is_seed, s);
         if (rc != DP_OK)
             return rc;
-        DP_HIP(c, hipStreamSynchronize(s));
     }
+    int rc = read_status(c, s, nc, d_counts, world, gs);
+    if (rc != DP_OK || (rc = take_refine_ms(c, &c->g_st.refine_ms)) != DP_OK)
+        return rc;
+    if (exchanged)
+        *exchanged = (int64_t)gs[4];
+    const int64_t acc = nc > 0 ? (int64_t)gs[0] : 0;
     int64_t head;
     if (gen->index == 0) {
         c->g_st.seed_patches = acc;
@@ -1199,6 +1235,40 @@ static int densify_commit_impl(dp_ctx *c, dp_generation *gen, const dp_patch *ca
     next_generation(c, gen, head);
     c->g_expected = gen->index;
     return DP_OK;
+}
+
+static int densify_commit_impl(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
+                               int64_t n_cand, bool dev, hipStream_t user)
+{
+    if (!c || !gen || n_cand != gen->items * gen->per_item || (n_cand > 0 && (!cand || !accept)))
+        return fail(c, DP_E_ARG, "dp_densify_commit: need all candidates of the generation");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_commit: generation out of sequence");
+    if (n_cand > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_commit: generation too large");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    const int32_t nc = (int32_t)n_cand;
+    const dp_patch *cp = cand;
+    const uint8_t *op = accept;
+    if (nc > 0) {
+        if (dev) {
+            // the gathered records are produced on the caller's stream (RCCL,
+            // torch ops; NULL = the legacy default stream): the context's
+            // stream waits for it on the device
+            int rc = join_streams(c, user, s);
+            if (rc != DP_OK)
+                return rc;
+        } else {
+            DP_HIP(c, c->cand.reserve(nc));
+            DP_HIP(c, c->ok.reserve(nc));
+            DP_HIP(c, hipMemcpyAsync(c->cand.p, cand, sizeof(dp_patch) * nc, hipMemcpyHostToDevice, s));
+            DP_HIP(c, hipMemcpyAsync(c->ok.p, accept, (size_t)nc, hipMemcpyHostToDevice, s));
+            cp = c->cand.p;
+            op = c->ok.p;
+        }
+    }
+    return commit_on_stream(c, gen, cp, op, nc, s);
 }
 
 extern "C" int dp_densify_commit(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
@@ -1219,7 +1289,8 @@ extern "C" int dp_densify_commit_device(dp_ctx *c, dp_generation *gen, const dp_
 // items stable-sorted by super-tile key, the order cut into `world` contiguous
 // shares lo[r] = floor(r n / world).  Leaves the order in c->porder (complete
 // on return), the shares in counts (host) and the statistics in c->part_stats.
-static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int tile_px, int64_t *counts)
+static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int tile_px, int64_t *counts,
+                          hipStream_t s = nullptr, bool sync = true)
 {
     const int64_t n = gen->items;
     for (int r = 0; r < world; ++r)
@@ -1231,13 +1302,13 @@ static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int ti
         return DP_OK;
     if (n > INT32_MAX)
         return fail(c, DP_E_OOM, "partition: generation too large");
-    hipStream_t s = c->stream;
+    if (!s)
+        s = c->stream;
     const dp_patch *items = gen->index == 0 ? c->seedp.p : c->store.p + gen->head;
     DP_HIP(c, c->tkeys.reserve((size_t)n));
     DP_HIP(c, c->okeys.reserve((size_t)n));
     DP_HIP(c, c->oiota.reserve((size_t)n));
     DP_HIP(c, c->porder.reserve((size_t)n));
-    DP_HIP(c, c->olo.reserve(65));
     DP_HIP(c, c->ocount.reserve(2));
     DP_HIP(c, dpk::launch_tile_keys(c->d_views, items, n, (double)tile_px, c->tkeys.p, s));
     DP_HIP(c, dpk::launch_iota(c->oiota.p, n, s));
@@ -1247,11 +1318,12 @@ static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int ti
     DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
     DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->scan_tmp.p, tmp, c->tkeys.p, c->okeys.p, c->oiota.p, c->porder.p,
                                                  (int)n, 0, 64, s));
-    std::vector<int64_t> lo((size_t)world + 1, 0);
-    for (int r = 1; r <= world; ++r)
-        lo[(size_t)r] = lo[(size_t)r - 1] + counts[r - 1];
-    DP_HIP(c, hipMemcpyAsync(c->olo.p, lo.data(), sizeof(int64_t) * (world + 1), hipMemcpyHostToDevice, s));
-    DP_HIP(c, dpk::launch_partition_stats(c->okeys.p, n, c->olo.p, world, c->ocount.p, s));
+    DP_HIP(c, dpk::launch_partition_stats(c->okeys.p, n, world, c->ocount.p, s));
+    if (!sync) {
+        // the statistics come back with the commit's status read
+        c->part_pending = true;
+        return DP_OK;
+    }
     unsigned long long st[2] = {0, 0};
     DP_HIP(c, hipMemcpyAsync(st, c->ocount.p, sizeof(st), hipMemcpyDeviceToHost, s));
     // the order is read on the caller's stream (refine, compaction): complete it
@@ -1303,7 +1375,9 @@ static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const 
     const int32_t nc = (int32_t)nc64;
     dpk::RefineArgs a{};
     const bool fast = c->fopt.densify != 0;
-    int rc;
+    int rc = take_refine_ms(c, &c->g_st.refine_ms);
+    if (rc != DP_OK)
+        return rc;
     if (gen->index == 0) {
         DP_HIP(c, dpk::launch_gather_patches(c->seedp.p, d_items, n, work, s));
         a = refine_args(c, work, nc, gen->cell, DP_MODE_SEED, okp);
@@ -1319,10 +1393,7 @@ static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const 
     }
     if (rc != DP_OK)
         return rc;
-    double ms = 0.0;
-    if ((rc = dp_last_kernel_ms(c, &ms)) != DP_OK)
-        return rc;
-    c->g_st.refine_ms += ms;
+    c->g_time_pending = true; // read at the commit's status sync
     return DP_OK;
 }
 
@@ -1387,8 +1458,9 @@ extern "C" int dp_densify_commit_items_device(dp_ctx *c, dp_generation *gen, con
     hipStream_t us = (hipStream_t)stream;
     const size_t nc = (size_t)n_items * gen->per_item;
     if (nc > 0) {
-        if (us != c->stream)
-            DP_HIP(c, hipStreamSynchronize(us));
+        int rc = join_streams(c, us, c->stream);
+        if (rc != DP_OK)
+            return rc;
         DP_HIP(c, c->cand.reserve(nc));
         DP_HIP(c, c->ok.reserve(nc));
         DP_HIP(c, dpk::launch_scatter_items(d_cand, d_accept, d_items, n_items, gen->per_item, c->cand.p, c->ok.p,
@@ -1464,8 +1536,9 @@ extern "C" int dp_densify_commit_accepted_device(dp_ctx *c, dp_generation *gen, 
     hipSetDevice(c->device);
     hipStream_t us = (hipStream_t)stream;
     if (nc > 0) {
-        if (us != c->stream)
-            DP_HIP(c, hipStreamSynchronize(us));
+        int rc = join_streams(c, us, c->stream);
+        if (rc != DP_OK)
+            return rc;
         DP_HIP(c, c->cand.reserve((size_t)nc));
         DP_HIP(c, c->ok.reserve((size_t)nc));
         // every other candidate of the generation failed the refine's filter
@@ -1473,6 +1546,90 @@ extern "C" int dp_densify_commit_accepted_device(dp_ctx *c, dp_generation *gen, 
         DP_HIP(c, dpk::launch_scatter_accepted(d_recs, n_recs, nc, c->cand.p, c->ok.p, c->stream));
     }
     return densify_commit_impl(c, gen, c->cand.p, c->ok.p, nc, true, c->stream);
+}
+
+// ---- the one-sync generation step (r05) -------------------------------------
+// partition -> refine -> compact -> [exchange] -> commit, all queued on the
+// caller's stream; the only host wait is the commit's status read.
+
+extern "C" int dp_densify_partition_async(dp_ctx *c, const dp_generation *gen, int world, int tile_px, void *stream,
+                                          const int64_t **d_order_out, int64_t *counts_out)
+{
+    if (!c || !gen || world < 1 || world > 64 || tile_px < 1 || !d_order_out || !counts_out)
+        return fail(c, DP_E_ARG, "dp_densify_partition_async: bad arguments (1 <= world <= 64)");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_partition_async: generation out of sequence");
+    *d_order_out = nullptr;
+    hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    // the library's own earlier work (begin's seed patches) precedes the keys
+    int rc = join_streams(c, c->stream, s);
+    if (rc == DP_OK)
+        rc = partition_impl(c, gen, world, tile_px, counts_out, s, false);
+    if (rc != DP_OK)
+        return rc;
+    if (gen->items > 0)
+        *d_order_out = c->porder.p;
+    return DP_OK;
+}
+
+struct FlagAt {
+    const uint8_t *a;
+    int64_t m;
+    __host__ __device__ uint32_t operator()(int64_t i) const { return i < m ? (uint32_t)a[i] : 0u; }
+};
+
+extern "C" int dp_densify_compact_accepted_async(dp_ctx *c, const dp_generation *gen, const int64_t *d_items,
+                                                 int64_t n, const dp_patch *d_cand, const uint8_t *d_accept,
+                                                 dp_patch *d_out, int64_t *d_count, void *stream)
+{
+    if (!c || !gen || n < 0 || !d_count || (n > 0 && (!d_items || !d_cand || !d_accept || !d_out)))
+        return fail(c, DP_E_ARG, "dp_densify_compact_accepted_async: bad arguments");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_compact_accepted_async: generation out of sequence");
+    const int64_t m = n * gen->per_item;
+    if (m > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_compact_accepted_async: too many candidates");
+    hipSetDevice(c->device);
+    hipStream_t us = stream ? (hipStream_t)stream : c->stream;
+    if (m == 0) {
+        DP_HIP(c, hipMemsetAsync(d_count, 0, sizeof(int64_t), us));
+        return DP_OK;
+    }
+    DP_HIP(c, c->prefix.reserve((size_t)m + 1));
+    // the flags read in place, index m as 0 (no copy of the flags)
+    hipcub::TransformInputIterator<uint32_t, FlagAt, hipcub::CountingInputIterator<int64_t>> it(
+        hipcub::CountingInputIterator<int64_t>(0), FlagAt{d_accept, m});
+    size_t tmp = 0;
+    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, c->prefix.p, (int)m + 1, us));
+    DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
+    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, it, c->prefix.p, (int)m + 1, us));
+    DP_HIP(c, dpk::launch_compact_accepted(d_cand, d_accept, c->prefix.p, d_items, n, gen->per_item, d_out, us));
+    DP_HIP(c, dpk::launch_count_out(c->prefix.p + m, d_count, us));
+    return DP_OK;
+}
+
+extern "C" int dp_densify_commit_gathered_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_recs, int64_t stride,
+                                                 const int64_t *d_counts, int world, void *stream,
+                                                 int64_t *exchanged_out)
+{
+    if (!c || !gen || world < 1 || world > 64 || stride < 0 || !d_counts || (stride > 0 && !d_recs))
+        return fail(c, DP_E_ARG, "dp_densify_commit_gathered_device: bad arguments");
+    if (gen->index != c->g_expected)
+        return fail(c, DP_E_STATE, "dp_densify_commit_gathered_device: generation out of sequence");
+    const int64_t nc = gen->items * gen->per_item;
+    if (nc > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_commit_gathered_device: generation too large");
+    hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (nc > 0) {
+        DP_HIP(c, c->cand.reserve((size_t)nc));
+        DP_HIP(c, c->ok.reserve((size_t)nc));
+        // every other candidate of the generation failed the refine's filter
+        DP_HIP(c, hipMemsetAsync(c->ok.p, 0, (size_t)nc, s));
+        DP_HIP(c, dpk::launch_scatter_gathered(d_recs, stride, d_counts, world, nc, c->cand.p, c->ok.p, s));
+    }
+    return commit_on_stream(c, gen, c->cand.p, c->ok.p, (int32_t)nc, s, d_counts, world, exchanged_out);
 }
 
 extern "C" int dp_densify_result(dp_ctx *c, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats)

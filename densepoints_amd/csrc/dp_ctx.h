@@ -113,6 +113,14 @@ struct dp_ctx {
     DevBuf<int64_t> oiota, porder, olo;
     DevBuf<unsigned long long> ocount;
     int64_t part_stats[4] = {0, 0, 0, 0}; // items, world, tiles, items in split tiles
+    bool part_pending = false;            // a partition's tiles/split counts wait in ocount
+    // one-sync generation step (r05): device status words gathered by one small
+    // kernel and read back with ONE copy per generation -- [0] organizer accepts,
+    // [1] store overflow, [2] tiles, [3] items in split tiles, [4] records
+    // exchanged; [7] the append's overflow flag (cleared when read)
+    DevBuf<unsigned long long> mbox;
+    hipEvent_t ej = nullptr;   // stream joins (no host wait)
+    bool g_time_pending = false; // a densify refine's events (e0, e1) not yet read
     int64_t g_np = 0;        // patches in the replicated store
     int64_t g_nseeds = 0;
     int64_t g_expected = -1; // generation index the next commit must carry

@@ -102,7 +102,12 @@ hipError_t launch_claims(const ClaimArgs &a, hipStream_t s);
 hipError_t launch_resolve(const ClaimArgs &a, uint8_t *accepted, hipStream_t s);
 hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand, const uint8_t *accepted,
                          const uint32_t *prefix, int32_t n, dp_patch *store, int64_t base,
-                         int64_t parent0, int is_seed, hipStream_t s);
+                         int64_t parent0, int is_seed, int64_t cap, unsigned long long *overflow, hipStream_t s);
+hipError_t launch_status(const uint32_t *prefix_end, const unsigned long long *ocount, const int64_t *counts,
+                         int world, unsigned long long *mbox, hipStream_t s);
+hipError_t launch_scatter_gathered(const dp_patch *recs, int64_t stride, const int64_t *counts, int world, int64_t nc,
+                                   dp_patch *cand, uint8_t *ok, hipStream_t s);
+hipError_t launch_count_out(const uint32_t *prefix_end, int64_t *count, hipStream_t s);
 hipError_t launch_render(const dp_synth_config &cfg, const double *P, uint32_t *out, int v,
                          hipStream_t s);
 // Seed::CreatePatchesFromPoints: seed patches of n points (xyz device, 3n f64)
@@ -113,8 +118,7 @@ hipError_t launch_seed_patches(const dpg::ViewDev *views, int V, const double *x
 // cut of the key-sorted order at lo[1..world-1] (stats[2], zeroed here)
 hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
                             uint64_t *key, hipStream_t s);
-hipError_t launch_partition_stats(const uint64_t *key, int64_t n, const int64_t *lo, int world,
-                                  unsigned long long *stats, hipStream_t s);
+hipError_t launch_partition_stats(const uint64_t *key, int64_t n, int world, unsigned long long *stats, hipStream_t s);
 hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s);
 hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s);
 // accepted candidates of items[0..n) (per_item each), out[prefix[j]] = cand[j]

@@ -1677,13 +1677,21 @@ __global__ void claimk_resolve_kernel(ClaimArgs a, uint8_t *accepted)
 // the reference's fp64 sums; lanes 0..19 copy the 80-byte record
 __global__ __launch_bounds__(256) void append_wave_kernel(const dpg::ViewDev *views, int V, const dp_patch *cand,
                                                           const uint8_t *accepted, const uint32_t *prefix, int32_t n,
-                                                          dp_patch *store, int64_t base, int64_t parent0, int is_seed)
+                                                          dp_patch *store, int64_t base, int64_t parent0, int is_seed,
+                                                          int64_t cap, unsigned long long *overflow)
 {
     const int i = (int)(blockIdx.x * 4u + (threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63u);
     if (i >= n || !accepted[i])
         return;
     const int64_t pos = base + (int64_t)prefix[i];
+    if (pos >= cap) {
+        // cannot happen with a correct organizer (store_capacity bounds the
+        // accepts); reported at the generation's status read, nothing written
+        if (lane == 0)
+            overflow[0] = 1ull;
+        return;
+    }
     const float p0 = cand[i].pos[0], p1 = cand[i].pos[1], p2 = cand[i].pos[2];
     uint32_t s0 = 0, s1 = 0, s2 = 0, cnt = 0;
     for (int v = lane; v < V; v += 64) {
@@ -2032,8 +2040,7 @@ __global__ void tile_keys_kernel(const dpg::ViewDev *views, const dp_patch *item
 
 // partition statistics over the key-sorted items: stats[0] = distinct tiles,
 // stats[1] = items of the tiles a cut lo[r] (0 < lo[r] < n) splits between ranks
-__global__ void partition_stats_kernel(const uint64_t *key, int64_t n, const int64_t *lo, int world,
-                                       unsigned long long *stats)
+__global__ void partition_stats_kernel(const uint64_t *key, int64_t n, int world, unsigned long long *stats)
 {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long heads = 0, split = 0;
@@ -2041,7 +2048,8 @@ __global__ void partition_stats_kernel(const uint64_t *key, int64_t n, const int
         const uint64_t k = key[j];
         heads = (j == 0 || key[j - 1] != k) ? 1ull : 0ull;
         for (int r = 1; r < world; ++r) {
-            const int64_t c = lo[r];
+            // the cut lo_r = floor(r n / world) (n < 2^31, world <= 64: no overflow)
+            const int64_t c = ((int64_t)r * n) / world;
             if (c > 0 && c < n && key[c - 1] == key[c] && key[c] == k) {
                 split = 1;
                 break;
@@ -2068,13 +2076,12 @@ hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, in
     return hipGetLastError();
 }
 
-hipError_t launch_partition_stats(const uint64_t *key, int64_t n, const int64_t *lo, int world,
-                                  unsigned long long *stats, hipStream_t s)
+hipError_t launch_partition_stats(const uint64_t *key, int64_t n, int world, unsigned long long *stats, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(unsigned long long), s);
     if (e != hipSuccess || n <= 0)
         return e;
-    hipLaunchKernelGGL(partition_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, key, n, lo, world,
+    hipLaunchKernelGGL(partition_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, key, n, world,
                        stats);
     return hipGetLastError();
 }
@@ -2206,12 +2213,83 @@ hipError_t launch_claims_k(const ClaimArgs &a, uint8_t *accepted, hipStream_t s)
 
 hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand, const uint8_t *accepted,
                          const uint32_t *prefix, int32_t n, dp_patch *store, int64_t base,
-                         int64_t parent0, int is_seed, hipStream_t s)
+                         int64_t parent0, int is_seed, int64_t cap, unsigned long long *overflow, hipStream_t s)
 {
     if (n <= 0)
         return hipSuccess;
     hipLaunchKernelGGL(append_wave_kernel, dim3((n + 3) / 4), dim3(256), 0, s, views, V, cand, accepted, prefix, n,
-                       store, base, parent0, is_seed);
+                       store, base, parent0, is_seed, cap, overflow);
+    return hipGetLastError();
+}
+
+// The generation's status in one place (one small copy per generation):
+// mbox[0] = the organizer's accepts (prefix[n], 0 without candidates), [1] =
+// the append's overflow flag (mbox[7], cleared), [2..3] = the partition's
+// tiles and split items (ocount, when given), [4] = records exchanged (the sum
+// of counts[world], when given).  One thread.
+__global__ void status_kernel(const uint32_t *prefix_end, const unsigned long long *ocount, const int64_t *counts,
+                              int world, unsigned long long *mbox)
+{
+    if (threadIdx.x != 0)
+        return;
+    mbox[0] = prefix_end ? (unsigned long long)prefix_end[0] : 0ull;
+    mbox[1] = mbox[7];
+    mbox[7] = 0ull;
+    mbox[2] = ocount ? ocount[0] : 0ull;
+    mbox[3] = ocount ? ocount[1] : 0ull;
+    unsigned long long t = 0;
+    for (int r = 0; counts && r < world; ++r)
+        t += (unsigned long long)counts[r];
+    mbox[4] = t;
+}
+
+hipError_t launch_status(const uint32_t *prefix_end, const unsigned long long *ocount, const int64_t *counts,
+                         int world, unsigned long long *mbox, hipStream_t s)
+{
+    hipLaunchKernelGGL(status_kernel, dim3(1), dim3(64), 0, s, prefix_end, ocount, counts, world, mbox);
+    return hipGetLastError();
+}
+
+// scatter of the gathered accepted records of `world` ranks (rank r's
+// counts[r] records at recs + r * stride, any order within a rank) to their
+// generation positions; ok must be zeroed first (every other candidate was
+// rejected by the refine's filter)
+__global__ void scatter_gathered_kernel(const dp_patch *recs, int64_t stride, const int64_t *counts, int world,
+                                        int64_t nc, dp_patch *cand, uint8_t *ok)
+{
+    const int r = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= world || i >= counts[r] || i >= stride)
+        return;
+    const dp_patch &p = recs[(int64_t)r * stride + i];
+    const uint32_t pos = p.seq;
+    if ((int64_t)pos < nc) {
+        cand[pos] = p;
+        ok[pos] = 1;
+    }
+}
+
+hipError_t launch_scatter_gathered(const dp_patch *recs, int64_t stride, const int64_t *counts, int world, int64_t nc,
+                                   dp_patch *cand, uint8_t *ok, hipStream_t s)
+{
+    if (stride <= 0 || world <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(scatter_gathered_kernel, dim3((unsigned)((stride + 255) / 256), (unsigned)world), dim3(256), 0, s,
+                       recs, stride, counts, world, nc, cand, ok);
+    return hipGetLastError();
+}
+
+// the compacted count of a rank's accepted candidates (prefix[m]) as the int64
+// the exchange carries
+__global__ void count_out_kernel(const uint32_t *prefix_end, int64_t *count)
+{
+    if (threadIdx.x == 0)
+        count[0] = (int64_t)prefix_end[0];
+}
+
+hipError_t launch_count_out(const uint32_t *prefix_end, int64_t *count, hipStream_t s)
+{
+    hipLaunchKernelGGL(count_out_kernel, dim3(1), dim3(64), 0, s, prefix_end, count);
     return hipGetLastError();
 }
 

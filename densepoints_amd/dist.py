@@ -267,6 +267,102 @@ class _DeviceBuffers:
 def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64,
                                probe_worlds: tuple = ()):
     """dp_densify with every generation partitioned by reference-view super-tile,
+    the records in HBM, only the ACCEPTED candidates exchanged, and ONE host
+    wait per generation (round 5; the round-4 protocol with four is
+    densify_partitioned_device_r04).  Per generation, all queued on the torch
+    current stream:
+      1. dp_densify_partition_async: the items sorted by their (ref, v/64, u/64)
+         super-tile key, cut into `world` contiguous equal shares (the shares
+         are floor(r n / world) cuts: known on the host without a read);
+      2. this rank refines its slice of that order (dp_densify_refine_items_device);
+      3. dp_densify_compact_accepted_async keeps the candidates whose filter
+         passed (each tagged with its generation position) and leaves their
+         count in device memory;
+      4. one all_gather_into_tensor of the counts (8 B per rank, device to
+         device) and ONE of fixed-capacity rank slots (the largest share x 4
+         records, host-known) over RCCL/xGMI -- no count has to reach the host;
+         with one rank there is no exchange;
+      5. dp_densify_commit_gathered_device scatters the slots to sequence order,
+         commits the replicated organizer step and reads the generation's
+         status (next generation size, partition statistics, records
+         exchanged): the one host wait.
+    Every rank's store equals dp_densify bit for bit.  stats as the r04
+    protocol's: "partition", "accepted" (records exchanged), "gathered_bytes",
+    "phase_ms" (host time: begin; launch = the queued partition, refine,
+    compaction and exchange calls; commit = the commit up to its status read,
+    i.e. mostly the GPU time of the generation)."""
+    rank = dist.get_rank() if dist is not None else 0
+    world = dist.get_world_size() if dist is not None else 1
+    rccl = dist is not None and dist.get_backend() == "nccl"
+    rec = PATCH_DTYPE.itemsize
+    stream = torch.cuda.current_stream(device)
+    sp = stream.cuda_stream
+    pool = _DeviceBuffers(device)
+    ph = {"begin": 0.0, "launch": 0.0, "commit": 0.0}
+    t = time.perf_counter()
+    gen = eng.densify_begin(seeds_xyz)
+    ph["begin"] += time.perf_counter() - t
+    parts, gathered, accepted = [], [], []
+    probe = {int(w): [] for w in probe_worlds}
+    d_cnt = torch.zeros(1, dtype=torch.int64, device=device)
+    all_cnt = torch.zeros(world, dtype=torch.int64, device=device)
+    while gen.items > 0:
+        per = gen.per_item
+        for w in probe:
+            _, pc, _ = eng.densify_partition_device(gen, w, tile_px)
+            probe[w].append(_part_record(eng, pc))
+        t = time.perf_counter()
+        d_order, counts = eng.densify_partition_async(gen, world, tile_px, sp)
+        offs = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+        mine = int(counts[rank])
+        stride = max(int(counts.max()) * per, 1)  # fixed-capacity rank slot (records)
+        buf = pool.get("cand", max(mine * per, 1) * rec)
+        acc = pool.get("acc", max(mine * per, 1))
+        send = pool.get("send", stride * rec)
+        if mine:
+            d_items = d_order + 8 * int(offs[rank])
+            eng.densify_refine_items_device(gen, d_items, mine, buf.data_ptr(), acc.data_ptr(), sp)
+            eng.densify_compact_accepted_async(gen, d_items, mine, buf.data_ptr(), acc.data_ptr(), send.data_ptr(),
+                                               d_cnt.data_ptr(), sp)
+        else:
+            d_cnt.zero_()
+        if dist is None:
+            recv, cnts = send, d_cnt
+        elif rccl:
+            recv = pool.get("recv", world * stride * rec)[: world * stride * rec]
+            dist.all_gather_into_tensor(all_cnt, d_cnt)
+            dist.all_gather_into_tensor(recv, send[: stride * rec])
+            cnts = all_cnt
+        else:
+            # gloo (one-device rehearsals): staged through the host
+            hc = torch.empty(world, dtype=torch.int64)
+            dist.all_gather_into_tensor(hc, d_cnt.cpu())
+            hr = torch.empty(world * stride * rec, dtype=torch.uint8)
+            dist.all_gather_into_tensor(hr, send[: stride * rec].cpu())
+            recv = hr.to(device)
+            all_cnt.copy_(hc.to(device))
+            cnts = all_cnt
+        t1 = time.perf_counter()
+        ph["launch"] += t1 - t
+        n_ex = eng.densify_commit_gathered_device(gen, recv.data_ptr(), stride, cnts.data_ptr(), world, sp)
+        ph["commit"] += time.perf_counter() - t1
+        parts.append(_part_record(eng, counts))
+        gathered.append(world * (stride * rec + 8) if dist is not None else 0)
+        accepted.append(n_ex)
+    patches, stats = eng.densify_result()
+    stats = _reduce_stats(stats, dist, device)
+    stats["phase_ms"] = {k: round(v * 1e3, 2) for k, v in ph.items()}
+    stats["partition"] = parts
+    stats["gathered_bytes"] = gathered or [0]
+    stats["accepted"] = accepted
+    if probe:
+        stats["partition_probe"] = probe
+    return patches, stats
+
+
+def densify_partitioned_device_r04(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64,
+                                   probe_worlds: tuple = ()):
+    """dp_densify with every generation partitioned by reference-view super-tile,
     the records in HBM and only the ACCEPTED candidates exchanged (SURVEY 8e,
     north star: "RCCL all-gather over xGMI of accepted patches").  Per
     generation:

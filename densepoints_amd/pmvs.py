@@ -465,6 +465,41 @@ class Engine:
                                                           ctypes.c_void_p(stream) if stream else None))
         return gen
 
+    # ---- the one-sync generation step (r05): everything on the caller's stream ----
+    def densify_partition_async(self, gen: N.DpGeneration, world: int, tile_px: int = 64,
+                                stream: int | None = None):
+        """(device address of the rank-major item order, items per rank):
+        dp_densify_partition_async -- queued on `stream`, no host wait (the
+        shares are floor(r n / world) cuts; the statistics come back with the
+        commit)."""
+        d_order = ctypes.c_void_p()
+        counts = np.zeros(world, dtype=np.int64)
+        self._check(lib.dp_densify_partition_async(self._ctx, ctypes.byref(gen), world, tile_px,
+                                                   ctypes.c_void_p(stream) if stream else None,
+                                                   ctypes.byref(d_order), ptr(counts)))
+        return int(d_order.value or 0), counts
+
+    def densify_compact_accepted_async(self, gen: N.DpGeneration, d_items: int, n: int, d_cand: int, d_accept: int,
+                                       d_out: int, d_count: int, stream: int | None = None) -> None:
+        """Accepted candidates of a rank's items into d_out, their count (int64)
+        into device memory d_count: no host wait."""
+        self._check(lib.dp_densify_compact_accepted_async(
+            self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_items), n, ctypes.c_void_p(d_cand),
+            ctypes.c_void_p(d_accept), ctypes.c_void_p(d_out), ctypes.c_void_p(d_count),
+            ctypes.c_void_p(stream) if stream else None))
+
+    def densify_commit_gathered_device(self, gen: N.DpGeneration, d_recs: int, stride: int, d_counts: int, world: int,
+                                       stream: int | None = None) -> int:
+        """Commit from the gathered fixed-capacity rank slots (rank r's
+        d_counts[r] records at d_recs + r * stride records); the generation's
+        one host wait.  Returns the records exchanged."""
+        ex = ctypes.c_int64()
+        self._check(lib.dp_densify_commit_gathered_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_recs), stride,
+                                                          ctypes.c_void_p(d_counts), world,
+                                                          ctypes.c_void_p(stream) if stream else None,
+                                                          ctypes.byref(ex)))
+        return int(ex.value)
+
     def densify_result(self):
         out = ctypes.c_void_p()
         n = ctypes.c_int64()

@@ -298,6 +298,32 @@ int dp_densify_compact_accepted_device(dp_ctx *ctx, const dp_generation *gen, co
                                        int64_t *n_out, void *stream);
 int dp_densify_commit_accepted_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_recs, int64_t n_recs,
                                       void *stream);
+/* The same protocol with ONE host wait per generation (round 5).  Everything is
+ * queued on `stream` (NULL = the context's stream), in this order:
+ *  - dp_densify_partition_async: the partition of dp_densify_partition_device
+ *    (same order, same shares counts_out[r] = floor((r+1) n / world) -
+ *    floor(r n / world), host, no device read); its statistics arrive with the
+ *    commit (dp_densify_partition_stats after it);
+ *  - dp_densify_refine_items_device on the rank's slice of *d_order_out;
+ *  - dp_densify_compact_accepted_async: as _compact_accepted_device, the
+ *    count (int64) written to device memory *d_count instead of the host;
+ *  - the exchange: all-gather of the counts (world int64) and of FIXED-CAPACITY
+ *    rank slots of `stride` records (stride >= max_r counts_out[r] *
+ *    per_item, host-known: no count has to reach the host first);
+ *  - dp_densify_commit_gathered_device: scatters rank r's d_counts[r]
+ *    records at d_recs + r * stride to their generation positions, commits the
+ *    organizer step and reads the generation's status (accepts, store overflow,
+ *    partition statistics, *exchanged_out = the records exchanged) with one
+ *    small copy -- the only host wait.  With one rank, pass the compacted
+ *    buffer and its count directly (world 1).
+ * Every rank's store equals dp_densify's bit for bit. */
+int dp_densify_partition_async(dp_ctx *ctx, const dp_generation *gen, int world, int tile_px, void *stream,
+                               const int64_t **d_order_out, int64_t *counts_out);
+int dp_densify_compact_accepted_async(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
+                                      const dp_patch *d_cand, const uint8_t *d_accept, dp_patch *d_out,
+                                      int64_t *d_count, void *stream);
+int dp_densify_commit_gathered_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_recs, int64_t stride,
+                                      const int64_t *d_counts, int world, void *stream, int64_t *exchanged_out);
 
 /* ---- patch filter ----------------------------------------
  * PMVS::FilterPatches is declared (methods/pmvs/pmvs.h:27) but never defined

@@ -98,6 +98,8 @@ def _worker_dev(rank, world, port, out_path, backend, partitioned=False, cap=1):
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
         if partitioned == "all":
             got, st = D.densify_partitioned_device_all(eng, seeds, group, torch.device("cuda", 0))
+        elif partitioned == "r04":
+            got, st = D.densify_partitioned_device_r04(eng, seeds, group, torch.device("cuda", 0))
         elif partitioned:
             got, st = D.densify_partitioned_device(eng, seeds, group, torch.device("cuda", 0))
         else:
@@ -130,13 +132,16 @@ def test_device_resident_sharded_densify(tmp_path, backend, world):
 
 @pytest.mark.parametrize("backend,world,variant,cap", [(None, 1, "accepted", 1), ("nccl", 1, "accepted", 1),
                                                       ("gloo", 2, "accepted", 1), ("gloo", 3, "accepted", 1),
-                                                      ("gloo", 2, "all", 1), ("gloo", 2, "accepted", 2)])
+                                                      ("gloo", 2, "all", 1), ("gloo", 2, "accepted", 2),
+                                                      ("nccl", 1, "r04", 1), ("gloo", 2, "r04", 1)])
 def test_partitioned_densify_device(tmp_path, backend, world, variant, cap):
     """Reference-view super-tile partition of every generation: the device
     partition, refine of the rank's items, all-gather of the ACCEPTED
     candidates only and dp_densify_commit_accepted_device (variant
-    "accepted", dist.densify_partitioned_device), or of every candidate slot
-    with dp_densify_commit_items_device ("all"): every rank's store equals
+    "accepted", dist.densify_partitioned_device: one host wait per generation,
+    fixed-capacity rank slots; "r04": the round-4 protocol with host-read
+    counts), or of every candidate slot with dp_densify_commit_items_device
+    ("all"): every rank's store equals
     dp_densify -- also with organizer cell capacity 2
     (max_patches_per_cell, patch_organizer.h:42-46)."""
     out = str(tmp_path / "dense")
