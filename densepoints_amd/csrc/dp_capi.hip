@@ -1197,8 +1197,19 @@ extern "C" int dp_densify_refine(dp_ctx *c, const dp_generation *gen, int64_t lo
 extern "C" int dp_densify_refine_device(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi,
                                         dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream)
 {
-    return densify_refine_impl(c, gen, lo, hi, d_cand_out, d_accept_out, true,
-                               stream ? (hipStream_t)stream : (c ? c->stream : nullptr));
+    if (c && !stream) {
+        hipSetDevice(c->device);
+        int rj = join_streams(c, nullptr, c->stream);
+        if (rj != DP_OK)
+            return rj;
+    }
+    int rc = densify_refine_impl(c, gen, lo, hi, d_cand_out, d_accept_out, true,
+                                 stream ? (hipStream_t)stream : (c ? c->stream : nullptr));
+    // NULL stream: the records are read on the legacy default stream (torch's
+    // default), which does not order with the context's non-blocking stream
+    if (rc == DP_OK && !stream)
+        rc = join_streams(c, c->stream, nullptr);
+    return rc;
 }
 
 // The organizer step of a whole generation on stream s (every input already
@@ -1442,8 +1453,14 @@ extern "C" int dp_densify_refine_items_device(dp_ctx *c, const dp_generation *ge
     if (!d_items || !d_cand_out || !d_accept_out)
         return fail(c, DP_E_ARG, "dp_densify_refine_items_device: null arrays");
     hipSetDevice(c->device);
-    return densify_refine_items_impl(c, gen, d_items, n, d_cand_out, d_accept_out,
-                                     stream ? (hipStream_t)stream : c->stream);
+    // NULL stream: the inputs (item list) may come from the legacy default stream
+    if (!stream && (rc = join_streams(c, nullptr, c->stream)) != DP_OK)
+        return rc;
+    rc = densify_refine_items_impl(c, gen, d_items, n, d_cand_out, d_accept_out,
+                                   stream ? (hipStream_t)stream : c->stream);
+    if (rc == DP_OK && !stream)
+        rc = join_streams(c, c->stream, nullptr); // see dp_densify_refine_device
+    return rc;
 }
 
 extern "C" int dp_densify_commit_items_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_cand,
@@ -1561,7 +1578,7 @@ extern "C" int dp_densify_partition_async(dp_ctx *c, const dp_generation *gen, i
         return fail(c, DP_E_STATE, "dp_densify_partition_async: generation out of sequence");
     *d_order_out = nullptr;
     hipSetDevice(c->device);
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream; // the caller's stream (NULL: the legacy default stream)
     // the library's own earlier work (begin's seed patches) precedes the keys
     int rc = join_streams(c, c->stream, s);
     if (rc == DP_OK)
@@ -1591,7 +1608,7 @@ extern "C" int dp_densify_compact_accepted_async(dp_ctx *c, const dp_generation 
     if (m > INT32_MAX)
         return fail(c, DP_E_OOM, "dp_densify_compact_accepted_async: too many candidates");
     hipSetDevice(c->device);
-    hipStream_t us = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t us = (hipStream_t)stream; // the caller's stream (NULL: the legacy default stream)
     if (m == 0) {
         DP_HIP(c, hipMemsetAsync(d_count, 0, sizeof(int64_t), us));
         return DP_OK;
@@ -1621,7 +1638,7 @@ extern "C" int dp_densify_commit_gathered_device(dp_ctx *c, dp_generation *gen, 
     if (nc > INT32_MAX)
         return fail(c, DP_E_OOM, "dp_densify_commit_gathered_device: generation too large");
     hipSetDevice(c->device);
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream; // the caller's stream (NULL: the legacy default stream)
     if (nc > 0) {
         DP_HIP(c, c->cand.reserve((size_t)nc));
         DP_HIP(c, c->ok.reserve((size_t)nc));

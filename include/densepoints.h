@@ -299,7 +299,7 @@ int dp_densify_compact_accepted_device(dp_ctx *ctx, const dp_generation *gen, co
 int dp_densify_commit_accepted_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_recs, int64_t n_recs,
                                       void *stream);
 /* The same protocol with ONE host wait per generation (round 5).  Everything is
- * queued on `stream` (NULL = the context's stream), in this order:
+ * queued on `stream` (NULL = the legacy default stream), in this order:
  *  - dp_densify_partition_async: the partition of dp_densify_partition_device
  *    (same order, same shares counts_out[r] = floor((r+1) n / world) -
  *    floor(r n / world), host, no device read); its statistics arrive with the
@@ -317,6 +317,8 @@ int dp_densify_commit_accepted_device(dp_ctx *ctx, dp_generation *gen, const dp_
  *    small copy -- the only host wait.  With one rank, pass the compacted
  *    buffer and its count directly (world 1).
  * Every rank's store equals dp_densify's bit for bit. */
+/* (here NULL `stream` = the legacy default stream itself, so a caller on it
+ * needs no other ordering; the context's own stream is joined in.) */
 int dp_densify_partition_async(dp_ctx *ctx, const dp_generation *gen, int world, int tile_px, void *stream,
                                const int64_t **d_order_out, int64_t *counts_out);
 int dp_densify_compact_accepted_async(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
