@@ -82,6 +82,9 @@ def parse():
                          "gradient (v4; keys *_an)")
     ap.add_argument("--no-fast", action="store_true", help="skip the perf_mode sub-object")
     ap.add_argument("--seed-stride", type=float, default=32.0, help="synthetic seed grid stride (px)")
+    ap.add_argument("--densify-protocol", choices=["r05", "r04"], default="r05",
+                    help="scaling_leg's generation protocol: r05 = one host wait per generation (default), r04 = the "
+                         "round-4 protocol (host-read partition and accepted counts), for A/B runs")
     return ap.parse_args()
 
 
@@ -351,7 +354,7 @@ def main():
     eng.close()
 
 
-def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
+def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast, protocol="r05"):
     """`steps` whole densifies with every generation partitioned over the ranks
     (dist.densify_partitioned_device), after `warmup` untimed ones, bracketed by
     barrier + synchronize; rate = candidates refined (seed stage + expansions)
@@ -360,11 +363,12 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
     from densepoints_amd import dist as D
 
     eng.set_fast_options(dp.FastOptions(densify=1 if fast else 0))
+    run = D.densify_partitioned_device if protocol == "r05" else D.densify_partitioned_device_r04
     probe = None
     for i in range(warmup):
         # the untimed warm-up also computes the partitions world sizes 2 and 8
         # would use on the same generations (statistics only)
-        _, wst = D.densify_partitioned_device(eng, seeds, dist, dev, probe_worlds=(2, 8) if i == 0 else ())
+        _, wst = run(eng, seeds, dist, dev, probe_worlds=(2, 8) if i == 0 else ())
         probe = probe or wst.get("partition_probe")
     torch.cuda.synchronize()
     if dist:
@@ -372,7 +376,7 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        got, st = D.densify_partitioned_device(eng, seeds, dist, dev)
+        got, st = run(eng, seeds, dist, dev)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -407,6 +411,11 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast):
             "store_crc32": f"{crc:08x}", "ranks_store_equal": len(set(crcs)) == 1,
             "generations": int(st["generations"]), "evals": int(st["evals"]),
             "refine_ms_max_rank": round(st["refine_ms"], 1),
+            # everything but the refine kernels (partition, compaction, exchange,
+            # replicated organizer commit, host waits): the part that does not
+            # shrink with the ranks
+            "non_refine_ms": round(wall / steps * 1e3 - st["refine_ms"], 2),
+            "protocol": protocol,
             # host time per phase of the last densify (each phase ends in a host sync;
             # refine_compact includes this rank's refine kernels), max over ranks
             "phase_ms_max_rank": {k: round(D.max_over_ranks(v, dist, coll_dev), 2)
@@ -463,7 +472,8 @@ def scaling_leg(args, stream, dist, coll_dev, dev):
         torch.cuda.synchronize()
         eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
         seeds = synth.seeds(cfg, P)
-        out = {m: partitioned_leg(eng, seeds, dist, coll_dev, dev, args.densify_steps, 1, m == "fast")
+        out = {m: partitioned_leg(eng, seeds, dist, coll_dev, dev, args.densify_steps, 1, m == "fast",
+                                  args.densify_protocol)
                for m in ("parity", "fast")}
         out["workload"] = (f"cfg4_64view_4k: {V} views {W}x{H}, one step = the whole densify (PMVS::Run minus "
                            f"matching) of {len(seeds)} seed points, every BFS generation partitioned by "
@@ -701,9 +711,20 @@ def attach_profile(roof, prof, B, launch_ms):
         roof["profile_lib_sha256"] = prof.get("lib_sha256")
         return
     roof["profiled_launch_ms"] = round(prof["trace_avg_ns"] * 1e-6, 3)
+    if prof.get("events_avg_ns_same_process"):
+        # attestation: the profiled run's kernel trace against that same
+        # process's HIP events (profiler overhead), and this run's events
+        # against the profiled run's (box / run variance)
+        pe = prof["events_avg_ns_same_process"] * 1e-6
+        roof["profiled_events_ms"] = round(pe, 3)
+        roof["profile_over_events"] = round(prof["trace_avg_ns"] * 1e-6 / pe, 4)
+        roof["live_over_profiled_events"] = round(launch_ms / pe, 4)
     if "hbm_bytes_corrected" in prof:
+        # per launch (counters summed over a dispatch's instances, averaged
+        # over the dispatches), and as a rate over this run's launch time
         roof["traffic"] = prof["hbm_bytes_corrected"]
         roof["traffic_raw"] = prof["hbm_bytes_raw"]
+        roof["traffic_GBps"] = round(prof["hbm_bytes_corrected"] / (launch_ms * 1e-3) / 1e9, 1)
     v = prof.get("valu")
     if v:
         per = v["insts_per_launch"] / B

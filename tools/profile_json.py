@@ -49,15 +49,20 @@ def one(d):
     args = open(os.path.join(d, "args.txt")).read().strip() if os.path.exists(os.path.join(d, "args.txt")) else ""
     toks = args.split()
     steps = int(toks[toks.index("--steps") + 1]) if "--steps" in toks else 5
-    # the library the profiled bench loaded: its own JSON line in the trace log
+    # the library the profiled bench loaded, and the same process's own HIP-event
+    # time of its timed launches: its JSON line in the trace log
     lib_sha = None
+    ev_ms, ev_list = None, None
     if os.path.exists(os.path.join(d, "trace.log")):
         for line in open(os.path.join(d, "trace.log")):
             if line.startswith("{"):
                 try:
-                    lib_sha = json.loads(line).get("lib_sha256", lib_sha)
+                    j = json.loads(line)
                 except ValueError:
-                    pass
+                    continue
+                lib_sha = j.get("lib_sha256", lib_sha)
+                ev_ms = j.get("kernel_ms_per_launch", ev_ms)
+                ev_list = j.get("kernel_ms_events", ev_list)
     for k in set(durs) | set(ctr):
         if not any(s in k for s in KEEP):
             continue
@@ -70,6 +75,14 @@ def one(d):
             e["trace_launches"] = len(timed)
             e["trace_avg_all_ns"] = statistics.fmean(durs[k])
             e["trace_launches_all"] = len(durs[k])
+            e["trace_timed_ns"] = timed
+            if ev_ms:
+                # the profiled process's own HIP events around the same launches
+                # (bench.py records them on the launch stream; they also cover
+                # the refine's dequeue-ordering kernels and the launch gaps)
+                e["events_avg_ns_same_process"] = ev_ms * 1e6
+                e["events_ms_same_process"] = ev_list
+                e["trace_over_events"] = e["trace_avg_ns"] / (ev_ms * 1e6)
         if k in stats:
             e["stats"] = stats[k]
         c = {n: statistics.fmean(v) for n, v in ctr.get(k, {}).items()}
