@@ -840,6 +840,14 @@ extern "C" int dp_last_kernel_ms(dp_ctx *c, double *ms)
 // densify: seeds -> organizer -> generation-synchronous BFS
 // ---------------------------------------------------------------------------
 
+// flags a[0 .. m-1] and a zero at index m (an exclusive scan of m + 1 of them
+// ends in the count) without a copy or a memset of the tail
+struct FlagAt {
+    const uint8_t *a;
+    int64_t m;
+    __host__ __device__ uint32_t operator()(int64_t i) const { return i < m ? (uint32_t)a[i] : 0u; }
+};
+
 struct U8ToU32 {
     __host__ __device__ uint32_t operator()(uint8_t v) const { return v; }
 };
@@ -906,11 +914,11 @@ static int organize_async(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, i
     }
     DP_HIP(c, c->prefix.reserve((size_t)n + 1));
     size_t tmp_bytes = 0;
-    hipcub::TransformInputIterator<uint32_t, U8ToU32, const uint8_t *> it(c->acc.p, U8ToU32());
+    // n + 1 flags, index n read as 0: prefix[n] = the accepts
+    hipcub::TransformInputIterator<uint32_t, FlagAt, hipcub::CountingInputIterator<int64_t>> it(
+        hipcub::CountingInputIterator<int64_t>(0), FlagAt{c->acc.p, (int64_t)n});
     DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, it, c->prefix.p, n + 1, s));
     DP_HIP(c, c->scan_tmp.reserve(tmp_bytes + 16));
-    // acc[n] must read as 0: scan n+1 items with a zeroed tail
-    DP_HIP(c, hipMemsetAsync(c->acc.p + n, 0, 1, s));
     DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp_bytes, it, c->prefix.p, n + 1, s));
     DP_HIP(c, dpk::launch_append(c->d_views, c->V, cand, c->acc.p, c->prefix.p, n, c->store.p, base, parent0, is_seed,
                                  (int64_t)c->store.cap, c->mbox.p + 7, s));
@@ -1321,8 +1329,7 @@ static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int ti
     DP_HIP(c, c->oiota.reserve((size_t)n));
     DP_HIP(c, c->porder.reserve((size_t)n));
     DP_HIP(c, c->ocount.reserve(2));
-    DP_HIP(c, dpk::launch_tile_keys(c->d_views, items, n, (double)tile_px, c->tkeys.p, s));
-    DP_HIP(c, dpk::launch_iota(c->oiota.p, n, s));
+    DP_HIP(c, dpk::launch_tile_keys(c->d_views, items, n, (double)tile_px, c->tkeys.p, c->oiota.p, c->ocount.p, s));
     size_t tmp = 0;
     DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, c->tkeys.p, c->okeys.p, c->oiota.p, c->porder.p, (int)n,
                                                  0, 64, s));
@@ -1532,7 +1539,8 @@ extern "C" int dp_densify_compact_accepted_device(dp_ctx *c, const dp_generation
     DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, c->prefix.p, (int)m + 1, us));
     DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
     DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, it, c->prefix.p, (int)m + 1, us));
-    DP_HIP(c, dpk::launch_compact_accepted(d_cand, c->acc.p, c->prefix.p, d_items, n, gen->per_item, d_out, us));
+    DP_HIP(c, dpk::launch_compact_accepted(d_cand, c->acc.p, c->prefix.p, d_items, n, gen->per_item, d_out, nullptr,
+                                           us));
     uint32_t total = 0;
     DP_HIP(c, hipMemcpyAsync(&total, c->prefix.p + m, sizeof(uint32_t), hipMemcpyDeviceToHost, us));
     DP_HIP(c, hipStreamSynchronize(us));
@@ -1590,12 +1598,6 @@ extern "C" int dp_densify_partition_async(dp_ctx *c, const dp_generation *gen, i
     return DP_OK;
 }
 
-struct FlagAt {
-    const uint8_t *a;
-    int64_t m;
-    __host__ __device__ uint32_t operator()(int64_t i) const { return i < m ? (uint32_t)a[i] : 0u; }
-};
-
 extern "C" int dp_densify_compact_accepted_async(dp_ctx *c, const dp_generation *gen, const int64_t *d_items,
                                                  int64_t n, const dp_patch *d_cand, const uint8_t *d_accept,
                                                  dp_patch *d_out, int64_t *d_count, void *stream)
@@ -1621,8 +1623,8 @@ extern "C" int dp_densify_compact_accepted_async(dp_ctx *c, const dp_generation 
     DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, c->prefix.p, (int)m + 1, us));
     DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
     DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, it, c->prefix.p, (int)m + 1, us));
-    DP_HIP(c, dpk::launch_compact_accepted(d_cand, d_accept, c->prefix.p, d_items, n, gen->per_item, d_out, us));
-    DP_HIP(c, dpk::launch_count_out(c->prefix.p + m, d_count, us));
+    DP_HIP(c, dpk::launch_compact_accepted(d_cand, d_accept, c->prefix.p, d_items, n, gen->per_item, d_out, d_count,
+                                           us));
     return DP_OK;
 }
 

@@ -72,6 +72,8 @@ struct FastArgs {
     float dminf;             // the same, rounded to fp32 (the refine objective's floor)
     float gs;                // gradient per objective unit: (1 / fd_step) 2^-24
     unsigned long long *stats; // dp_fast_stats: patches, evals, view_evals, staged_bytes
+    uint32_t chunk;          // candidates per dequeue: 4 (siblings share one parent read), or 1
+                             // when the launch has fewer than 4 candidates per resident wave
 };
 
 // per evaluation, per staged view: A.xyz 2^23+umax | B1.xyz 2^23+vmax | B2.xyz
@@ -1389,10 +1391,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
     const Slots sl = make_slots<G, NS, kMask>(L, a.cell);
     unsigned long long wave_evals = 0, wave_vev = 0, wave_bytes = 0, wave_patches = 0, wave_clip = 0;
     dp_patch &p = L.p;
-    // work is dequeued in chunks of 4 (one atomic per chunk): the 4 children of
-    // one parent, whose record is read once into LDS (with the children's
-    // centres), or 4 consecutive patches
-    uint32_t chunk_idx = 0xffffffffu, q4 = 4;
+    // work is dequeued in chunks of cs = 4 (one atomic per chunk): the 4 children
+    // of one parent, whose record is read once into LDS (with the children's
+    // centres), or 4 consecutive patches.  A launch with fewer than 4
+    // candidates per resident wave (the BFS's tail generations) dequeues them
+    // one at a time (cs = 1), so siblings run on different waves instead of one
+    // after another on one: its latency is one candidate's, not four.
+    const uint32_t cs = a.chunk == 1u ? 1u : 4u;
+    uint32_t chunk_idx = 0xffffffffu, q4 = cs;
     bool par_live = true;
 #ifdef DP_FAST_TIMING
     for (int k = 0; k < 16; ++k)
@@ -1401,16 +1407,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
     const unsigned long long t_start = L.tlast;
 #endif
     for (;;) {
-        if (q4 == 4) {
+        if (q4 == cs) {
             uint32_t c = 0;
             if (lane == 0)
                 c = atomicAdd(a.work, 1u);
             chunk_idx = (uint32_t)uni((int)c);
             q4 = 0;
-            if ((uint64_t)chunk_idx * 4u >= (uint64_t)a.n)
+            if ((uint64_t)chunk_idx * cs >= (uint64_t)a.n)
                 break;
             if (a.parents) {
-                const int64_t q = a.parent0 + (a.items ? a.items[chunk_idx] : (int64_t)chunk_idx);
+                const uint32_t pk = cs == 4u ? chunk_idx : chunk_idx >> 2; // the parent's item
+                const int64_t q = a.parent0 + (a.items ? a.items[pk] : (int64_t)pk);
                 par_live = q < a.max_pops;
                 const uint32_t *src = (const uint32_t *)(a.parents + q);
                 if (lane < (int)(sizeof(dp_patch) / 4))
@@ -1424,9 +1431,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
             }
         }
         TMARK(L, 0);
-        const uint32_t idx = chunk_idx * 4u + q4++;
+        const uint32_t idx = chunk_idx * cs + q4++;
         if (idx >= (uint32_t)a.n) {
-            q4 = 4;
+            q4 = cs;
             continue;
         }
         bool live = true;
@@ -1688,16 +1695,18 @@ static hipError_t launch_fast_m(const FastArgs &a, hipStream_t s)
     static_assert(kBudget != 6656 || sizeof(FastLds<kBudget>) <= 160 * 1024 / 16,
                   "the default arena must keep 16 waves per CU");
 #endif
-    const int64_t want = ((int64_t)a.n + 3) / 4;
-    const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
+    const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1); // resident waves (1-wave workgroups)
+    FastArgs b = a;
+    b.chunk = (int64_t)a.n < 4 * cap ? 1u : 4u;
+    const int64_t want = ((int64_t)a.n + b.chunk - 1) / b.chunk;
     const int grid = (int)(want < cap ? want : cap);
     if (a.mode == DP_MODE_FAST_EVAL)
-        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, b);
     else if (a.fo.gradient)
-        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, kFastRefineGrad>), dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, kFastRefineGrad>), dim3(grid), dim3(64), 0, s, b);
     else
         hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_REFINE>), dim3(grid), dim3(64), 0, s,
-                           a);
+                           b);
     return hipGetLastError();
 }
 

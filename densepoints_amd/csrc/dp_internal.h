@@ -107,7 +107,6 @@ hipError_t launch_status(const uint32_t *prefix_end, const unsigned long long *o
                          int world, unsigned long long *mbox, hipStream_t s);
 hipError_t launch_scatter_gathered(const dp_patch *recs, int64_t stride, const int64_t *counts, int world, int64_t nc,
                                    dp_patch *cand, uint8_t *ok, hipStream_t s);
-hipError_t launch_count_out(const uint32_t *prefix_end, int64_t *count, hipStream_t s);
 hipError_t launch_render(const dp_synth_config &cfg, const double *P, uint32_t *out, int v,
                          hipStream_t s);
 // Seed::CreatePatchesFromPoints: seed patches of n points (xyz device, 3n f64)
@@ -117,14 +116,15 @@ hipError_t launch_seed_patches(const dpg::ViewDev *views, int V, const double *x
 // (ref, tile row, tile column) of the items' centres, and the statistics of a
 // cut of the key-sorted order at lo[1..world-1] (stats[2], zeroed here)
 hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
-                            uint64_t *key, hipStream_t s);
+                            uint64_t *key, int64_t *iota, unsigned long long *stats, hipStream_t s);
 hipError_t launch_partition_stats(const uint64_t *key, int64_t n, int world, unsigned long long *stats, hipStream_t s);
 hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s);
 hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s);
 // accepted candidates of items[0..n) (per_item each), out[prefix[j]] = cand[j]
 // with seq = items[j / per] * per + j % per (the generation position)
 hipError_t launch_compact_accepted(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
-                                   const int64_t *items, int64_t n, int per, dp_patch *out, hipStream_t s);
+                                   const int64_t *items, int64_t n, int per, dp_patch *out, int64_t *count,
+                                   hipStream_t s);
 // cand[r.seq] = r, ok[r.seq] = 1 for each gathered accepted record r (seq < nc)
 hipError_t launch_scatter_accepted(const dp_patch *recs, int64_t n, int64_t nc, dp_patch *cand, uint8_t *ok,
                                    hipStream_t s);

@@ -2026,11 +2026,14 @@ __device__ __forceinline__ uint64_t tile_coord(double q)
 }
 
 __global__ void tile_keys_kernel(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
-                                 uint64_t *key)
+                                 uint64_t *key, int64_t *iota, unsigned long long *stats)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) // the partition statistics' counters (partition_stats_kernel adds to them)
+        stats[0] = stats[1] = 0ull;
     if (i >= n)
         return;
+    iota[i] = i; // the sort's values: item indices
     const dp_patch &p = items[i];
     const dpg::ViewDev &v = views[p.ref];
     double u, w;
@@ -2067,20 +2070,20 @@ __global__ void partition_stats_kernel(const uint64_t *key, int64_t n, int world
 }
 
 hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
-                            uint64_t *key, hipStream_t s)
+                            uint64_t *key, int64_t *iota, unsigned long long *stats, hipStream_t s)
 {
     if (n <= 0)
         return hipSuccess;
     hipLaunchKernelGGL(tile_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, views, items, n, tile,
-                       key);
+                       key, iota, stats);
     return hipGetLastError();
 }
 
+// (the counters were zeroed by tile_keys_kernel)
 hipError_t launch_partition_stats(const uint64_t *key, int64_t n, int world, unsigned long long *stats, hipStream_t s)
 {
-    hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(unsigned long long), s);
-    if (e != hipSuccess || n <= 0)
-        return e;
+    if (n <= 0)
+        return hipSuccess;
     hipLaunchKernelGGL(partition_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, key, n, world,
                        stats);
     return hipGetLastError();
@@ -2112,9 +2115,11 @@ __global__ void iota_kernel(int64_t *v, int64_t n)
 }
 
 __global__ void compact_accepted_kernel(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
-                                        const int64_t *items, int64_t m, int per, dp_patch *out)
+                                        const int64_t *items, int64_t m, int per, dp_patch *out, int64_t *count)
 {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j == 0 && count)
+        count[0] = (int64_t)prefix[m]; // the compacted count (exclusive scan of m + 1 flags)
     if (j >= m || !acc[j])
         return;
     dp_patch r = cand[j];
@@ -2143,13 +2148,14 @@ hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s)
 }
 
 hipError_t launch_compact_accepted(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
-                                   const int64_t *items, int64_t n, int per, dp_patch *out, hipStream_t s)
+                                   const int64_t *items, int64_t n, int per, dp_patch *out, int64_t *count,
+                                   hipStream_t s)
 {
     const int64_t m = n * per;
     if (m <= 0)
         return hipSuccess;
     hipLaunchKernelGGL(compact_accepted_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, cand, acc, prefix,
-                       items, m, per, out);
+                       items, m, per, out, count);
     return hipGetLastError();
 }
 
@@ -2279,18 +2285,6 @@ hipError_t launch_scatter_gathered(const dp_patch *recs, int64_t stride, const i
     return hipGetLastError();
 }
 
-// the compacted count of a rank's accepted candidates (prefix[m]) as the int64
-// the exchange carries
-__global__ void count_out_kernel(const uint32_t *prefix_end, int64_t *count)
-{
-    if (threadIdx.x == 0)
-        count[0] = (int64_t)prefix_end[0];
-}
 
-hipError_t launch_count_out(const uint32_t *prefix_end, int64_t *count, hipStream_t s)
-{
-    hipLaunchKernelGGL(count_out_kernel, dim3(1), dim3(64), 0, s, prefix_end, count);
-    return hipGetLastError();
-}
 
 } // namespace dpk
