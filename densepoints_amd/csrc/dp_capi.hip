@@ -244,6 +244,7 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->olo.release();
     c->ocount.release();
     c->mbox.release();
+    c->result.release();
     c->items.release();
     c->seedp.release();
     c->seedx.release();
@@ -1068,7 +1069,7 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         ++gens;
     }
     st.pops = std::min<int64_t>(np, o.max_pops);
-    c->result.resize((size_t)np);
+    DP_HIP(c, c->result.resize((size_t)np));
     if (np)
         DP_HIP(c, hipMemcpyAsync(c->result.data(), c->store.p, sizeof(dp_patch) * np, hipMemcpyDeviceToHost, s));
     unsigned long long ev = 0;
@@ -1660,7 +1661,7 @@ extern "C" int dp_densify_result(dp_ctx *c, const dp_patch **out, int64_t *n_out
     hipSetDevice(c->device);
     hipStream_t s = c->stream;
     const int64_t np = c->g_np;
-    c->result.resize((size_t)np);
+    DP_HIP(c, c->result.resize((size_t)np));
     if (np)
         DP_HIP(c, hipMemcpyAsync(c->result.data(), c->store.p, sizeof(dp_patch) * np, hipMemcpyDeviceToHost, s));
     unsigned long long ev = 0;

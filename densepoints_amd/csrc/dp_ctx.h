@@ -63,6 +63,39 @@ template <typename T> struct DevBuf {
     }
 };
 
+// pinned host memory (grown, never shrunk): device->host copies of a result run
+// at DMA speed instead of through a staging buffer
+template <typename T> struct HostBuf {
+    T *p = nullptr;
+    size_t cap = 0, n = 0;
+    hipError_t resize(size_t k)
+    {
+        if (k > cap) {
+            if (p)
+                hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            const size_t want = k + k / 4;
+            hipError_t e = hipHostMalloc((void **)&p, want * sizeof(T), hipHostMallocDefault);
+            if (e != hipSuccess)
+                return e;
+            cap = want;
+        }
+        n = k;
+        return hipSuccess;
+    }
+    void clear() { n = 0; }
+    bool empty() const { return n == 0; }
+    T *data() { return p; }
+    void release()
+    {
+        if (p)
+            hipHostFree(p);
+        p = nullptr;
+        cap = n = 0;
+    }
+};
+
 } // namespace
 
 struct dp_ctx {
@@ -101,7 +134,7 @@ struct dp_ctx {
     DevBuf<uint8_t> f_alive, f_keep;
     DevBuf<double> f_rho;
     DevBuf<dp_patch> f_pat;
-    std::vector<dp_patch> result;
+    HostBuf<dp_patch> result; // dp_densify / dp_densify_result output (pinned)
     // generation-at-a-time densify (dp_densify_begin/refine/commit/result)
     DevBuf<dp_patch> seedp;  // seed patches of generation 0
     DevBuf<double> seedx;    // seed points (3 f64 each) on the device

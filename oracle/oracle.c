@@ -202,6 +202,29 @@ double or_ncc_int(const int32_t *a, const int32_t *b, int n, double denom_min)
  * corners: 4 x xyz (order X-sx-sy, X+sx-sy, X+sx+sy, X-sx+sy).  Returns 1 and
  * writes cell*cell gray values, or 0 for the reference's empty texture.
  */
+/* ROI trace for the parity-kernel staging study (tools/roi_footprint.py; test
+ * infrastructure, single-threaded use only): when set, every textured window
+ * appends (view, tl.x, tl.y, br.x, br.y) and every refine a marker (-1, mode). */
+static int32_t *g_trace = NULL;
+static int64_t g_trace_n = 0, g_trace_cap = 0;
+
+void or_trace_set(int32_t *buf, int64_t cap_records)
+{
+    g_trace = buf;
+    g_trace_cap = cap_records;
+    g_trace_n = 0;
+}
+
+int64_t or_trace_count(void) { return g_trace_n; }
+
+static void trace_rec(int32_t a, int32_t b, int32_t c, int32_t d, int32_t e)
+{
+    if (!g_trace || g_trace_n >= g_trace_cap)
+        return;
+    int32_t *r = g_trace + 5 * g_trace_n++;
+    r[0] = a; r[1] = b; r[2] = c; r[3] = d; r[4] = e;
+}
+
 int or_texture(const or_scene *s, int view, const double corners[12], int cell, int32_t *gray)
 {
     const or_view *v = &s->v[view];
@@ -223,6 +246,7 @@ int or_texture(const or_scene *s, int view, const double corners[12], int cell, 
     int rw = brx - tlx, rh = bry - tly; /* patch.cpp:144-147 */
     if (rw <= 0 || rh <= 0)             /* optimization.cpp:44 */
         return 0;
+    trace_rec(view, tlx, tly, brx, bry);
     double x[4], y[4];
     for (int i = 0; i < 4; ++i) {
         x[i] = (double)(qx[i] - (float)tlx); /* f32 '-=' int, patch.cpp:148-151 */
@@ -595,6 +619,7 @@ static int filter(const or_scene *s, or_patch *p, int cell)
 static int refine_one(const or_scene *s, or_patch *p, int cell, int mode)
 {
     int ok = 1;
+    trace_rec(-1, mode, 0, 0, 0);
     switch (mode) {
     case OR_MODE_EVAL: {
         double nn[3], pp[3], sc[OR_MAX_VIEWS];

@@ -130,6 +130,9 @@ int or_filter_patches(const or_scene *s, const or_patch *p, int64_t n, int passe
 /* performance mode (or_fast.c) */
 void or_fast_default_options(or_fast_options *f);
 int or_gray_plane(const or_scene *s, int view, uint8_t *out);
+/* ROI trace (tools/roi_footprint.py; single-threaded): 5 int32 per record */
+void or_trace_set(int32_t *buf, int64_t cap_records);
+int64_t or_trace_count(void);
 /* spec v4 gradient quantiser: rint(dncc 2^24) saturated to int32 (NaN -> INT32_MIN) */
 int32_t or_fast_grad_q24(double dncc);
 int or_fast_grad_probe(const or_scene *s, const or_patch *p, int cell, const or_fast_options *fo, int32_t *f,

@@ -109,6 +109,8 @@ def _load():
         "or_fast_expand_batch": (ctypes.c_int, [P, P, ctypes.c_int, P, P, P, ctypes.c_int]),
         "or_fast_grad_probe": (ctypes.c_int, [P, P, ctypes.c_int, P, P, P]),
         "or_fast_grad_q24": (ctypes.c_int32, [ctypes.c_double]),
+        "or_trace_set": (None, [P, ctypes.c_int64]),
+        "or_trace_count": (ctypes.c_int64, []),
         # seed generation (or_seeds.c)
         "or_orb_pattern": (None, [P]),
         "or_features_per_level": (None, [ctypes.c_int, ctypes.c_double, ctypes.c_int, P]),
