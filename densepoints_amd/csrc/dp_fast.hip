@@ -607,8 +607,7 @@ __device__ __forceinline__ uint32_t lane_select(uint64_t mask, uint32_t x)
 struct Tap {
     uint32_t a0, a1;   // aligned LDS byte addresses of rows y0, y0 + 1
     uint32_t sh;       // 16 if the pair starts at an odd pixel
-    uint32_t w0, w1;   // packed bilinear weights of the two rows
-    uint32_t wx, fy;   // (32 - fx) | fx << 16 and fy (the gradient's slopes only)
+    uint32_t wx, fy;   // (32 - fx) | fx << 16 and fy
 };
 
 __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, const float4 &qc, uint32_t off,
@@ -629,17 +628,16 @@ __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, cons
     Tap t;
     // row: bv >> 5 is y0 plus the exponent bits' 0x2580000, whose 24-bit part
     // times the row bytes is taken off the view's offset (u32 wrap-around);
-    // aligned word of the pair: byte (x0 >> 1) * 4 of the row; x0 odd -> the
-    // pair straddles two words, shifted by 16 bits
-    t.a0 = __umul24(bv >> 5, rowb) + (((bu >> 4) & 0x3FFFCu) + off);
+    // aligned word of the pair: byte (x0 >> 1) * 4 of the row = bits 6..21 of
+    // bu shifted left by 2 (one v_bfe + one v_lshl_add, the row term by one
+    // v_mad_u32_u24); x0 odd -> the pair straddles two words, shifted by 16 bits
+    const uint32_t row = __umul24(bv >> 5, rowb) + off;
+    t.a0 = (__builtin_amdgcn_ubfe(bu, 6u, 16u) << 2) + row;
     t.a1 = t.a0 + rowb;
     t.sh = (bu >> 1) & 16u;
-    const uint32_t fx = bu & 31u, fy = bv & 31u;
-    const uint32_t wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
-    t.w0 = __umul24(wx, 32u - fy);
-    t.w1 = __umul24(wx, fy);
-    t.wx = wx;
-    t.fy = fy;
+    const uint32_t fx = bu & 31u;
+    t.fy = bv & 31u;
+    t.wx = 32u + fx * 65535u; // (32 - fx) | fx << 16
     return t;
 }
 
@@ -661,15 +659,19 @@ __device__ __forceinline__ TapWords tap_load(const char *tiles, const Tap &t)
 }
 
 // (p(x0), p(x0+1)) of each row as u16 pairs, each value 0x6400 + gray (fp16 of
-// 1024 + gray): sum w (0x6400 + p) + 32 = sum w p + 32 + 0x6400 * 1024
+// 1024 + gray).  Vertical first, as wrapping packed u16 arithmetic: per column
+// c = (32 - fy) p0 + fy p1 = 0x6400 * 32 + v with v <= 255 * 32, i.e. 0x8000 + v
+// mod 2^16 (no wrap of v); then the horizontal dot product with (32 - fx, fx):
+// 0x8000 * 32 + sum w p, the bias removed by the accumulator's start value.
+// Equal to sum_taps (32 - fx | fx)(32 - fy | fy) p, the spec's blend.
 __device__ __forceinline__ uint32_t tap_blend_rows(const Tap &t, uint32_t r0, uint32_t r1)
 {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r0), __builtin_bit_cast(us2, t.w0),
-                                              __builtin_amdgcn_udot2(__builtin_bit_cast(us2, r1),
-                                                                     __builtin_bit_cast(us2, t.w1),
-                                                                     32u - 0x6400u * 1024u, false),
-                                              false);
+    uint32_t c;
+    asm("v_pk_mul_lo_u16 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(c) : "v"(r0), "v"(32u - t.fy));
+    asm("v_pk_mad_u16 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(c) : "v"(r1), "v"(t.fy), "v"(c));
+    const uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, c), __builtin_bit_cast(us2, t.wx),
+                                              32u - 0x8000u * 32u, false);
     return b >> 6;
 }
 
@@ -929,10 +931,17 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
                 if (kGrad)
                     qt = sample_q(tt, r0, r1, tgc, sl.tail, sl.tail);
             }
+            // samples are < 2^12 (1/16 gray levels): two of them pack into one
+            // register as u16 halves (slot pairs 2k, 2k + 1)
+            constexpr int NP = (NS + 1) / 2;
+            uint32_t bp[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                bp[k] = 2 * k + 1 < NS ? (b[2 * k + 1] << 16) | b[2 * k] : b[2 * k];
             if (p == 0) {
 #pragma unroll
                 for (int s2 = 0; s2 < NS; ++s2) {
-                    a0s[s2] = b[s2];
+                    a0s[s2] = kGrad ? b[s2] : (s2 < NP ? bp[s2] : 0u);
                     if (kGrad) {
                         aq1[s2] = pack_lo(sq[s2].qd, sq[s2].qa);
                         aq2[s2] = sq[s2].qb;
@@ -942,15 +951,31 @@ __device__ void evaluate_poses(const FastArgs &a, FastLds<kArena> &L, const Slot
             // the anchor samples of this item's pose through the LDS crossbar
             const int src = (int)__float_as_uint(qb.z) + (g << 2);
             uint32_t av[NS];
+            uint32_t s = 0, ss = 0, sx = 0;
+            if (!kGrad) {
+                // moments by u16 dot products on the packed pairs (one
+                // ds_bpermute per pair of anchor samples)
+                typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-            for (int s2 = 0; s2 < NS; ++s2)
-                av[s2] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a0s[s2]);
-            uint32_t s = b[0], ss = __umul24(b[0], b[0]), sx = __umul24(av[0], b[0]);
+                for (int k = 0; k < NP; ++k) {
+                    const uint32_t ap = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a0s[k]);
+                    s = 2 * k + 1 < NS ? s + b[2 * k] + b[2 * k + 1] : s + b[2 * k];
+                    ss = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bp[k]), __builtin_bit_cast(us2, bp[k]), ss, false);
+                    sx = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, ap), __builtin_bit_cast(us2, bp[k]), sx, false);
+                }
+            } else {
 #pragma unroll
-            for (int s2 = 1; s2 < NS; ++s2) {
-                s += b[s2];
-                ss = __umul24(b[s2], b[s2]) + ss;
-                sx = __umul24(av[s2], b[s2]) + sx;
+                for (int s2 = 0; s2 < NS; ++s2)
+                    av[s2] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a0s[s2]);
+                s = b[0];
+                ss = __umul24(b[0], b[0]);
+                sx = __umul24(av[0], b[0]);
+#pragma unroll
+                for (int s2 = 1; s2 < NS; ++s2) {
+                    s += b[s2];
+                    ss = __umul24(b[s2], b[s2]) + ss;
+                    sx = __umul24(av[s2], b[s2]) + sx;
+                }
             }
             if (!kGrad) {
                 // four partial sums per moment (DPP within rows of 16 down to

@@ -72,6 +72,7 @@ def main():
     B = 4 * NP
     work = torch.empty(B * N.PATCH_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
     accept = torch.empty(B, dtype=torch.uint8, device="cuda")
+    base = None  # the first variant's accepted set: paired quality on the intersection
     for var in a.variants.split(";"):
         fo = dp.FastOptions()
         for kv in filter(None, var.split(",")):
@@ -93,7 +94,17 @@ def main():
         out = np.frombuffer(work.cpu().numpy().tobytes(), dtype=N.PATCH_DTYPE)
         acc = accept.cpu().numpy()
         kms = float(np.mean(ms))
-        print(json.dumps({"variant": var, "cell": a.cell, "Mpatches_per_s": round(B / kms / 1e3, 3),
+        if base is None:
+            base = (out.copy(), acc.copy())
+        both = (acc == 1) & (base[1] == 1)
+        z, _ = synth.surface(cfg, out["pos"][both][:, :2].astype(np.float64))
+        zb, _ = synth.surface(cfg, base[0]["pos"][both][:, :2].astype(np.float64))
+        paired = {"n": int(both.sum()),
+                  "median_abs_dz": round(float(np.median(np.abs(out["pos"][both][:, 2] - z))), 6),
+                  "baseline_median_abs_dz": round(float(np.median(np.abs(base[0]["pos"][both][:, 2] - zb))), 6)}
+        refined = out["evals"] > 1
+        print(json.dumps({"variant": var, "paired_with_first": paired,
+                          "all_refined": quality(cfg, out, refined.astype(np.uint8)), "cell": a.cell, "Mpatches_per_s": round(B / kms / 1e3, 3),
                           "kernel_ms": round(kms, 3), "E": round(st["evals"] / max(st["patches"], 1), 3),
                           "views_per_eval": round(st["view_evals"] / max(st["evals"], 1), 3),
                           "accept_rate": round(float(acc.mean()), 4), "quality": quality(cfg, out, acc)}), flush=True)
