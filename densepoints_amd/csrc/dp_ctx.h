@@ -162,7 +162,7 @@ struct dp_ctx {
     // seed generation (Features::Matcher, dp_seeds.hip)
     dp_seedgen *seeds = nullptr;
     // performance mode (dp_fast.hip): options and the fp16 gray planes of one level
-    dp_fast_options fopt{4, 2, 6656, 32, 0.5f, 1.0f, 0, 0}; // = dp_default_fast_options (tests/test_gpu_fast.py)
+    dp_fast_options fopt{4, 2, 6656, 8, 0.5f, 1.0f, 0, 0, 32}; // = dp_default_fast_options (tests/test_gpu_fast.py)
     void *gray_pool = nullptr; // __half planes, pitch = width rounded up to 64
     size_t gray_cap = 0;       // elements
     void *d_gray = nullptr;    // device GrayPlane table

@@ -431,7 +431,7 @@ __device__ __forceinline__ Rect tile_rect(const Geo &g, int W, int H, int M)
 // views, margin, the views' records and tiles into the arena.  Returns m
 // (uniform); record r describes the view of rank r.
 template <int kArena>
-__device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned long long &staged_bytes,
+__device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, int fmv, unsigned long long &staged_bytes,
                      unsigned long long &clipped)
 {
     const int lane = lane_id();
@@ -449,7 +449,6 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
     }
     wave_sync();
     const int nconsider = nvis < 64 ? nvis : 64;
-    const int fmv = DP_FKARG(int32_t, fo.max_views);
     const int maxv = fmv < kFastMaxV ? fmv : kFastMaxV;
     const int view = lane < nconsider ? (int)L.vlist[lane] : 0;
     const FastCam &cam = a.cams[view];
@@ -546,6 +545,14 @@ __device__ int stage(const FastArgs &a, FastLds<kArena> &L, int margin, unsigned
     wave_sync();
     TMARK(L, 4);
     return m;
+}
+
+// staged-view cap of the scoring evaluations (filter, FAST_EVAL): spec v5's
+// filter_max_views, 0 = max_views
+__device__ __forceinline__ int filter_views(const FastArgs &a)
+{
+    const int f = DP_FKARG(int32_t, fo.filter_max_views);
+    return f > 0 ? f : DP_FKARG(int32_t, fo.max_views);
 }
 
 // Per-lane sample slots of a view pass (fixed per launch).  A pass of G views
@@ -1496,7 +1503,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
             TMARK(L, 1);
             if (kMode == DP_MODE_FAST_EVAL) {
                 const bool degen = L.F.degenerate != 0;
-                const int m = degen ? 0 : stage(a, L, 0, wave_bytes, wave_clip);
+                const int m = degen ? 0 : stage(a, L, 0, filter_views(a), wave_bytes, wave_clip);
                 p.evals += 1;
                 if (degen)
                     p.flags |= DP_PATCH_DEGENERATE;
@@ -1518,7 +1525,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
                     p.score = -1.0f;
                     rejected = true;
                 } else {
-                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), wave_bytes, wave_clip);
+                    const int m = stage(a, L, min(a.fo.margin, kFastMaxMargin), DP_FKARG(int32_t, fo.max_views),
+                                        wave_bytes, wave_clip);
                     if (m >= 2) {
                         const int E = cg_refine<G, NS, kTail, kMask, kArena, kMode == kFastRefineGrad>(a, L, sl, m);
                         TMARK(L, 5);
@@ -1557,7 +1565,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
                     wave_sync();
                     TMARK(L, 7);
                     const bool degen = L.F.degenerate != 0;
-                    const int m = degen ? 0 : stage(a, L, 0, wave_bytes, wave_clip);
+                    const int m = degen ? 0 : stage(a, L, 0, filter_views(a), wave_bytes, wave_clip);
                     p.evals += 1;
                     if (degen)
                         p.flags |= DP_PATCH_DEGENERATE;
@@ -1768,9 +1776,11 @@ int fast_check_options(dp_ctx *c, const dp_fast_options &f)
     if (f.iters < 0 || f.iters > 64 || f.margin < 0 || f.margin > dpk::kFastMaxMargin || f.tile_budget < 64 ||
         f.tile_budget > kFastBudget || f.max_views < 2 || f.max_views > dpk::kFastMaxV ||
         !(f.fd_step >= 0x1p-20f && f.fd_step <= 0x1p+20f) || !(f.ls_step > 0.0f && f.ls_step <= 0x1p+20f) ||
-        (f.densify != 0 && f.densify != 1) || (f.gradient != 0 && f.gradient != 1))
+        (f.densify != 0 && f.densify != 1) || (f.gradient != 0 && f.gradient != 1) ||
+        (f.filter_max_views != 0 && (f.filter_max_views < 2 || f.filter_max_views > dpk::kFastMaxV)))
         return fail(c, DP_E_ARG, "dp_fast_options out of range (margin <= 7, tile_budget <= 16384, 2 <= max_views "
-                                 "<= 32, fd_step in [2^-20, 2^20], 0 < ls_step <= 2^20, gradient 0 or 1)");
+                                 "<= 32, fd_step in [2^-20, 2^20], 0 < ls_step <= 2^20, gradient 0 or 1, "
+                                 "filter_max_views 0 or 2..32)");
     return DP_OK;
 }
 
@@ -1958,11 +1968,12 @@ extern "C" void dp_default_fast_options(dp_fast_options *f)
     f->iters = 4;
     f->margin = 2;
     f->tile_budget = 6656; // 4 waves per SIMD (the 6.5 KiB arena); up to kFastBudget
-    f->max_views = dpk::kFastMaxV;
+    f->max_views = 8; // spec v5 (r05): the refine's views keep their tile margin (was 32)
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;
     f->densify = 0;
     f->gradient = 0;
+    f->filter_max_views = dpk::kFastMaxV; // the filter scores every view that fits the budget
 }
 
 extern "C" int dp_set_fast_options(dp_ctx *c, const dp_fast_options *f)

@@ -49,11 +49,12 @@ class FastOptions:
     iters: int = 4            # CG iterations: E <= 1 + 3 iters (gradient 1) / 1 + 5 iters (0), +1 filter evaluation
     margin: int = 2           # tile margin around the initial window, pixels (<= 7)
     tile_budget: int = 6656   # LDS bytes per patch: tiles + 64 per view (<= 16384; <= 6656: 4 waves/SIMD)
-    max_views: int = 32       # staged views per patch (<= 32)
+    max_views: int = 8        # staged views of the refine (<= 32; spec v5, was 32)
     fd_step: float = 0.5      # forward-difference step, scaled units (gradient 0)
     ls_step: float = 1.0      # initial line-search step, scaled units
     densify: int = 0          # 1: dp_densify expands with the fast refine
     gradient: int = 0         # 0: forward differences (spec v3); 1: analytic gradient (spec v4)
+    filter_max_views: int = 32  # staged views of the filter / FAST_EVAL scoring (0 = max_views; spec v5)
 
     def to_c(self) -> N.DpFastOptions:
         o = N.DpFastOptions()

@@ -511,7 +511,7 @@ typedef struct dp_fast_options {
     int32_t margin;       /* 2     tile margin around the initial window, px       */
     int32_t tile_budget;  /* 6656  bytes of LDS tiles per patch (<= 16384; the
                                    kernel's arena is 6, 8 or 16 KiB by this value) */
-    int32_t max_views;    /* 32    staged views per patch (<= 32)                   */
+    int32_t max_views;    /* 8     staged views of the refine (<= 32; r04: 32)      */
     float fd_step;        /* 0.5   forward-difference step, scaled units (gradient 0) */
     float ls_step;        /* 1.0   initial line-search step, scaled units           */
     int32_t densify;      /* 0     1: dp_densify runs the seed stage (at
@@ -521,6 +521,12 @@ typedef struct dp_fast_options {
     int32_t gradient;     /* 0     0: forward differences (spec v3), 1: analytic
                                    gradient (spec v4: better children from
                                    refined parents, worse from raw ones)          */
+    int32_t filter_max_views; /* 32 staged views of the scoring evaluations (the
+                                   filter after the refine, DP_MODE_FAST_EVAL);
+                                   0 = max_views.  Spec v5 (r05): the refine
+                                   stages at most max_views (default 8) so that
+                                   its tiles keep their margin; the filter
+                                   scores every view that fits the budget      */
 } dp_fast_options;
 
 void dp_default_fast_options(dp_fast_options *fo);

@@ -62,10 +62,18 @@ void or_fast_default_options(or_fast_options *f)
     f->iters = 4;
     f->margin = 2;
     f->tile_budget = 6656;
-    f->max_views = FAST_MAX_VIEWS;
+    f->max_views = 8; /* spec v5: the refine's staged views (was 32) */
     f->fd_step = 0.5f;
     f->ls_step = 1.0f;
     f->gradient = 0;
+    f->filter_max_views = FAST_MAX_VIEWS; /* the scoring stagings' views */
+}
+
+/* spec v5: the scoring stagings (the filter, FAST_EVAL) stage up to
+ * filter_max_views views (0 = max_views), the refine up to max_views */
+static inline int filter_views(const or_fast_options *fo)
+{
+    return fo->filter_max_views > 0 ? fo->filter_max_views : fo->max_views;
 }
 
 /* BGR2GRAY on 8U (the parity spec's 14-bit fixed point); the product stores
@@ -270,7 +278,7 @@ static void tile_rect(const or_view *v, const fast_geo *g, int M, fast_view *t)
  * view count.
  */
 static int fast_stage(const or_scene *s, const or_patch *p, int cell, const or_fast_options *fo, int margin,
-                      fast_patch *fp)
+                      int max_views, fast_patch *fp)
 {
     memset(fp, 0, sizeof(*fp));
     if (!fast_frame(s, p, cell, fp)) {
@@ -282,7 +290,7 @@ static int fast_stage(const or_scene *s, const or_patch *p, int cell, const or_f
     int nvis = decode_mask(p->vis, vis);
     fast_geo geo[FAST_MAX_VIEWS];
     int m = 0;
-    const int maxv = fo->max_views < FAST_MAX_VIEWS ? fo->max_views : FAST_MAX_VIEWS;
+    const int maxv = max_views < FAST_MAX_VIEWS ? max_views : FAST_MAX_VIEWS;
     /* the first 64 visible views are considered (one wavefront lane each) */
     for (int i = 0; i < nvis && i < 64 && m < maxv; ++i) {
         fast_geo g;
@@ -723,7 +731,7 @@ static int fast_cg(const fast_patch *fp, int cell, double dmin0, const or_fast_o
 static int fast_filter(const or_scene *s, or_patch *p, int cell, const or_fast_options *fo)
 {
     fast_patch fp;
-    fast_stage(s, p, cell, fo, 0, &fp);
+    fast_stage(s, p, cell, fo, 0, filter_views(fo), &fp);
     p->evals += 1;
     if (fp.degenerate) p->flags |= OR_FLAG_DEGENERATE;
     if (fp.m < 2) {
@@ -793,7 +801,7 @@ static void fast_init_related(const or_scene *s, or_patch *p)
 static int fast_refine_one(const or_scene *s, or_patch *p, int cell, const or_fast_options *fo)
 {
     fast_patch fp;
-    fast_stage(s, p, cell, fo, fo->margin < 7 ? fo->margin : 7, &fp);
+    fast_stage(s, p, cell, fo, fo->margin < 7 ? fo->margin : 7, fo->max_views, &fp);
     if (fp.degenerate) {
         p->flags |= OR_FLAG_DEGENERATE;
         p->flags &= (uint8_t)~OR_FLAG_ACCEPTED;
@@ -824,7 +832,7 @@ static int fast_refine_one(const or_scene *s, or_patch *p, int cell, const or_fa
 static int fast_eval_one(const or_scene *s, or_patch *p, int cell, const or_fast_options *fo)
 {
     fast_patch fp;
-    fast_stage(s, p, cell, fo, 0, &fp);
+    fast_stage(s, p, cell, fo, 0, filter_views(fo), &fp);
     p->evals += 1;
     if (fp.degenerate) p->flags |= OR_FLAG_DEGENERATE;
     int ok = fp.m >= 2;
@@ -848,7 +856,7 @@ int or_fast_grad_probe(const or_scene *s, const or_patch *p, int cell, const or_
                        float g[3])
 {
     fast_patch fp;
-    fast_stage(s, p, cell, fo, 0, &fp);
+    fast_stage(s, p, cell, fo, 0, fo->max_views, &fp);
     const float x[3] = {0.0f, 0.0f, 0.0f};
     g[0] = g[1] = g[2] = 0.0f;
     *f = fp.degenerate ? 0 : fast_objective_grad(&fp, cell, s->opt.ncc_denom_min, x, g);

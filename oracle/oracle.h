@@ -79,6 +79,7 @@ typedef struct or_fast_options {
     float ls_step;        /* initial line-search step, scaled units          */
     int32_t densify;      /* product only: fast expansions in dp_densify     */
     int32_t gradient;     /* 0: forward differences (spec v3), 1: analytic gradient (v4) */
+    int32_t filter_max_views; /* staged views of the scoring stagings (filter, FAST_EVAL); 0 = max_views (v5) */
 } or_fast_options;
 
 #ifdef __cplusplus

@@ -65,6 +65,7 @@ class OrFastOptions(ctypes.Structure):
         ("ls_step", ctypes.c_float),
         ("densify", ctypes.c_int32),
         ("gradient", ctypes.c_int32),
+        ("filter_max_views", ctypes.c_int32),
     ]
 
 

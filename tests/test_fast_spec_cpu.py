@@ -166,7 +166,10 @@ def _fast_eval_numpy(orc, S, P, imgs, p, cell, fo, grad=False):
         x0, y0 = max(xa, 0) & ~1, max(ya, 0)  # even left edge (32-bit fp16 pairs on the device)
         tw, th = min(xb, Ww - 1) - x0 + 1, min(yb, Hh - 1) - y0 + 1
         staged.append((v, g, x0, y0, tw, th, 4 * ((tw + 2) // 2) * (th + 1) + 64))
-        if len(staged) == fo.max_views:
+        # spec v5: the scoring staging (FAST_EVAL) takes up to filter_max_views
+        # views (0 = max_views), the refine's (the gradient probe) max_views
+        cap = fo.max_views if grad else (fo.filter_max_views or fo.max_views)
+        if len(staged) == cap:
             break
     tot, keep = 0, []
     for t in staged:

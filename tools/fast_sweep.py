@@ -107,6 +107,7 @@ def main():
                           "all_refined": quality(cfg, out, refined.astype(np.uint8)), "cell": a.cell, "Mpatches_per_s": round(B / kms / 1e3, 3),
                           "kernel_ms": round(kms, 3), "E": round(st["evals"] / max(st["patches"], 1), 3),
                           "views_per_eval": round(st["view_evals"] / max(st["evals"], 1), 3),
+                          "clipped_stagings_per_patch": round(st["clipped_stagings"] / max(st["patches"], 1), 4),
                           "accept_rate": round(float(acc.mean()), 4), "quality": quality(cfg, out, acc)}), flush=True)
     eng.close()
 
