@@ -36,7 +36,7 @@ def geometry(cfg, p):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg4_64view_4k")
-    ap.add_argument("--variants", default="0:4,1:4,0:3,1:3", help="gradient:iters,...")
+    ap.add_argument("--variants", default="0:4,1:4,0:3,1:3", help="gradient:iters[:max_views],...")
     a = ap.parse_args()
     import densepoints_amd as dp
     from densepoints_amd import _native as N
@@ -57,8 +57,10 @@ def main():
         eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
         seeds = synth.seeds(cfg, P)
         for v in a.variants.split(","):
-            gr, it = (int(x) for x in v.split(":"))
-            eng.set_fast_options(dp.FastOptions(densify=1, gradient=gr, iters=it))
+            f = [int(x) for x in v.split(":")]
+            gr, it = f[0], f[1]
+            mv = f[2] if len(f) > 2 else dp.FastOptions().max_views
+            eng.set_fast_options(dp.FastOptions(densify=1, gradient=gr, iters=it, max_views=mv))
             eng.densify(seeds)  # warm-up (gray planes, clocks)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -66,7 +68,7 @@ def main():
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3
             keep = eng.filter_patches(np.ascontiguousarray(pat)) == 1
-            print(json.dumps({"config": a.config, "gradient": gr, "iters": it, "densify_ms": round(ms, 2),
+            print(json.dumps({"config": a.config, "gradient": gr, "iters": it, "max_views": mv, "densify_ms": round(ms, 2),
                               "candidates": int(st["seeds_in"]) + int(st["candidates"]),
                               "all": geometry(cfg, pat), "filter_kept": geometry(cfg, pat[keep])}), flush=True)
         eng.set_fast_options(dp.FastOptions())
