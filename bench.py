@@ -256,6 +256,9 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
+        "scaling_note": "value at every N is the config-3 refine batch, weak-scaled (N x batch_per_gpu "
+                        "candidates, no data-path collective); BASELINE.md's config-4 strong-scaling densify "
+                        "(super-tile partition + RCCL all-gather) is scaling_leg.{parity,fast}.Mpatches_per_s",
         "vs_baseline": None,
         "dtype": "u8 gray texels in LDS (fp16 planes), fp32 sampling, int32 moments, fp64 CG" if fast else
                  "u8 texels, fp64 geometry, int32 moments",
