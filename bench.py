@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--fast-gradients", default="0,1",
                     help="perf_mode refine specs: 0 = forward differences (v3, the default), 1 = the analytic "
                          "gradient (v4; keys *_an)")
+    ap.add_argument("--fast-extra-max-views", default="6",
+                    help="perf_mode speed points: the default spec with the refine's view cap lowered to each "
+                         "value (keys n*_mv<k>, headline parents)")
     ap.add_argument("--no-fast", action="store_true", help="skip the perf_mode sub-object")
     ap.add_argument("--seed-stride", type=float, default=32.0, help="synthetic seed grid stride (px)")
     ap.add_argument("--densify-protocol", choices=["r05", "r04"], default="r05",
@@ -592,9 +595,12 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
     budgets = [int(b) for b in args.fast_budgets.split(",") if b] or [None]
     margins = [int(b) for b in args.fast_margins.split(",") if b] or [None]
     grads = [int(x) for x in args.fast_gradients.split(",") if x]
-    combos = [(int(c), b, mg, ps, gr) for gr in grads for ps in ("", "_fast_seeds") for c in args.fast_cells.split(",")
-              if c for b in budgets for mg in margins]
-    for cell, tb, mg, pset, gr in combos:
+    combos = [(int(c), b, mg, ps, gr, None) for gr in grads for ps in ("", "_fast_seeds")
+              for c in args.fast_cells.split(",") if c for b in budgets for mg in margins]
+    # speed points: the default spec with a smaller refine view cap (keys n*_mv<k>)
+    combos += [(int(c), None, None, "", grads[0], int(mv)) for mv in args.fast_extra_max_views.split(",") if mv
+               for c in args.fast_cells.split(",") if c]
+    for cell, tb, mg, pset, gr, mv in combos:
         d_par = d_fparents if pset else d_parents
         fo = dp.FastOptions()
         if tb:
@@ -604,6 +610,8 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
         if args.fast_iters is not None:
             fo.iters = args.fast_iters
         fo.gradient = gr
+        if mv is not None:
+            fo.max_views = mv
         eng.set_fast_options(fo)
         eng.set_options(dp.Options(expand_cell_size=cell))
         # untimed warm-up launches (the clocks settle over the first ~15 ms of a new launch shape)
@@ -637,9 +645,10 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                           "bytes_per_launch_algorithmic": alg, "bytes_per_launch_compulsory": comp,
                           "compulsory_GBps": round(comp / kms / 1e6, 2)},
              "quality": quality(cfg, out, acc), "stats": {k: int(v) for k, v in st.items()},
-             "fast_options": {k: getattr(fo, k) for k in ("iters", "margin", "tile_budget", "max_views", "gradient")}}
+             "fast_options": {k: getattr(fo, k) for k in ("iters", "margin", "tile_budget", "max_views", "gradient",
+                                                          "filter_max_views")}}
         fprof = profiled("fast%d" % cell, fast_kernel_tag(cell, gr), B, lib_stamp(N.LIB_PATH)) \
-            if not pset and fo.tile_budget == 6656 and fo.iters == 4 and gr == 0 else None
+            if not pset and fo.tile_budget == 6656 and fo.iters == 4 and gr == 0 and mv is None else None
         if fprof:
             attach_profile(r["roofline"], fprof, B, kms)
         if not args.no_cpu and not pset and gr == grads[0]:
@@ -662,7 +671,8 @@ def perf_mode(eng, args, cfg, stream, d_parents, NP, work, accept, parity_out, p
                                                                         for f in fields) and
                                                                     np.array_equal(kacc, acc[: 4 * n]))}
         res["n%d" % cell + ("_b%d" % tb if tb and len(budgets) > 1 else "") +
-            ("_m%d" % mg if mg is not None and len(margins) > 1 else "") + pset + ("_an" if gr == 1 else "")] = r
+            ("_m%d" % mg if mg is not None and len(margins) > 1 else "") + pset + ("_an" if gr == 1 else "") +
+            ("_mv%d" % mv if mv is not None else "")] = r
     eng.set_options(dp.Options(expand_cell_size=args.cell))
     eng.set_fast_options(dp.FastOptions())
     return res

@@ -128,7 +128,9 @@ def test_fast_modes_bit_exact(engine, orc, cell, mode, gradient):
 @pytest.mark.parametrize("opts", [dict(), dict(iters=0), dict(iters=1), dict(iters=7, margin=7),
                                   dict(margin=0, tile_budget=2048), dict(max_views=3, ls_step=2.0),
                                   dict(gradient=0), dict(gradient=0, iters=7, margin=7),
-                                  dict(gradient=0, max_views=3, fd_step=0.25, ls_step=2.0)])
+                                  dict(gradient=0, max_views=3, fd_step=0.25, ls_step=2.0),
+                                  dict(max_views=6), dict(filter_max_views=0),
+                                  dict(max_views=6, filter_max_views=12)])
 def test_fast_expand_bit_exact_options(orc, opts):
     sc = scene("hf6")
     S = orc.Scene(sc.P, sc.imgs)
