@@ -143,6 +143,8 @@ class DpMatcherOptions(ctypes.Structure):
         ("max_epipolar_distance", ctypes.c_float),
         ("nn_match_ratio", ctypes.c_float),
         ("matcher_type", ctypes.c_int32),
+        ("detector_type", ctypes.c_int32),
+        ("akaze_threshold", ctypes.c_float),
     ]
 
 
@@ -242,6 +244,8 @@ SIGNATURES = [
     ("dp_seed_keypoints", _I, [_P, _I, _P, _P, _P]),
     ("dp_seed_matches", _I, [_P, _I, _P, _P, _P, _P]),
     ("dp_knn_match", _I, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P]),
+    ("dp_knn_match_wide", _I, [_P, _P, ctypes.c_int64, _P, ctypes.c_int64, _I, _P, _P]),
+    ("dp_seed_descriptor_bytes", _I, [_P]),
     ("dp_fundamental_matrix", _I, [_P, _P, _P]),
     ("dp_triangulate", _I, [_P, ctypes.c_int64, _P, _P, _P, _P]),
     ("dp_synth_default", None, [_P]),

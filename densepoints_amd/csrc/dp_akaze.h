@@ -1,0 +1,107 @@
+// dp_akaze.h -- AKAZE keypoints and M-LDB descriptors on the device
+// (Matcher::DetectKeypoints / ComputeDescriptors with DetectorType::AKAZE,
+// modules/features/matcher.cpp:56-60, 166-170: cv::AKAZE::create() defaults).
+// The arithmetic is oracle/or_akaze.c's, stated in its header and DESIGN.md
+// ("Seed generation"); every launch covers all views of a chunk
+// (blockIdx.z = view), one launch per evolution level and filter pass.
+#pragma once
+
+#include "dp_internal.h"
+
+namespace dpk {
+
+constexpr int kAkLevels = 16;        // 4 octaves x 4 sublevels
+constexpr int kAkMaxFed = 64;        // FED steps per level (29 at most for the defaults)
+constexpr int kAkDescWords = 16;     // 486 bits in 64 bytes
+constexpr int kAkBits = 486;
+
+// one (view, level) of a chunk: Lt, Lx, Ly, Ldet at off + {0, 1, 2, 3} w h
+// floats of the plane pool; w = 0 where the view has no such level
+struct AkPlane {
+    int64_t off;
+    int64_t det_base;    // first index of this Ldet plane in the chunk's pixel index space
+    int32_t w, h, octave, sigma_size;
+    float esigma;
+    int32_t pad;
+};
+
+// per view of a chunk: five level-0-sized temporaries at tmp + k n0
+struct AkView {
+    const uint32_t *bgra;  // level-0 BGRA8 plane
+    int32_t pitch, w0, h0, view;
+    int64_t tmp, n0;
+};
+
+struct AkArgs {
+    const AkPlane *planes; // chunk views x kAkLevels
+    const AkView *views;
+    float *pool, *tmp;
+    uint32_t *hmax;        // per view: max gradient magnitude (float bits)
+    uint32_t *hist;        // per view: 300 bins + npoints (301 words)
+    float *k0;             // per view: contrast factor of level 0
+};
+
+// plane selectors: level planes and view temporaries
+enum AkSel { kLt = 0, kLx = 1, kLy = 2, kLdet = 3, kT0 = 4, kT1 = 5, kT2 = 6, kT3 = 7, kT4 = 8 };
+
+struct AkTaps {
+    float w[16];
+    int32_t n;       // dense Gaussian taps (mode 0)
+    int32_t mode;    // 0 Gaussian (replicate), 1 3-tap derivative, 2 3-tap smoothing (reflect-101)
+    int32_t spacing; // 3-tap spacing; < 0: the level's sigma_size
+    int32_t pad;
+};
+
+hipError_t launch_akz_gray(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_conv(const AkArgs &a, int level, int src, int dst, int dir, const AkTaps &t, int nv,
+                           int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_half(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_copy(const AkArgs &a, int level, int src, int dst, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float tau, int nv, int max_w, int max_h,
+                          hipStream_t s);
+hipError_t launch_akz_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_flag(const AkArgs &a, int level, float thr, uint8_t *flag, int nv, int max_w, int max_h,
+                           hipStream_t s);
+
+// candidate list (sorted global Ldet indices) -> keypoints (suppression +
+// subpixel refinement), keep flags
+struct AkCandArgs {
+    const AkPlane *planes;
+    const float *pool;
+    const int64_t *cand;
+    int64_t n;
+    const int32_t *plane_ids;   // existing planes sorted by det_base
+    const int64_t *plane_base;  // their det_base
+    int32_t n_planes;
+    const int32_t *view_ids;    // chunk view -> global view
+    dp_keypoint *kp;
+    int32_t *kv;
+    uint8_t *keep;
+};
+hipError_t launch_akz_candidates(const AkCandArgs &a, hipStream_t s);
+
+// orientation + M-LDB of filtered keypoints (one wave each)
+struct AkDescArgs {
+    const AkPlane *planes;
+    const float *pool;
+    const int32_t *kv;          // per keypoint: global view; chunk-local = kv - v0
+    int32_t v0;
+    dp_keypoint *kp;            // angle written (degrees)
+    int64_t n;
+    const float *g25;           // 7 x 7
+    const uint32_t *bit_pairs;  // kAkBits: cell a | cell b << 8 | channel << 16
+    int32_t n_windows;          // orientation windows (a1 = 0, 0.15, ... < 2 pi)
+    uint32_t *desc;             // kAkDescWords per keypoint
+};
+hipError_t launch_akz_describe(const AkDescArgs &a, hipStream_t s);
+
+// host helpers (the same arithmetic as oracle/or_akaze.c's host-side parts)
+int akaze_gauss_kernel(float sigma, float *w);
+int akaze_fed_tau(float T, float tau_max, float *tau);
+void akaze_g25(float *g);             // 49
+void akaze_bit_pairs(uint32_t *pairs); // kAkBits
+int akaze_windows();
+
+} // namespace dpk

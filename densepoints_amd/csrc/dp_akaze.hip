@@ -1,0 +1,730 @@
+// dp_akaze.hip -- AKAZE (cv::AKAZE::create() defaults) on the device for
+// Matcher's DetectorType::AKAZE (modules/features/matcher.cpp:56-60,
+// 166-170): the nonlinear scale space (FED diffusion with the g2
+// conductance), the Hessian-determinant detector, orientation and the full
+// M-LDB descriptor.  Every float expression is one IEEE rounding in the order
+// oracle/or_akaze.c writes it (-ffp-contract=off), so the two agree bit for
+// bit; the restated semantics and where they leave OpenCV are in that file's
+// header.
+//
+// Layout: per chunk of views, one float pool of (view, level) planes Lt, Lx,
+// Ly, Ldet (row-major, pitch = level width) and five level-0-sized
+// temporaries per view.  The image filters are memory-bound streaming passes
+// (one pixel per lane, coalesced rows, the 3- to 9-tap neighbourhood from
+// L1/L2); the per-keypoint orientation and descriptor run one wave each, with
+// the 109 orientation samples, the 42 window sums and the 29 M-LDB cells
+// spread over its lanes.
+#include "dp_akaze.h"
+#include "dp_detmath.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace dpk {
+
+namespace {
+
+__device__ __forceinline__ float *ak_ptr(const AkArgs &a, int z, int level, int sel)
+{
+    if (sel < kT0) {
+        const AkPlane &p = a.planes[z * kAkLevels + level];
+        return a.pool + p.off + (int64_t)sel * ((int64_t)p.w * p.h);
+    }
+    const AkView &v = a.views[z];
+    return a.tmp + v.tmp + (int64_t)(sel - kT0) * v.n0;
+}
+
+__device__ __forceinline__ int ak_rep(int i, int n) { return i < 0 ? 0 : (i >= n ? n - 1 : i); }
+
+__device__ __forceinline__ int ak_r101(int i, int n)
+{
+    if (n == 1)
+        return 0;
+    if (i < 0)
+        i = -i;
+    if (i >= n)
+        i = 2 * (n - 1) - i;
+    return i;
+}
+
+} // namespace
+
+// cvtColor(BGR2GRAY) fixed point, then x (1/255.f): view temporary T0
+__global__ void akz_gray_kernel(AkArgs a)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkView v = a.views[z];
+    if (x >= v.w0 || y >= v.h0)
+        return;
+    const uint32_t p = v.bgra[(size_t)y * v.pitch + x];
+    const uint32_t b = p & 255u, g = (p >> 8) & 255u, r = (p >> 16) & 255u;
+    const uint32_t gray = (b * 1868u + g * 9617u + r * 4899u + 8192u) >> 14;
+    const float inv255 = 1.0f / 255.0f;
+    a.tmp[v.tmp + (size_t)y * v.w0 + x] = (float)gray * inv255;
+}
+
+hipError_t launch_akz_gray(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_gray_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// one separable pass along x (dir 0) or y (dir 1) of plane src into dst:
+// mode 0 the dense Gaussian (replicate), 1 / 2 the 3-tap derivative /
+// smoothing at spacing s (reflect-101)
+__global__ void akz_conv_kernel(AkArgs a, int level, int src, int dst, int dir, AkTaps t)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int w = P.w, h = P.h;
+    if (w == 0 || x >= w || y >= h)
+        return;
+    const float *S = ak_ptr(a, z, level, src);
+    float *D = ak_ptr(a, z, level, dst);
+    float out;
+    if (t.mode == 0) {
+        const int r = t.n / 2;
+        if (dir == 0) {
+            const float *row = S + (size_t)y * w;
+            float acc = t.w[0] * row[ak_rep(x - r, w)];
+            for (int k = 1; k < t.n; ++k)
+                acc = acc + t.w[k] * row[ak_rep(x + k - r, w)];
+            out = acc;
+        } else {
+            float acc = t.w[0] * S[(size_t)ak_rep(y - r, h) * w + x];
+            for (int k = 1; k < t.n; ++k)
+                acc = acc + t.w[k] * S[(size_t)ak_rep(y + k - r, h) * w + x];
+            out = acc;
+        }
+    } else {
+        const int sp = t.spacing > 0 ? t.spacing : P.sigma_size;
+        float va, vb, vc;
+        if (dir == 0) {
+            const float *row = S + (size_t)y * w;
+            va = row[ak_r101(x - sp, w)];
+            vb = row[x];
+            vc = row[ak_r101(x + sp, w)];
+        } else {
+            va = S[(size_t)ak_r101(y - sp, h) * w + x];
+            vb = S[(size_t)y * w + x];
+            vc = S[(size_t)ak_r101(y + sp, h) * w + x];
+        }
+        if (t.mode == 1) {
+            out = vc - va;
+        } else {
+            float k0 = t.w[0], k1 = t.w[1];
+            if (t.spacing <= 0) {
+                // normalised Scharr smoothing of scale s: (1, 10/3, 1) / (2 s (10/3 + 2))
+                const float wgt = 10.0f / 3.0f;
+                k0 = 1.0f / (2.0f * (float)sp * (wgt + 2.0f));
+                k1 = wgt * k0;
+            }
+            out = (k0 * va + k1 * vb) + k0 * vc;
+        }
+    }
+    D[(size_t)y * w + x] = out;
+}
+
+hipError_t launch_akz_conv(const AkArgs &a, int level, int src, int dst, int dir, const AkTaps &t, int nv,
+                           int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_conv_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, src, dst,
+                       dir, t);
+    return hipGetLastError();
+}
+
+// compute_k_percentile (0.7, 300 bins) from the unnormalised Scharr gradient
+// of Gaussian(img, 1) in T2 (x) / T4 (y): the interior maximum, the histogram,
+// then one lane per view
+__global__ void akz_modg_max_kernel(AkArgs a)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkView v = a.views[z];
+    float m = 0.0f;
+    if (x >= 1 && x < v.w0 - 1 && y >= 1 && y < v.h0 - 1) {
+        const size_t i = (size_t)y * v.w0 + x;
+        const float lx = a.tmp[v.tmp + 2 * v.n0 + i], ly = a.tmp[v.tmp + 4 * v.n0 + i];
+        m = sqrtf(lx * lx + ly * ly);
+    }
+    // non-negative floats order as their bit patterns
+    uint32_t b = __float_as_uint(m);
+    for (int o = 32; o >= 1; o >>= 1)
+        b = max(b, (uint32_t)__shfl_xor((int)b, o));
+    if ((threadIdx.x & 63) == 0 && b)
+        atomicMax(&a.hmax[z], b);
+}
+
+__global__ void akz_hist_kernel(AkArgs a)
+{
+    __shared__ uint32_t h[301];
+    for (int i = threadIdx.x; i < 301; i += blockDim.x)
+        h[i] = 0;
+    __syncthreads();
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkView v = a.views[z];
+    const float hmax = __uint_as_float(a.hmax[z]);
+    if (hmax > 0.0f && x >= 1 && x < v.w0 - 1 && y >= 1 && y < v.h0 - 1) {
+        const size_t i = (size_t)y * v.w0 + x;
+        const float lx = a.tmp[v.tmp + 2 * v.n0 + i], ly = a.tmp[v.tmp + 4 * v.n0 + i];
+        const float m = sqrtf(lx * lx + ly * ly);
+        if (m != 0.0f) {
+            int bin = (int)floorf(300.0f * (m / hmax));
+            if (bin == 300)
+                bin--;
+            atomicAdd(&h[bin], 1u);
+            atomicAdd(&h[300], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 301; i += blockDim.x)
+        if (h[i])
+            atomicAdd(&a.hist[(size_t)z * 301 + i], h[i]);
+}
+
+__global__ void akz_kc_kernel(AkArgs a, int nv)
+{
+    const int z = blockIdx.x * blockDim.x + threadIdx.x;
+    if (z >= nv)
+        return;
+    const uint32_t *h = a.hist + (size_t)z * 301;
+    const float hmax = __uint_as_float(a.hmax[z]);
+    const int64_t npoints = h[300];
+    const int64_t nthr = (int64_t)((float)npoints * 0.7f);
+    int64_t nel = 0;
+    int k = 0;
+    for (k = 0; nel < nthr && k < 300; k++)
+        nel += h[k];
+    float kp = (nel < nthr || npoints == 0) ? 0.03f : hmax * ((float)k / 300.0f);
+    if (!(kp > 0.0f))
+        kp = 0.03f;
+    a.k0[z] = kp;
+}
+
+hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_modg_max_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(akz_hist_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(akz_kc_kernel, dim3((nv + 63) / 64), dim3(64), 0, s, a, nv);
+    return hipGetLastError();
+}
+
+// halfsample: the 2x2 box average of the previous level's Lt
+__global__ void akz_half_kernel(AkArgs a, int level)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &L = a.planes[z * kAkLevels + level];
+    if (L.w == 0 || x >= L.w || y >= L.h)
+        return;
+    const AkPlane &P = a.planes[z * kAkLevels + level - 1];
+    const float *r0 = a.pool + P.off + (size_t)(2 * y) * P.w + 2 * x, *r1 = r0 + P.w;
+    a.pool[L.off + (size_t)y * L.w + x] = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
+}
+
+hipError_t launch_akz_half(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_half_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
+    return hipGetLastError();
+}
+
+// copy a plane; src/dst selectors of `level`, except src = -1: the previous level's Lt
+__global__ void akz_copy_kernel(AkArgs a, int level, int src, int dst)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &L = a.planes[z * kAkLevels + level];
+    if (L.w == 0 || x >= L.w || y >= L.h)
+        return;
+    const float *S = src < 0 ? ak_ptr(a, z, level - 1, kLt) : ak_ptr(a, z, level, src);
+    ak_ptr(a, z, level, dst)[(size_t)y * L.w + x] = S[(size_t)y * L.w + x];
+}
+
+hipError_t launch_akz_copy(const AkArgs &a, int level, int src, int dst, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_copy_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, src, dst);
+    return hipGetLastError();
+}
+
+// g2 conductance into T4 from the unnormalised Scharr gradient in Lx / Ly;
+// k = k0 x 0.75 per octave, multiplied in order
+__global__ void akz_g2_kernel(AkArgs a, int level)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &L = a.planes[z * kAkLevels + level];
+    if (L.w == 0 || x >= L.w || y >= L.h)
+        return;
+    float k = a.k0[z];
+    for (int o = 0; o < L.octave; ++o)
+        k = k * 0.75f;
+    const float k2inv = 1.0f / (k * k);
+    const size_t i = (size_t)y * L.w + x;
+    const float lx = ak_ptr(a, z, level, kLx)[i], ly = ak_ptr(a, z, level, kLy)[i];
+    ak_ptr(a, z, level, kT4)[i] = 1.0f / (1.0f + k2inv * (lx * lx + ly * ly));
+}
+
+hipError_t launch_akz_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_g2_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
+    return hipGetLastError();
+}
+
+// one explicit FED step (zero flux across the border), conductance in T4:
+// dst = src + tau/2 ((xp - xn) + (yp - yn))
+__global__ void akz_fed_kernel(AkArgs a, int level, int src, int dst, float tau)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int w = P.w, h = P.h;
+    if (w == 0 || x >= w || y >= h)
+        return;
+    const float *L = ak_ptr(a, z, level, src), *c = ak_ptr(a, z, level, kT4);
+    const size_t i = (size_t)y * w + x;
+    const float l0 = L[i], c0 = c[i];
+    const float xp = x + 1 < w ? (c0 + c[i + 1]) * (L[i + 1] - l0) : 0.0f;
+    const float xn = x > 0 ? (c[i - 1] + c0) * (l0 - L[i - 1]) : 0.0f;
+    const float yp = y + 1 < h ? (c0 + c[i + w]) * (L[i + w] - l0) : 0.0f;
+    const float yn = y > 0 ? (c[i - w] + c0) * (l0 - L[i - w]) : 0.0f;
+    const float ht = 0.5f * tau;
+    ak_ptr(a, z, level, dst)[i] = l0 + ht * ((xp - xn) + (yp - yn));
+}
+
+hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float tau, int nv, int max_w, int max_h,
+                          hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_fed_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, src, dst,
+                       tau);
+    return hipGetLastError();
+}
+
+// Lx, Ly x s in place; Ldet from Lxx (T2), Lxy (T0), Lyy (T4), each x s^2
+__global__ void akz_det_kernel(AkArgs a, int level)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    if (P.w == 0 || x >= P.w || y >= P.h)
+        return;
+    const size_t i = (size_t)y * P.w + x;
+    const float fs = (float)P.sigma_size, fs2 = (float)(P.sigma_size * P.sigma_size);
+    float *lx = ak_ptr(a, z, level, kLx), *ly = ak_ptr(a, z, level, kLy);
+    lx[i] = lx[i] * fs;
+    ly[i] = ly[i] * fs;
+    const float xx = ak_ptr(a, z, level, kT2)[i] * fs2, yy = ak_ptr(a, z, level, kT4)[i] * fs2;
+    const float xy = ak_ptr(a, z, level, kT0)[i] * fs2;
+    ak_ptr(a, z, level, kLdet)[i] = xx * yy - xy * xy;
+}
+
+hipError_t launch_akz_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_det_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
+    return hipGetLastError();
+}
+
+// 3x3 maxima of Ldet above the threshold inside the descriptor border
+__global__ void akz_flag_kernel(AkArgs a, int level, float thr, uint8_t *flag)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int w = P.w, h = P.h;
+    if (w == 0 || x >= w || y >= h)
+        return;
+    uint8_t f = 0;
+    if (x >= 1 && x < w - 1 && y >= 1 && y < h - 1) {
+        const float *p = a.pool + P.off + 3 * ((int64_t)w * h) + (size_t)y * w + x;
+        const float v = p[0];
+        if (v > thr && v >= 0.00001f && v > p[-1] && v > p[1] && v > p[-w - 1] && v > p[-w] && v > p[-w + 1] &&
+            v > p[w - 1] && v > p[w] && v > p[w + 1]) {
+            const float sm = (10.0f * sqrtf(2.0f)) * (float)P.sigma_size;
+            const int lx = __float2int_rn((float)x - sm) - 1, rx = __float2int_rn((float)x + sm) + 1;
+            const int uy = __float2int_rn((float)y - sm) - 1, dy = __float2int_rn((float)y + sm) + 1;
+            f = lx >= 0 && rx < w && uy >= 0 && dy < h;
+        }
+    }
+    flag[P.det_base + (size_t)y * w + x] = f;
+}
+
+hipError_t launch_akz_flag(const AkArgs &a, int level, float thr, uint8_t *flag, int nv, int max_w, int max_h,
+                           hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_flag_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, thr, flag);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// candidates: scale-space suppression and subpixel refinement, one lane each
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t ak_lower(const int64_t *c, int64_t lo, int64_t hi, int64_t v)
+{
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (c[m] < v)
+            lo = m + 1;
+        else
+            hi = m;
+    }
+    return lo;
+}
+
+__global__ void akz_cand_kernel(AkCandArgs a)
+{
+    const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ci >= a.n)
+        return;
+    const int64_t g = a.cand[ci];
+    // the plane of g: the last existing plane with det_base <= g
+    int lo = 0, hi = a.n_planes - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.plane_base[mid] <= g)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const int pid = a.plane_ids[lo];
+    const int z = pid / kAkLevels, lev = pid % kAkLevels;
+    const AkPlane &P = a.planes[pid];
+    const int64_t li = g - P.det_base;
+    const int cy = (int)(li / P.w), cx = (int)(li - (int64_t)cy * P.w);
+    const float *det = a.pool + P.off + 3 * ((int64_t)P.w * P.h);
+    const float r = det[li];
+    const float ra = (float)(1 << P.octave);
+    const float S = P.esigma * 1.5f, S2 = S * S;
+    const float px = (float)cx * ra, py = (float)cy * ra;
+    bool drop = false;
+    for (int j = lev - 1; j <= lev + 1 && !drop; ++j) {
+        if (j < 0 || j >= kAkLevels)
+            continue;
+        const AkPlane &Q = a.planes[z * kAkLevels + j];
+        if (Q.w == 0)
+            continue;
+        const float rj = (float)(1 << Q.octave);
+        const int y0 = (int)floorf((py - S) / rj), y1 = (int)ceilf((py + S) / rj);
+        const int64_t qn = (int64_t)Q.w * Q.h;
+        const int64_t beg = ak_lower(a.cand, 0, a.n, Q.det_base), end = ak_lower(a.cand, beg, a.n, Q.det_base + qn);
+        const int64_t ylo = y0 < 0 ? 0 : (int64_t)y0 * Q.w;
+        const float *qdet = a.pool + Q.off + 3 * qn;
+        for (int64_t b = ak_lower(a.cand, beg, end, Q.det_base + ylo); b < end; ++b) {
+            const int64_t lb = a.cand[b] - Q.det_base;
+            const int by = (int)(lb / Q.w), bx = (int)(lb - (int64_t)by * Q.w);
+            if (by > y1)
+                break;
+            if (b == ci)
+                continue;
+            const float dx = px - (float)bx * rj, dy = py - (float)by * rj;
+            const float rb = qdet[lb];
+            if (dx * dx + dy * dy <= S2 && (rb > r || (rb == r && b < ci))) {
+                drop = true;
+                break;
+            }
+        }
+    }
+    uint8_t keep = 0;
+    if (!drop) {
+        const int w = P.w;
+        const float *p = det + li;
+        const float Dx = 0.5f * (p[1] - p[-1]), Dy = 0.5f * (p[w] - p[-w]);
+        const float Dxx = (p[1] + p[-1]) - 2.0f * p[0], Dyy = (p[w] + p[-w]) - 2.0f * p[0];
+        const float Dxy = 0.25f * (p[w + 1] + p[-w - 1]) - 0.25f * (p[-w + 1] + p[w - 1]);
+        const float dt = Dxx * Dyy - Dxy * Dxy;
+        if (dt != 0.0f) {
+            const float ox = (Dxy * Dy - Dx * Dyy) / dt, oy = (Dxy * Dx - Dy * Dxx) / dt;
+            if (fabsf(ox) <= 1.0f && fabsf(oy) <= 1.0f) {
+                dp_keypoint k;
+                k.x = ((float)cx + ox) * ra;
+                k.y = ((float)cy + oy) * ra;
+                k.response = r;
+                k.angle = 0.0f;
+                k.octave = P.octave;
+                k.reserved = lev;
+                a.kp[ci] = k;
+                a.kv[ci] = a.view_ids[z];
+                keep = 1;
+            }
+        }
+    }
+    a.keep[ci] = keep;
+}
+
+hipError_t launch_akz_candidates(const AkCandArgs &a, hipStream_t s)
+{
+    if (a.n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(akz_cand_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// orientation + M-LDB, one wave per keypoint
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float ak_atan2_deg(float y, float x)
+{
+    const float k = (float)(180.0 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+    float ax = fabsf(x), ay = fabsf(y), r, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)2.220446049250313e-16);
+        c2 = c * c;
+        r = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)2.220446049250313e-16);
+        c2 = c * c;
+        r = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0)
+        r = 180.f - r;
+    if (y < 0)
+        r = 360.f - r;
+    return r;
+}
+
+__device__ __forceinline__ float ak_angle(float x, float y)
+{
+    return ak_atan2_deg(y, x) * (float)(3.14159265358979323846 / 180.0);
+}
+
+__device__ __forceinline__ int ak_clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__global__ __launch_bounds__(256) void akz_desc_kernel(AkDescArgs a)
+{
+    __shared__ float s_rx[4][112], s_ry[4][112], s_an[4][112];
+    __shared__ float s_val[4][29 * 3];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t kid = (int64_t)blockIdx.x * 4 + wv;
+    const bool live = kid < a.n;
+    dp_keypoint kp{};
+    AkPlane P{};
+    if (live) {
+        kp = a.kp[kid];
+        P = a.planes[(a.kv[kid] - a.v0) * kAkLevels + kp.reserved];
+    }
+    const float ra = (float)(1 << P.octave);
+    const float xf = kp.x / ra, yf = kp.y / ra;
+    const int s = P.sigma_size;
+    const float *Lt = a.pool + P.off, *Lx = Lt + (int64_t)P.w * P.h, *Ly = Lx + (int64_t)P.w * P.h;
+    // the 109 samples (i outer, j inner, i^2 + j^2 < 36), two per lane
+    if (live) {
+        for (int q = lane; q < 109; q += 64) {
+            int cnt = 0, si = 0, sj = 0;
+            for (int i = -6; i <= 6; ++i)
+                for (int j = -6; j <= 6; ++j)
+                    if (i * i + j * j < 36) {
+                        if (cnt == q) {
+                            si = i;
+                            sj = j;
+                        }
+                        ++cnt;
+                    }
+            const int iy = ak_clampi(__float2int_rn(yf + (float)(sj * s)), 0, P.h - 1);
+            const int ix = ak_clampi(__float2int_rn(xf + (float)(si * s)), 0, P.w - 1);
+            const float gw = a.g25[abs(si) * 7 + abs(sj)];
+            const float rx = gw * Lx[(size_t)iy * P.w + ix], ry = gw * Ly[(size_t)iy * P.w + ix];
+            s_rx[wv][q] = rx;
+            s_ry[wv][q] = ry;
+            s_an[wv][q] = ak_angle(rx, ry);
+        }
+    }
+    __syncthreads();
+    // windows: lane w slides the pi/3 window to a1 = w x 0.15f (sequential adds)
+    const float two_pi = (float)(2.0 * 3.14159265358979323846), pi3 = (float)(3.14159265358979323846 / 3.0);
+    const float pi53 = (float)(5.0 * 3.14159265358979323846 / 3.0);
+    float m = -1.0f, sx = 0.0f, sy = 0.0f;
+    if (live && lane < a.n_windows) {
+        float a1 = 0.0f;
+        for (int k = 0; k < lane; ++k)
+            a1 += 0.15f;
+        const float a2 = a1 + pi3 > two_pi ? a1 - pi53 : a1 + pi3;
+        for (int k = 0; k < 109; ++k) {
+            const float an = s_an[wv][k];
+            if ((a1 < a2 && a1 < an && an < a2) || (a2 < a1 && ((an > 0 && an < a2) || (an > a1 && an < two_pi)))) {
+                sx = sx + s_rx[wv][k];
+                sy = sy + s_ry[wv][k];
+            }
+        }
+        m = sx * sx + sy * sy;
+    }
+    // the first window (smallest a1) with the largest m > 0 wins
+    float bm = m;
+    int bw = (live && lane < a.n_windows && m > 0.0f) ? lane : 64;
+    if (!(m > 0.0f))
+        bm = -1.0f;
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float om = __shfl_xor(bm, o);
+        const int ow = __shfl_xor(bw, o);
+        if (om > bm || (om == bm && ow < bw)) {
+            bm = om;
+            bw = ow;
+        }
+    }
+    float angle = 0.0f;
+    {
+        const float ang_l = ak_angle(sx, sy);
+        const float got = __shfl(ang_l, bw < 64 ? bw : 0);
+        angle = bw < 64 ? got : 0.0f;
+    }
+    // M-LDB cells: lanes 0..3 the 2x2 grid, 4..12 the 3x3, 13..28 the 4x4
+    double sd = 0.0, cd = 1.0;
+    dpm::sincos((double)angle, sd, cd);
+    const float co = (float)cd, si = (float)sd, scale = (float)s;
+    if (live && lane < 29) {
+        int lvl, c;
+        if (lane < 4) {
+            lvl = 0;
+            c = lane;
+        } else if (lane < 13) {
+            lvl = 1;
+            c = lane - 4;
+        } else {
+            lvl = 2;
+            c = lane - 13;
+        }
+        const int st = lvl == 0 ? 10 : (lvl == 1 ? 7 : 5), g = lvl + 2;
+        const int i = -10 + (c / g) * st, j = -10 + (c % g) * st;
+        float di = 0.0f, dx = 0.0f, dy = 0.0f;
+        int ns = 0;
+        for (int k = i; k < i + st; ++k)
+            for (int l = j; l < j + st; ++l) {
+                const float syy = yf + (((float)l * co) * scale + ((float)k * si) * scale);
+                const float sxx = xf + (((float)-l * si) * scale + ((float)k * co) * scale);
+                const int y1 = ak_clampi(__float2int_rn(syy), 0, P.h - 1);
+                const int x1 = ak_clampi(__float2int_rn(sxx), 0, P.w - 1);
+                const size_t q = (size_t)y1 * P.w + x1;
+                di = di + Lt[q];
+                const float gx = Lx[q], gy = Ly[q];
+                dx = dx + (-gx * si + gy * co);
+                dy = dy + (gx * co + gy * si);
+                ++ns;
+            }
+        s_val[wv][3 * lane] = di / (float)ns;
+        s_val[wv][3 * lane + 1] = dx / (float)ns;
+        s_val[wv][3 * lane + 2] = dy / (float)ns;
+    }
+    __syncthreads();
+    if (!live)
+        return;
+    // 486 comparisons: bit b by lane b mod 64 in round b / 64
+    for (int rd = 0; rd < (kAkBits + 63) / 64; ++rd) {
+        const int b = rd * 64 + lane;
+        bool bit = false;
+        if (b < kAkBits) {
+            const uint32_t pr = a.bit_pairs[b];
+            const int ca = pr & 255u, cb = (pr >> 8) & 255u, ch = (pr >> 16) & 255u;
+            const float fa = s_val[wv][3 * ca + ch], fb = s_val[wv][3 * cb + ch];
+            int32_t ia = __float_as_int(fa), ib = __float_as_int(fb);
+            ia ^= ia < 0 ? 0x7fffffff : 0;
+            ib ^= ib < 0 ? 0x7fffffff : 0;
+            bit = ia > ib;
+        }
+        const unsigned long long word = __ballot(bit);
+        if (lane == 0) {
+            a.desc[(size_t)kid * kAkDescWords + 2 * rd] = (uint32_t)word;
+            a.desc[(size_t)kid * kAkDescWords + 2 * rd + 1] = (uint32_t)(word >> 32);
+        }
+    }
+    if (lane == 0)
+        a.kp[kid].angle = angle * (float)(180.0 / 3.14159265358979323846);
+}
+
+hipError_t launch_akz_describe(const AkDescArgs &a, hipStream_t s)
+{
+    if (a.n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(akz_desc_kernel, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// host helpers
+// ---------------------------------------------------------------------------
+int akaze_gauss_kernel(float sigma, float *w)
+{
+    int n = (int)std::ceil(2.0f * (1.0f + (sigma - 0.8f) / 0.3f));
+    if (n % 2 == 0)
+        n += 1;
+    double t[64], sum = 0.0;
+    const double s2 = -0.5 / ((double)sigma * (double)sigma);
+    for (int i = 0; i < n; ++i) {
+        const double x = i - (n - 1) * 0.5;
+        t[i] = std::exp(s2 * x * x);
+        sum += t[i];
+    }
+    for (int i = 0; i < n; ++i)
+        w[i] = (float)(t[i] / sum);
+    return n;
+}
+
+static bool akaze_prime(int n)
+{
+    if (n <= 1)
+        return false;
+    for (int p = 2; p * p <= n; ++p)
+        if (n % p == 0)
+            return false;
+    return true;
+}
+
+int akaze_fed_tau(float T, float tau_max, float *tau)
+{
+    const int n = (int)(std::ceil(std::sqrt(3.0f * T / tau_max + 0.25f) - 0.5f - 1.0e-8f) + 0.5f);
+    if (n <= 0)
+        return 0;
+    if (n > kAkMaxFed)
+        return -1;
+    const float scale = 3.0f * T / (tau_max * (float)(n * (n + 1)));
+    const float c = 1.0f / (4.0f * (float)n + 2.0f), d = scale * tau_max / 2.0f;
+    float tauh[kAkMaxFed];
+    for (int k = 0; k < n; ++k) {
+        const float h = (float)std::cos(3.14159265358979323846 * (double)((2.0f * (float)k + 1.0f) * c));
+        tauh[k] = d / (h * h);
+    }
+    const int kappa = n / 2;
+    if (kappa == 0) {
+        for (int l = 0; l < n; ++l)
+            tau[l] = tauh[l];
+        return n;
+    }
+    int prime = n + 1;
+    while (!akaze_prime(prime))
+        prime++;
+    for (int k = 0, l = 0; l < n; ++k, ++l) {
+        int index;
+        while ((index = ((k + 1) * kappa) % prime - 1) >= n)
+            k++;
+        tau[l] = tauh[index];
+    }
+    return n;
+}
+
+void akaze_g25(float *g)
+{
+    for (int a = 0; a < 7; ++a)
+        for (int b = 0; b < 7; ++b)
+            g[a * 7 + b] = (float)(std::exp(-(double)(a * a + b * b) / 12.5) / (12.5 * 3.14159265358979323846));
+}
+
+void akaze_bit_pairs(uint32_t *pairs)
+{
+    int b = 0, base = 0;
+    for (int lvl = 0; lvl < 3; ++lvl) {
+        const int cnt = (lvl + 2) * (lvl + 2);
+        for (int ch = 0; ch < 3; ++ch)
+            for (int i = 0; i < cnt; ++i)
+                for (int j = i + 1; j < cnt; ++j)
+                    pairs[b++] = (uint32_t)(base + i) | (uint32_t)(base + j) << 8 | (uint32_t)ch << 16;
+        base += cnt;
+    }
+}
+
+int akaze_windows()
+{
+    const float two_pi = (float)(2.0 * 3.14159265358979323846);
+    int n = 0;
+    for (float a1 = 0.0f; a1 < two_pi; a1 += 0.15f)
+        ++n;
+    return n;
+}
+
+} // namespace dpk

@@ -25,12 +25,16 @@ struct KnnBlock {
 };
 
 struct KnnArgs {
-    const uint32_t *desc;  // packed descriptors, 32 B each
+    const uint32_t *desc;  // packed descriptors, `words` dwords each
     const KnnJob *jobs;
     const KnnBlock *blocks;
-    uint32_t *keys;        // per slot, 2 per query: (acc + 256) << 22 | train row, ~0 = none
+    uint32_t *keys;        // per slot, 2 per query: (acc + 32 words) << rowbits | train row, ~0 = none
     int64_t slot_stride;   // elements between slots (train-range splits)
+    int32_t words;         // 8 (ORB, 256 bits) or 16 (AKAZE M-LDB, 486 bits zero-padded to 512)
 };
+
+// key layout per descriptor width: rowbits = 22 (8 words) / 21 (16 words)
+__host__ __device__ constexpr int knn_row_bits(int words) { return words == 16 ? 21 : 22; }
 
 // merge the per-split (smallest, second) keys of every query into slot 0 order
 hipError_t launch_knn_merge(const uint32_t *partial, int nsplit, int64_t slot_stride, int64_t nq, uint32_t *keys,
@@ -51,6 +55,7 @@ struct MatchArgs {
     const uint32_t *keys;
     const uint32_t *desc;
     const dp_keypoint *kp;
+    int32_t words;         // descriptor dwords (KnnArgs::words)
     float ratio;
     float max_dist;
     int32_t flann;         // DP_MATCHER_FLANN: exact 1-NN, kept iff distance < 30
@@ -74,8 +79,8 @@ struct TriangArgs {
 };
 
 hipError_t launch_knn(const KnnArgs &a, int nblocks, hipStream_t s);
-hipError_t launch_knn_decode(const uint32_t *desc, int64_t q_off, int64_t nq, const uint32_t *keys, int32_t *idx2,
-                             int32_t *dist2, hipStream_t s);
+hipError_t launch_knn_decode(const uint32_t *desc, int words, int64_t q_off, int64_t nq, const uint32_t *keys,
+                             int32_t *idx2, int32_t *dist2, hipStream_t s);
 hipError_t launch_match(const MatchArgs &a, hipStream_t s);
 hipError_t launch_triang(const TriangArgs &a, hipStream_t s);
 // DirectEpipolarMatching (matcher.cpp:267-317): every train keypoint within

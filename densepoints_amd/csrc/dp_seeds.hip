@@ -3,7 +3,7 @@
 //
 // Kernels:
 //   knn_kernel      BruteForce-Hamming knnMatch(k=2) on MFMA: Hamming distances
-//                   of 256-bit descriptors as an i8 GEMM (train bits 0/1 x
+//                   of 256-bit (ORB) or 512-bit (AKAZE) descriptors as an i8 GEMM (train bits 0/1 x
 //                   query bits +-1), top-2 per query kept in registers
 //   match_kernel    ratio test (matcher.cpp:221) + epipolar filter
 //                   (matcher.cpp:319-372) + the GetAllMatches lookup tables
@@ -33,7 +33,8 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 // acc = sum_k trainbit_k * (1 - 2 querybit_k) = popcnt(t & ~q) - popcnt(t & q)
 //     = hamming(t, q) - popcnt(q)
 // so within one query column the order of acc is the order of the Hamming
-// distance.  Per element the key (acc + 256) << 22 | train_row (mod 2^32) is
+// distance.  Per element the key (acc + 32 kW) << rowbits | train_row (mod 2^32;
+// rowbits 22 for 256-bit ORB rows, 21 for 512-bit AKAZE rows) is
 // kept as a running (smallest, second) pair: m1 = med3(m0, k, m1),
 // m0 = min(m0, k).  Ties go to the lower train row, which is batchDistance's
 // strict-< insertion order (the first of equal distances wins).
@@ -82,9 +83,11 @@ __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
+template <int kW>
 __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
 {
-    __shared__ v4i tileA[kKnnTiles][8][64]; // A fragments of one stage, 32 KB
+    __shared__ v4i tileA[kKnnTiles][kW][64]; // A fragments of one stage, 32 KB per 8 words
+    constexpr int kRB = knn_row_bits(kW);
 
     const KnnBlock kb = a.blocks[blockIdx.x];
     const int2 blk = make_int2(kb.job, kb.q0);
@@ -92,18 +95,18 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
     const int tid = threadIdx.x;
     const int w = tid >> 6, l = tid & 63;
     const int col = l & 31, h = l >> 5;
-    const uint32_t *qd = a.desc + (size_t)job.q_off * 8;
-    const uint32_t *td = a.desc + (size_t)job.t_off * 8;
+    const uint32_t *qd = a.desc + (size_t)job.q_off * kW;
+    const uint32_t *td = a.desc + (size_t)job.t_off * kW;
 
     // query fragments: B[k][col], k = 32 s + 16 h + j for element j
-    v4i bq[kKnnQB][8];
+    v4i bq[kKnnQB][kW];
 #pragma unroll
     for (int b = 0; b < kKnnQB; ++b) {
         const int q = blk.y + w * kKnnWQ + b * 32 + col;
         const bool ok = q < job.nq;
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const uint32_t d = ok ? qd[(size_t)q * 8 + s] : 0u;
+        for (int s = 0; s < kW; ++s) {
+            const uint32_t d = ok ? qd[(size_t)q * kW + s] : 0u;
             bq[b][s] = bits16_pm1(d >> (16 * h));
         }
     }
@@ -115,41 +118,47 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
     // train rows [t_lo, t_end) of this workgroup; stage loads are prefetched
     // into registers one stage ahead, so the global latency hides behind MFMA
     const int t_end = min(kb.t_hi, job.nt);
-    const int sr = tid >> 1, shh = tid & 1; // stage slot of this thread: (row, 4 dwords)
-    auto stage_load = [&](int t0) {
-        uint4 d = make_uint4(0, 0, 0, 0);
-        if (t0 + sr < t_end)
-            d = *reinterpret_cast<const uint4 *>(td + (size_t)(t0 + sr) * 8 + 4 * shh);
-        return d;
+    // stage slot of this thread: (row, kW / 2 dwords)
+    constexpr int kQ = kW / 8; // 16-byte pieces per thread
+    const int sr = tid >> 1, shh = tid & 1;
+    auto stage_load = [&](int t0, uint4 *d) {
+#pragma unroll
+        for (int u = 0; u < kQ; ++u) {
+            d[u] = make_uint4(0, 0, 0, 0);
+            if (t0 + sr < t_end)
+                d[u] = *reinterpret_cast<const uint4 *>(td + (size_t)(t0 + sr) * kW + (kW / 2) * shh + 4 * u);
+        }
     };
-    uint4 dnext = stage_load(kb.t_lo);
+    uint4 dnext[kQ];
+    stage_load(kb.t_lo, dnext);
     for (int t0 = kb.t_lo; t0 < t_end; t0 += kKnnRows) {
-        // stage: unpack this thread's 128 bits to 0/1 bytes in A-fragment order
-        {
-            const uint32_t dv[4] = {dnext.x, dnext.y, dnext.z, dnext.w};
+        // stage: unpack this thread's bits to 0/1 bytes in A-fragment order
+#pragma unroll
+        for (int u = 0; u < kQ; ++u) {
+            const uint32_t dv[4] = {dnext[u].x, dnext[u].y, dnext[u].z, dnext[u].w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int s = 4 * shh + i;
+                const int s = (kW / 2) * shh + 4 * u + i;
                 tileA[sr >> 5][s][sr & 31] = bits16_01(dv[i] & 0xFFFFu);
                 tileA[sr >> 5][s][32 + (sr & 31)] = bits16_01(dv[i] >> 16);
             }
         }
         __syncthreads();
-        dnext = stage_load(t0 + kKnnRows);
+        stage_load(t0 + kKnnRows, dnext);
 #pragma unroll 1
         for (int ti = 0; ti < kKnnTiles; ++ti) {
             const int tb = t0 + ti * 32;
             if (tb >= t_end)
                 break;
-            v4i af[8];
+            v4i af[kW];
 #pragma unroll
-            for (int s = 0; s < 8; ++s)
+            for (int s = 0; s < kW; ++s)
                 af[s] = tileA[ti][s][l];
             // key base per accumulator register: rows tb + (r&3) + 8 (r>>2) + 4 h.
             // The lane-half term 4 h is left out of every key of this lane (the
             // same offset for all of its rows, so its order is unchanged) and
             // added back at the half merge: the 16 bases are wave-uniform (SGPRs).
-            const uint32_t base = (256u << 22) + (uint32_t)tb;
+            const uint32_t base = ((uint32_t)(32 * kW) << kRB) + (uint32_t)tb;
             const bool partial = tb + 32 > t_end;
             // the blocks' accumulation chains interleaved (independent MFMAs back to back)
             v16i acc[kKnnQB];
@@ -157,14 +166,14 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
             for (int b = 0; b < kKnnQB; ++b)
                 acc[b] = v16i{};
 #pragma unroll
-            for (int s = 0; s < 8; ++s)
+            for (int s = 0; s < kW; ++s)
 #pragma unroll
                 for (int b = 0; b < kKnnQB; ++b)
                     acc[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[b][s], acc[b], 0, 0, 0);
             // (a wave-uniform skip when no lane's tile minimum beats its second
             // best was measured slower: with ~2.5k-row train ranges it rarely fires)
             if (!partial) {
-                // key = (acc << 22) + R[r]: one v_lshl_add_u32 per element, R shared by the blocks
+                // key = (acc << rowbits) + R[r]: one v_lshl_add_u32 per element, R shared by the blocks
                 uint32_t R[16];
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
@@ -173,8 +182,8 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
                 for (int b = 0; b < kKnnQB; ++b)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        uint32_t k; // (acc << 22) + R[r] (the compiler otherwise emits shift + add3)
-                        asm("v_lshl_add_u32 %0, %1, 22, %2" : "=v"(k) : "v"(acc[b][r]), "s"(R[r]));
+                        uint32_t k; // (acc << rowbits) + R[r] (the compiler otherwise emits shift + add3)
+                        asm("v_lshl_add_u32 %0, %1, %3, %2" : "=v"(k) : "v"(acc[b][r]), "s"(R[r]), "i"(kRB));
                         m1[b] = med3u(m0[b], k, m1[b]);
                         m0[b] = min(m0[b], k);
                     }
@@ -184,7 +193,7 @@ __global__ __launch_bounds__(256) void knn_kernel(KnnArgs a)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const uint32_t roff = (uint32_t)((r & 3) + 8 * (r >> 2));
-                        uint32_t k = ((uint32_t)acc[b][r] << 22) + base + roff;
+                        uint32_t k = ((uint32_t)acc[b][r] << kRB) + base + roff;
                         if (tb + 4 * h + (int)roff >= t_end)
                             k = 0xFFFFFFFFu;
                         m1[b] = med3u(m0[b], k, m1[b]);
@@ -241,24 +250,25 @@ hipError_t launch_knn_merge(const uint32_t *partial, int nsplit, int64_t slot_st
     return hipGetLastError();
 }
 
-// keys -> (index, distance); distance = (key >> 22) - 256 + popcnt(query)
-__global__ void knn_decode_kernel(const uint32_t *desc, int64_t q_off, int64_t nq, const uint32_t *keys,
+// keys -> (index, distance); distance = (key >> rowbits) - 32 words + popcnt(query)
+__global__ void knn_decode_kernel(const uint32_t *desc, int words, int64_t q_off, int64_t nq, const uint32_t *keys,
                                   int32_t *idx2, int32_t *dist2)
 {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq)
         return;
+    const int rb = knn_row_bits(words);
     int pq = 0;
-    for (int s = 0; s < 8; ++s)
-        pq += __popc(desc[(size_t)(q_off + q) * 8 + s]);
+    for (int s = 0; s < words; ++s)
+        pq += __popc(desc[(size_t)(q_off + q) * words + s]);
     for (int j = 0; j < 2; ++j) {
         const uint32_t k = keys[2 * q + j];
         if (k == 0xFFFFFFFFu) {
             idx2[2 * q + j] = -1;
             dist2[2 * q + j] = -1;
         } else {
-            idx2[2 * q + j] = (int32_t)(k & ((1u << 22) - 1));
-            dist2[2 * q + j] = (int32_t)(k >> 22) - 256 + pq;
+            idx2[2 * q + j] = (int32_t)(k & ((1u << rb) - 1));
+            dist2[2 * q + j] = (int32_t)(k >> rb) - 32 * words + pq;
         }
     }
 }
@@ -267,7 +277,12 @@ hipError_t launch_knn(const KnnArgs &a, int nblocks, hipStream_t s)
 {
     if (nblocks <= 0)
         return hipSuccess;
-    hipLaunchKernelGGL(knn_kernel, dim3(nblocks), dim3(256), 0, s, a);
+    if (a.words == 16)
+        hipLaunchKernelGGL(knn_kernel<16>, dim3(nblocks), dim3(256), 0, s, a);
+    else if (a.words == 8)
+        hipLaunchKernelGGL(knn_kernel<8>, dim3(nblocks), dim3(256), 0, s, a);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
@@ -296,15 +311,16 @@ __global__ void match_kernel(MatchArgs a)
     // FLANN form's match() needs one
     if (job.nt >= (a.flann ? 1 : 2)) {
         const uint32_t k0 = a.keys[2 * i], k1 = a.keys[2 * i + 1];
-        // Hamming distances: (key >> 22) - 256 + popcnt(query)
+        // Hamming distances: (key >> rowbits) - 32 words + popcnt(query)
+        const int rb = knn_row_bits(a.words);
         int pq = 0;
-        for (int s = 0; s < 8; ++s)
-            pq += __popc(a.desc[(size_t)(job.q_off + q) * 8 + s]);
-        const int32_t h0 = (int32_t)(k0 >> 22) - 256 + pq, h1 = (int32_t)(k1 >> 22) - 256 + pq;
+        for (int s = 0; s < a.words; ++s)
+            pq += __popc(a.desc[(size_t)(job.q_off + q) * a.words + s]);
+        const int32_t h0 = (int32_t)(k0 >> rb) - 32 * a.words + pq, h1 = (int32_t)(k1 >> rb) - 32 * a.words + pq;
         // DMatch::distance is float; nn_match_ratio is a float constant; FLANN
         // keeps matches with distance < 30 (matcher.cpp:235)
         if (a.flann ? (float)h0 < 30.0f : (float)h0 < a.ratio * (float)h1) {
-            const int32_t tt = (int32_t)(k0 & ((1u << 22) - 1));
+            const int32_t tt = (int32_t)(k0 & ((1u << rb) - 1));
             atomicAdd(a.n_ratio, 1ull);
             const dp_keypoint &kl = a.kp[job.q_off + q];
             const dp_keypoint &kr = a.kp[job.t_off + tt];
@@ -459,13 +475,13 @@ hipError_t launch_dlt_batch(int64_t n, const int32_t *off, const double *P, cons
     return hipGetLastError();
 }
 
-hipError_t launch_knn_decode(const uint32_t *desc, int64_t q_off, int64_t nq, const uint32_t *keys, int32_t *idx2,
-                             int32_t *dist2, hipStream_t s)
+hipError_t launch_knn_decode(const uint32_t *desc, int words, int64_t q_off, int64_t nq, const uint32_t *keys,
+                             int32_t *idx2, int32_t *dist2, hipStream_t s)
 {
     if (nq <= 0)
         return hipSuccess;
-    hipLaunchKernelGGL(knn_decode_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, desc, q_off, nq, keys,
-                       idx2, dist2);
+    hipLaunchKernelGGL(knn_decode_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, desc, words, q_off, nq,
+                       keys, idx2, dist2);
     return hipGetLastError();
 }
 

@@ -2,6 +2,7 @@
 // "seed generation"): Features::Matcher::GenerateSeeds
 // (modules/features/matcher.cpp:18-43) on the device, plus the standalone
 // operators (knnMatch, ComputeFundamentalMatrix, DirectLinearTriangulation).
+#include "dp_akaze.h"
 #include "dp_ctx.h"
 #include "dp_dlt.h"
 #include "dp_orb.h"
@@ -49,6 +50,15 @@ struct dp_seedgen {
     DevBuf<int64_t> kp_off;
     DevBuf<uint8_t> valid;
     DevBuf<unsigned long long> counters;
+    // AKAZE (DetectorType::AKAZE): scale-space pools and tables
+    DevBuf<float> akz_pool, akz_tmp, akz_k0, akz_g25;
+    DevBuf<dpk::AkPlane> akz_planes;
+    DevBuf<dpk::AkView> akz_views;
+    DevBuf<uint32_t> akz_hmax, akz_hist, akz_bits;
+    DevBuf<uint8_t> akz_flag;
+    DevBuf<int64_t> akz_cand, akz_pbase;
+    DevBuf<int32_t> akz_pids, akz_vids;
+    int desc_words = 8; // 8 (ORB) or 16 (AKAZE) dwords per descriptor
     std::vector<dpk::SeedPair> h_pairs;
     std::vector<dpk::KnnJob> h_jobs;
     std::vector<int64_t> h_kp_off;
@@ -103,6 +113,17 @@ void dp_seedgen_free(dp_seedgen *s)
     s->kp_off.release();
     s->valid.release();
     s->counters.release();
+    for (auto *b : {&s->akz_pool, &s->akz_tmp, &s->akz_k0, &s->akz_g25})
+        b->release();
+    s->akz_planes.release();
+    s->akz_views.release();
+    for (auto *b : {&s->akz_hmax, &s->akz_hist, &s->akz_bits})
+        b->release();
+    s->akz_flag.release();
+    s->akz_cand.release();
+    s->akz_pbase.release();
+    s->akz_pids.release();
+    s->akz_vids.release();
     delete s;
 }
 
@@ -129,6 +150,8 @@ extern "C" void dp_default_matcher_options(dp_matcher_options *mo)
     mo->max_epipolar_distance = 1.5f;
     mo->nn_match_ratio = 0.7f;
     mo->matcher_type = DP_MATCHER_KNN;
+    mo->detector_type = DP_DETECTOR_ORB;
+    mo->akaze_threshold = 0.001f;
 }
 
 extern "C" int dp_orb_pattern(int8_t *xy_out)
@@ -239,7 +262,7 @@ static int knn_blocks(const std::vector<dpk::KnnJob> &jobs, std::vector<dpk::Knn
 
 // knn over uploaded jobs (device copy in s->jobs); final keys into `keys`
 static int run_knn(dp_ctx *c, dp_seedgen *s, const std::vector<dpk::KnnJob> &jobs, int64_t q_total, uint32_t *keys,
-                   bool timed)
+                   bool timed, int words)
 {
     std::vector<dpk::KnnBlock> blocks;
     const int nsplit = knn_blocks(jobs, blocks);
@@ -253,7 +276,7 @@ static int run_knn(dp_ctx *c, dp_seedgen *s, const std::vector<dpk::KnnJob> &job
         DP_HIP(c, s->pkeys.reserve((size_t)nsplit * stride + 1));
         out = s->pkeys.p;
     }
-    dpk::KnnArgs ka{s->desc.p, s->jobs.p, s->blocks.p, out, stride};
+    dpk::KnnArgs ka{s->desc.p, s->jobs.p, s->blocks.p, out, stride, words};
     if (timed)
         DP_HIP(c, hipEventRecord(c->e0, c->stream));
     DP_HIP(c, dpk::launch_knn(ka, (int)blocks.size(), c->stream));
@@ -266,13 +289,14 @@ static int run_knn(dp_ctx *c, dp_seedgen *s, const std::vector<dpk::KnnJob> &job
     return DP_OK;
 }
 
-extern "C" int dp_knn_match(dp_ctx *c, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt,
-                            int32_t *idx2, int32_t *dist2)
+static int knn_match_impl(dp_ctx *c, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt, int bytes,
+                          int32_t *idx2, int32_t *dist2)
 {
     if (!c)
         return DP_E_ARG;
-    if (nq < 0 || nt < 0 || nt >= (1 << 22) || nq > INT32_MAX || (nq > 0 && (!query || !idx2 || !dist2)) ||
-        (nt > 0 && !train))
+    const int words = bytes / 4;
+    if ((bytes != 32 && bytes != 64) || nq < 0 || nt < 0 || nt >= (1 << dpk::knn_row_bits(words)) || nq > INT32_MAX ||
+        (nq > 0 && (!query || !idx2 || !dist2)) || (nt > 0 && !train))
         return fail(c, DP_E_ARG, "dp_knn_match: bad arguments");
     if (nq == 0)
         return DP_OK;
@@ -280,13 +304,13 @@ extern "C" int dp_knn_match(dp_ctx *c, const uint8_t *query, int64_t nq, const u
     if (!s)
         return fail(c, DP_E_OOM, "seedgen state");
     DP_HIP(c, hipSetDevice(c->device));
-    DP_HIP(c, s->desc.reserve((size_t)(nq + nt) * 8));
+    DP_HIP(c, s->desc.reserve((size_t)(nq + nt) * words));
     DP_HIP(c, s->keys.reserve((size_t)nq * 2));
     DP_HIP(c, s->i2.reserve((size_t)nq * 2));
     DP_HIP(c, s->d2.reserve((size_t)nq * 2));
-    DP_HIP(c, hipMemcpyAsync(s->desc.p, query, (size_t)nq * 32, hipMemcpyHostToDevice, c->stream));
+    DP_HIP(c, hipMemcpyAsync(s->desc.p, query, (size_t)nq * bytes, hipMemcpyHostToDevice, c->stream));
     if (nt > 0)
-        DP_HIP(c, hipMemcpyAsync(s->desc.p + nq * 8, train, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream));
+        DP_HIP(c, hipMemcpyAsync(s->desc.p + nq * words, train, (size_t)nt * bytes, hipMemcpyHostToDevice, c->stream));
     std::vector<dpk::KnnJob> jobs(1);
     jobs[0].q_off = 0;
     jobs[0].t_off = nq;
@@ -295,14 +319,26 @@ extern "C" int dp_knn_match(dp_ctx *c, const uint8_t *query, int64_t nq, const u
     jobs[0].nt = (int32_t)nt;
     DP_HIP(c, s->jobs.reserve(1));
     DP_HIP(c, hipMemcpyAsync(s->jobs.p, jobs.data(), sizeof(dpk::KnnJob), hipMemcpyHostToDevice, c->stream));
-    int rc = run_knn(c, s, jobs, nq, s->keys.p, true);
+    int rc = run_knn(c, s, jobs, nq, s->keys.p, true, words);
     if (rc != DP_OK)
         return rc;
-    DP_HIP(c, dpk::launch_knn_decode(s->desc.p, 0, nq, s->keys.p, s->i2.p, s->d2.p, c->stream));
+    DP_HIP(c, dpk::launch_knn_decode(s->desc.p, words, 0, nq, s->keys.p, s->i2.p, s->d2.p, c->stream));
     DP_HIP(c, hipMemcpyAsync(idx2, s->i2.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
     DP_HIP(c, hipMemcpyAsync(dist2, s->d2.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
     DP_HIP(c, hipStreamSynchronize(c->stream));
     return DP_OK;
+}
+
+extern "C" int dp_knn_match(dp_ctx *c, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt,
+                            int32_t *idx2, int32_t *dist2)
+{
+    return knn_match_impl(c, query, nq, train, nt, 32, idx2, dist2);
+}
+
+extern "C" int dp_knn_match_wide(dp_ctx *c, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt,
+                                 int descriptor_bytes, int32_t *idx2, int32_t *dist2)
+{
+    return knn_match_impl(c, query, nq, train, nt, descriptor_bytes, idx2, dist2);
 }
 
 // ---------------------------------------------------------------------------
@@ -379,8 +415,358 @@ static int check_matcher_options(dp_ctx *c, const dp_matcher_options &m)
         m.edge_threshold < 19 || m.fast_threshold < 0 || m.fast_threshold > 254 || m.cell_size < 1 ||
         m.max_keypoints_per_cell < 0 || (m.epipolar_matching != 0 && m.epipolar_matching != 1) ||
         !(m.nn_match_ratio >= 0.0f) || !(m.max_epipolar_distance >= 0.0f) ||
-        (m.matcher_type != DP_MATCHER_KNN && m.matcher_type != DP_MATCHER_FLANN))
-        return fail(c, DP_E_ARG, "dp_matcher_options: value out of range (edge_threshold >= 19, 1 <= n_levels <= 16)");
+        (m.matcher_type != DP_MATCHER_KNN && m.matcher_type != DP_MATCHER_FLANN) ||
+        (m.detector_type != DP_DETECTOR_AKAZE && m.detector_type != DP_DETECTOR_ORB) ||
+        !(m.akaze_threshold > 0.0f) || !std::isfinite(m.akaze_threshold))
+        return fail(c, DP_E_ARG, "dp_matcher_options: value out of range (edge_threshold >= 19, 1 <= n_levels <= 16, "
+                                 "detector_type AKAZE/ORB, akaze_threshold > 0)");
+    return DP_OK;
+}
+
+// FilterKeypoints (matcher.cpp:89-153): s->kp_a / kv_a (n3, view-major) ->
+// s->kp_b / kv_b (*n4): per cell (row-major per view) its keypoints in order,
+// or the best max_keypoints_per_cell by (response desc, index)
+static int cell_filter(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, const std::vector<int32_t> &vw,
+                       const std::vector<int32_t> &vh, int64_t n3, int64_t *n4)
+{
+    hipStream_t st = c->stream;
+    const int V = c->V;
+    std::vector<int32_t> gcols(V);
+    std::vector<int64_t> cell_off(V + 1, 0);
+    for (int v = 0; v < V; ++v) {
+        gcols[v] = (vw[v] + mo.cell_size - 1) / mo.cell_size;
+        const int64_t grows = (vh[v] + mo.cell_size - 1) / mo.cell_size;
+        if ((int64_t)gcols[v] * grows >= (1ll << 24))
+            return fail(c, DP_E_ARG, "dp_generate_seeds: more than 2^24 keypoint cells per view");
+        cell_off[v + 1] = cell_off[v] + (int64_t)gcols[v] * grows;
+    }
+    DP_HIP(c, s->gcols.reserve(V));
+    DP_HIP(c, s->cell_off.reserve(V + 1));
+    DP_HIP(c, s->cell_cnt.reserve(cell_off[V] + 1));
+    DP_HIP(c, hipMemcpyAsync(s->gcols.p, gcols.data(), V * 4, hipMemcpyHostToDevice, st));
+    DP_HIP(c, hipMemcpyAsync(s->cell_off.p, cell_off.data(), (V + 1) * 8, hipMemcpyHostToDevice, st));
+    DP_HIP(c, hipMemsetAsync(s->cell_cnt.p, 0, (size_t)(cell_off[V] + 1) * 4, st));
+    DP_HIP(c, s->ckey.reserve(n3 + 1));
+    DP_HIP(c, s->ckey_sorted.reserve(n3 + 1));
+    DP_HIP(c, s->idx_a.reserve(n3 + 1));
+    DP_HIP(c, s->idx_b.reserve(n3 + 1));
+    DP_HIP(c, s->flag.reserve(n3 + 1));
+    DP_HIP(c, dpk::launch_cell_count(s->kp_a.p, s->kv_a.p, n3, s->gcols.p, s->cell_off.p, mo.cell_size, s->cell_cnt.p,
+                                     st));
+    DP_HIP(c, dpk::launch_cell_key(s->kp_a.p, s->kv_a.p, n3, s->gcols.p, s->cell_off.p, mo.cell_size,
+                                   mo.max_keypoints_per_cell, s->cell_cnt.p, s->ckey.p, s->idx_a.p, st));
+    if (n3 > 0)
+        DP_CUB(c, s, hipcub::DeviceRadixSort::SortPairs(_tmp, _bytes, s->ckey.p, s->ckey_sorted.p, s->idx_a.p,
+                                                         s->idx_b.p, (int)n3, 0, 64, st));
+    DP_HIP(c, dpk::launch_cell_keep(s->ckey_sorted.p, n3, mo.max_keypoints_per_cell, s->flag.p, st));
+    DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, s->idx_b.p, s->flag.p, s->idx_a.p, s->n_sel.p, (int)n3,
+                                                st));
+    DP_HIP(c, hipMemcpyAsync(n4, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    DP_HIP(c, s->kp_b.reserve(*n4 + 1));
+    DP_HIP(c, s->kv_b.reserve(*n4 + 1));
+    DP_HIP(c, dpk::launch_gather_kp(s->kp_a.p, s->kv_a.p, s->idx_a.p, *n4, s->kp_b.p, s->kv_b.p, st));
+
+    return DP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// DetectorType::AKAZE (matcher.cpp:56-60 detect, 166-170 compute): the scale
+// space, detector, FilterKeypoints and M-LDB per chunk of views (the chunk's
+// planes fit DP_AKAZE_CHUNK_BYTES, 8 GiB by default); keypoints come out in
+// (view, level, y, x) order, cells filtered as for ORB.  Leaves s->kp_b /
+// kv_b / desc (16 dwords per keypoint) and the host keypoints.
+// ---------------------------------------------------------------------------
+struct AkGeom {
+    int n = 0;
+    int w[dpk::kAkLevels], h[dpk::kAkLevels], octave[dpk::kAkLevels], ss[dpk::kAkLevels];
+    float esigma[dpk::kAkLevels];
+};
+
+static AkGeom akaze_geom(int W, int H)
+{
+    AkGeom g;
+    for (int o = 0; o < 4; ++o) {
+        const int w = W >> o, h = H >> o;
+        if (o > 0 && (w < 80 || h < 40))
+            break;
+        for (int j = 0; j < 4; ++j) {
+            g.w[g.n] = w;
+            g.h[g.n] = h;
+            g.octave[g.n] = o;
+            g.esigma[g.n] = (float)(1.6 * std::pow(2.0, (double)j / 4.0 + (double)o));
+            g.ss[g.n] = (int)std::lrint(g.esigma[g.n] * 1.5f / (float)(1 << o));
+            ++g.n;
+        }
+    }
+    return g;
+}
+
+static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, const std::vector<int32_t> &vw,
+                       const std::vector<int32_t> &vh, hipEvent_t e0, hipEvent_t e1, hipEvent_t e2, dp_seed_stats &S,
+                       int64_t *n_out, std::vector<int32_t> &h_kv)
+{
+    using namespace dpk;
+    hipStream_t st = c->stream;
+    const int V = c->V;
+    for (int v = 0; v < V; ++v)
+        if (vw[v] < 16 || vh[v] < 16)
+            return fail(c, DP_E_ARG, "dp_generate_seeds: AKAZE needs views of at least 16 x 16 px");
+    std::vector<AkGeom> geo(V);
+    for (int v = 0; v < V; ++v)
+        geo[v] = akaze_geom(vw[v], vh[v]);
+    // FED time steps per level (the same esigma sequence for every view)
+    const AkGeom full = akaze_geom(1 << 20, 1 << 20);
+    std::vector<std::vector<float>> tau(kAkLevels);
+    for (int i = 1; i < full.n; ++i) {
+        const float e_prev = 0.5f * (full.esigma[i - 1] * full.esigma[i - 1]);
+        const float e_cur = 0.5f * (full.esigma[i] * full.esigma[i]);
+        float t[kAkMaxFed];
+        const int n = akaze_fed_tau(e_cur - e_prev, 0.25f, t);
+        if (n < 0)
+            return fail(c, DP_E_ARG, "dp_generate_seeds: AKAZE FED schedule too long");
+        tau[i].assign(t, t + n);
+    }
+    // host tables
+    float g25[49];
+    akaze_g25(g25);
+    std::vector<uint32_t> bits(kAkBits);
+    akaze_bit_pairs(bits.data());
+    DP_HIP(c, s->akz_g25.reserve(49));
+    DP_HIP(c, s->akz_bits.reserve(kAkBits));
+    DP_HIP(c, hipMemcpyAsync(s->akz_g25.p, g25, sizeof(g25), hipMemcpyHostToDevice, st));
+    DP_HIP(c, hipMemcpyAsync(s->akz_bits.p, bits.data(), kAkBits * 4, hipMemcpyHostToDevice, st));
+    const int n_windows = akaze_windows();
+
+    auto taps_gauss = [](float sigma) {
+        AkTaps t{};
+        t.mode = 0;
+        t.n = akaze_gauss_kernel(sigma, t.w);
+        return t;
+    };
+    const AkTaps g16 = taps_gauss(1.6f), g10 = taps_gauss(1.0f);
+    AkTaps sd1{}, ss1{}, dS{}, sS{};
+    sd1.mode = 1;
+    sd1.spacing = 1;
+    ss1.mode = 2;
+    ss1.spacing = 1;
+    ss1.w[0] = 3.0f;
+    ss1.w[1] = 10.0f;
+    dS.mode = 1;
+    dS.spacing = -1;
+    sS.mode = 2;
+    sS.spacing = -1;
+
+    const char *env = std::getenv("DP_AKAZE_CHUNK_BYTES");
+    const int64_t budget = env ? std::max<int64_t>(1, std::atoll(env)) : (int64_t)8 << 30;
+    auto view_bytes = [&](int v) {
+        int64_t px = 0;
+        for (int i = 0; i < geo[v].n; ++i)
+            px += (int64_t)geo[v].w[i] * geo[v].h[i];
+        return 17 * px + 20 * (int64_t)vw[v] * vh[v];
+    };
+    std::vector<dp_keypoint> all_kp;
+    std::vector<uint32_t> all_desc;
+    h_kv.clear();
+    int64_t n_det_total = 0;
+    bool e1_done = false;
+    DP_HIP(c, hipEventRecord(e0, st));
+    for (int v0 = 0; v0 < V;) {
+        int v1 = v0;
+        int64_t bytes = 0;
+        while (v1 < V && (v1 == v0 || bytes + view_bytes(v1) <= budget)) {
+            bytes += view_bytes(v1);
+            ++v1;
+        }
+        const int nv = v1 - v0;
+        std::vector<AkPlane> planes((size_t)nv * kAkLevels);
+        std::vector<AkView> views(nv);
+        std::memset(planes.data(), 0, planes.size() * sizeof(AkPlane));
+        int64_t pool = 0, tmp = 0, det = 0;
+        int mw[kAkLevels] = {0}, mh[kAkLevels] = {0}, nlev = 0;
+        for (int z = 0; z < nv; ++z) {
+            const int v = v0 + z;
+            const AkGeom &g = geo[v];
+            for (int i = 0; i < g.n; ++i) {
+                AkPlane &P = planes[(size_t)z * kAkLevels + i];
+                P.off = pool;
+                P.det_base = det;
+                P.w = g.w[i];
+                P.h = g.h[i];
+                P.octave = g.octave[i];
+                P.sigma_size = g.ss[i];
+                P.esigma = g.esigma[i];
+                pool += 4 * (int64_t)P.w * P.h;
+                det += (int64_t)P.w * P.h;
+                mw[i] = std::max(mw[i], P.w);
+                mh[i] = std::max(mh[i], P.h);
+            }
+            nlev = std::max(nlev, g.n);
+            const PyrPlane &pl = c->planes[0][v];
+            views[z].bgra = pl.img;
+            views[z].pitch = pl.pitch;
+            views[z].w0 = vw[v];
+            views[z].h0 = vh[v];
+            views[z].view = v;
+            views[z].tmp = tmp;
+            views[z].n0 = (int64_t)vw[v] * vh[v];
+            tmp += 5 * views[z].n0;
+        }
+        if (det >= INT32_MAX)
+            return fail(c, DP_E_ARG, "dp_generate_seeds: AKAZE chunk above 2^31 pixels (lower DP_AKAZE_CHUNK_BYTES)");
+        DP_HIP(c, s->akz_pool.reserve(pool + 1));
+        DP_HIP(c, s->akz_tmp.reserve(tmp + 1));
+        DP_HIP(c, s->akz_planes.reserve(planes.size()));
+        DP_HIP(c, s->akz_views.reserve(nv));
+        DP_HIP(c, s->akz_hmax.reserve(nv));
+        DP_HIP(c, s->akz_hist.reserve((size_t)nv * 301));
+        DP_HIP(c, s->akz_k0.reserve(nv));
+        DP_HIP(c, s->akz_flag.reserve(det + 1));
+        DP_HIP(c, hipMemcpyAsync(s->akz_planes.p, planes.data(), planes.size() * sizeof(AkPlane),
+                                 hipMemcpyHostToDevice, st));
+        DP_HIP(c, hipMemcpyAsync(s->akz_views.p, views.data(), nv * sizeof(AkView), hipMemcpyHostToDevice, st));
+        DP_HIP(c, hipMemsetAsync(s->akz_hmax.p, 0, nv * 4, st));
+        DP_HIP(c, hipMemsetAsync(s->akz_hist.p, 0, (size_t)nv * 301 * 4, st));
+        const AkArgs a{s->akz_planes.p, s->akz_views.p, s->akz_pool.p, s->akz_tmp.p, s->akz_hmax.p, s->akz_hist.p,
+                       s->akz_k0.p};
+        auto conv = [&](int i, int src, int dst, int dir, const AkTaps &t) {
+            return launch_akz_conv(a, i, src, dst, dir, t, nv, mw[i], mh[i], st);
+        };
+        // the detector's derivatives of Lsmooth (plane ls) and Ldet
+        auto deriv = [&](int i, int ls) -> hipError_t {
+            const int seq[10][4] = {{ls, kT1, 0, 1}, {kT1, kLx, 1, 2}, {ls, kT1, 0, 2},  {kT1, kLy, 1, 1},
+                                    {kLx, kT1, 0, 1}, {kT1, kT2, 1, 2}, {kLx, kT1, 0, 2}, {kT1, kT0, 1, 1},
+                                    {kLy, kT1, 0, 2}, {kT1, kT4, 1, 1}};
+            for (const auto &q : seq) {
+                const hipError_t e = conv(i, q[0], q[1], q[2], q[3] == 1 ? dS : sS);
+                if (e != hipSuccess)
+                    return e;
+            }
+            return launch_akz_det(a, i, nv, mw[i], mh[i], st);
+        };
+        // level 0: gray, L0 = Gaussian(img, 1.6), the contrast factor
+        DP_HIP(c, launch_akz_gray(a, nv, mw[0], mh[0], st));
+        DP_HIP(c, conv(0, kT0, kT1, 0, g16));
+        DP_HIP(c, conv(0, kT1, kLt, 1, g16));
+        DP_HIP(c, conv(0, kT0, kT1, 0, g10));
+        DP_HIP(c, conv(0, kT1, kT3, 1, g10));
+        DP_HIP(c, conv(0, kT3, kT1, 0, sd1));
+        DP_HIP(c, conv(0, kT1, kT2, 1, ss1));
+        DP_HIP(c, conv(0, kT3, kT1, 0, ss1));
+        DP_HIP(c, conv(0, kT1, kT4, 1, sd1));
+        DP_HIP(c, launch_akz_kcontrast(a, nv, mw[0], mh[0], st));
+        DP_HIP(c, deriv(0, kLt));
+        for (int i = 1; i < nlev; ++i) {
+            if (full.octave[i] > full.octave[i - 1])
+                DP_HIP(c, launch_akz_half(a, i, nv, mw[i], mh[i], st));
+            else
+                DP_HIP(c, launch_akz_copy(a, i, -1, kLt, nv, mw[i], mh[i], st));
+            // Lsmooth, g2 conductance from its unnormalised Scharr gradient
+            DP_HIP(c, conv(i, kLt, kT1, 0, g10));
+            DP_HIP(c, conv(i, kT1, kT3, 1, g10));
+            DP_HIP(c, conv(i, kT3, kT1, 0, sd1));
+            DP_HIP(c, conv(i, kT1, kLx, 1, ss1));
+            DP_HIP(c, conv(i, kT3, kT1, 0, ss1));
+            DP_HIP(c, conv(i, kT1, kLy, 1, sd1));
+            DP_HIP(c, launch_akz_g2(a, i, nv, mw[i], mh[i], st));
+            // FED steps, ping-pong between Lt and T2
+            int src = kLt;
+            for (size_t k = 0; k < tau[i].size(); ++k) {
+                const int dst = (k % 2 == 0) ? kT2 : kLt;
+                DP_HIP(c, launch_akz_fed(a, i, src, dst, tau[i][k], nv, mw[i], mh[i], st));
+                src = dst;
+            }
+            if (src != kLt)
+                DP_HIP(c, launch_akz_copy(a, i, kT2, kLt, nv, mw[i], mh[i], st));
+            DP_HIP(c, deriv(i, kT3));
+        }
+        // extrema flags over every Ldet plane, candidates in (view, level, y, x) order
+        for (int i = 0; i < nlev; ++i)
+            DP_HIP(c, launch_akz_flag(a, i, mo.akaze_threshold, s->akz_flag.p, nv, mw[i], mh[i], st));
+        DP_HIP(c, s->akz_cand.reserve(det + 1));
+        {
+            hipcub::CountingInputIterator<int64_t> iota(0);
+            DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, iota, s->akz_flag.p, s->akz_cand.p, s->n_sel.p,
+                                                        (int)det, st));
+        }
+        int64_t n_cand = 0;
+        DP_HIP(c, hipMemcpyAsync(&n_cand, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        DP_HIP(c, hipStreamSynchronize(st));
+        std::vector<int32_t> pids, vids(nv);
+        std::vector<int64_t> pbase;
+        for (int z = 0; z < nv; ++z) {
+            vids[z] = v0 + z;
+            for (int i = 0; i < kAkLevels; ++i)
+                if (planes[(size_t)z * kAkLevels + i].w > 0) {
+                    pids.push_back(z * kAkLevels + i);
+                    pbase.push_back(planes[(size_t)z * kAkLevels + i].det_base);
+                }
+        }
+        DP_HIP(c, s->akz_pids.reserve(pids.size() + nv));
+        DP_HIP(c, s->akz_pbase.reserve(pbase.size()));
+        DP_HIP(c, s->akz_vids.reserve(nv));
+        DP_HIP(c, hipMemcpyAsync(s->akz_pids.p, pids.data(), pids.size() * 4, hipMemcpyHostToDevice, st));
+        DP_HIP(c, hipMemcpyAsync(s->akz_pbase.p, pbase.data(), pbase.size() * 8, hipMemcpyHostToDevice, st));
+        DP_HIP(c, hipMemcpyAsync(s->akz_vids.p, vids.data(), nv * 4, hipMemcpyHostToDevice, st));
+        DP_HIP(c, s->kp_a.reserve(n_cand + 1));
+        DP_HIP(c, s->kv_a.reserve(n_cand + 1));
+        DP_HIP(c, s->kp_b.reserve(n_cand + 1));
+        DP_HIP(c, s->kv_b.reserve(n_cand + 1));
+        DP_HIP(c, s->flag.reserve(n_cand + 1));
+        DP_HIP(c, s->idx_a.reserve(n_cand + 1));
+        AkCandArgs ca{s->akz_planes.p, s->akz_pool.p, s->akz_cand.p, n_cand, s->akz_pids.p, s->akz_pbase.p,
+                      (int32_t)pids.size(), s->akz_vids.p, s->kp_b.p, s->kv_b.p, s->flag.p};
+        DP_HIP(c, launch_akz_candidates(ca, st));
+        {
+            hipcub::CountingInputIterator<int32_t> iota(0);
+            DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, iota, s->flag.p, s->idx_a.p, s->n_sel.p,
+                                                        (int)n_cand, st));
+        }
+        int64_t n_det = 0;
+        DP_HIP(c, hipMemcpyAsync(&n_det, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        DP_HIP(c, hipStreamSynchronize(st));
+        DP_HIP(c, dpk::launch_gather_kp(s->kp_b.p, s->kv_b.p, s->idx_a.p, n_det, s->kp_a.p, s->kv_a.p, st));
+        n_det_total += n_det;
+        int64_t n_f = 0;
+        int rc = cell_filter(c, s, mo, vw, vh, n_det, &n_f);
+        if (rc != DP_OK)
+            return rc;
+        if (v0 == 0 && v1 == V) {
+            DP_HIP(c, hipEventRecord(e1, st));
+            e1_done = true;
+        }
+        DP_HIP(c, s->desc.reserve((size_t)(n_f + 1) * kAkDescWords));
+        AkDescArgs da{s->akz_planes.p, s->akz_pool.p, s->kv_b.p, v0, s->kp_b.p, n_f, s->akz_g25.p, s->akz_bits.p,
+                      n_windows, s->desc.p};
+        DP_HIP(c, launch_akz_describe(da, st));
+        const size_t k0 = all_kp.size();
+        all_kp.resize(k0 + n_f);
+        h_kv.resize(k0 + n_f);
+        all_desc.resize((k0 + n_f) * kAkDescWords);
+        DP_HIP(c, hipMemcpyAsync(all_kp.data() + k0, s->kp_b.p, n_f * sizeof(dp_keypoint), hipMemcpyDeviceToHost, st));
+        DP_HIP(c, hipMemcpyAsync(h_kv.data() + k0, s->kv_b.p, n_f * 4, hipMemcpyDeviceToHost, st));
+        DP_HIP(c, hipMemcpyAsync(all_desc.data() + k0 * kAkDescWords, s->desc.p, n_f * kAkDescWords * 4,
+                                 hipMemcpyDeviceToHost, st));
+        DP_HIP(c, hipStreamSynchronize(st));
+        v0 = v1;
+    }
+    if (!e1_done)
+        DP_HIP(c, hipEventRecord(e1, st));
+    const int64_t n = (int64_t)all_kp.size();
+    DP_HIP(c, s->kp_b.reserve(n + 1));
+    DP_HIP(c, s->kv_b.reserve(n + 1));
+    DP_HIP(c, s->desc.reserve((size_t)(n + 1) * kAkDescWords));
+    if (n > 0) {
+        DP_HIP(c, hipMemcpyAsync(s->kp_b.p, all_kp.data(), n * sizeof(dp_keypoint), hipMemcpyHostToDevice, st));
+        DP_HIP(c, hipMemcpyAsync(s->kv_b.p, h_kv.data(), n * 4, hipMemcpyHostToDevice, st));
+        DP_HIP(c, hipMemcpyAsync(s->desc.p, all_desc.data(), n * kAkDescWords * 4, hipMemcpyHostToDevice, st));
+    }
+    DP_HIP(c, hipEventRecord(e2, st));
+    DP_HIP(c, hipStreamSynchronize(st));
+    s->h_kp = all_kp;
+    S.keypoints_detected = n_det_total;
+    S.keypoints = n;
+    *n_out = n;
     return DP_OK;
 }
 
@@ -412,7 +798,22 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     const auto t_wall0 = std::chrono::steady_clock::now();
     const int V = c->V, L = mo.n_levels;
     dp_seed_stats S{};
-
+    std::vector<int32_t> vw(V), vh(V);
+    for (int v = 0; v < V; ++v) {
+        vw[v] = c->hv[v].W;
+        vh[v] = c->hv[v].H;
+    }
+    Timer t0, t1, t2, t3, t4;
+    int64_t n5 = 0;
+    std::vector<int32_t> h_kv;
+    DP_HIP(c, s->n_sel.reserve(1));
+    if (mo.detector_type == DP_DETECTOR_AKAZE) {
+        s->desc_words = dpk::kAkDescWords;
+        rc = akaze_stage(c, s, mo, vw, vh, t0.e, t1.e, t2.e, S, &n5, h_kv);
+        if (rc != DP_OK)
+            return rc;
+    } else {
+    s->desc_words = 8;
     // ---- pyramid geometry (ORB_Impl: layerScale, level sizes, features/level)
     std::vector<int32_t> nfeat(L);
     dpk::orb_features_per_level(mo.n_features, mo.scale_factor, L, nfeat.data());
@@ -420,10 +821,7 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     int64_t pool = 0, rows = 0;
     int max_w = 0, max_h = 0;
     std::vector<int> lw(L, 0), lh(L, 0); // per-level launch extents (max over views)
-    std::vector<int32_t> vw(V), vh(V);
     for (int v = 0; v < V; ++v) {
-        vw[v] = c->hv[v].W;
-        vh[v] = c->hv[v].H;
         for (int l = 0; l < L; ++l) {
             const float sc = (float)std::pow(mo.scale_factor, (double)l);
             dpk::OrbLevel &o = lv[(size_t)v * L + l];
@@ -458,7 +856,6 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     DP_HIP(c, s->row_off.reserve(rows + 1));
     dpk::OrbGeom g{s->lv.p, V, L, s->gray.p};
 
-    Timer t0, t1, t2, t3, t4;
     DP_HIP(c, hipEventRecord(t0.e, st));
     // ---- DetectKeypoints (matcher.cpp:45-87)
     DP_HIP(c, dpk::launch_orb_gray(s->planes0.p, g, lv[0].w > 0 ? max_w : 0, max_h, st));
@@ -530,40 +927,10 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     S.keypoints_detected = n3;
 
     // ---- FilterKeypoints (matcher.cpp:89-153)
-    std::vector<int32_t> gcols(V);
-    std::vector<int64_t> cell_off(V + 1, 0);
-    for (int v = 0; v < V; ++v) {
-        gcols[v] = (vw[v] + mo.cell_size - 1) / mo.cell_size;
-        const int64_t grows = (vh[v] + mo.cell_size - 1) / mo.cell_size;
-        if ((int64_t)gcols[v] * grows >= (1ll << 24))
-            return fail(c, DP_E_ARG, "dp_generate_seeds: more than 2^24 keypoint cells per view");
-        cell_off[v + 1] = cell_off[v] + (int64_t)gcols[v] * grows;
-    }
-    DP_HIP(c, s->gcols.reserve(V));
-    DP_HIP(c, s->cell_off.reserve(V + 1));
-    DP_HIP(c, s->cell_cnt.reserve(cell_off[V] + 1));
-    DP_HIP(c, hipMemcpyAsync(s->gcols.p, gcols.data(), V * 4, hipMemcpyHostToDevice, st));
-    DP_HIP(c, hipMemcpyAsync(s->cell_off.p, cell_off.data(), (V + 1) * 8, hipMemcpyHostToDevice, st));
-    DP_HIP(c, hipMemsetAsync(s->cell_cnt.p, 0, (size_t)(cell_off[V] + 1) * 4, st));
-    DP_HIP(c, s->ckey.reserve(n3 + 1));
-    DP_HIP(c, s->ckey_sorted.reserve(n3 + 1));
-    DP_HIP(c, s->idx_a.reserve(n3 + 1));
-    DP_HIP(c, s->idx_b.reserve(n3 + 1));
-    DP_HIP(c, s->flag.reserve(n3 + 1));
-    DP_HIP(c, dpk::launch_cell_count(s->kp_a.p, s->kv_a.p, n3, s->gcols.p, s->cell_off.p, mo.cell_size, s->cell_cnt.p,
-                                     st));
-    DP_HIP(c, dpk::launch_cell_key(s->kp_a.p, s->kv_a.p, n3, s->gcols.p, s->cell_off.p, mo.cell_size,
-                                   mo.max_keypoints_per_cell, s->cell_cnt.p, s->ckey.p, s->idx_a.p, st));
-    if (n3 > 0)
-        DP_CUB(c, s, hipcub::DeviceRadixSort::SortPairs(_tmp, _bytes, s->ckey.p, s->ckey_sorted.p, s->idx_a.p,
-                                                         s->idx_b.p, (int)n3, 0, 64, st));
-    DP_HIP(c, dpk::launch_cell_keep(s->ckey_sorted.p, n3, mo.max_keypoints_per_cell, s->flag.p, st));
-    DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, s->idx_b.p, s->flag.p, s->idx_a.p, s->n_sel.p, (int)n3,
-                                                st));
     int64_t n4 = 0;
-    DP_HIP(c, hipMemcpyAsync(&n4, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    DP_HIP(c, hipStreamSynchronize(st));
-    DP_HIP(c, dpk::launch_gather_kp(s->kp_a.p, s->kv_a.p, s->idx_a.p, n4, s->kp_b.p, s->kv_b.p, st));
+    rc = cell_filter(c, s, mo, vw, vh, n3, &n4);
+    if (rc != DP_OK)
+        return rc;
 
     // ---- ComputeDescriptors (matcher.cpp:155-183): runByImageBorder, stable by octave
     DP_HIP(c, s->vw.reserve(V));
@@ -578,7 +945,6 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
         hipcub::CountingInputIterator<int32_t> iota(0);
         DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, iota, s->flag.p, s->idx_a.p, s->n_sel.p, (int)n4, st));
     }
-    int64_t n5 = 0;
     DP_HIP(c, hipMemcpyAsync(&n5, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     DP_HIP(c, hipStreamSynchronize(st));
     DP_HIP(c, dpk::launch_gather_kp(s->kp_b.p, s->kv_b.p, s->idx_a.p, n5, s->kp_a.p, s->kv_a.p, st));
@@ -592,7 +958,7 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     S.keypoints = n5;
     // per-view counts (host)
     s->h_kp.resize(n5);
-    std::vector<int32_t> h_kv(n5);
+    h_kv.resize(n5);
     DP_HIP(c, hipMemcpyAsync(s->h_kp.data(), s->kp_b.p, n5 * sizeof(dp_keypoint), hipMemcpyDeviceToHost, st));
     DP_HIP(c, hipMemcpyAsync(h_kv.data(), s->kv_b.p, n5 * 4, hipMemcpyDeviceToHost, st));
     DP_HIP(c, hipEventRecord(t1.e, st));
@@ -605,14 +971,15 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     DP_HIP(c, dpk::launch_orb_desc(g, s->kp_b.p, s->kv_b.p, n5, s->pattern.p, s->desc.p, st));
     DP_HIP(c, hipEventRecord(t2.e, st));
     DP_HIP(c, hipStreamSynchronize(st));
+    }
     s->h_kp_off.assign(V + 1, 0);
     for (int64_t i = 0; i < n5; ++i)
         s->h_kp_off[h_kv[i] + 1]++;
     for (int v = 0; v < V; ++v)
         s->h_kp_off[v + 1] += s->h_kp_off[v];
     for (int v = 0; v < V; ++v)
-        if (s->h_kp_off[v + 1] - s->h_kp_off[v] >= (1 << 22))
-            return fail(c, DP_E_ARG, "dp_generate_seeds: more than 2^22 keypoints in one view");
+        if (s->h_kp_off[v + 1] - s->h_kp_off[v] >= (1 << dpk::knn_row_bits(s->desc_words)))
+            return fail(c, DP_E_ARG, "dp_generate_seeds: more than 2^22 (ORB) / 2^21 (AKAZE) keypoints in one view");
 
     // ---- DefaultPairsList + MatchKeypoints + FilterMatches
     s->h_pairs.clear();
@@ -652,13 +1019,13 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     static_assert(dpk::kNoMatch == 0x7F7F7F7F, "t2q sentinel is the 0x7F byte fill");
     DP_HIP(c, hipMemsetAsync(s->t2q.p, 0x7F, (size_t)(t2q_total + 1) * 4, st)); // kNoMatch > any index
     DP_HIP(c, hipMemsetAsync(s->counters.p, 0, 2 * sizeof(unsigned long long), st));
-    dpk::MatchArgs ma{s->jobs.p, s->pairs.p, np, q_total, s->keys.p, s->desc.p, s->kp_b.p,
+    dpk::MatchArgs ma{s->jobs.p, s->pairs.p, np, q_total, s->keys.p, s->desc.p, s->kp_b.p, s->desc_words,
                       mo.nn_match_ratio, mo.max_epipolar_distance, mo.matcher_type == DP_MATCHER_FLANN,
                       s->q2t.p, s->t2q.p, s->counters.p, s->counters.p + 1};
     if (mo.epipolar_matching) {
         DP_HIP(c, dpk::launch_epipolar_match(ma, st));
     } else {
-        rc = run_knn(c, s, s->h_jobs, q_total, s->keys.p, false);
+        rc = run_knn(c, s, s->h_jobs, q_total, s->keys.p, false, s->desc_words);
         if (rc != DP_OK)
             return rc;
         DP_HIP(c, dpk::launch_match(ma, st));
@@ -690,10 +1057,11 @@ extern "C" int dp_generate_seeds(dp_ctx *c, const dp_matcher_options *mo_in, con
     DP_HIP(c, hipMemcpyAsync(cnt, s->counters.p, sizeof(cnt), hipMemcpyDeviceToHost, st));
     DP_HIP(c, hipStreamSynchronize(st));
     s->h_xyz.resize((size_t)3 * n6);
-    s->h_desc.resize((size_t)32 * n5);
+    const size_t dbytes = (size_t)4 * s->desc_words;
+    s->h_desc.resize(dbytes * n5);
     s->h_q2t.resize(q_total);
     DP_HIP(c, hipMemcpyAsync(s->h_xyz.data(), s->obs.p, (size_t)n6 * 24, hipMemcpyDeviceToHost, st));
-    DP_HIP(c, hipMemcpyAsync(s->h_desc.data(), s->desc.p, (size_t)n5 * 32, hipMemcpyDeviceToHost, st));
+    DP_HIP(c, hipMemcpyAsync(s->h_desc.data(), s->desc.p, (size_t)n5 * dbytes, hipMemcpyDeviceToHost, st));
     DP_HIP(c, hipMemcpyAsync(s->h_q2t.data(), s->q2t.p, (size_t)q_total * 4, hipMemcpyDeviceToHost, st));
     DP_HIP(c, hipStreamSynchronize(st));
     S.ratio_matches = (int64_t)cnt[0];
@@ -725,9 +1093,19 @@ extern "C" int dp_seed_keypoints(dp_ctx *c, int view, const dp_keypoint **kp, co
     if (kp)
         *kp = s->h_kp.data() + a;
     if (desc32)
-        *desc32 = s->h_desc.data() + 32 * a;
+        *desc32 = s->h_desc.data() + (size_t)4 * s->desc_words * a;
     *n = b - a;
     return DP_OK;
+}
+
+extern "C" int dp_seed_descriptor_bytes(dp_ctx *c)
+{
+    if (!c)
+        return DP_E_ARG;
+    dp_seedgen *s = c->seeds;
+    if (!s || !s->have_stages)
+        return fail(c, DP_E_STATE, "dp_seed_descriptor_bytes: no dp_generate_seeds result");
+    return 4 * s->desc_words;
 }
 
 extern "C" int dp_seed_matches(dp_ctx *c, int pair, int32_t *first, int32_t *second, const int32_t **q2t, int64_t *nq)

@@ -1,8 +1,8 @@
 """Features::Matcher (modules/features/matcher.h:35-69) over the C ABI.
 
-GenerateSeeds (matcher.cpp:18-43) runs entirely on the device: ORB detect,
-per-cell filter, rBRIEF descriptors, brute-force Hamming kNN on MFMA, ratio
-and epipolar filters, multi-view DLT.  The standalone operators mirror the
+GenerateSeeds (matcher.cpp:18-43) runs entirely on the device: ORB (default)
+or AKAZE detect, per-cell filter, rBRIEF / M-LDB descriptors, brute-force
+Hamming kNN on MFMA, ratio and epipolar filters, multi-view DLT.  The standalone operators mirror the
 reference's free functions (knnMatch, Geometry::ComputeFundamentalMatrix,
 Geometry::DirectLinearTriangulation).
 """
@@ -35,6 +35,10 @@ class MatcherOptions:
     # MatcherType (matcher.h:12): KNN (default) or FLANN -- the LSH match() kept
     # iff distance < 30, answered exactly (include/densepoints.h DP_MATCHER_FLANN)
     matcher_type: int = 0
+    # DetectorType (matcher.h:11): ORB (default) or AKAZE (AKAZE::create()
+    # defaults, M-LDB 486-bit descriptors; threshold 0.001 unless set)
+    detector_type: int = 1
+    akaze_threshold: float = 0.001
 
     def to_c(self) -> N.DpMatcherOptions:
         o = N.DpMatcherOptions()
@@ -46,6 +50,7 @@ class MatcherOptions:
 
 
 MATCHER_KNN, MATCHER_FLANN = 0, 1
+DETECTOR_AKAZE, DETECTOR_ORB = 0, 1
 
 
 class Matcher:
@@ -78,11 +83,13 @@ class Matcher:
         n = ctypes.c_int64()
         check(lib.dp_seed_keypoints(self.engine.handle, view, ctypes.byref(kp), ctypes.byref(desc), ctypes.byref(n)),
               self.engine.handle)
+        db = lib.dp_seed_descriptor_bytes(self.engine.handle)
+        check(min(db, 0), self.engine.handle)
         k = np.zeros(n.value, dtype=KEYPOINT_DTYPE)
-        d = np.zeros((n.value, 32), dtype=np.uint8)
+        d = np.zeros((n.value, db), dtype=np.uint8)
         if n.value:
             ctypes.memmove(k.ctypes.data, kp.value, n.value * KEYPOINT_DTYPE.itemsize)
-            ctypes.memmove(d.ctypes.data, desc.value, n.value * 32)
+            ctypes.memmove(d.ctypes.data, desc.value, n.value * db)
         return k, d
 
     def matches(self, pair: int):
@@ -99,13 +106,15 @@ class Matcher:
         return a.value, b.value, m
 
 
-def knn_match(engine, query: np.ndarray, train: np.ndarray):
-    """BFMatcher(NORM_HAMMING).knnMatch(query, train, 2): (idx2, dist2), -1 where absent."""
-    q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, 32)
-    t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, 32)
+def knn_match(engine, query: np.ndarray, train: np.ndarray, width: int = 32):
+    """BFMatcher(NORM_HAMMING).knnMatch(query, train, 2) on `width`-byte rows
+    (32 ORB, 64 AKAZE): (idx2, dist2), -1 where absent."""
+    q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, width)
+    t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, width)
     idx = np.zeros((len(q), 2), dtype=np.int32)
     dist = np.zeros((len(q), 2), dtype=np.int32)
-    check(lib.dp_knn_match(engine.handle, ptr(q), len(q), ptr(t), len(t), ptr(idx), ptr(dist)), engine.handle)
+    check(lib.dp_knn_match_wide(engine.handle, ptr(q), len(q), ptr(t), len(t), width, ptr(idx), ptr(dist)),
+          engine.handle)
     return idx, dist
 
 

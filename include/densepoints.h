@@ -371,6 +371,12 @@ int dp_filter_patches_device(dp_ctx *ctx, const dp_patch *d_patches, int64_t n, 
  *   FilterMatches     matcher.cpp:319-372 epipolar distance <= 1.5f, F from
  *                                         geometry/fundamental_matrix.cpp:6-53
  *   TriangulateMatches matcher.cpp:374-450 DLT, geometry/triangulation.cpp:15-34
+ * DetectorType::AKAZE (matcher.cpp:56-60, 166-170: cv::AKAZE::create()
+ * defaults -- MLDB 486 bits, threshold 0.001, 4 octaves x 4 sublevels, PM_G2)
+ * is selected by detector_type = DP_DETECTOR_AKAZE: descriptors are then 64
+ * bytes (486 bits, zero padded; dp_seed_descriptor_bytes), FilterKeypoints and
+ * the matching stages are unchanged.  Its restated arithmetic is
+ * oracle/or_akaze.c's header (parity unpinned against OpenCV).
  * OpenCV's ORB is restated, not reproduced bit-for-bit (OpenCV is absent from
  * the image; DESIGN.md "Seed generation" lists the restated semantics and the
  * points that are parity-unpinned; the rBRIEF sampling pattern is OpenCV's own
@@ -390,7 +396,12 @@ typedef struct dp_matcher_options {
     float max_epipolar_distance;    /* 1.5f  matcher.h:24                             */
     float nn_match_ratio;           /* 0.7f  matcher.cpp:217                          */
     int32_t matcher_type;           /* DP_MATCHER_KNN  MatcherOptions::matcher_type    */
+    int32_t detector_type;          /* DP_DETECTOR_ORB MatcherOptions::detector_type   */
+    float akaze_threshold;          /* 0.001f  AKAZE::create() detector threshold      */
 } dp_matcher_options;
+/* DetectorType (matcher.h:11, the reference's enum order) */
+#define DP_DETECTOR_AKAZE 0
+#define DP_DETECTOR_ORB 1
 /* MatcherType (matcher.h:12, MatchKeypoints matcher.cpp:206-265):
  *  DP_MATCHER_KNN    BruteForce-Hamming knnMatch k = 2, ratio test d0 < 0.7 d1
  *  DP_MATCHER_FLANN  FlannBasedMatcher(LshIndexParams(12, 20, 2)).match, kept iff
@@ -433,8 +444,11 @@ int dp_orb_pattern(int8_t *xy_out);
  * is context-owned, valid until the next dp_generate_seeds or destroy. */
 int dp_generate_seeds(dp_ctx *ctx, const dp_matcher_options *mo, const double **xyz_out, int64_t *n_out,
                       dp_seed_stats *stats);
-/* Stage results of the last dp_generate_seeds (context-owned, host copies). */
+/* Stage results of the last dp_generate_seeds (context-owned, host copies);
+ * descriptor rows are dp_seed_descriptor_bytes wide (32 ORB, 64 AKAZE).  An
+ * AKAZE keypoint's `reserved` holds its evolution level (class_id). */
 int dp_seed_keypoints(dp_ctx *ctx, int view, const dp_keypoint **kp, const uint8_t **desc32, int64_t *n);
+int dp_seed_descriptor_bytes(dp_ctx *ctx);
 int dp_seed_matches(dp_ctx *ctx, int pair, int32_t *first, int32_t *second, const int32_t **query_to_train,
                     int64_t *nq);
 
@@ -444,6 +458,9 @@ int dp_seed_matches(dp_ctx *ctx, int pair, int32_t *first, int32_t *second, cons
  * -1 / -1 where train has fewer rows.  nt < 2^22. */
 int dp_knn_match(dp_ctx *ctx, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt,
                  int32_t *idx2, int32_t *dist2);
+/* the same for descriptor_bytes 32 or 64 (AKAZE rows; nt < 2^21 for 64) */
+int dp_knn_match_wide(dp_ctx *ctx, const uint8_t *query, int64_t nq, const uint8_t *train, int64_t nt,
+                      int descriptor_bytes, int32_t *idx2, int32_t *dist2);
 /* Geometry::ComputeFundamentalMatrix (fundamental_matrix.cpp:6-34), F 3x3 row-major. */
 int dp_fundamental_matrix(const double P1[12], const double P2[12], double F[9]);
 /* Geometry::DirectLinearTriangulation (triangulation.cpp:15-34), batched: point

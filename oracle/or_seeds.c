@@ -26,18 +26,7 @@
 #include "or_detmath.h"
 #include "or_orb_pattern.h"
 
-typedef struct or_keypoint {
-    float x, y, response, angle;
-    int32_t octave, reserved;
-} or_keypoint;
-
-typedef struct or_matcher_options {
-    int32_t n_features, n_levels;
-    double scale_factor;
-    int32_t edge_threshold, fast_threshold, cell_size, max_keypoints_per_cell, epipolar_matching;
-    float max_epipolar_distance, nn_match_ratio;
-    int32_t matcher_type; /* 0 kNN ratio test, 1 FLANN (exact 1-NN, distance < 30) */
-} or_matcher_options;
+#include "or_seeds_types.h"
 
 /* ------------------------------------------------------------------------ */
 /* pattern, umax, features per level                                         */
@@ -377,9 +366,8 @@ static int cmp_ri(const void *a, const void *b)
     return x->idx - y->idx;
 }
 
-static int filter_keypoints(or_keypoint *kp, int n, int W, int H, const or_matcher_options *mo)
+int or_cell_filter(or_keypoint *kp, int n, int W, int H, int cs, int maxk)
 {
-    const int cs = mo->cell_size, maxk = mo->max_keypoints_per_cell;
     const int cols = (W + cs - 1) / cs, rows = (H + cs - 1) / cs;
     const int ncell = cols * rows;
     int *cnt = (int *)calloc((size_t)ncell + 1, sizeof(int));
@@ -415,13 +403,27 @@ static int filter_keypoints(or_keypoint *kp, int n, int W, int H, const or_match
                 out[m++] = kp[tmp[j].idx];
         }
     }
+    memcpy(kp, out, sizeof(or_keypoint) * (size_t)m);
+    free(cnt);
+    free(cell);
+    free(members);
+    free(fill);
+    free(out);
+    free(tmp);
+    return m;
+}
+
+static int filter_keypoints(or_keypoint *kp, int n, int W, int H, const or_matcher_options *mo)
+{
+    const int m = or_cell_filter(kp, n, W, H, mo->cell_size, mo->max_keypoints_per_cell);
     /* runByImageBorder(image, edge): Rect<int>::contains(Point(cvRound(pt))) */
     const int e = mo->edge_threshold;
+    or_keypoint *out = (or_keypoint *)malloc(sizeof(or_keypoint) * (size_t)(m + 1));
     int m2 = 0;
     for (int i = 0; i < m; ++i) {
-        int px = (int)lrintf(out[i].x), py = (int)lrintf(out[i].y);
+        int px = (int)lrintf(kp[i].x), py = (int)lrintf(kp[i].y);
         if (W > 2 * e && H > 2 * e && px >= e && px < W - e && py >= e && py < H - e)
-            out[m2++] = out[i];
+            out[m2++] = kp[i];
     }
     /* stable bucketing by octave */
     int k = 0;
@@ -429,12 +431,7 @@ static int filter_keypoints(or_keypoint *kp, int n, int W, int H, const or_match
         for (int i = 0; i < m2; ++i)
             if (out[i].octave == l)
                 kp[k++] = out[i];
-    free(cnt);
-    free(cell);
-    free(members);
-    free(fill);
     free(out);
-    free(tmp);
     return k;
 }
 
@@ -470,10 +467,10 @@ static void describe(const Level *lv, const or_keypoint *kp, int n, const int8_t
 /* ------------------------------------------------------------------------ */
 /* matching                                                                  */
 /* ------------------------------------------------------------------------ */
-static int hamming32(const uint8_t *a, const uint8_t *b)
+static int hamming_n(const uint8_t *a, const uint8_t *b, int bytes)
 {
     int d = 0;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < bytes / 8; ++i) {
         uint64_t x, y;
         memcpy(&x, a + 8 * i, 8);
         memcpy(&y, b + 8 * i, 8);
@@ -483,12 +480,13 @@ static int hamming32(const uint8_t *a, const uint8_t *b)
 }
 
 /* BFMatcher(NORM_HAMMING).knnMatch(k = 2): batchDistance's strict-< insertion */
-int or_knn_match(const uint8_t *q, int64_t nq, const uint8_t *t, int64_t nt, int32_t *idx2, int32_t *dist2)
+int or_knn_match_w(const uint8_t *q, int64_t nq, const uint8_t *t, int64_t nt, int bytes, int32_t *idx2,
+                   int32_t *dist2)
 {
     for (int64_t i = 0; i < nq; ++i) {
         int d0 = 1 << 30, d1 = 1 << 30, i0 = -1, i1 = -1;
         for (int64_t j = 0; j < nt; ++j) {
-            int d = hamming32(q + 32 * i, t + 32 * j);
+            int d = hamming_n(q + (size_t)bytes * i, t + (size_t)bytes * j, bytes);
             if (d < d1) {
                 if (d < d0) {
                     d1 = d0;
@@ -507,6 +505,11 @@ int or_knn_match(const uint8_t *q, int64_t nq, const uint8_t *t, int64_t nt, int
         dist2[2 * i + 1] = i1 < 0 ? -1 : d1;
     }
     return 0;
+}
+
+int or_knn_match(const uint8_t *q, int64_t nq, const uint8_t *t, int64_t nt, int32_t *idx2, int32_t *dist2)
+{
+    return or_knn_match_w(q, nq, t, nt, 32, idx2, dist2);
 }
 
 static double det3c(const double *a, const double *b, const double *c)
@@ -679,7 +682,8 @@ typedef struct or_seeds {
     int V, npairs;
     int64_t *kp_off;      /* V + 1 */
     or_keypoint *kp;      /* all views */
-    uint8_t *desc;        /* 32 B per keypoint */
+    uint8_t *desc;        /* dbytes per keypoint */
+    int dbytes;           /* 32 (ORB) or 64 (AKAZE: 486 bits, zero padded) */
     int64_t n_detected;
     int32_t *pair_first, *pair_second;
     int64_t *q_off;       /* npairs + 1 */
@@ -702,34 +706,46 @@ or_seeds *or_seeds_run(int V, const double *P, const int32_t *W, const int32_t *
     int *nv = (int *)calloc((size_t)V, sizeof(int));
     int8_t pat[1024];
     or_orb_pattern(pat);
+    const int akaze = mo->detector_type == 0;
+    const int db = akaze ? 64 : 32;
+    r->dbytes = db;
     for (int v = 0; v < V; ++v) {
-        Level lv[16];
-        memset(lv, 0, sizeof(lv));
-        if (build_levels(bgr[v], W[v], H[v], mo, lv) != 0) {
-            for (int l = 0; l < 16; ++l) {
+        int n;
+        if (akaze) {
+            int64_t nd = 0;
+            n = or_akaze_view(bgr[v], W[v], H[v], mo, &kv[v], &dv[v], &nd);
+            if (n < 0)
+                return NULL;
+            r->n_detected += nd;
+        } else {
+            Level lv[16];
+            memset(lv, 0, sizeof(lv));
+            if (build_levels(bgr[v], W[v], H[v], mo, lv) != 0) {
+                for (int l = 0; l < 16; ++l) {
+                    free(lv[l].img);
+                    free(lv[l].blur);
+                }
+                return NULL;
+            }
+            n = orb_detect(lv, mo, &kv[v]);
+            r->n_detected += n;
+            n = filter_keypoints(kv[v], n, W[v], H[v], mo);
+            dv[v] = (uint8_t *)malloc((size_t)32 * (n + 1));
+            describe(lv, kv[v], n, pat, dv[v]);
+            for (int l = 0; l < mo->n_levels; ++l) {
                 free(lv[l].img);
                 free(lv[l].blur);
             }
-            return NULL;
         }
-        int n = orb_detect(lv, mo, &kv[v]);
-        r->n_detected += n;
-        n = filter_keypoints(kv[v], n, W[v], H[v], mo);
         nv[v] = n;
-        dv[v] = (uint8_t *)malloc((size_t)32 * (n + 1));
-        describe(lv, kv[v], n, pat, dv[v]);
-        for (int l = 0; l < mo->n_levels; ++l) {
-            free(lv[l].img);
-            free(lv[l].blur);
-        }
         r->kp_off[v + 1] = r->kp_off[v] + n;
     }
     int64_t nk = r->kp_off[V];
     r->kp = (or_keypoint *)malloc(sizeof(or_keypoint) * (size_t)(nk + 1));
-    r->desc = (uint8_t *)malloc((size_t)32 * (nk + 1));
+    r->desc = (uint8_t *)malloc((size_t)db * (nk + 1));
     for (int v = 0; v < V; ++v) {
         memcpy(r->kp + r->kp_off[v], kv[v], sizeof(or_keypoint) * (size_t)nv[v]);
-        memcpy(r->desc + 32 * r->kp_off[v], dv[v], (size_t)32 * nv[v]);
+        memcpy(r->desc + db * r->kp_off[v], dv[v], (size_t)db * nv[v]);
         free(kv[v]);
         free(dv[v]);
     }
@@ -765,7 +781,7 @@ or_seeds *or_seeds_run(int V, const double *P, const int32_t *W, const int32_t *
         if (!mo->epipolar_matching) {
             int32_t *i2 = (int32_t *)malloc(sizeof(int32_t) * 2 * (size_t)(nq + 1));
             int32_t *d2 = (int32_t *)malloc(sizeof(int32_t) * 2 * (size_t)(nq + 1));
-            or_knn_match(r->desc + 32 * r->kp_off[i], nq, r->desc + 32 * r->kp_off[j], nt, i2, d2);
+            or_knn_match_w(r->desc + db * r->kp_off[i], nq, r->desc + db * r->kp_off[j], nt, db, i2, d2);
             const int flann = mo->matcher_type == 1;
             for (int64_t q = 0; q < nq; ++q) {
                 q2t[q] = -1;
@@ -877,9 +893,11 @@ int64_t or_seeds_view(const or_seeds *r, int v, or_keypoint *kp, uint8_t *desc)
     if (kp)
         memcpy(kp, r->kp + a, sizeof(or_keypoint) * (size_t)n);
     if (desc)
-        memcpy(desc, r->desc + 32 * a, (size_t)(32 * n));
+        memcpy(desc, r->desc + (size_t)r->dbytes * a, (size_t)r->dbytes * n);
     return n;
 }
+
+int or_seeds_desc_bytes(const or_seeds *r) { return r->dbytes; }
 
 int64_t or_seeds_pair(const or_seeds *r, int p, int32_t *first_second, int32_t *q2t)
 {

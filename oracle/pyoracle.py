@@ -125,6 +125,11 @@ def _load():
         "or_seeds_view": (ctypes.c_int64, [P, ctypes.c_int, P, P]),
         "or_seeds_pair": (ctypes.c_int64, [P, ctypes.c_int, P, P]),
         "or_seeds_points": (None, [P, P]),
+        "or_seeds_desc_bytes": (ctypes.c_int, [P]),
+        "or_knn_match_w": (ctypes.c_int, [P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int, P, P]),
+        # AKAZE (or_akaze.c)
+        "or_akaze_levels": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P, P]),
+        "or_akaze_plane": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)
@@ -501,8 +506,12 @@ class OrMatcherOptions(ctypes.Structure):
         ("max_epipolar_distance", ctypes.c_float),
         ("nn_match_ratio", ctypes.c_float),
         ("matcher_type", ctypes.c_int32),
+        ("detector_type", ctypes.c_int32),
+        ("akaze_threshold", ctypes.c_float),
     ]
 
+
+DETECTOR_AKAZE, DETECTOR_ORB = 0, 1
 
 KEYPOINT_DTYPE = np.dtype(
     [("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("angle", "<f4"), ("octave", "<i4"), ("reserved", "<i4")]
@@ -512,7 +521,7 @@ KEYPOINT_DTYPE = np.dtype(
 def matcher_options(**kw) -> OrMatcherOptions:
     o = OrMatcherOptions(n_features=40000, n_levels=8, scale_factor=1.2, edge_threshold=31, fast_threshold=20,
                          cell_size=16, max_keypoints_per_cell=4, epipolar_matching=0, max_epipolar_distance=1.5,
-                         nn_match_ratio=0.7, matcher_type=0)
+                         nn_match_ratio=0.7, matcher_type=0, detector_type=DETECTOR_ORB, akaze_threshold=0.001)
     for k, v in kw.items():
         setattr(o, k, int(v) if isinstance(v, bool) else v)
     return o
@@ -530,13 +539,35 @@ def features_per_level(n, sf, L) -> np.ndarray:
     return a
 
 
-def knn_match(q: np.ndarray, t: np.ndarray):
-    q = np.ascontiguousarray(q, dtype=np.uint8).reshape(-1, 32)
-    t = np.ascontiguousarray(t, dtype=np.uint8).reshape(-1, 32)
+def knn_match(q: np.ndarray, t: np.ndarray, width: int = 32):
+    q = np.ascontiguousarray(q, dtype=np.uint8).reshape(-1, width)
+    t = np.ascontiguousarray(t, dtype=np.uint8).reshape(-1, width)
     idx = np.zeros((len(q), 2), dtype=np.int32)
     dist = np.zeros((len(q), 2), dtype=np.int32)
-    lib.or_knn_match(_p(q), len(q), _p(t), len(t), _p(idx), _p(dist))
+    lib.or_knn_match_w(_p(q), len(q), _p(t), len(t), width, _p(idx), _p(dist))
     return idx, dist
+
+
+def akaze_levels(W: int, H: int):
+    """AKAZE evolution levels: (w, h, octave, sigma_size, FED steps) rows, esigma"""
+    info = np.zeros((16, 5), dtype=np.int32)
+    es = np.zeros(16, dtype=np.float32)
+    n = lib.or_akaze_levels(W, H, _p(info), _p(es))
+    return info[:n], es[:n]
+
+
+def akaze_plane(img_bgr: np.ndarray, level: int, which: int):
+    """one plane of the AKAZE scale space of a BGR8 view (0 Lt, 1 Lx, 2 Ly,
+    3 Ldet) and the contrast factor per level"""
+    img = np.ascontiguousarray(img_bgr, dtype=np.uint8)
+    H, W = img.shape[:2]
+    info, _ = akaze_levels(W, H)
+    w, h = int(info[level, 0]), int(info[level, 1])
+    out = np.zeros((h, w), dtype=np.float32)
+    kc = np.zeros(16, dtype=np.float32)
+    if lib.or_akaze_plane(_p(img), W, H, level, which, _p(out), _p(kc)) != 0:
+        raise ValueError("or_akaze_plane failed")
+    return out, kc[: len(info)]
 
 
 def fundamental_matrix(P1, P2) -> np.ndarray:
@@ -580,10 +611,11 @@ def seeds_run(P: np.ndarray, images: list, mo: OrMatcherOptions | None = None) -
         out = {"counts": dict(zip(["views", "pairs", "detected", "keypoints", "ratio_matches", "matches", "points"],
                                   c.tolist())),
                "keypoints": [], "descriptors": [], "pairs": [], "q2t": []}
+        db = lib.or_seeds_desc_bytes(h)
         for v in range(V):
             n = lib.or_seeds_view(h, v, None, None)
             kp = np.zeros(n, dtype=KEYPOINT_DTYPE)
-            d = np.zeros((n, 32), dtype=np.uint8)
+            d = np.zeros((n, db), dtype=np.uint8)
             lib.or_seeds_view(h, v, _p(kp), _p(d))
             out["keypoints"].append(kp)
             out["descriptors"].append(d)

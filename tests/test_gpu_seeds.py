@@ -250,3 +250,50 @@ def test_generate_seeds_flann_matcher(orc):
     with engine_with(P, imgs) as eng:
         m = compare_run(eng, r, kw, 4)
         assert m.stats["points"] > 100
+
+
+# ---- DetectorType::AKAZE (matcher.cpp:56-60, 166-170; oracle/or_akaze.c) ----
+@pytest.mark.parametrize("kind,thr", [(0, 0.0002), (1, 0.001)])
+def test_generate_seeds_akaze_matches_oracle(orc, kind, thr):
+    """AKAZE detect + FilterKeypoints + M-LDB + kNN on 512-bit rows + DLT:
+    every stage bit-exact against the oracle (threshold 0.001 is
+    AKAZE::create()'s default)."""
+    cfg = synth.config(n_views=3, width=640, height=480, kind=kind)
+    P, imgs, _ = synth.scene_host(cfg)
+    kw = dict(detector_type=M.DETECTOR_AKAZE, akaze_threshold=thr)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    assert r["counts"]["keypoints"] > 20
+    with engine_with(P, imgs) as eng:
+        m = compare_run(eng, r, kw, 3)
+        assert m.keypoints(0)[1].shape[1] == 64
+
+
+def test_akaze_chunks_and_mixed_sizes(orc, monkeypatch):
+    """Views of different sizes (different level counts: 400 x 150 has two
+    octaves) and a chunk budget that puts every view in its own chunk give
+    the same keypoints, descriptors and seeds."""
+    cfg = synth.config(n_views=3, width=480, height=360, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    imgs = [imgs[0], np.ascontiguousarray(imgs[1][:150, :400]), imgs[2]]
+    kw = dict(detector_type=M.DETECTOR_AKAZE, akaze_threshold=0.0002, max_keypoints_per_cell=2, cell_size=24)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    with engine_with(P, imgs) as eng:
+        compare_run(eng, r, kw, 3)
+    monkeypatch.setenv("DP_AKAZE_CHUNK_BYTES", "1")
+    with engine_with(P, imgs) as eng:
+        compare_run(eng, r, kw, 3)
+
+
+@pytest.mark.parametrize("nq,nt", [(1, 0), (33, 2), (300, 129), (1000, 2500)])
+def test_knn_match_wide_matches_oracle(orc, nq, nt):
+    """knnMatch on 64-byte rows (the AKAZE descriptor width), ties included."""
+    rng = np.random.default_rng(nq * 31 + nt)
+    t = rng.integers(0, 256, size=(nt, 64), dtype=np.uint8)
+    q = rng.integers(0, 256, size=(nq, 64), dtype=np.uint8)
+    if nt > 8:
+        t[nt - 1] = t[3]
+        q[: nq // 3] = t[rng.integers(0, nt, nq // 3)]
+    io, do = orc.knn_match(q, t, width=64)
+    with dp.Engine() as eng:
+        ig, dg = M.knn_match(eng, q, t, width=64)
+    assert np.array_equal(dg, do) and np.array_equal(ig, io)

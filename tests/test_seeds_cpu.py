@@ -239,3 +239,99 @@ def test_oracle_flann_matcher_is_exact_nn_below_30(orc):
         q2t = r["q2t"][p]
         hit = q2t >= 0
         assert np.array_equal(q2t[hit], nn[hit]) and np.all(d0[hit] < 30)
+
+
+# ---- DetectorType::AKAZE (matcher.cpp:56-60, 166-170; oracle/or_akaze.c) ----
+def test_akaze_levels_and_fed_schedule(orc):
+    """cv::AKAZE defaults: 4 octaves x 4 sublevels (the octave stops below
+    80 x 40), esigma = 1.6 2^(j/4 + o), sigma_size = round(1.5 esigma / 2^o),
+    and fed.cpp's step count n = ceil(sqrt(3 T / tau_max + 1/4) - 1/2) for the
+    evolution time T between consecutive levels."""
+    info, es = orc.akaze_levels(640, 480)
+    assert len(info) == 16
+    assert [tuple(r[:3]) for r in info[::4]] == [(640, 480, 0), (320, 240, 1), (160, 120, 2), (80, 60, 3)]
+    for i, r in enumerate(info):
+        o, j = divmod(i, 4)
+        assert es[i] == np.float32(1.6 * 2.0 ** (j / 4 + o))
+        assert r[3] == int(np.rint(np.float32(es[i] * np.float32(1.5) / np.float32(2 ** o))))
+    assert info[0, 4] == 0 and np.all(info[1:, 4] >= 3) and np.all(np.diff(info[1:, 4]) >= 0)
+    assert len(orc.akaze_levels(640, 150)[0]) == 8  # 160 x 37 is below 40 rows: two octaves
+    # fed_tau_by_cycle_time's step count for the evolution time between levels
+    et = 0.5 * es.astype(np.float64) ** 2
+    n = info[1:, 4]
+    assert np.all(n == np.ceil(np.sqrt(3 * np.diff(et) / 0.25 + 0.25) - 0.5 - 1e-8).astype(int))
+
+
+def test_akaze_scale_space_is_diffusion(orc):
+    """The evolution is a diffusion: Lt of every level keeps the image mean
+    (zero-flux border, 2x2 averages between octaves) within fp32 rounding and
+    never sharpens (the gradient energy falls level by level inside an
+    octave); Ldet is the scaled Hessian determinant of a smoothed image."""
+    cfg = synth.config(n_views=1, width=320, height=240, kind=1)
+    _, imgs, _ = synth.scene_host(cfg)
+    m0, _ = orc.akaze_plane(imgs[0], 0, 0)
+    prev = None
+    for lev in range(1, 8):
+        lt, kc = orc.akaze_plane(imgs[0], lev, 0)
+        assert abs(lt.mean() - m0.mean()) < 2e-3
+        gx, gy = np.diff(lt, axis=1), np.diff(lt, axis=0)
+        e = (gx ** 2).mean() + (gy ** 2).mean()
+        if prev is not None and lev % 4 != 0:
+            assert e < prev
+        prev = e * (4 if lev % 4 == 3 else 1)
+    assert kc[0] > 0 and np.allclose(kc[4], kc[0] * np.float32(0.75))
+
+
+def test_akaze_oracle_keypoints_and_descriptors(orc):
+    """AKAZE through GenerateSeeds: 486-bit descriptors in 64-byte rows (the
+    padding bits zero), at most max_keypoints_per_cell per cell, keypoints
+    inside the descriptor border of their level, and seeds on the textured
+    plane (z = 0)."""
+    cfg = synth.config(n_views=3, width=640, height=480, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(detector_type=orc.DETECTOR_AKAZE, akaze_threshold=0.0002))
+    c = r["counts"]
+    assert c["keypoints"] > 300 and c["points"] > 50
+    info, _ = orc.akaze_levels(640, 480)
+    for kp, d in zip(r["keypoints"], r["descriptors"]):
+        assert d.shape[1] == 64 and not d[:, 61:].any() and not (d[:, 60] & 0xC0).any()
+        cells = (kp["y"].astype(np.int64) // 16) * 1000 + kp["x"].astype(np.int64) // 16
+        assert np.bincount(np.unique(cells, return_inverse=True)[1]).max() <= 4
+        lev = kp["reserved"]
+        assert np.all(kp["octave"] == info[lev, 2])
+        ss = info[lev, 3]
+        ra = 2.0 ** kp["octave"]
+        border = 10 * np.sqrt(2) * ss
+        assert np.all(kp["x"] / ra >= border - 1) and np.all(kp["x"] / ra <= info[lev, 0] - border)
+        assert np.all((kp["angle"] >= 0) & (kp["angle"] <= 360))
+    z = np.abs(r["points"][:, 2])
+    assert np.median(z) < 0.02
+
+
+def test_akaze_oracle_rotation_covariance(orc):
+    """Rotating a view by 90 degrees rotates its AKAZE keypoints with it: the
+    filters are symmetric, so the same points come out (moved) with their
+    orientation turned by 90 degrees (up to the 0.15-rad window grid) and
+    nearly the same rotation-invariant M-LDB descriptor."""
+    cfg = synth.config(n_views=1, width=320, height=320, kind=1)
+    P, imgs, _ = synth.scene_host(cfg)
+    im = imgs[0]
+    rot = np.ascontiguousarray(np.rot90(im))  # new[i, j] = old[j, W - 1 - i]
+    kw = dict(detector_type=orc.DETECTOR_AKAZE, akaze_threshold=0.0002, max_keypoints_per_cell=1000)
+    a = orc.seeds_run(P, [im], orc.matcher_options(**kw))
+    b = orc.seeds_run(P, [rot], orc.matcher_options(**kw))
+    ka, da = a["keypoints"][0], a["descriptors"][0]
+    kb, db = b["keypoints"][0], b["descriptors"][0]
+    assert len(ka) > 50
+    W = im.shape[1]
+    # old (x, y) -> new (y, W - 1 - x)
+    ex, ey = ka["y"], (W - 1) - ka["x"]
+    d2 = (ex[:, None] - kb["x"][None, :]) ** 2 + (ey[:, None] - kb["y"][None, :]) ** 2
+    j = d2.argmin(axis=1)
+    hit = d2[np.arange(len(ka)), j] < 0.25
+    assert hit.mean() > 0.8
+    # a gradient (dx, dy) becomes (dy, -dx): its angle (image axes, y down) turns by -90
+    dang = (kb["angle"][j[hit]] - ka["angle"][hit] + 90.0 + 180.0) % 360.0 - 180.0
+    assert np.median(np.abs(dang)) < 5.0
+    ham = np.unpackbits(da[hit] ^ db[j[hit]], axis=1).sum(axis=1)
+    assert np.median(ham) < 60  # of 486 bits (random pairs: ~243)
