@@ -520,6 +520,30 @@ def seed_generation(eng, args):
            "knn_kernel": {"rows": n, "kernel_ms": round(kms, 4), "Gpairs_per_s": round(n * n / kms / 1e6, 1),
                           "roofline": {"bound": "mfma", "achieved": round(ops / kms / 1e9, 1), "peak": peak,
                                        "unit": "TOPS (i8)", "frac": round(ops / kms / 1e9 / peak, 4)}}}
+    # DetectorType::AKAZE (matcher.cpp:56-60, 166-170) with AKAZE::create()'s
+    # defaults, and the 512-bit kNN kernel at the same row count
+    ma = M.Matcher(eng, M.MatcherOptions(detector_type=M.DETECTOR_AKAZE))
+    ma.generate_seeds()
+    t0 = time.perf_counter()
+    ma.generate_seeds()
+    wall_a = time.perf_counter() - t0
+    q64 = rng.integers(0, 256, size=(n, 64), dtype=np.uint8)
+    t64 = rng.integers(0, 256, size=(n, 64), dtype=np.uint8)
+    ms = []
+    for _ in range(3):
+        M.knn_match(eng, q64, t64, width=64)
+        ms.append(eng.last_kernel_ms())
+    kms64 = float(np.mean(ms[1:]))
+    ops64 = 2.0 * 512 * n * n
+    out["akaze"] = {"settings": "AKAZE::create() defaults (MLDB 486 bits, threshold 0.001, 4 octaves x 4 "
+                                "sublevels, PM_G2), the same cells / ratio / epipolar settings",
+                    "wall_s": round(wall_a, 4),
+                    **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in ma.stats.items()},
+                    "knn_kernel_512bit": {"rows": n, "kernel_ms": round(kms64, 4),
+                                          "Gpairs_per_s": round(n * n / kms64 / 1e6, 1),
+                                          "roofline": {"bound": "mfma", "achieved": round(ops64 / kms64 / 1e9, 1),
+                                                       "peak": peak, "unit": "TOPS (i8)",
+                                                       "frac": round(ops64 / kms64 / 1e9 / peak, 4)}}}
     if not args.no_cpu:
         from oracle import pyoracle as orc
 

@@ -20,6 +20,7 @@ constexpr int kAkBits = 486;
 struct AkPlane {
     int64_t off;
     int64_t det_base;    // first index of this Ldet plane in the chunk's pixel index space
+    int64_t seg_base;    // first (row, 256-px segment) counter of this plane
     int32_t w, h, octave, sigma_size;
     float esigma;
     int32_t pad;
@@ -58,12 +59,22 @@ hipError_t launch_akz_conv(const AkArgs &a, int level, int src, int dst, int dir
 hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_half(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_copy(const AkArgs &a, int level, int src, int dst, int nv, int max_w, int max_h, hipStream_t s);
-hipError_t launch_akz_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float tau, int nv, int max_w, int max_h,
                           hipStream_t s);
-hipError_t launch_akz_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
-hipError_t launch_akz_flag(const AkArgs &a, int level, float thr, uint8_t *flag, int nv, int max_w, int max_h,
-                           hipStream_t s);
+// fused 3-tap passes: mode 0 the normalised Scharr of scale sigma_size, mode 1
+// the unnormalised 3x3 Scharr
+hipError_t launch_akz_rows2(const AkArgs &a, int level, int src, int dD, int dS, int mode, int nv, int max_w,
+                            int max_h, hipStream_t s);
+hipError_t launch_akz_cols2(const AkArgs &a, int level, int srcS, int dstS, int srcD, int dstD, int mode, int nv,
+                            int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_cols_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
+// extrema candidates in (view, level, y, x) order: per-segment counts, an
+// exclusive scan of them (host side, hipcub), then the indices
+hipError_t launch_akz_count(const AkArgs &a, int level, float thr, uint32_t *cnt, int nv, int max_w, int max_h,
+                            hipStream_t s);
+hipError_t launch_akz_emit(const AkArgs &a, int level, float thr, const uint32_t *off, int64_t *cand, int nv,
+                           int max_w, int max_h, hipStream_t s);
 
 // candidate list (sorted global Ldet indices) -> keypoints (suppression +
 // subpixel refinement), keep flags

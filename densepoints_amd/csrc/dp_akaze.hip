@@ -134,45 +134,59 @@ hipError_t launch_akz_conv(const AkArgs &a, int level, int src, int dst, int dir
 }
 
 // compute_k_percentile (0.7, 300 bins) from the unnormalised Scharr gradient
-// of Gaussian(img, 1) in T2 (x) / T4 (y): the interior maximum, the histogram,
+// of Gaussian(img, 1) in T0 (x) / T4 (y): the interior maximum, the histogram,
 // then one lane per view
-__global__ void akz_modg_max_kernel(AkArgs a)
+constexpr int kAkRowsPerBlock = 16;
+
+__global__ __launch_bounds__(256) void akz_modg_max_kernel(AkArgs a)
 {
-    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ uint32_t wmax[4];
+    const int z = blockIdx.z, x = blockIdx.x * blockDim.x + threadIdx.x;
     const AkView v = a.views[z];
-    float m = 0.0f;
-    if (x >= 1 && x < v.w0 - 1 && y >= 1 && y < v.h0 - 1) {
-        const size_t i = (size_t)y * v.w0 + x;
-        const float lx = a.tmp[v.tmp + 2 * v.n0 + i], ly = a.tmp[v.tmp + 4 * v.n0 + i];
-        m = sqrtf(lx * lx + ly * ly);
-    }
     // non-negative floats order as their bit patterns
-    uint32_t b = __float_as_uint(m);
+    uint32_t b = 0;
+    for (int r = 0; r < kAkRowsPerBlock; ++r) {
+        const int y = blockIdx.y * kAkRowsPerBlock + r;
+        if (x >= 1 && x < v.w0 - 1 && y >= 1 && y < v.h0 - 1) {
+            const size_t i = (size_t)y * v.w0 + x;
+            const float lx = a.tmp[v.tmp + i], ly = a.tmp[v.tmp + 4 * v.n0 + i];
+            b = max(b, __float_as_uint(sqrtf(lx * lx + ly * ly)));
+        }
+    }
     for (int o = 32; o >= 1; o >>= 1)
         b = max(b, (uint32_t)__shfl_xor((int)b, o));
-    if ((threadIdx.x & 63) == 0 && b)
-        atomicMax(&a.hmax[z], b);
+    if ((threadIdx.x & 63) == 0)
+        wmax[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (m)
+            atomicMax(&a.hmax[z], m);
+    }
 }
 
-__global__ void akz_hist_kernel(AkArgs a)
+__global__ __launch_bounds__(256) void akz_hist_kernel(AkArgs a)
 {
     __shared__ uint32_t h[301];
     for (int i = threadIdx.x; i < 301; i += blockDim.x)
         h[i] = 0;
     __syncthreads();
-    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int z = blockIdx.z, x = blockIdx.x * blockDim.x + threadIdx.x;
     const AkView v = a.views[z];
     const float hmax = __uint_as_float(a.hmax[z]);
-    if (hmax > 0.0f && x >= 1 && x < v.w0 - 1 && y >= 1 && y < v.h0 - 1) {
-        const size_t i = (size_t)y * v.w0 + x;
-        const float lx = a.tmp[v.tmp + 2 * v.n0 + i], ly = a.tmp[v.tmp + 4 * v.n0 + i];
-        const float m = sqrtf(lx * lx + ly * ly);
-        if (m != 0.0f) {
-            int bin = (int)floorf(300.0f * (m / hmax));
-            if (bin == 300)
-                bin--;
-            atomicAdd(&h[bin], 1u);
-            atomicAdd(&h[300], 1u);
+    for (int r = 0; r < kAkRowsPerBlock; ++r) {
+        const int y = blockIdx.y * kAkRowsPerBlock + r;
+        if (hmax > 0.0f && x >= 1 && x < v.w0 - 1 && y >= 1 && y < v.h0 - 1) {
+            const size_t i = (size_t)y * v.w0 + x;
+            const float lx = a.tmp[v.tmp + i], ly = a.tmp[v.tmp + 4 * v.n0 + i];
+            const float m = sqrtf(lx * lx + ly * ly);
+            if (m != 0.0f) {
+                int bin = (int)floorf(300.0f * (m / hmax));
+                if (bin == 300)
+                    bin--;
+                atomicAdd(&h[bin], 1u);
+                atomicAdd(&h[300], 1u);
+            }
         }
     }
     __syncthreads();
@@ -202,11 +216,12 @@ __global__ void akz_kc_kernel(AkArgs a, int nv)
 
 hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s)
 {
-    hipLaunchKernelGGL(akz_modg_max_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a);
+    const int by = (max_h + kAkRowsPerBlock - 1) / kAkRowsPerBlock;
+    hipLaunchKernelGGL(akz_modg_max_kernel, dim3((max_w + 255) / 256, by, nv), dim3(256), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL(akz_hist_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(akz_hist_kernel, dim3((max_w + 255) / 256, by, nv), dim3(256), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess)
         return e;
@@ -249,29 +264,6 @@ hipError_t launch_akz_copy(const AkArgs &a, int level, int src, int dst, int nv,
     return hipGetLastError();
 }
 
-// g2 conductance into T4 from the unnormalised Scharr gradient in Lx / Ly;
-// k = k0 x 0.75 per octave, multiplied in order
-__global__ void akz_g2_kernel(AkArgs a, int level)
-{
-    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    const AkPlane &L = a.planes[z * kAkLevels + level];
-    if (L.w == 0 || x >= L.w || y >= L.h)
-        return;
-    float k = a.k0[z];
-    for (int o = 0; o < L.octave; ++o)
-        k = k * 0.75f;
-    const float k2inv = 1.0f / (k * k);
-    const size_t i = (size_t)y * L.w + x;
-    const float lx = ak_ptr(a, z, level, kLx)[i], ly = ak_ptr(a, z, level, kLy)[i];
-    ak_ptr(a, z, level, kT4)[i] = 1.0f / (1.0f + k2inv * (lx * lx + ly * ly));
-}
-
-hipError_t launch_akz_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
-{
-    hipLaunchKernelGGL(akz_g2_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
-    return hipGetLastError();
-}
-
 // one explicit FED step (zero flux across the border), conductance in T4:
 // dst = src + tau/2 ((xp - xn) + (yp - yn))
 __global__ void akz_fed_kernel(AkArgs a, int level, int src, int dst, float tau)
@@ -300,56 +292,213 @@ hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float ta
     return hipGetLastError();
 }
 
-// Lx, Ly x s in place; Ldet from Lxx (T2), Lxy (T0), Lyy (T4), each x s^2
-__global__ void akz_det_kernel(AkArgs a, int level)
+// ---------------------------------------------------------------------------
+// fused 3-tap passes (the same expressions as one pass each): mode 0 the
+// normalised Scharr of scale s = sigma_size (smoothing (1, 10/3, 1) /
+// (2 s (10/3 + 2)) at spacing s), mode 1 the unnormalised 3x3 Scharr
+// (smoothing (3, 10, 3), spacing 1); derivative (-1, 0, 1): c - a
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void akz_coef(const AkPlane &P, int mode, int &sp, float &k0, float &k1)
+{
+    if (mode == 0) {
+        sp = P.sigma_size;
+        const float wgt = 10.0f / 3.0f;
+        k0 = 1.0f / (2.0f * (float)sp * (wgt + 2.0f));
+        k1 = wgt * k0;
+    } else {
+        sp = 1;
+        k0 = 3.0f;
+        k1 = 10.0f;
+    }
+}
+
+// rows of src: derivative into dD, smoothing into dS (either may be -1)
+__global__ void akz_rows2_kernel(AkArgs a, int level, int src, int dD, int dS, int mode)
 {
     const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     const AkPlane &P = a.planes[z * kAkLevels + level];
-    if (P.w == 0 || x >= P.w || y >= P.h)
+    const int w = P.w;
+    if (w == 0 || x >= w || y >= P.h)
         return;
-    const size_t i = (size_t)y * P.w + x;
-    const float fs = (float)P.sigma_size, fs2 = (float)(P.sigma_size * P.sigma_size);
-    float *lx = ak_ptr(a, z, level, kLx), *ly = ak_ptr(a, z, level, kLy);
-    lx[i] = lx[i] * fs;
-    ly[i] = ly[i] * fs;
-    const float xx = ak_ptr(a, z, level, kT2)[i] * fs2, yy = ak_ptr(a, z, level, kT4)[i] * fs2;
-    const float xy = ak_ptr(a, z, level, kT0)[i] * fs2;
-    ak_ptr(a, z, level, kLdet)[i] = xx * yy - xy * xy;
+    int sp;
+    float k0, k1;
+    akz_coef(P, mode, sp, k0, k1);
+    const float *row = ak_ptr(a, z, level, src) + (size_t)y * w;
+    const float va = row[ak_r101(x - sp, w)], vb = row[x], vc = row[ak_r101(x + sp, w)];
+    const size_t i = (size_t)y * w + x;
+    if (dD >= 0)
+        ak_ptr(a, z, level, dD)[i] = vc - va;
+    if (dS >= 0)
+        ak_ptr(a, z, level, dS)[i] = (k0 * va + k1 * vb) + k0 * vc;
 }
 
-hipError_t launch_akz_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
+hipError_t launch_akz_rows2(const AkArgs &a, int level, int src, int dD, int dS, int mode, int nv, int max_w,
+                            int max_h, hipStream_t s)
 {
-    hipLaunchKernelGGL(akz_det_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
+    hipLaunchKernelGGL(akz_rows2_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, src, dD, dS,
+                       mode);
     return hipGetLastError();
 }
 
-// 3x3 maxima of Ldet above the threshold inside the descriptor border
-__global__ void akz_flag_kernel(AkArgs a, int level, float thr, uint8_t *flag)
+__device__ __forceinline__ void akz_col3(const float *S, int w, int h, int x, int y, int sp, float &va, float &vb,
+                                         float &vc)
+{
+    va = S[(size_t)ak_r101(y - sp, h) * w + x];
+    vb = S[(size_t)y * w + x];
+    vc = S[(size_t)ak_r101(y + sp, h) * w + x];
+}
+
+// columns: dstS = smoothing of srcS, dstD = derivative of srcD
+__global__ void akz_cols2_kernel(AkArgs a, int level, int srcS, int dstS, int srcD, int dstD, int mode)
 {
     const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     const AkPlane &P = a.planes[z * kAkLevels + level];
     const int w = P.w, h = P.h;
     if (w == 0 || x >= w || y >= h)
         return;
-    uint8_t f = 0;
-    if (x >= 1 && x < w - 1 && y >= 1 && y < h - 1) {
-        const float *p = a.pool + P.off + 3 * ((int64_t)w * h) + (size_t)y * w + x;
-        const float v = p[0];
-        if (v > thr && v >= 0.00001f && v > p[-1] && v > p[1] && v > p[-w - 1] && v > p[-w] && v > p[-w + 1] &&
-            v > p[w - 1] && v > p[w] && v > p[w + 1]) {
-            const float sm = (10.0f * sqrtf(2.0f)) * (float)P.sigma_size;
-            const int lx = __float2int_rn((float)x - sm) - 1, rx = __float2int_rn((float)x + sm) + 1;
-            const int uy = __float2int_rn((float)y - sm) - 1, dy = __float2int_rn((float)y + sm) + 1;
-            f = lx >= 0 && rx < w && uy >= 0 && dy < h;
-        }
-    }
-    flag[P.det_base + (size_t)y * w + x] = f;
+    int sp;
+    float k0, k1, va, vb, vc;
+    akz_coef(P, mode, sp, k0, k1);
+    const size_t i = (size_t)y * w + x;
+    akz_col3(ak_ptr(a, z, level, srcS), w, h, x, y, sp, va, vb, vc);
+    ak_ptr(a, z, level, dstS)[i] = (k0 * va + k1 * vb) + k0 * vc;
+    akz_col3(ak_ptr(a, z, level, srcD), w, h, x, y, sp, va, vb, vc);
+    ak_ptr(a, z, level, dstD)[i] = vc - va;
 }
 
-hipError_t launch_akz_flag(const AkArgs &a, int level, float thr, uint8_t *flag, int nv, int max_w, int max_h,
-                           hipStream_t s)
+hipError_t launch_akz_cols2(const AkArgs &a, int level, int srcS, int dstS, int srcD, int dstD, int mode, int nv,
+                            int max_w, int max_h, hipStream_t s)
 {
-    hipLaunchKernelGGL(akz_flag_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, thr, flag);
+    hipLaunchKernelGGL(akz_cols2_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, srcS, dstS,
+                       srcD, dstD, mode);
+    return hipGetLastError();
+}
+
+// columns of the unnormalised Scharr rows (T1 derivative, T2 smoothing) and
+// the g2 conductance into T4: k = k0 x 0.75 per octave, multiplied in order
+__global__ void akz_cols_g2_kernel(AkArgs a, int level)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int w = P.w, h = P.h;
+    if (w == 0 || x >= w || y >= h)
+        return;
+    float va, vb, vc;
+    akz_col3(ak_ptr(a, z, level, kT1), w, h, x, y, 1, va, vb, vc);
+    const float lx = (3.0f * va + 10.0f * vb) + 3.0f * vc;
+    akz_col3(ak_ptr(a, z, level, kT2), w, h, x, y, 1, va, vb, vc);
+    const float ly = vc - va;
+    float k = a.k0[z];
+    for (int o = 0; o < P.octave; ++o)
+        k = k * 0.75f;
+    const float k2inv = 1.0f / (k * k);
+    ak_ptr(a, z, level, kT4)[(size_t)y * w + x] = 1.0f / (1.0f + k2inv * (lx * lx + ly * ly));
+}
+
+hipError_t launch_akz_cols_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_cols_g2_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
+    return hipGetLastError();
+}
+
+// the detector's second derivatives from the rows of Lx (T1 derivative, T2
+// smoothing) and of Ly (T4 smoothing): Lxx, Lxy, Lyy x s^2, Ldet; Lx, Ly x s
+__global__ void akz_cols_det_kernel(AkArgs a, int level)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int w = P.w, h = P.h;
+    if (w == 0 || x >= w || y >= h)
+        return;
+    int sp;
+    float k0, k1, va, vb, vc;
+    akz_coef(P, 0, sp, k0, k1);
+    akz_col3(ak_ptr(a, z, level, kT1), w, h, x, y, sp, va, vb, vc);
+    const float lxx = (k0 * va + k1 * vb) + k0 * vc;
+    akz_col3(ak_ptr(a, z, level, kT2), w, h, x, y, sp, va, vb, vc);
+    const float lxy = vc - va;
+    akz_col3(ak_ptr(a, z, level, kT4), w, h, x, y, sp, va, vb, vc);
+    const float lyy = vc - va;
+    const size_t i = (size_t)y * w + x;
+    const float fs = (float)P.sigma_size, fs2 = (float)(P.sigma_size * P.sigma_size);
+    float *lx = ak_ptr(a, z, level, kLx), *ly = ak_ptr(a, z, level, kLy);
+    lx[i] = lx[i] * fs;
+    ly[i] = ly[i] * fs;
+    const float xx = lxx * fs2, yy = lyy * fs2, xy = lxy * fs2;
+    ak_ptr(a, z, level, kLdet)[i] = xx * yy - xy * xy;
+}
+
+hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_cols_det_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
+    return hipGetLastError();
+}
+
+// 3x3 maxima of Ldet above the threshold inside the descriptor border
+__device__ __forceinline__ bool akz_is_cand(const AkArgs &a, const AkPlane &P, int x, int y, float thr)
+{
+    const int w = P.w, h = P.h;
+    if (x < 1 || x >= w - 1 || y < 1 || y >= h - 1)
+        return false;
+    const float *p = a.pool + P.off + 3 * ((int64_t)w * h) + (size_t)y * w + x;
+    const float v = p[0];
+    if (!(v > thr && v >= 0.00001f && v > p[-1] && v > p[1] && v > p[-w - 1] && v > p[-w] && v > p[-w + 1] &&
+          v > p[w - 1] && v > p[w] && v > p[w + 1]))
+        return false;
+    const float sm = (10.0f * sqrtf(2.0f)) * (float)P.sigma_size;
+    const int lx = __float2int_rn((float)x - sm) - 1, rx = __float2int_rn((float)x + sm) + 1;
+    const int uy = __float2int_rn((float)y - sm) - 1, dy = __float2int_rn((float)y + sm) + 1;
+    return lx >= 0 && rx < w && uy >= 0 && dy < h;
+}
+
+// pass 1: candidates per (plane row, 256-px segment), at P.seg_base + y nbx + bx
+__global__ __launch_bounds__(256) void akz_count_kernel(AkArgs a, int level, float thr, uint32_t *cnt)
+{
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int nbx = (P.w + 255) >> 8;
+    if (P.w == 0 || y >= P.h || (int)blockIdx.x >= nbx) // uniform per block
+        return;
+    const int c = __syncthreads_count(x < P.w && akz_is_cand(a, P, x, y, thr));
+    if (threadIdx.x == 0)
+        cnt[P.seg_base + (int64_t)y * nbx + blockIdx.x] = (uint32_t)c;
+}
+
+// pass 2: each segment's candidates at its exclusive-scan offset, in x order
+__global__ __launch_bounds__(256) void akz_emit_kernel(AkArgs a, int level, float thr, const uint32_t *off,
+                                                       int64_t *cand)
+{
+    __shared__ uint32_t wc[4];
+    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int nbx = (P.w + 255) >> 8;
+    if (P.w == 0 || y >= P.h || (int)blockIdx.x >= nbx)
+        return;
+    const bool f = x < P.w && akz_is_cand(a, P, x, y, thr);
+    const unsigned long long m = __ballot(f);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0)
+        wc[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t base = off[P.seg_base + (int64_t)y * nbx + blockIdx.x];
+    for (int k = 0; k < wv; ++k)
+        base += wc[k];
+    if (f)
+        cand[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = P.det_base + (int64_t)y * P.w + x;
+}
+
+hipError_t launch_akz_count(const AkArgs &a, int level, float thr, uint32_t *cnt, int nv, int max_w, int max_h,
+                            hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_count_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, thr, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_akz_emit(const AkArgs &a, int level, float thr, const uint32_t *off, int64_t *cand, int nv,
+                           int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_emit_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, thr, off,
+                       cand);
     return hipGetLastError();
 }
 

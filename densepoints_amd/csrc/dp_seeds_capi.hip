@@ -55,7 +55,7 @@ struct dp_seedgen {
     DevBuf<dpk::AkPlane> akz_planes;
     DevBuf<dpk::AkView> akz_views;
     DevBuf<uint32_t> akz_hmax, akz_hist, akz_bits;
-    DevBuf<uint8_t> akz_flag;
+    DevBuf<uint32_t> akz_seg;
     DevBuf<int64_t> akz_cand, akz_pbase;
     DevBuf<int32_t> akz_pids, akz_vids;
     int desc_words = 8; // 8 (ORB) or 16 (AKAZE) dwords per descriptor
@@ -119,7 +119,7 @@ void dp_seedgen_free(dp_seedgen *s)
     s->akz_views.release();
     for (auto *b : {&s->akz_hmax, &s->akz_hist, &s->akz_bits})
         b->release();
-    s->akz_flag.release();
+    s->akz_seg.release();
     s->akz_cand.release();
     s->akz_pbase.release();
     s->akz_pids.release();
@@ -545,25 +545,22 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         return t;
     };
     const AkTaps g16 = taps_gauss(1.6f), g10 = taps_gauss(1.0f);
-    AkTaps sd1{}, ss1{}, dS{}, sS{};
-    sd1.mode = 1;
-    sd1.spacing = 1;
-    ss1.mode = 2;
-    ss1.spacing = 1;
-    ss1.w[0] = 3.0f;
-    ss1.w[1] = 10.0f;
-    dS.mode = 1;
-    dS.spacing = -1;
-    sS.mode = 2;
-    sS.spacing = -1;
 
+    // chunk budget: DP_AKAZE_CHUNK_BYTES, else 40% of the free device memory
     const char *env = std::getenv("DP_AKAZE_CHUNK_BYTES");
-    const int64_t budget = env ? std::max<int64_t>(1, std::atoll(env)) : (int64_t)8 << 30;
+    int64_t budget = (int64_t)8 << 30;
+    if (env) {
+        budget = std::max<int64_t>(1, std::atoll(env));
+    } else {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0)
+            budget = (int64_t)(0.4 * (double)fr);
+    }
     auto view_bytes = [&](int v) {
         int64_t px = 0;
         for (int i = 0; i < geo[v].n; ++i)
             px += (int64_t)geo[v].w[i] * geo[v].h[i];
-        return 17 * px + 20 * (int64_t)vw[v] * vh[v];
+        return 16 * px + 20 * (int64_t)vw[v] * vh[v] + 8 * (px / 16);
     };
     std::vector<dp_keypoint> all_kp;
     std::vector<uint32_t> all_desc;
@@ -582,7 +579,7 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         std::vector<AkPlane> planes((size_t)nv * kAkLevels);
         std::vector<AkView> views(nv);
         std::memset(planes.data(), 0, planes.size() * sizeof(AkPlane));
-        int64_t pool = 0, tmp = 0, det = 0;
+        int64_t pool = 0, tmp = 0, det = 0, segs = 0;
         int mw[kAkLevels] = {0}, mh[kAkLevels] = {0}, nlev = 0;
         for (int z = 0; z < nv; ++z) {
             const int v = v0 + z;
@@ -591,6 +588,7 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
                 AkPlane &P = planes[(size_t)z * kAkLevels + i];
                 P.off = pool;
                 P.det_base = det;
+                P.seg_base = segs;
                 P.w = g.w[i];
                 P.h = g.h[i];
                 P.octave = g.octave[i];
@@ -598,6 +596,7 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
                 P.esigma = g.esigma[i];
                 pool += 4 * (int64_t)P.w * P.h;
                 det += (int64_t)P.w * P.h;
+                segs += (int64_t)P.h * ((P.w + 255) / 256);
                 mw[i] = std::max(mw[i], P.w);
                 mh[i] = std::max(mh[i], P.h);
             }
@@ -621,7 +620,7 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         DP_HIP(c, s->akz_hmax.reserve(nv));
         DP_HIP(c, s->akz_hist.reserve((size_t)nv * 301));
         DP_HIP(c, s->akz_k0.reserve(nv));
-        DP_HIP(c, s->akz_flag.reserve(det + 1));
+        DP_HIP(c, s->akz_seg.reserve(2 * (segs + 1)));
         DP_HIP(c, hipMemcpyAsync(s->akz_planes.p, planes.data(), planes.size() * sizeof(AkPlane),
                                  hipMemcpyHostToDevice, st));
         DP_HIP(c, hipMemcpyAsync(s->akz_views.p, views.data(), nv * sizeof(AkView), hipMemcpyHostToDevice, st));
@@ -632,28 +631,28 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         auto conv = [&](int i, int src, int dst, int dir, const AkTaps &t) {
             return launch_akz_conv(a, i, src, dst, dir, t, nv, mw[i], mh[i], st);
         };
-        // the detector's derivatives of Lsmooth (plane ls) and Ldet
+        // the detector's derivatives of Lsmooth (plane ls), Ldet; Lx, Ly scaled
         auto deriv = [&](int i, int ls) -> hipError_t {
-            const int seq[10][4] = {{ls, kT1, 0, 1}, {kT1, kLx, 1, 2}, {ls, kT1, 0, 2},  {kT1, kLy, 1, 1},
-                                    {kLx, kT1, 0, 1}, {kT1, kT2, 1, 2}, {kLx, kT1, 0, 2}, {kT1, kT0, 1, 1},
-                                    {kLy, kT1, 0, 2}, {kT1, kT4, 1, 1}};
-            for (const auto &q : seq) {
-                const hipError_t e = conv(i, q[0], q[1], q[2], q[3] == 1 ? dS : sS);
-                if (e != hipSuccess)
-                    return e;
-            }
-            return launch_akz_det(a, i, nv, mw[i], mh[i], st);
+            hipError_t e = launch_akz_rows2(a, i, ls, kT1, kT2, 0, nv, mw[i], mh[i], st);
+            if (e == hipSuccess)
+                e = launch_akz_cols2(a, i, kT1, kLx, kT2, kLy, 0, nv, mw[i], mh[i], st);
+            if (e == hipSuccess)
+                e = launch_akz_rows2(a, i, kLx, kT1, kT2, 0, nv, mw[i], mh[i], st);
+            if (e == hipSuccess)
+                e = launch_akz_rows2(a, i, kLy, -1, kT4, 0, nv, mw[i], mh[i], st);
+            if (e == hipSuccess)
+                e = launch_akz_cols_det(a, i, nv, mw[i], mh[i], st);
+            return e;
         };
-        // level 0: gray, L0 = Gaussian(img, 1.6), the contrast factor
+        // level 0: gray, L0 = Gaussian(img, 1.6), the contrast factor from the
+        // unnormalised Scharr gradient of Gaussian(img, 1) (x in T0, y in T4)
         DP_HIP(c, launch_akz_gray(a, nv, mw[0], mh[0], st));
         DP_HIP(c, conv(0, kT0, kT1, 0, g16));
         DP_HIP(c, conv(0, kT1, kLt, 1, g16));
         DP_HIP(c, conv(0, kT0, kT1, 0, g10));
         DP_HIP(c, conv(0, kT1, kT3, 1, g10));
-        DP_HIP(c, conv(0, kT3, kT1, 0, sd1));
-        DP_HIP(c, conv(0, kT1, kT2, 1, ss1));
-        DP_HIP(c, conv(0, kT3, kT1, 0, ss1));
-        DP_HIP(c, conv(0, kT1, kT4, 1, sd1));
+        DP_HIP(c, launch_akz_rows2(a, 0, kT3, kT1, kT2, 1, nv, mw[0], mh[0], st));
+        DP_HIP(c, launch_akz_cols2(a, 0, kT1, kT0, kT2, kT4, 1, nv, mw[0], mh[0], st));
         DP_HIP(c, launch_akz_kcontrast(a, nv, mw[0], mh[0], st));
         DP_HIP(c, deriv(0, kLt));
         for (int i = 1; i < nlev; ++i) {
@@ -661,14 +660,11 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
                 DP_HIP(c, launch_akz_half(a, i, nv, mw[i], mh[i], st));
             else
                 DP_HIP(c, launch_akz_copy(a, i, -1, kLt, nv, mw[i], mh[i], st));
-            // Lsmooth, g2 conductance from its unnormalised Scharr gradient
+            // Lsmooth (T3), g2 conductance (T4) from its unnormalised Scharr gradient
             DP_HIP(c, conv(i, kLt, kT1, 0, g10));
             DP_HIP(c, conv(i, kT1, kT3, 1, g10));
-            DP_HIP(c, conv(i, kT3, kT1, 0, sd1));
-            DP_HIP(c, conv(i, kT1, kLx, 1, ss1));
-            DP_HIP(c, conv(i, kT3, kT1, 0, ss1));
-            DP_HIP(c, conv(i, kT1, kLy, 1, sd1));
-            DP_HIP(c, launch_akz_g2(a, i, nv, mw[i], mh[i], st));
+            DP_HIP(c, launch_akz_rows2(a, i, kT3, kT1, kT2, 1, nv, mw[i], mh[i], st));
+            DP_HIP(c, launch_akz_cols_g2(a, i, nv, mw[i], mh[i], st));
             // FED steps, ping-pong between Lt and T2
             int src = kLt;
             for (size_t k = 0; k < tau[i].size(); ++k) {
@@ -680,18 +676,20 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
                 DP_HIP(c, launch_akz_copy(a, i, kT2, kLt, nv, mw[i], mh[i], st));
             DP_HIP(c, deriv(i, kT3));
         }
-        // extrema flags over every Ldet plane, candidates in (view, level, y, x) order
+        // extrema candidates in (view, level, y, x) order: counts per
+        // (row, 256-px segment), their exclusive scan, the indices
+        uint32_t *seg_cnt = s->akz_seg.p, *seg_off = s->akz_seg.p + segs + 1;
+        DP_HIP(c, hipMemsetAsync(seg_cnt, 0, (size_t)(segs + 1) * 4, st));
         for (int i = 0; i < nlev; ++i)
-            DP_HIP(c, launch_akz_flag(a, i, mo.akaze_threshold, s->akz_flag.p, nv, mw[i], mh[i], st));
-        DP_HIP(c, s->akz_cand.reserve(det + 1));
-        {
-            hipcub::CountingInputIterator<int64_t> iota(0);
-            DP_CUB(c, s, hipcub::DeviceSelect::Flagged(_tmp, _bytes, iota, s->akz_flag.p, s->akz_cand.p, s->n_sel.p,
-                                                        (int)det, st));
-        }
-        int64_t n_cand = 0;
-        DP_HIP(c, hipMemcpyAsync(&n_cand, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+            DP_HIP(c, launch_akz_count(a, i, mo.akaze_threshold, seg_cnt, nv, mw[i], mh[i], st));
+        DP_CUB(c, s, hipcub::DeviceScan::ExclusiveSum(_tmp, _bytes, seg_cnt, seg_off, (int)(segs + 1), st));
+        uint32_t n_cand32 = 0;
+        DP_HIP(c, hipMemcpyAsync(&n_cand32, seg_off + segs, 4, hipMemcpyDeviceToHost, st));
         DP_HIP(c, hipStreamSynchronize(st));
+        const int64_t n_cand = n_cand32;
+        DP_HIP(c, s->akz_cand.reserve(n_cand + 1));
+        for (int i = 0; i < nlev; ++i)
+            DP_HIP(c, launch_akz_emit(a, i, mo.akaze_threshold, seg_off, s->akz_cand.p, nv, mw[i], mh[i], st));
         std::vector<int32_t> pids, vids(nv);
         std::vector<int64_t> pbase;
         for (int z = 0; z < nv; ++z) {

@@ -10,6 +10,7 @@
 //   densify -i scene.json [--seeds seeds.xyz] [-s settings.json] [-o points.ply]
 //           [--device N] [--max-pops N] [--level L] [--filter] [--check-only]
 //           [--features N] [--fast-threshold T] [--epipolar-matching] [--matcher knn|flann]
+//           [--detector orb|akaze] [--akaze-threshold T]
 //   densify --synthetic V,W,H,KIND --write-scene DIR   (deterministic test scene
 //           written as scene.json + PPM images + seeds.xyz; no GPU needed)
 #include "scene_io.h"
@@ -36,6 +37,7 @@ void usage()
                  "               [--device N] [--max-pops N] [--level L] [--filter] [--check-only]\n"
                  "               [--features N] [--fast-threshold T] [--epipolar-matching]\n"
                  "               [--matcher knn|flann]  (MatcherType, matcher.h:12)\n"
+                 "               [--detector orb|akaze] [--akaze-threshold T]  (DetectorType, matcher.h:11)\n"
                  "               [--gpus N]   (one context per GPU, generations partitioned by\n"
                  "                             reference-view super-tile; output identical to 1 GPU)\n"
                  "               [--mode parity|fast] [--fast-iters N] [--fast-gradient 0|1]\n"
@@ -263,6 +265,17 @@ int main(int argc, char **argv)
                 return 2;
             }
         }
+        else if (a == "--detector") {
+            const std::string v = next();
+            if (v == "orb")
+                mopt.detector_type = DP_DETECTOR_ORB;
+            else if (v == "akaze")
+                mopt.detector_type = DP_DETECTOR_AKAZE;
+            else {
+                std::fprintf(stderr, "densify: --detector expects orb or akaze\n");
+                return 2;
+            }
+        } else if (a == "--akaze-threshold") mopt.akaze_threshold = (float)std::atof(next().c_str());
         else if (a == "--mode") {
             const std::string m = next();
             if (m != "parity" && m != "fast") {

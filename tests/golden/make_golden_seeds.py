@@ -13,7 +13,11 @@ product's synthetic renderer at generation time only) and their projection
 matrices.  Options: 3000 features, 4 levels, FAST threshold 8 (the synthetic
 texture is low-contrast), everything else the reference defaults.
 
-usage: python tests/golden/make_golden_seeds.py   (rewrites seeds_small.npz)
+A second fixture, seeds_akaze_small.npz, holds the same stages with
+DetectorType::AKAZE (oracle/or_akaze.c; threshold 0.0002 for the
+low-contrast texture, 64-byte descriptor rows) on seeds_small.npz's inputs.
+
+usage: python tests/golden/make_golden_seeds.py   (rewrites both fixtures)
 """
 import os
 import sys
@@ -28,12 +32,16 @@ from densepoints_amd import synth  # noqa: E402
 from oracle import pyoracle  # noqa: E402
 
 OPTIONS = {"n_features": 3000, "n_levels": 4, "fast_threshold": 8}
+AKAZE_OPTIONS = {"detector_type": 0, "akaze_threshold": 0.0002}
 
 
-def generate():
-    cfg = synth.config(3, 320, 240, 1)
-    P, imgs, _ = synth.scene_host(cfg)
-    r = pyoracle.seeds_run(P, imgs, pyoracle.matcher_options(**OPTIONS))
+def generate(options=OPTIONS, inputs=None):
+    if inputs is None:
+        cfg = synth.config(3, 320, 240, 1)
+        P, imgs, _ = synth.scene_host(cfg)
+    else:
+        P, imgs = inputs
+    r = pyoracle.seeds_run(P, imgs, pyoracle.matcher_options(**options))
     out = {"P": P.astype(np.float64), "images": np.stack(imgs).astype(np.uint8)}
     c = r["counts"]
     out["counts"] = np.array([c[k] for k in ("detected", "keypoints", "ratio_matches", "matches", "points")],
@@ -51,3 +59,7 @@ if __name__ == "__main__":
     out = generate()
     np.savez_compressed(os.path.join(HERE, "seeds_small.npz"), **out)
     print({k: v.shape for k, v in out.items()}, out["counts"])
+    ak = generate(AKAZE_OPTIONS, (out["P"], list(out["images"])))
+    del ak["P"], ak["images"]  # the inputs are seeds_small.npz's
+    np.savez_compressed(os.path.join(HERE, "seeds_akaze_small.npz"), **ak)
+    print({k: v.shape for k, v in ak.items()}, ak["counts"])

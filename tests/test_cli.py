@@ -331,3 +331,28 @@ def test_cli_flann_matcher_pipeline(tmp_path_factory, tmp_path, orc):
     write_ply(str(ref), op)
     assert out.read_bytes() == ref.read_bytes()
     assert run("-i", os.path.join(d, "scene.json"), "--matcher", "lsh", check=False).returncode == 2
+
+
+@pytest.mark.gpu
+def test_cli_akaze_detector_pipeline(tmp_path_factory, tmp_path, orc):
+    """densify --detector akaze (DetectorType::AKAZE, matcher.cpp:56-60,
+    166-170): AKAZE seeds, then the densify; the PLY equals the oracle's
+    AKAZE seed generation + densify byte for byte."""
+    from densepoints_amd.pmvs import write_ply
+
+    d = str(tmp_path_factory.mktemp("scene_akaze"))
+    run("--synthetic", "4,320,240,1", "--write-scene", d)
+    out = tmp_path / "points.ply"
+    res = json.loads(run("-i", os.path.join(d, "scene.json"), "--detector", "akaze", "--akaze-threshold", "0.0002",
+                         "-o", str(out)).stdout)
+    cfg = synth.config(4, 320, 240, 1)
+    P = synth.cameras(cfg)
+    imgs = [synth.render_host(cfg, P, v) for v in range(4)]
+    r = orc.seeds_run(P, imgs, orc.matcher_options(detector_type=orc.DETECTOR_AKAZE, akaze_threshold=0.0002))
+    assert res["generated_seeds"] is True and res["seeds"] == len(r["points"]) > 0
+    op, ost = orc.Scene(P, imgs).densify(r["points"])
+    assert res["patches"] == ost["patches"] > 0
+    ref = tmp_path / "oracle.ply"
+    write_ply(str(ref), op)
+    assert out.read_bytes() == ref.read_bytes()
+    assert run("-i", os.path.join(d, "scene.json"), "--detector", "sift", check=False).returncode == 2

@@ -99,6 +99,21 @@ def test_generate_seeds_golden_fixture():
     assert np.array_equal(bits(pts), bits(g["points"]))
 
 
+def test_generate_seeds_akaze_golden_fixture():
+    g = np.load(os.path.join(ROOT, "tests", "golden", "seeds_small.npz"))
+    a = np.load(os.path.join(ROOT, "tests", "golden", "seeds_akaze_small.npz"))
+    with engine_with(g["P"], list(g["images"])) as eng:
+        m = M.Matcher(eng, M.MatcherOptions(detector_type=M.DETECTOR_AKAZE, akaze_threshold=0.0002))
+        pts = m.generate_seeds()
+        kps = np.concatenate([m.keypoints(v)[0] for v in range(3)])
+        desc = np.concatenate([m.keypoints(v)[1] for v in range(3)])
+        q2t = np.concatenate([m.matches(p)[2] for p in range(3)])
+    assert np.array_equal(bits(kps), bits(a["keypoints"]))
+    assert np.array_equal(desc, a["descriptors"])
+    assert np.array_equal(q2t, a["q2t"])
+    assert np.array_equal(bits(pts), bits(a["points"]))
+
+
 def _random_desc(rng, n, pool=None):
     d = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     if pool is not None and len(pool) and n:

@@ -217,6 +217,17 @@ def test_golden_seeds_fixture_pins_the_oracle(orc):
     assert np.array_equal(r["points"], g["points"])
 
 
+def test_golden_akaze_fixture_pins_the_oracle(orc):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "seeds_small.npz"))
+    a = np.load(os.path.join(ROOT, "tests", "golden", "seeds_akaze_small.npz"))
+    r = orc.seeds_run(g["P"], list(g["images"]),
+                      orc.matcher_options(detector_type=orc.DETECTOR_AKAZE, akaze_threshold=0.0002))
+    assert np.array_equal(np.concatenate(r["keypoints"]), a["keypoints"])
+    assert np.array_equal(np.concatenate(r["descriptors"]), a["descriptors"])
+    assert np.array_equal(np.concatenate(r["q2t"]), a["q2t"])
+    assert np.array_equal(r["points"], a["points"])
+
+
 def test_oracle_flann_matcher_is_exact_nn_below_30(orc):
     """MatcherType::FLANN (matcher.cpp:229-240: LSH match, distance < 30),
     stated as the exact Hamming nearest neighbour it approximates: every

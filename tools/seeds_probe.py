@@ -25,6 +25,7 @@ ap.add_argument("--views", type=int, default=0)
 ap.add_argument("--repeat", type=int, default=2)
 ap.add_argument("--knn", type=int, default=40000, help="rows per side of the bare kNN timing (0 = skip)")
 ap.add_argument("--fast-threshold", type=int, default=20)
+ap.add_argument("--detector", default="orb", choices=["orb", "akaze"])
 args = ap.parse_args()
 cfg = synth.named(args.config)
 if args.views:
@@ -38,14 +39,15 @@ for v in range(V):
             eng.handle)
 torch.cuda.synchronize()
 eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
-m = M.Matcher(eng, M.MatcherOptions(fast_threshold=args.fast_threshold))
+m = M.Matcher(eng, M.MatcherOptions(fast_threshold=args.fast_threshold,
+                                     detector_type=M.DETECTOR_AKAZE if args.detector == "akaze" else M.DETECTOR_ORB))
 walls = []
 for _ in range(args.repeat):
     t0 = time.perf_counter()
     pts = m.generate_seeds()
     walls.append(time.perf_counter() - t0)
 st = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in m.stats.items()}
-out = {"config": args.config, "views": V, "fast_threshold": args.fast_threshold,
+out = {"config": args.config, "views": V, "detector": args.detector, "fast_threshold": args.fast_threshold,
        "wall_s": [round(w, 3) for w in walls], **st}
 if args.knn:
     rng = np.random.default_rng(1)
