@@ -1328,6 +1328,9 @@ __device__ void child_position(const RefineArgs &a, const dp_patch &par, int dir
 #ifndef DP_XCD_RANGES
 #define DP_XCD_RANGES 0
 #endif
+#ifndef DP_SIBLING_DEQUEUE
+#define DP_SIBLING_DEQUEUE 1
+#endif
 #if DP_XCD_RANGES
 constexpr int kXcds = 8;
 #else
@@ -1370,23 +1373,35 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
     int left = kXcds;
     const uint32_t gs = a.parents ? 4u : 1u;                     // LPT group size
     const int npos = a.order ? (int)(((uint32_t)a.n + gs - 1) / gs * gs) : a.n; // dequeue positions
+    // positions per dequeue: DP_SIBLING_DEQUEUE = 4 takes a parent's 4 children
+    // at once (one wave refines them back to back: their windows overlap)
+    const uint32_t step = (a.order && gs == 4u) ? (uint32_t)DP_SIBLING_DEQUEUE : 1u;
+    uint32_t run_pos = 0, run_left = 0;
     for (;;) {
         uint32_t idx = (uint32_t)npos;
-        if (lane == 0) {
-            while (left > 0) {
-                const uint32_t lo = range_lo(npos, cur), hi = range_lo(npos, cur + 1);
-                const uint32_t t = lo + atomicAdd(a.work + kWorkStride * cur, 1u);
-                if (t < hi) {
-                    idx = t;
-                    break;
+        if (run_left == 0) {
+            if (lane == 0) {
+                while (left > 0) {
+                    const uint32_t lo = range_lo(npos, cur), hi = range_lo(npos, cur + 1);
+                    const uint32_t t = lo + atomicAdd(a.work + kWorkStride * cur, step);
+                    if (t < hi) {
+                        idx = t;
+                        break;
+                    }
+                    cur = (cur + 1) & (kXcds - 1);
+                    --left;
                 }
-                cur = (cur + 1) & (kXcds - 1);
-                --left;
             }
+            idx = (uint32_t)uni((int)idx);
+            if (idx >= (uint32_t)npos)
+                break;
+            run_pos = idx;
+            run_left = step;
         }
-        idx = (uint32_t)uni((int)idx);
+        idx = run_pos++;
+        --run_left;
         if (idx >= (uint32_t)npos)
-            break;
+            continue;
         if (a.order) {
             idx = (uint32_t)uni((int)(a.order[idx / gs] * gs + idx % gs));
             if (idx >= (uint32_t)a.n) // the last group's missing children
