@@ -47,20 +47,22 @@ enum AkSel { kLt = 0, kLx = 1, kLy = 2, kLdet = 3, kT0 = 4, kT1 = 5, kT2 = 6, kT
 
 struct AkTaps {
     float w[16];
-    int32_t n;       // dense Gaussian taps (mode 0)
-    int32_t mode;    // 0 Gaussian (replicate), 1 3-tap derivative, 2 3-tap smoothing (reflect-101)
-    int32_t spacing; // 3-tap spacing; < 0: the level's sigma_size
-    int32_t pad;
+    int32_t n;       // Gaussian taps (getGaussianKernel weights)
+    int32_t mode, spacing, pad;
 };
 
 hipError_t launch_akz_gray(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s);
-hipError_t launch_akz_conv(const AkArgs &a, int level, int src, int dst, int dir, const AkTaps &t, int nv,
-                           int max_w, int max_h, hipStream_t s);
+// the separable Gaussian of src into dst in one LDS-tiled pass (<= 9 taps)
+hipError_t launch_akz_gauss2(const AkArgs &a, int level, int src, int dst, const AkTaps &t, int nv, int max_w,
+                             int max_h, hipStream_t s);
 hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_half(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_copy(const AkArgs &a, int level, int src, int dst, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float tau, int nv, int max_w, int max_h,
                           hipStream_t s);
+// two FED steps per launch through an LDS tile (bit-identical to two launches)
+hipError_t launch_akz_fed2(const AkArgs &a, int level, int src, int dst, float tau1, float tau2, int nv, int max_w,
+                           int max_h, hipStream_t s);
 // fused 3-tap passes: mode 0 the normalised Scharr of scale sigma_size, mode 1
 // the unnormalised 3x3 Scharr
 hipError_t launch_akz_rows2(const AkArgs &a, int level, int src, int dD, int dS, int mode, int nv, int max_w,

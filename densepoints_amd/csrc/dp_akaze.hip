@@ -69,67 +69,58 @@ hipError_t launch_akz_gray(const AkArgs &a, int nv, int max_w, int max_h, hipStr
     return hipGetLastError();
 }
 
-// one separable pass along x (dir 0) or y (dir 1) of plane src into dst:
-// mode 0 the dense Gaussian (replicate), 1 / 2 the 3-tap derivative /
-// smoothing at spacing s (reflect-101)
-__global__ void akz_conv_kernel(AkArgs a, int level, int src, int dst, int dir, AkTaps t)
+// the separable Gaussian (replicate border) in one pass: a 64 x 16 output
+// tile, the source rows it needs (clamped) in LDS, the row pass over the tile
+// plus the r-row halo, then the column pass -- the same expressions in the
+// same order as oracle/or_akaze.c's row and column passes (ak_gauss)
+constexpr int kGTX = 64, kGTY = 16, kGMaxR = 4;
+
+__global__ __launch_bounds__(256) void akz_gauss2_kernel(AkArgs a, int level, int src, int dst, AkTaps t)
 {
-    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ float sS[kGTY + 2 * kGMaxR][kGTX + 2 * kGMaxR];
+    __shared__ float sR[kGTY + 2 * kGMaxR][kGTX];
+    const int z = blockIdx.z;
     const AkPlane &P = a.planes[z * kAkLevels + level];
     const int w = P.w, h = P.h;
-    if (w == 0 || x >= w || y >= h)
+    const int x0 = blockIdx.x * kGTX, y0 = blockIdx.y * kGTY;
+    if (w == 0 || x0 >= w || y0 >= h) // uniform per block
         return;
+    const int r = t.n / 2;
+    const int SW = kGTX + 2 * r, SH = kGTY + 2 * r;
     const float *S = ak_ptr(a, z, level, src);
-    float *D = ak_ptr(a, z, level, dst);
-    float out;
-    if (t.mode == 0) {
-        const int r = t.n / 2;
-        if (dir == 0) {
-            const float *row = S + (size_t)y * w;
-            float acc = t.w[0] * row[ak_rep(x - r, w)];
-            for (int k = 1; k < t.n; ++k)
-                acc = acc + t.w[k] * row[ak_rep(x + k - r, w)];
-            out = acc;
-        } else {
-            float acc = t.w[0] * S[(size_t)ak_rep(y - r, h) * w + x];
-            for (int k = 1; k < t.n; ++k)
-                acc = acc + t.w[k] * S[(size_t)ak_rep(y + k - r, h) * w + x];
-            out = acc;
-        }
-    } else {
-        const int sp = t.spacing > 0 ? t.spacing : P.sigma_size;
-        float va, vb, vc;
-        if (dir == 0) {
-            const float *row = S + (size_t)y * w;
-            va = row[ak_r101(x - sp, w)];
-            vb = row[x];
-            vc = row[ak_r101(x + sp, w)];
-        } else {
-            va = S[(size_t)ak_r101(y - sp, h) * w + x];
-            vb = S[(size_t)y * w + x];
-            vc = S[(size_t)ak_r101(y + sp, h) * w + x];
-        }
-        if (t.mode == 1) {
-            out = vc - va;
-        } else {
-            float k0 = t.w[0], k1 = t.w[1];
-            if (t.spacing <= 0) {
-                // normalised Scharr smoothing of scale s: (1, 10/3, 1) / (2 s (10/3 + 2))
-                const float wgt = 10.0f / 3.0f;
-                k0 = 1.0f / (2.0f * (float)sp * (wgt + 2.0f));
-                k1 = wgt * k0;
-            }
-            out = (k0 * va + k1 * vb) + k0 * vc;
-        }
+    for (int q = threadIdx.x; q < SW * SH; q += blockDim.x) {
+        const int ty = q / SW, tx = q - ty * SW;
+        sS[ty][tx] = S[(size_t)ak_rep(y0 - r + ty, h) * w + ak_rep(x0 - r + tx, w)];
     }
-    D[(size_t)y * w + x] = out;
+    __syncthreads();
+    for (int q = threadIdx.x; q < kGTX * SH; q += blockDim.x) {
+        const int ty = q / kGTX, tx = q - ty * kGTX;
+        float acc = t.w[0] * sS[ty][tx];
+        for (int k = 1; k < t.n; ++k)
+            acc = acc + t.w[k] * sS[ty][tx + k];
+        sR[ty][tx] = acc;
+    }
+    __syncthreads();
+    float *D = ak_ptr(a, z, level, dst);
+    for (int q = threadIdx.x; q < kGTX * kGTY; q += blockDim.x) {
+        const int ty = q / kGTX, tx = q - ty * kGTX;
+        const int gx = x0 + tx, gy = y0 + ty;
+        if (gx >= w || gy >= h)
+            continue;
+        float acc = t.w[0] * sR[ty][tx];
+        for (int k = 1; k < t.n; ++k)
+            acc = acc + t.w[k] * sR[ty + k][tx];
+        D[(size_t)gy * w + gx] = acc;
+    }
 }
 
-hipError_t launch_akz_conv(const AkArgs &a, int level, int src, int dst, int dir, const AkTaps &t, int nv,
-                           int max_w, int max_h, hipStream_t s)
+hipError_t launch_akz_gauss2(const AkArgs &a, int level, int src, int dst, const AkTaps &t, int nv, int max_w,
+                             int max_h, hipStream_t s)
 {
-    hipLaunchKernelGGL(akz_conv_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, src, dst,
-                       dir, t);
+    if (t.n > 2 * kGMaxR + 1)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(akz_gauss2_kernel, dim3((max_w + kGTX - 1) / kGTX, (max_h + kGTY - 1) / kGTY, nv), dim3(256),
+                       0, s, a, level, src, dst, t);
     return hipGetLastError();
 }
 
@@ -289,6 +280,66 @@ hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float ta
 {
     hipLaunchKernelGGL(akz_fed_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, src, dst,
                        tau);
+    return hipGetLastError();
+}
+
+// two explicit FED steps in one pass: a 64 x 16 output tile, its 2-px halo of
+// Lt and the conductance in LDS, the first step over the tile + 1 px, the
+// second over the tile.  The same expressions as akz_fed_kernel, so the result
+// is that of two launches bit for bit (zero flux where a neighbour is outside
+// the image).
+constexpr int kFedTX = 64, kFedTY = 16, kFedW = kFedTX + 4, kFedH = kFedTY + 4;
+
+__global__ __launch_bounds__(256) void akz_fed2_kernel(AkArgs a, int level, int src, int dst, float tau1, float tau2)
+{
+    __shared__ float sL[kFedH][kFedW], sC[kFedH][kFedW], sM[kFedH][kFedW];
+    const int z = blockIdx.z;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int w = P.w, h = P.h;
+    const int x0 = blockIdx.x * kFedTX, y0 = blockIdx.y * kFedTY;
+    if (w == 0 || x0 >= w || y0 >= h) // uniform per block
+        return;
+    const float *L = ak_ptr(a, z, level, src), *c = ak_ptr(a, z, level, kT4);
+    for (int q = threadIdx.x; q < kFedW * kFedH; q += blockDim.x) {
+        const int ty = q / kFedW, tx = q - ty * kFedW;
+        const int gx = x0 - 2 + tx, gy = y0 - 2 + ty;
+        const bool in = gx >= 0 && gx < w && gy >= 0 && gy < h;
+        sL[ty][tx] = in ? L[(size_t)gy * w + gx] : 0.0f;
+        sC[ty][tx] = in ? c[(size_t)gy * w + gx] : 0.0f;
+    }
+    __syncthreads();
+    // one step at tile position (tx, ty) of the image point (gx, gy), reading V
+    auto step = [&](float (*V)[kFedW], int tx, int ty, int gx, int gy, float ht) {
+        const float l0 = V[ty][tx], c0 = sC[ty][tx];
+        const float xp = gx + 1 < w ? (c0 + sC[ty][tx + 1]) * (V[ty][tx + 1] - l0) : 0.0f;
+        const float xn = gx > 0 ? (sC[ty][tx - 1] + c0) * (l0 - V[ty][tx - 1]) : 0.0f;
+        const float yp = gy + 1 < h ? (c0 + sC[ty + 1][tx]) * (V[ty + 1][tx] - l0) : 0.0f;
+        const float yn = gy > 0 ? (sC[ty - 1][tx] + c0) * (l0 - V[ty - 1][tx]) : 0.0f;
+        return l0 + ht * ((xp - xn) + (yp - yn));
+    };
+    const float ht1 = 0.5f * tau1, ht2 = 0.5f * tau2;
+    // first step over the tile and a 1-px ring (image points only)
+    for (int q = threadIdx.x; q < (kFedTX + 2) * (kFedTY + 2); q += blockDim.x) {
+        const int ty = 1 + q / (kFedTX + 2), tx = 1 + q % (kFedTX + 2);
+        const int gx = x0 - 2 + tx, gy = y0 - 2 + ty;
+        if (gx >= 0 && gx < w && gy >= 0 && gy < h)
+            sM[ty][tx] = step(sL, tx, ty, gx, gy, ht1);
+    }
+    __syncthreads();
+    float *D = ak_ptr(a, z, level, dst);
+    for (int q = threadIdx.x; q < kFedTX * kFedTY; q += blockDim.x) {
+        const int ty = 2 + q / kFedTX, tx = 2 + q % kFedTX;
+        const int gx = x0 - 2 + tx, gy = y0 - 2 + ty;
+        if (gx < w && gy < h)
+            D[(size_t)gy * w + gx] = step(sM, tx, ty, gx, gy, ht2);
+    }
+}
+
+hipError_t launch_akz_fed2(const AkArgs &a, int level, int src, int dst, float tau1, float tau2, int nv, int max_w,
+                           int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_fed2_kernel, dim3((max_w + kFedTX - 1) / kFedTX, (max_h + kFedTY - 1) / kFedTY, nv),
+                       dim3(256), 0, s, a, level, src, dst, tau1, tau2);
     return hipGetLastError();
 }
 

@@ -628,9 +628,6 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         DP_HIP(c, hipMemsetAsync(s->akz_hist.p, 0, (size_t)nv * 301 * 4, st));
         const AkArgs a{s->akz_planes.p, s->akz_views.p, s->akz_pool.p, s->akz_tmp.p, s->akz_hmax.p, s->akz_hist.p,
                        s->akz_k0.p};
-        auto conv = [&](int i, int src, int dst, int dir, const AkTaps &t) {
-            return launch_akz_conv(a, i, src, dst, dir, t, nv, mw[i], mh[i], st);
-        };
         // the detector's derivatives of Lsmooth (plane ls), Ldet; Lx, Ly scaled
         auto deriv = [&](int i, int ls) -> hipError_t {
             hipError_t e = launch_akz_rows2(a, i, ls, kT1, kT2, 0, nv, mw[i], mh[i], st);
@@ -647,10 +644,8 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         // level 0: gray, L0 = Gaussian(img, 1.6), the contrast factor from the
         // unnormalised Scharr gradient of Gaussian(img, 1) (x in T0, y in T4)
         DP_HIP(c, launch_akz_gray(a, nv, mw[0], mh[0], st));
-        DP_HIP(c, conv(0, kT0, kT1, 0, g16));
-        DP_HIP(c, conv(0, kT1, kLt, 1, g16));
-        DP_HIP(c, conv(0, kT0, kT1, 0, g10));
-        DP_HIP(c, conv(0, kT1, kT3, 1, g10));
+        DP_HIP(c, launch_akz_gauss2(a, 0, kT0, kLt, g16, nv, mw[0], mh[0], st));
+        DP_HIP(c, launch_akz_gauss2(a, 0, kT0, kT3, g10, nv, mw[0], mh[0], st));
         DP_HIP(c, launch_akz_rows2(a, 0, kT3, kT1, kT2, 1, nv, mw[0], mh[0], st));
         DP_HIP(c, launch_akz_cols2(a, 0, kT1, kT0, kT2, kT4, 1, nv, mw[0], mh[0], st));
         DP_HIP(c, launch_akz_kcontrast(a, nv, mw[0], mh[0], st));
@@ -661,15 +656,20 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
             else
                 DP_HIP(c, launch_akz_copy(a, i, -1, kLt, nv, mw[i], mh[i], st));
             // Lsmooth (T3), g2 conductance (T4) from its unnormalised Scharr gradient
-            DP_HIP(c, conv(i, kLt, kT1, 0, g10));
-            DP_HIP(c, conv(i, kT1, kT3, 1, g10));
+            DP_HIP(c, launch_akz_gauss2(a, i, kLt, kT3, g10, nv, mw[i], mh[i], st));
             DP_HIP(c, launch_akz_rows2(a, i, kT3, kT1, kT2, 1, nv, mw[i], mh[i], st));
             DP_HIP(c, launch_akz_cols_g2(a, i, nv, mw[i], mh[i], st));
             // FED steps, ping-pong between Lt and T2
             int src = kLt;
-            for (size_t k = 0; k < tau[i].size(); ++k) {
-                const int dst = (k % 2 == 0) ? kT2 : kLt;
-                DP_HIP(c, launch_akz_fed(a, i, src, dst, tau[i][k], nv, mw[i], mh[i], st));
+            for (size_t k = 0; k < tau[i].size();) {
+                const int dst = src == kLt ? kT2 : kLt;
+                if (k + 1 < tau[i].size()) {
+                    DP_HIP(c, launch_akz_fed2(a, i, src, dst, tau[i][k], tau[i][k + 1], nv, mw[i], mh[i], st));
+                    k += 2;
+                } else {
+                    DP_HIP(c, launch_akz_fed(a, i, src, dst, tau[i][k], nv, mw[i], mh[i], st));
+                    k += 1;
+                }
                 src = dst;
             }
             if (src != kLt)
