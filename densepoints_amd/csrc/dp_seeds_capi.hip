@@ -537,6 +537,8 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
     DP_HIP(c, hipMemcpyAsync(s->akz_g25.p, g25, sizeof(g25), hipMemcpyHostToDevice, st));
     DP_HIP(c, hipMemcpyAsync(s->akz_bits.p, bits.data(), kAkBits * 4, hipMemcpyHostToDevice, st));
     const int n_windows = akaze_windows();
+    if (n_windows > 64)
+        return fail(c, DP_E_ARG, "dp_generate_seeds: AKAZE orientation windows exceed a wave");
 
     auto taps_gauss = [](float sigma) {
         AkTaps t{};

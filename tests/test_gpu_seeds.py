@@ -312,3 +312,19 @@ def test_knn_match_wide_matches_oracle(orc, nq, nt):
     with dp.Engine() as eng:
         ig, dg = M.knn_match(eng, q, t, width=64)
     assert np.array_equal(dg, do) and np.array_equal(ig, io)
+
+
+def test_akaze_edge_blank_views_and_no_keypoints(orc):
+    """A uniform view (no gradient: the contrast factor's 0.03 fallback, no
+    extrema) beside textured ones, and a threshold no response reaches: the
+    GPU path equals the oracle and an empty keypoint set flows through the
+    matching stages."""
+    cfg = synth.config(n_views=3, width=320, height=240, kind=1)
+    P, imgs, _ = synth.scene_host(cfg)
+    blank = np.full_like(imgs[1], 128)
+    kw = dict(detector_type=M.DETECTOR_AKAZE, akaze_threshold=0.0002)
+    r, m = _run_both(orc, P, [imgs[0], blank, imgs[2]], kw)
+    assert r["keypoints"][1].size == 0 and m.stats["keypoints"] > 0
+    kw = dict(detector_type=M.DETECTOR_AKAZE, akaze_threshold=10.0)
+    r, m = _run_both(orc, P, imgs, kw)
+    assert m.stats["keypoints"] == 0 and m.stats["points"] == 0
