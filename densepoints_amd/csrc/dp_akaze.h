@@ -71,6 +71,10 @@ hipError_t launch_akz_cols2(const AkArgs &a, int level, int srcS, int dstS, int 
                             int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_cols_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
+// the detector-derivative stage of a level in one LDS-tiled pass (sigma_size <= 4)
+hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_w, int max_h, hipStream_t s);
+// a level's Lsmooth (T3) and g2 conductance (T4) from Lt in one LDS-tiled pass
+hipError_t launch_akz_flow(const AkArgs &a, int level, const AkTaps &t, int nv, int max_w, int max_h, hipStream_t s);
 // extrema candidates in (view, level, y, x) order: per-segment counts, an
 // exclusive scan of them (host side, hipcub), then the indices
 hipError_t launch_akz_count(const AkArgs &a, int level, float thr, uint32_t *cnt, int nv, int max_w, int max_h,

@@ -485,6 +485,165 @@ hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, in
     return hipGetLastError();
 }
 
+// the whole detector-derivative stage of one level in one pass: a 64 x 16
+// output tile reads its Lsmooth neighbourhood (+-2s, reflect-101 per axis) into
+// LDS, computes the first derivatives Lx0, Ly0 at the tile's in-image points
+// +- s, then Lxx, Lxy, Lyy, Ldet and the scaled Lx, Ly at the tile.  Every
+// value is the one the separate passes compute (each 1-D pass reflects per
+// axis, and the second passes read the first derivatives at reflected in-image
+// points, which the +-s ring holds), in the same expression order.
+constexpr int kDTX = 64, kDTY = 16, kDMaxS = 4;
+
+__global__ __launch_bounds__(256) void akz_deriv_kernel(AkArgs a, int level, int ls)
+{
+    __shared__ float sL[kDTY + 4 * kDMaxS][kDTX + 4 * kDMaxS];
+    __shared__ float sX[kDTY + 2 * kDMaxS][kDTX + 2 * kDMaxS], sY[kDTY + 2 * kDMaxS][kDTX + 2 * kDMaxS];
+    const int z = blockIdx.z;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int w = P.w, h = P.h;
+    const int x0 = blockIdx.x * kDTX, y0 = blockIdx.y * kDTY;
+    if (w == 0 || x0 >= w || y0 >= h) // uniform per block
+        return;
+    int sp;
+    float k0, k1;
+    akz_coef(P, 0, sp, k0, k1);
+    const int s2 = 2 * sp;
+    const int LW = kDTX + 2 * s2, LH = kDTY + 2 * s2; // Lsmooth tile: origin (x0 - 2s, y0 - 2s)
+    const int RW = kDTX + s2, RH = kDTY + s2;         // first-derivative ring: origin (x0 - s, y0 - s)
+    const float *S = ak_ptr(a, z, level, ls);
+    for (int q = threadIdx.x; q < LW * LH; q += blockDim.x) {
+        const int ty = q / LW, tx = q - ty * LW;
+        sL[ty][tx] = S[(size_t)ak_r101(y0 - s2 + ty, h) * w + ak_r101(x0 - s2 + tx, w)];
+    }
+    __syncthreads();
+    // Lx0 = smooth_y(deriv_x(Ls)), Ly0 = deriv_y(smooth_x(Ls)) at the ring's in-image points
+    for (int q = threadIdx.x; q < RW * RH; q += blockDim.x) {
+        const int ry = q / RW, rx = q - ry * RW;
+        const int gx = x0 - sp + rx, gy = y0 - sp + ry;
+        if (gx < 0 || gx >= w || gy < 0 || gy >= h)
+            continue;
+        const int tx = rx + sp, ty = ry + sp; // the point in the Lsmooth tile
+        const float da = sL[ty - sp][tx + sp] - sL[ty - sp][tx - sp];
+        const float db = sL[ty][tx + sp] - sL[ty][tx - sp];
+        const float dc = sL[ty + sp][tx + sp] - sL[ty + sp][tx - sp];
+        sX[ry][rx] = (k0 * da + k1 * db) + k0 * dc;
+        const float sa = (k0 * sL[ty - sp][tx - sp] + k1 * sL[ty - sp][tx]) + k0 * sL[ty - sp][tx + sp];
+        const float sc = (k0 * sL[ty + sp][tx - sp] + k1 * sL[ty + sp][tx]) + k0 * sL[ty + sp][tx + sp];
+        sY[ry][rx] = sc - sa;
+    }
+    __syncthreads();
+    const float fs = (float)sp, fs2 = (float)(sp * sp);
+    float *LX = ak_ptr(a, z, level, kLx), *LY = ak_ptr(a, z, level, kLy), *LD = ak_ptr(a, z, level, kLdet);
+    for (int q = threadIdx.x; q < kDTX * kDTY; q += blockDim.x) {
+        const int oy = q / kDTX, ox = q - oy * kDTX;
+        const int gx = x0 + ox, gy = y0 + oy;
+        if (gx >= w || gy >= h)
+            continue;
+        // ring coordinates of the reflected in-image neighbours
+        const int xm = ak_r101(gx - sp, w) - (x0 - sp), xc = gx - (x0 - sp), xp = ak_r101(gx + sp, w) - (x0 - sp);
+        const int ym = ak_r101(gy - sp, h) - (y0 - sp), yc = gy - (y0 - sp), yp = ak_r101(gy + sp, h) - (y0 - sp);
+        // Lxx = smooth_y(deriv_x(Lx0))
+        const float ea = sX[ym][xp] - sX[ym][xm], eb = sX[yc][xp] - sX[yc][xm], ec = sX[yp][xp] - sX[yp][xm];
+        const float lxx = (k0 * ea + k1 * eb) + k0 * ec;
+        // Lxy = deriv_y(smooth_x(Lx0)), Lyy = deriv_y(smooth_x(Ly0))
+        const float xa = (k0 * sX[ym][xm] + k1 * sX[ym][xc]) + k0 * sX[ym][xp];
+        const float xc2 = (k0 * sX[yp][xm] + k1 * sX[yp][xc]) + k0 * sX[yp][xp];
+        const float lxy = xc2 - xa;
+        const float ya = (k0 * sY[ym][xm] + k1 * sY[ym][xc]) + k0 * sY[ym][xp];
+        const float yc2 = (k0 * sY[yp][xm] + k1 * sY[yp][xc]) + k0 * sY[yp][xp];
+        const float lyy = yc2 - ya;
+        const size_t i = (size_t)gy * w + gx;
+        LX[i] = sX[yc][xc] * fs;
+        LY[i] = sY[yc][xc] * fs;
+        const float xx = lxx * fs2, yy = lyy * fs2, xy = lxy * fs2;
+        LD[i] = xx * yy - xy * xy;
+    }
+}
+
+hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_deriv_kernel, dim3((max_w + kDTX - 1) / kDTX, (max_h + kDTY - 1) / kDTY, nv), dim3(256), 0,
+                       s, a, level, ls);
+    return hipGetLastError();
+}
+
+// a level's flow stage in one pass: Lsmooth = Gaussian(Lt) (replicate) over the
+// tile +- 1 px, written to T3 at the tile; the unnormalised Scharr gradient of
+// Lsmooth (reflect-101, read at the reflected in-image ring points) and the g2
+// conductance into T4 -- the values of gauss2 + rows2 + cols_g2, in their order
+constexpr int kFTX = 64, kFTY = 16;
+
+__global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, AkTaps t)
+{
+    __shared__ float sS[kFTY + 2 + 2 * kGMaxR][kFTX + 2 + 2 * kGMaxR];
+    __shared__ float sR[kFTY + 2 + 2 * kGMaxR][kFTX + 2];
+    __shared__ float sM[kFTY + 2][kFTX + 2];
+    const int z = blockIdx.z;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int w = P.w, h = P.h;
+    const int x0 = blockIdx.x * kFTX, y0 = blockIdx.y * kFTY;
+    if (w == 0 || x0 >= w || y0 >= h) // uniform per block
+        return;
+    const int r = t.n / 2;
+    const int SW = kFTX + 2 + 2 * r, SH = kFTY + 2 + 2 * r; // origin (x0 - 1 - r, y0 - 1 - r)
+    const float *L = ak_ptr(a, z, level, kLt);
+    for (int q = threadIdx.x; q < SW * SH; q += blockDim.x) {
+        const int ty = q / SW, tx = q - ty * SW;
+        sS[ty][tx] = L[(size_t)ak_rep(y0 - 1 - r + ty, h) * w + ak_rep(x0 - 1 - r + tx, w)];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < (kFTX + 2) * SH; q += blockDim.x) {
+        const int ty = q / (kFTX + 2), tx = q - ty * (kFTX + 2);
+        float acc = t.w[0] * sS[ty][tx];
+        for (int k = 1; k < t.n; ++k)
+            acc = acc + t.w[k] * sS[ty][tx + k];
+        sR[ty][tx] = acc;
+    }
+    __syncthreads();
+    // Lsmooth over the ring (origin x0 - 1, y0 - 1); the tile's values into T3
+    float *T3 = ak_ptr(a, z, level, kT3);
+    for (int q = threadIdx.x; q < (kFTX + 2) * (kFTY + 2); q += blockDim.x) {
+        const int ry = q / (kFTX + 2), rx = q - ry * (kFTX + 2);
+        float acc = t.w[0] * sR[ry][rx];
+        for (int k = 1; k < t.n; ++k)
+            acc = acc + t.w[k] * sR[ry + k][rx];
+        sM[ry][rx] = acc;
+        const int gx = x0 - 1 + rx, gy = y0 - 1 + ry;
+        if (rx >= 1 && rx <= kFTX && ry >= 1 && ry <= kFTY && gx < w && gy < h)
+            T3[(size_t)gy * w + gx] = acc;
+    }
+    __syncthreads();
+    float k = a.k0[z];
+    for (int o = 0; o < P.octave; ++o)
+        k = k * 0.75f;
+    const float k2inv = 1.0f / (k * k);
+    float *T4 = ak_ptr(a, z, level, kT4);
+    for (int q = threadIdx.x; q < kFTX * kFTY; q += blockDim.x) {
+        const int oy = q / kFTX, ox = q - oy * kFTX;
+        const int gx = x0 + ox, gy = y0 + oy;
+        if (gx >= w || gy >= h)
+            continue;
+        const int xm = ak_r101(gx - 1, w) - (x0 - 1), xp = ak_r101(gx + 1, w) - (x0 - 1), xc = gx - (x0 - 1);
+        const int ym = ak_r101(gy - 1, h) - (y0 - 1), yp = ak_r101(gy + 1, h) - (y0 - 1), yc = gy - (y0 - 1);
+        // x: rows derivative, columns (3, 10, 3); y: rows (3, 10, 3), columns derivative
+        const float da = sM[ym][xp] - sM[ym][xm], db = sM[yc][xp] - sM[yc][xm], dc = sM[yp][xp] - sM[yp][xm];
+        const float lx = (3.0f * da + 10.0f * db) + 3.0f * dc;
+        const float sa = (3.0f * sM[ym][xm] + 10.0f * sM[ym][xc]) + 3.0f * sM[ym][xp];
+        const float sc = (3.0f * sM[yp][xm] + 10.0f * sM[yp][xc]) + 3.0f * sM[yp][xp];
+        const float ly = sc - sa;
+        T4[(size_t)gy * w + gx] = 1.0f / (1.0f + k2inv * (lx * lx + ly * ly));
+    }
+}
+
+hipError_t launch_akz_flow(const AkArgs &a, int level, const AkTaps &t, int nv, int max_w, int max_h, hipStream_t s)
+{
+    if (t.n > 2 * kGMaxR + 1)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(akz_flow_kernel, dim3((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv), dim3(256), 0,
+                       s, a, level, t);
+    return hipGetLastError();
+}
+
 // 3x3 maxima of Ldet above the threshold inside the descriptor border
 __device__ __forceinline__ bool akz_is_cand(const AkArgs &a, const AkPlane &P, int x, int y, float thr)
 {

@@ -632,6 +632,8 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
                        s->akz_k0.p};
         // the detector's derivatives of Lsmooth (plane ls), Ldet; Lx, Ly scaled
         auto deriv = [&](int i, int ls) -> hipError_t {
+            if (full.ss[i] <= 4)
+                return launch_akz_deriv(a, i, ls, nv, mw[i], mh[i], st);
             hipError_t e = launch_akz_rows2(a, i, ls, kT1, kT2, 0, nv, mw[i], mh[i], st);
             if (e == hipSuccess)
                 e = launch_akz_cols2(a, i, kT1, kLx, kT2, kLy, 0, nv, mw[i], mh[i], st);
@@ -658,9 +660,7 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
             else
                 DP_HIP(c, launch_akz_copy(a, i, -1, kLt, nv, mw[i], mh[i], st));
             // Lsmooth (T3), g2 conductance (T4) from its unnormalised Scharr gradient
-            DP_HIP(c, launch_akz_gauss2(a, i, kLt, kT3, g10, nv, mw[i], mh[i], st));
-            DP_HIP(c, launch_akz_rows2(a, i, kT3, kT1, kT2, 1, nv, mw[i], mh[i], st));
-            DP_HIP(c, launch_akz_cols_g2(a, i, nv, mw[i], mh[i], st));
+            DP_HIP(c, launch_akz_flow(a, i, g10, nv, mw[i], mh[i], st));
             // FED steps, ping-pong between Lt and T2
             int src = kLt;
             for (size_t k = 0; k < tau[i].size();) {
