@@ -43,7 +43,7 @@ struct AkArgs {
 };
 
 // plane selectors: level planes and view temporaries
-enum AkSel { kLt = 0, kLx = 1, kLy = 2, kLdet = 3, kT0 = 4, kT1 = 5, kT2 = 6, kT3 = 7, kT4 = 8 };
+enum AkSel { kPrevLt = -2, kLt = 0, kLx = 1, kLy = 2, kLdet = 3, kT0 = 4, kT1 = 5, kT2 = 6, kT3 = 7, kT4 = 8 };
 
 struct AkTaps {
     float w[16];
@@ -56,7 +56,7 @@ hipError_t launch_akz_gray(const AkArgs &a, int nv, int max_w, int max_h, hipStr
 hipError_t launch_akz_gauss2(const AkArgs &a, int level, int src, int dst, const AkTaps &t, int nv, int max_w,
                              int max_h, hipStream_t s);
 hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s);
-hipError_t launch_akz_half(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_half(const AkArgs &a, int level, int dst, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_copy(const AkArgs &a, int level, int src, int dst, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float tau, int nv, int max_w, int max_h,
                           hipStream_t s);
@@ -73,14 +73,15 @@ hipError_t launch_akz_cols_g2(const AkArgs &a, int level, int nv, int max_w, int
 hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
 // the detector-derivative stage of a level in one LDS-tiled pass (sigma_size <= 4)
 hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_w, int max_h, hipStream_t s);
-// a level's Lsmooth (T3) and g2 conductance (T4) from Lt in one LDS-tiled pass
-hipError_t launch_akz_flow(const AkArgs &a, int level, const AkTaps &t, int nv, int max_w, int max_h, hipStream_t s);
+// a level's Lsmooth (T3) and g2 conductance (T4) from its starting Lt (plane src) in one LDS-tiled pass
+hipError_t launch_akz_flow(const AkArgs &a, int level, int src, const AkTaps &t, int nv, int max_w, int max_h,
+                           hipStream_t s);
 // extrema candidates in (view, level, y, x) order: per-segment counts, an
 // exclusive scan of them (host side, hipcub), then the indices
-hipError_t launch_akz_count(const AkArgs &a, int level, float thr, uint32_t *cnt, int nv, int max_w, int max_h,
-                            hipStream_t s);
-hipError_t launch_akz_emit(const AkArgs &a, int level, float thr, const uint32_t *off, int64_t *cand, int nv,
-                           int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_count(const AkArgs &a, int level, float thr, uint32_t *cnt, unsigned long long *mask, int nv,
+                            int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_emit(const AkArgs &a, int level, const unsigned long long *mask, const uint32_t *off,
+                           int64_t *cand, int nv, int max_w, int max_h, hipStream_t s);
 
 // candidate list (sorted global Ldet indices) -> keypoints (suppression +
 // subpixel refinement), keep flags

@@ -26,6 +26,10 @@ namespace {
 
 __device__ __forceinline__ float *ak_ptr(const AkArgs &a, int z, int level, int sel)
 {
+    if (sel == kPrevLt) {
+        level -= 1;
+        sel = kLt;
+    }
     if (sel < kT0) {
         const AkPlane &p = a.planes[z * kAkLevels + level];
         return a.pool + p.off + (int64_t)sel * ((int64_t)p.w * p.h);
@@ -220,8 +224,8 @@ hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, h
     return hipGetLastError();
 }
 
-// halfsample: the 2x2 box average of the previous level's Lt
-__global__ void akz_half_kernel(AkArgs a, int level)
+// halfsample: the 2x2 box average of the previous level's Lt into plane dst
+__global__ void akz_half_kernel(AkArgs a, int level, int dst)
 {
     const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     const AkPlane &L = a.planes[z * kAkLevels + level];
@@ -229,23 +233,23 @@ __global__ void akz_half_kernel(AkArgs a, int level)
         return;
     const AkPlane &P = a.planes[z * kAkLevels + level - 1];
     const float *r0 = a.pool + P.off + (size_t)(2 * y) * P.w + 2 * x, *r1 = r0 + P.w;
-    a.pool[L.off + (size_t)y * L.w + x] = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
+    ak_ptr(a, z, level, dst)[(size_t)y * L.w + x] = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
 }
 
-hipError_t launch_akz_half(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
+hipError_t launch_akz_half(const AkArgs &a, int level, int dst, int nv, int max_w, int max_h, hipStream_t s)
 {
-    hipLaunchKernelGGL(akz_half_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
+    hipLaunchKernelGGL(akz_half_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, dst);
     return hipGetLastError();
 }
 
-// copy a plane; src/dst selectors of `level`, except src = -1: the previous level's Lt
+// copy a plane; src/dst selectors of `level` (src kPrevLt: the previous level's Lt)
 __global__ void akz_copy_kernel(AkArgs a, int level, int src, int dst)
 {
     const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
     const AkPlane &L = a.planes[z * kAkLevels + level];
     if (L.w == 0 || x >= L.w || y >= L.h)
         return;
-    const float *S = src < 0 ? ak_ptr(a, z, level - 1, kLt) : ak_ptr(a, z, level, src);
+    const float *S = ak_ptr(a, z, level, src);
     ak_ptr(a, z, level, dst)[(size_t)y * L.w + x] = S[(size_t)y * L.w + x];
 }
 
@@ -573,7 +577,7 @@ hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_
 // conductance into T4 -- the values of gauss2 + rows2 + cols_g2, in their order
 constexpr int kFTX = 64, kFTY = 16;
 
-__global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, AkTaps t)
+__global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, int src, AkTaps t)
 {
     __shared__ float sS[kFTY + 2 + 2 * kGMaxR][kFTX + 2 + 2 * kGMaxR];
     __shared__ float sR[kFTY + 2 + 2 * kGMaxR][kFTX + 2];
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, AkTa
         return;
     const int r = t.n / 2;
     const int SW = kFTX + 2 + 2 * r, SH = kFTY + 2 + 2 * r; // origin (x0 - 1 - r, y0 - 1 - r)
-    const float *L = ak_ptr(a, z, level, kLt);
+    const float *L = ak_ptr(a, z, level, src);
     for (int q = threadIdx.x; q < SW * SH; q += blockDim.x) {
         const int ty = q / SW, tx = q - ty * SW;
         sS[ty][tx] = L[(size_t)ak_rep(y0 - 1 - r + ty, h) * w + ak_rep(x0 - 1 - r + tx, w)];
@@ -635,12 +639,13 @@ __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, AkTa
     }
 }
 
-hipError_t launch_akz_flow(const AkArgs &a, int level, const AkTaps &t, int nv, int max_w, int max_h, hipStream_t s)
+hipError_t launch_akz_flow(const AkArgs &a, int level, int src, const AkTaps &t, int nv, int max_w, int max_h,
+                           hipStream_t s)
 {
     if (t.n > 2 * kGMaxR + 1)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(akz_flow_kernel, dim3((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv), dim3(256), 0,
-                       s, a, level, t);
+                       s, a, level, src, t);
     return hipGetLastError();
 }
 
@@ -661,54 +666,81 @@ __device__ __forceinline__ bool akz_is_cand(const AkArgs &a, const AkPlane &P, i
     return lx >= 0 && rx < w && uy >= 0 && dy < h;
 }
 
-// pass 1: candidates per (plane row, 256-px segment), at P.seg_base + y nbx + bx
-__global__ __launch_bounds__(256) void akz_count_kernel(AkArgs a, int level, float thr, uint32_t *cnt)
-{
-    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    const AkPlane &P = a.planes[z * kAkLevels + level];
-    const int nbx = (P.w + 255) >> 8;
-    if (P.w == 0 || y >= P.h || (int)blockIdx.x >= nbx) // uniform per block
-        return;
-    const int c = __syncthreads_count(x < P.w && akz_is_cand(a, P, x, y, thr));
-    if (threadIdx.x == 0)
-        cnt[P.seg_base + (int64_t)y * nbx + blockIdx.x] = (uint32_t)c;
-}
+// candidates per (plane row, 256-px segment), at P.seg_base + y nbx + bx: a
+// workgroup covers one segment of kCandRows rows, a wave kCandRows / 4 of them,
+// the segment in four coalesced 64-px chunks
+constexpr int kCandRows = 16;
 
-// pass 2: each segment's candidates at its exclusive-scan offset, in x order
-__global__ __launch_bounds__(256) void akz_emit_kernel(AkArgs a, int level, float thr, const uint32_t *off,
-                                                       int64_t *cand)
+// pass 1: the counts, and the four chunk ballots per segment into mask
+__global__ __launch_bounds__(256) void akz_count_kernel(AkArgs a, int level, float thr, uint32_t *cnt,
+                                                        unsigned long long *mask)
 {
-    __shared__ uint32_t wc[4];
-    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int z = blockIdx.z;
     const AkPlane &P = a.planes[z * kAkLevels + level];
     const int nbx = (P.w + 255) >> 8;
-    if (P.w == 0 || y >= P.h || (int)blockIdx.x >= nbx)
+    const int y0 = blockIdx.y * kCandRows;
+    if (P.w == 0 || y0 >= P.h || (int)blockIdx.x >= nbx) // uniform per block
         return;
-    const bool f = x < P.w && akz_is_cand(a, P, x, y, thr);
-    const unsigned long long m = __ballot(f);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (lane == 0)
-        wc[wv] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t base = off[P.seg_base + (int64_t)y * nbx + blockIdx.x];
-    for (int k = 0; k < wv; ++k)
-        base += wc[k];
-    if (f)
-        cand[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = P.det_base + (int64_t)y * P.w + x;
+    for (int r = 0; r < kCandRows / 4; ++r) {
+        const int y = y0 + wv * (kCandRows / 4) + r;
+        if (y >= P.h)
+            break;
+        unsigned long long m[4];
+        for (int k = 0; k < 4; ++k) {
+            const int x = (int)blockIdx.x * 256 + k * 64 + lane;
+            m[k] = __ballot(x < P.w && akz_is_cand(a, P, x, y, thr));
+        }
+        const int64_t sg = P.seg_base + (int64_t)y * nbx + blockIdx.x;
+        if (lane < 4)
+            mask[4 * sg + lane] = lane == 0 ? m[0] : (lane == 1 ? m[1] : (lane == 2 ? m[2] : m[3]));
+        if (lane == 0)
+            cnt[sg] = (uint32_t)(__popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]));
+    }
 }
 
-hipError_t launch_akz_count(const AkArgs &a, int level, float thr, uint32_t *cnt, int nv, int max_w, int max_h,
-                            hipStream_t s)
+// pass 2: each segment's candidates at its exclusive-scan offset, in x order,
+// from pass 1's ballots
+__global__ __launch_bounds__(256) void akz_emit_kernel(AkArgs a, int level, const unsigned long long *mask,
+                                                       const uint32_t *off, int64_t *cand)
 {
-    hipLaunchKernelGGL(akz_count_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, thr, cnt);
+    const int z = blockIdx.z;
+    const AkPlane &P = a.planes[z * kAkLevels + level];
+    const int nbx = (P.w + 255) >> 8;
+    const int y0 = blockIdx.y * kCandRows;
+    if (P.w == 0 || y0 >= P.h || (int)blockIdx.x >= nbx)
+        return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int r = 0; r < kCandRows / 4; ++r) {
+        const int y = y0 + wv * (kCandRows / 4) + r;
+        if (y >= P.h)
+            break;
+        const int64_t sg = P.seg_base + (int64_t)y * nbx + blockIdx.x;
+        uint32_t base = off[sg];
+        for (int k = 0; k < 4; ++k) {
+            const unsigned long long m = mask[4 * sg + k];
+            if ((m >> lane) & 1ull)
+                cand[base + (uint32_t)__popcll(m & below)] =
+                    P.det_base + (int64_t)y * P.w + (int)blockIdx.x * 256 + k * 64 + lane;
+            base += (uint32_t)__popcll(m);
+        }
+    }
+}
+
+hipError_t launch_akz_count(const AkArgs &a, int level, float thr, uint32_t *cnt, unsigned long long *mask, int nv,
+                            int max_w, int max_h, hipStream_t s)
+{
+    hipLaunchKernelGGL(akz_count_kernel, dim3((max_w + 255) / 256, (max_h + kCandRows - 1) / kCandRows, nv), dim3(256),
+                       0, s, a, level, thr, cnt, mask);
     return hipGetLastError();
 }
 
-hipError_t launch_akz_emit(const AkArgs &a, int level, float thr, const uint32_t *off, int64_t *cand, int nv,
-                           int max_w, int max_h, hipStream_t s)
+hipError_t launch_akz_emit(const AkArgs &a, int level, const unsigned long long *mask, const uint32_t *off,
+                           int64_t *cand, int nv, int max_w, int max_h, hipStream_t s)
 {
-    hipLaunchKernelGGL(akz_emit_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, thr, off,
-                       cand);
+    hipLaunchKernelGGL(akz_emit_kernel, dim3((max_w + 255) / 256, (max_h + kCandRows - 1) / kCandRows, nv), dim3(256),
+                       0, s, a, level, mask, off, cand);
     return hipGetLastError();
 }
 

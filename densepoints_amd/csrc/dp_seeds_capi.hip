@@ -622,7 +622,7 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         DP_HIP(c, s->akz_hmax.reserve(nv));
         DP_HIP(c, s->akz_hist.reserve((size_t)nv * 301));
         DP_HIP(c, s->akz_k0.reserve(nv));
-        DP_HIP(c, s->akz_seg.reserve(2 * (segs + 1)));
+        DP_HIP(c, s->akz_seg.reserve(2 * (segs + 1) + 8 * segs)); // counts, offsets, 4 u64 ballots per segment
         DP_HIP(c, hipMemcpyAsync(s->akz_planes.p, planes.data(), planes.size() * sizeof(AkPlane),
                                  hipMemcpyHostToDevice, st));
         DP_HIP(c, hipMemcpyAsync(s->akz_views.p, views.data(), nv * sizeof(AkView), hipMemcpyHostToDevice, st));
@@ -655,17 +655,20 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         DP_HIP(c, launch_akz_kcontrast(a, nv, mw[0], mh[0], st));
         DP_HIP(c, deriv(0, kLt));
         for (int i = 1; i < nlev; ++i) {
-            if (full.octave[i] > full.octave[i - 1])
-                DP_HIP(c, launch_akz_half(a, i, nv, mw[i], mh[i], st));
-            else
-                DP_HIP(c, launch_akz_copy(a, i, -1, kLt, nv, mw[i], mh[i], st));
+            // the level starts from the previous level's Lt (read in place) or its
+            // half-sample; the FED steps ping-pong between T2 and Lt with the
+            // parity that ends in Lt (no copies)
+            const int nt = (int)tau[i].size(), nl = nt / 2 + nt % 2; // steps, launches
+            int src = kPrevLt;
+            if (full.octave[i] > full.octave[i - 1]) {
+                src = nl % 2 ? kT2 : kLt;
+                DP_HIP(c, launch_akz_half(a, i, src, nv, mw[i], mh[i], st));
+            }
             // Lsmooth (T3), g2 conductance (T4) from its unnormalised Scharr gradient
-            DP_HIP(c, launch_akz_flow(a, i, g10, nv, mw[i], mh[i], st));
-            // FED steps, ping-pong between Lt and T2
-            int src = kLt;
-            for (size_t k = 0; k < tau[i].size();) {
-                const int dst = src == kLt ? kT2 : kLt;
-                if (k + 1 < tau[i].size()) {
+            DP_HIP(c, launch_akz_flow(a, i, src, g10, nv, mw[i], mh[i], st));
+            for (int k = 0, j = 0; k < nt; ++j) {
+                const int dst = (nl - 1 - j) % 2 ? kT2 : kLt;
+                if (k + 1 < nt) {
                     DP_HIP(c, launch_akz_fed2(a, i, src, dst, tau[i][k], tau[i][k + 1], nv, mw[i], mh[i], st));
                     k += 2;
                 } else {
@@ -675,15 +678,16 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
                 src = dst;
             }
             if (src != kLt)
-                DP_HIP(c, launch_akz_copy(a, i, kT2, kLt, nv, mw[i], mh[i], st));
+                DP_HIP(c, launch_akz_copy(a, i, src, kLt, nv, mw[i], mh[i], st));
             DP_HIP(c, deriv(i, kT3));
         }
         // extrema candidates in (view, level, y, x) order: counts per
         // (row, 256-px segment), their exclusive scan, the indices
         uint32_t *seg_cnt = s->akz_seg.p, *seg_off = s->akz_seg.p + segs + 1;
+        auto *seg_mask = reinterpret_cast<unsigned long long *>(s->akz_seg.p + 2 * (segs + 1));
         DP_HIP(c, hipMemsetAsync(seg_cnt, 0, (size_t)(segs + 1) * 4, st));
         for (int i = 0; i < nlev; ++i)
-            DP_HIP(c, launch_akz_count(a, i, mo.akaze_threshold, seg_cnt, nv, mw[i], mh[i], st));
+            DP_HIP(c, launch_akz_count(a, i, mo.akaze_threshold, seg_cnt, seg_mask, nv, mw[i], mh[i], st));
         DP_CUB(c, s, hipcub::DeviceScan::ExclusiveSum(_tmp, _bytes, seg_cnt, seg_off, (int)(segs + 1), st));
         uint32_t n_cand32 = 0;
         DP_HIP(c, hipMemcpyAsync(&n_cand32, seg_off + segs, 4, hipMemcpyDeviceToHost, st));
@@ -691,7 +695,7 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         const int64_t n_cand = n_cand32;
         DP_HIP(c, s->akz_cand.reserve(n_cand + 1));
         for (int i = 0; i < nlev; ++i)
-            DP_HIP(c, launch_akz_emit(a, i, mo.akaze_threshold, seg_off, s->akz_cand.p, nv, mw[i], mh[i], st));
+            DP_HIP(c, launch_akz_emit(a, i, seg_mask, seg_off, s->akz_cand.p, nv, mw[i], mh[i], st));
         std::vector<int32_t> pids, vids(nv);
         std::vector<int64_t> pbase;
         for (int z = 0; z < nv; ++z) {
