@@ -55,13 +55,20 @@ hipError_t launch_akz_gray(const AkArgs &a, int nv, int max_w, int max_h, hipStr
 // the separable Gaussian of src into dst in one LDS-tiled pass (<= 9 taps)
 hipError_t launch_akz_gauss2(const AkArgs &a, int level, int src, int dst, const AkTaps &t, int nv, int max_w,
                              int max_h, hipStream_t s);
-hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s);
+// Gaussian(gray, sigma 1) + its unnormalised Scharr magnitude and maximum in one
+// LDS-tiled pass, then the histogram and the percentile (the contrast factor)
+hipError_t launch_akz_contrast(const AkArgs &a, const AkTaps &t, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_half(const AkArgs &a, int level, int dst, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_copy(const AkArgs &a, int level, int src, int dst, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float tau, int nv, int max_w, int max_h,
                           hipStream_t s);
-// two FED steps per launch through an LDS tile (bit-identical to two launches)
-hipError_t launch_akz_fed2(const AkArgs &a, int level, int src, int dst, float tau1, float tau2, int nv, int max_w,
+// k <= kAkFedPerLaunch FED steps (tau[0 .. k-1]) per launch through an LDS tile
+// (bit-identical to k launches)
+constexpr int kAkFedPerLaunch = 4;
+struct AkFedTaus {
+    float tau[kAkFedPerLaunch];
+};
+hipError_t launch_akz_fedk(const AkArgs &a, int level, int src, int dst, const float *tau, int k, int nv, int max_w,
                            int max_h, hipStream_t s);
 // fused 3-tap passes: mode 0 the normalised Scharr of scale sigma_size, mode 1
 // the unnormalised 3x3 Scharr
@@ -69,7 +76,6 @@ hipError_t launch_akz_rows2(const AkArgs &a, int level, int src, int dD, int dS,
                             int max_h, hipStream_t s);
 hipError_t launch_akz_cols2(const AkArgs &a, int level, int srcS, int dstS, int srcD, int dstD, int mode, int nv,
                             int max_w, int max_h, hipStream_t s);
-hipError_t launch_akz_cols_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
 // the detector-derivative stage of a level in one LDS-tiled pass (sigma_size <= 4)
 hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_w, int max_h, hipStream_t s);

@@ -128,37 +128,10 @@ hipError_t launch_akz_gauss2(const AkArgs &a, int level, int src, int dst, const
     return hipGetLastError();
 }
 
-// compute_k_percentile (0.7, 300 bins) from the unnormalised Scharr gradient
-// of Gaussian(img, 1) in T0 (x) / T4 (y): the interior maximum, the histogram,
-// then one lane per view
+// compute_k_percentile (0.7, 300 bins) from the magnitude of the unnormalised
+// Scharr gradient of Gaussian(img, 1) in T1 and its interior maximum in hmax
+// (both from launch_akz_contrast): the histogram, then one lane per view
 constexpr int kAkRowsPerBlock = 16;
-
-__global__ __launch_bounds__(256) void akz_modg_max_kernel(AkArgs a)
-{
-    __shared__ uint32_t wmax[4];
-    const int z = blockIdx.z, x = blockIdx.x * blockDim.x + threadIdx.x;
-    const AkView v = a.views[z];
-    // non-negative floats order as their bit patterns
-    uint32_t b = 0;
-    for (int r = 0; r < kAkRowsPerBlock; ++r) {
-        const int y = blockIdx.y * kAkRowsPerBlock + r;
-        if (x >= 1 && x < v.w0 - 1 && y >= 1 && y < v.h0 - 1) {
-            const size_t i = (size_t)y * v.w0 + x;
-            const float lx = a.tmp[v.tmp + i], ly = a.tmp[v.tmp + 4 * v.n0 + i];
-            b = max(b, __float_as_uint(sqrtf(lx * lx + ly * ly)));
-        }
-    }
-    for (int o = 32; o >= 1; o >>= 1)
-        b = max(b, (uint32_t)__shfl_xor((int)b, o));
-    if ((threadIdx.x & 63) == 0)
-        wmax[threadIdx.x >> 6] = b;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-        if (m)
-            atomicMax(&a.hmax[z], m);
-    }
-}
 
 __global__ __launch_bounds__(256) void akz_hist_kernel(AkArgs a)
 {
@@ -173,8 +146,7 @@ __global__ __launch_bounds__(256) void akz_hist_kernel(AkArgs a)
         const int y = blockIdx.y * kAkRowsPerBlock + r;
         if (hmax > 0.0f && x >= 1 && x < v.w0 - 1 && y >= 1 && y < v.h0 - 1) {
             const size_t i = (size_t)y * v.w0 + x;
-            const float lx = a.tmp[v.tmp + i], ly = a.tmp[v.tmp + 4 * v.n0 + i];
-            const float m = sqrtf(lx * lx + ly * ly);
+            const float m = a.tmp[v.tmp + v.n0 + i];
             if (m != 0.0f) {
                 int bin = (int)floorf(300.0f * (m / hmax));
                 if (bin == 300)
@@ -212,12 +184,8 @@ __global__ void akz_kc_kernel(AkArgs a, int nv)
 hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, hipStream_t s)
 {
     const int by = (max_h + kAkRowsPerBlock - 1) / kAkRowsPerBlock;
-    hipLaunchKernelGGL(akz_modg_max_kernel, dim3((max_w + 255) / 256, by, nv), dim3(256), 0, s, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess)
-        return e;
     hipLaunchKernelGGL(akz_hist_kernel, dim3((max_w + 255) / 256, by, nv), dim3(256), 0, s, a);
-    e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;
     hipLaunchKernelGGL(akz_kc_kernel, dim3((nv + 63) / 64), dim3(64), 0, s, a, nv);
@@ -287,33 +255,34 @@ hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float ta
     return hipGetLastError();
 }
 
-// two explicit FED steps in one pass: a 64 x 16 output tile, its 2-px halo of
-// Lt and the conductance in LDS, the first step over the tile + 1 px, the
-// second over the tile.  The same expressions as akz_fed_kernel, so the result
-// is that of two launches bit for bit (zero flux where a neighbour is outside
-// the image).
-constexpr int kFedTX = 64, kFedTY = 16, kFedW = kFedTX + 4, kFedH = kFedTY + 4;
+// K explicit FED steps in one pass: a 64 x TY output tile, its K-px halo of
+// Lt and the conductance in LDS, step j over the tile + (K - j) px, the last
+// into dst.  The same expressions as akz_fed_kernel, so the result is that of
+// K launches bit for bit (zero flux where a neighbour is outside the image).
+constexpr int kFedTX = 64;
 
-__global__ __launch_bounds__(256) void akz_fed2_kernel(AkArgs a, int level, int src, int dst, float tau1, float tau2)
+template <int K, int TY>
+__global__ __launch_bounds__(256) void akz_fedk_kernel(AkArgs a, int level, int src, int dst, AkFedTaus t)
 {
-    __shared__ float sL[kFedH][kFedW], sC[kFedH][kFedW], sM[kFedH][kFedW];
+    constexpr int W = kFedTX + 2 * K, H = TY + 2 * K;
+    __shared__ float sC[H][W], sB[2][H][W];
     const int z = blockIdx.z;
     const AkPlane &P = a.planes[z * kAkLevels + level];
     const int w = P.w, h = P.h;
-    const int x0 = blockIdx.x * kFedTX, y0 = blockIdx.y * kFedTY;
+    const int x0 = blockIdx.x * kFedTX, y0 = blockIdx.y * TY;
     if (w == 0 || x0 >= w || y0 >= h) // uniform per block
         return;
     const float *L = ak_ptr(a, z, level, src), *c = ak_ptr(a, z, level, kT4);
-    for (int q = threadIdx.x; q < kFedW * kFedH; q += blockDim.x) {
-        const int ty = q / kFedW, tx = q - ty * kFedW;
-        const int gx = x0 - 2 + tx, gy = y0 - 2 + ty;
+    for (int q = threadIdx.x; q < W * H; q += blockDim.x) {
+        const int ty = q / W, tx = q - ty * W;
+        const int gx = x0 - K + tx, gy = y0 - K + ty;
         const bool in = gx >= 0 && gx < w && gy >= 0 && gy < h;
-        sL[ty][tx] = in ? L[(size_t)gy * w + gx] : 0.0f;
+        sB[0][ty][tx] = in ? L[(size_t)gy * w + gx] : 0.0f;
         sC[ty][tx] = in ? c[(size_t)gy * w + gx] : 0.0f;
     }
     __syncthreads();
     // one step at tile position (tx, ty) of the image point (gx, gy), reading V
-    auto step = [&](float (*V)[kFedW], int tx, int ty, int gx, int gy, float ht) {
+    auto step = [&](float (*V)[W], int tx, int ty, int gx, int gy, float ht) {
         const float l0 = V[ty][tx], c0 = sC[ty][tx];
         const float xp = gx + 1 < w ? (c0 + sC[ty][tx + 1]) * (V[ty][tx + 1] - l0) : 0.0f;
         const float xn = gx > 0 ? (sC[ty][tx - 1] + c0) * (l0 - V[ty][tx - 1]) : 0.0f;
@@ -321,29 +290,53 @@ __global__ __launch_bounds__(256) void akz_fed2_kernel(AkArgs a, int level, int 
         const float yn = gy > 0 ? (sC[ty - 1][tx] + c0) * (l0 - V[ty - 1][tx]) : 0.0f;
         return l0 + ht * ((xp - xn) + (yp - yn));
     };
-    const float ht1 = 0.5f * tau1, ht2 = 0.5f * tau2;
-    // first step over the tile and a 1-px ring (image points only)
-    for (int q = threadIdx.x; q < (kFedTX + 2) * (kFedTY + 2); q += blockDim.x) {
-        const int ty = 1 + q / (kFedTX + 2), tx = 1 + q % (kFedTX + 2);
-        const int gx = x0 - 2 + tx, gy = y0 - 2 + ty;
-        if (gx >= 0 && gx < w && gy >= 0 && gy < h)
-            sM[ty][tx] = step(sL, tx, ty, gx, gy, ht1);
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+        // step j over the tile and a (K - j)-px ring (image points only)
+        const float ht = 0.5f * t.tau[j - 1];
+        const int rw = W - 2 * j, rh = H - 2 * j;
+        for (int q = threadIdx.x; q < rw * rh; q += blockDim.x) {
+            const int ty = j + q / rw, tx = j + q % rw;
+            const int gx = x0 - K + tx, gy = y0 - K + ty;
+            if (gx >= 0 && gx < w && gy >= 0 && gy < h)
+                sB[j & 1][ty][tx] = step(sB[(j - 1) & 1], tx, ty, gx, gy, ht);
+        }
+        __syncthreads();
     }
-    __syncthreads();
+    const float ht = 0.5f * t.tau[K - 1];
     float *D = ak_ptr(a, z, level, dst);
-    for (int q = threadIdx.x; q < kFedTX * kFedTY; q += blockDim.x) {
-        const int ty = 2 + q / kFedTX, tx = 2 + q % kFedTX;
-        const int gx = x0 - 2 + tx, gy = y0 - 2 + ty;
+    for (int q = threadIdx.x; q < kFedTX * TY; q += blockDim.x) {
+        const int ty = K + q / kFedTX, tx = K + q % kFedTX;
+        const int gx = x0 - K + tx, gy = y0 - K + ty;
         if (gx < w && gy < h)
-            D[(size_t)gy * w + gx] = step(sM, tx, ty, gx, gy, ht2);
+            D[(size_t)gy * w + gx] = step(sB[(K - 1) & 1], tx, ty, gx, gy, ht);
     }
 }
 
-hipError_t launch_akz_fed2(const AkArgs &a, int level, int src, int dst, float tau1, float tau2, int nv, int max_w,
+hipError_t launch_akz_fedk(const AkArgs &a, int level, int src, int dst, const float *tau, int k, int nv, int max_w,
                            int max_h, hipStream_t s)
 {
-    hipLaunchKernelGGL(akz_fed2_kernel, dim3((max_w + kFedTX - 1) / kFedTX, (max_h + kFedTY - 1) / kFedTY, nv),
-                       dim3(256), 0, s, a, level, src, dst, tau1, tau2);
+    AkFedTaus t{};
+    for (int j = 0; j < k && j < kAkFedPerLaunch; ++j)
+        t.tau[j] = tau[j];
+    switch (k) {
+    case 1:
+        return launch_akz_fed(a, level, src, dst, tau[0], nv, max_w, max_h, s);
+    case 2:
+        hipLaunchKernelGGL((akz_fedk_kernel<2, 16>), dim3((max_w + kFedTX - 1) / kFedTX, (max_h + 15) / 16, nv),
+                           dim3(256), 0, s, a, level, src, dst, t);
+        break;
+    case 3:
+        hipLaunchKernelGGL((akz_fedk_kernel<3, 32>), dim3((max_w + kFedTX - 1) / kFedTX, (max_h + 31) / 32, nv),
+                           dim3(256), 0, s, a, level, src, dst, t);
+        break;
+    case 4:
+        hipLaunchKernelGGL((akz_fedk_kernel<4, 32>), dim3((max_w + kFedTX - 1) / kFedTX, (max_h + 31) / 32, nv),
+                           dim3(256), 0, s, a, level, src, dst, t);
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -426,33 +419,6 @@ hipError_t launch_akz_cols2(const AkArgs &a, int level, int srcS, int dstS, int 
 {
     hipLaunchKernelGGL(akz_cols2_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level, srcS, dstS,
                        srcD, dstD, mode);
-    return hipGetLastError();
-}
-
-// columns of the unnormalised Scharr rows (T1 derivative, T2 smoothing) and
-// the g2 conductance into T4: k = k0 x 0.75 per octave, multiplied in order
-__global__ void akz_cols_g2_kernel(AkArgs a, int level)
-{
-    const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
-    const AkPlane &P = a.planes[z * kAkLevels + level];
-    const int w = P.w, h = P.h;
-    if (w == 0 || x >= w || y >= h)
-        return;
-    float va, vb, vc;
-    akz_col3(ak_ptr(a, z, level, kT1), w, h, x, y, 1, va, vb, vc);
-    const float lx = (3.0f * va + 10.0f * vb) + 3.0f * vc;
-    akz_col3(ak_ptr(a, z, level, kT2), w, h, x, y, 1, va, vb, vc);
-    const float ly = vc - va;
-    float k = a.k0[z];
-    for (int o = 0; o < P.octave; ++o)
-        k = k * 0.75f;
-    const float k2inv = 1.0f / (k * k);
-    ak_ptr(a, z, level, kT4)[(size_t)y * w + x] = 1.0f / (1.0f + k2inv * (lx * lx + ly * ly));
-}
-
-hipError_t launch_akz_cols_g2(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s)
-{
-    hipLaunchKernelGGL(akz_cols_g2_kernel, dim3((max_w + 255) / 256, max_h, nv), dim3(256), 0, s, a, level);
     return hipGetLastError();
 }
 
@@ -574,9 +540,13 @@ hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_
 // a level's flow stage in one pass: Lsmooth = Gaussian(Lt) (replicate) over the
 // tile +- 1 px, written to T3 at the tile; the unnormalised Scharr gradient of
 // Lsmooth (reflect-101, read at the reflected in-image ring points) and the g2
-// conductance into T4 -- the values of gauss2 + rows2 + cols_g2, in their order
+// conductance into T4 -- the values of Gaussian, Scharr rows, Scharr columns + g2, in their order.
+// kContrast (level 0, src the gray image T0, Gaussian sigma 1): no T3; the
+// gradient magnitude into T1 and its interior maximum into hmax instead (the
+// values of gauss2 + rows2 + cols2 + the magnitude/maximum pass)
 constexpr int kFTX = 64, kFTY = 16;
 
+template <bool kContrast>
 __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, int src, AkTaps t)
 {
     __shared__ float sS[kFTY + 2 + 2 * kGMaxR][kFTX + 2 + 2 * kGMaxR];
@@ -613,10 +583,43 @@ __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, int 
             acc = acc + t.w[k] * sR[ry + k][rx];
         sM[ry][rx] = acc;
         const int gx = x0 - 1 + rx, gy = y0 - 1 + ry;
-        if (rx >= 1 && rx <= kFTX && ry >= 1 && ry <= kFTY && gx < w && gy < h)
+        if (!kContrast && rx >= 1 && rx <= kFTX && ry >= 1 && ry <= kFTY && gx < w && gy < h)
             T3[(size_t)gy * w + gx] = acc;
     }
     __syncthreads();
+    if (kContrast) {
+        __shared__ uint32_t wmax[4];
+        float *T1 = ak_ptr(a, z, level, kT1);
+        uint32_t b = 0; // non-negative floats order as their bit patterns
+        for (int q = threadIdx.x; q < kFTX * kFTY; q += blockDim.x) {
+            const int oy = q / kFTX, ox = q - oy * kFTX;
+            const int gx = x0 + ox, gy = y0 + oy;
+            if (gx >= w || gy >= h)
+                continue;
+            const int xm = ak_r101(gx - 1, w) - (x0 - 1), xp = ak_r101(gx + 1, w) - (x0 - 1), xc = gx - (x0 - 1);
+            const int ym = ak_r101(gy - 1, h) - (y0 - 1), yp = ak_r101(gy + 1, h) - (y0 - 1), yc = gy - (y0 - 1);
+            const float da = sM[ym][xp] - sM[ym][xm], db = sM[yc][xp] - sM[yc][xm], dc = sM[yp][xp] - sM[yp][xm];
+            const float lx = (3.0f * da + 10.0f * db) + 3.0f * dc;
+            const float sa = (3.0f * sM[ym][xm] + 10.0f * sM[ym][xc]) + 3.0f * sM[ym][xp];
+            const float sc = (3.0f * sM[yp][xm] + 10.0f * sM[yp][xc]) + 3.0f * sM[yp][xp];
+            const float ly = sc - sa;
+            const float m = sqrtf(lx * lx + ly * ly);
+            T1[(size_t)gy * w + gx] = m;
+            if (gx >= 1 && gx < w - 1 && gy >= 1 && gy < h - 1)
+                b = max(b, __float_as_uint(m));
+        }
+        for (int o = 32; o >= 1; o >>= 1)
+            b = max(b, (uint32_t)__shfl_xor((int)b, o));
+        if ((threadIdx.x & 63) == 0)
+            wmax[threadIdx.x >> 6] = b;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t mx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+            if (mx)
+                atomicMax(&a.hmax[z], mx);
+        }
+        return;
+    }
     float k = a.k0[z];
     for (int o = 0; o < P.octave; ++o)
         k = k * 0.75f;
@@ -644,9 +647,21 @@ hipError_t launch_akz_flow(const AkArgs &a, int level, int src, const AkTaps &t,
 {
     if (t.n > 2 * kGMaxR + 1)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(akz_flow_kernel, dim3((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv), dim3(256), 0,
-                       s, a, level, src, t);
+    hipLaunchKernelGGL(akz_flow_kernel<false>, dim3((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv), dim3(256),
+                       0, s, a, level, src, t);
     return hipGetLastError();
+}
+
+hipError_t launch_akz_contrast(const AkArgs &a, const AkTaps &t, int nv, int max_w, int max_h, hipStream_t s)
+{
+    if (t.n > 2 * kGMaxR + 1)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(akz_flow_kernel<true>, dim3((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv), dim3(256),
+                       0, s, a, 0, kT0, t);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    return launch_akz_kcontrast(a, nv, max_w, max_h, s);
 }
 
 // 3x3 maxima of Ldet above the threshold inside the descriptor border

@@ -649,16 +649,20 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         // unnormalised Scharr gradient of Gaussian(img, 1) (x in T0, y in T4)
         DP_HIP(c, launch_akz_gray(a, nv, mw[0], mh[0], st));
         DP_HIP(c, launch_akz_gauss2(a, 0, kT0, kLt, g16, nv, mw[0], mh[0], st));
-        DP_HIP(c, launch_akz_gauss2(a, 0, kT0, kT3, g10, nv, mw[0], mh[0], st));
-        DP_HIP(c, launch_akz_rows2(a, 0, kT3, kT1, kT2, 1, nv, mw[0], mh[0], st));
-        DP_HIP(c, launch_akz_cols2(a, 0, kT1, kT0, kT2, kT4, 1, nv, mw[0], mh[0], st));
-        DP_HIP(c, launch_akz_kcontrast(a, nv, mw[0], mh[0], st));
         DP_HIP(c, deriv(0, kLt));
+        DP_HIP(c, launch_akz_contrast(a, g10, nv, mw[0], mh[0], st));
+        // FED steps per launch: 3 (config 3, 32 views: 57.9 / 45.0 / 43.6 / 44.5 ms
+        // detect at 1 / 2 / 3 / 4); DP_AKAZE_FED_STEPS (1 .. kAkFedPerLaunch) for
+        // A/B timing -- every grouping gives the same values
+        int fed_k = 3;
+        if (const char *fk = std::getenv("DP_AKAZE_FED_STEPS"))
+            fed_k = std::max(1, std::min(kAkFedPerLaunch, std::atoi(fk)));
         for (int i = 1; i < nlev; ++i) {
             // the level starts from the previous level's Lt (read in place) or its
             // half-sample; the FED steps ping-pong between T2 and Lt with the
             // parity that ends in Lt (no copies)
-            const int nt = (int)tau[i].size(), nl = nt / 2 + nt % 2; // steps, launches
+            const int nt = (int)tau[i].size();
+            const int nl = (nt + fed_k - 1) / fed_k; // launches
             int src = kPrevLt;
             if (full.octave[i] > full.octave[i - 1]) {
                 src = nl % 2 ? kT2 : kLt;
@@ -666,15 +670,12 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
             }
             // Lsmooth (T3), g2 conductance (T4) from its unnormalised Scharr gradient
             DP_HIP(c, launch_akz_flow(a, i, src, g10, nv, mw[i], mh[i], st));
-            for (int k = 0, j = 0; k < nt; ++j) {
+            // the steps in nl near-equal groups of at most fed_k
+            for (int k = 0, j = 0; j < nl; ++j) {
                 const int dst = (nl - 1 - j) % 2 ? kT2 : kLt;
-                if (k + 1 < nt) {
-                    DP_HIP(c, launch_akz_fed2(a, i, src, dst, tau[i][k], tau[i][k + 1], nv, mw[i], mh[i], st));
-                    k += 2;
-                } else {
-                    DP_HIP(c, launch_akz_fed(a, i, src, dst, tau[i][k], nv, mw[i], mh[i], st));
-                    k += 1;
-                }
+                const int g = (nt - k) / (nl - j) + ((nt - k) % (nl - j) ? 1 : 0);
+                DP_HIP(c, launch_akz_fedk(a, i, src, dst, tau[i].data() + k, g, nv, mw[i], mh[i], st));
+                k += g;
                 src = dst;
             }
             if (src != kLt)
