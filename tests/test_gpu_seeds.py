@@ -299,6 +299,20 @@ def test_akaze_chunks_and_mixed_sizes(orc, monkeypatch):
         compare_run(eng, r, kw, 3)
 
 
+@pytest.mark.parametrize("steps", [1, 2, 4])
+def test_akaze_fed_steps_per_launch_equal(orc, monkeypatch, steps):
+    """The FED steps of a level grouped 1, 2 or 4 per launch (the default is 3;
+    DP_AKAZE_FED_STEPS) give the oracle's values bit for bit: the multi-step
+    LDS tiles recompute their halo with the single step's expressions."""
+    cfg = synth.config(n_views=2, width=640, height=480, kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    kw = dict(detector_type=M.DETECTOR_AKAZE, akaze_threshold=0.0002)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    monkeypatch.setenv("DP_AKAZE_FED_STEPS", str(steps))
+    with engine_with(P, imgs) as eng:
+        compare_run(eng, r, kw, 2)
+
+
 @pytest.mark.parametrize("nq,nt", [(1, 0), (33, 2), (300, 129), (1000, 2500)])
 def test_knn_match_wide_matches_oracle(orc, nq, nt):
     """knnMatch on 64-byte rows (the AKAZE descriptor width), ties included."""
