@@ -462,7 +462,13 @@ hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, in
 // value is the one the separate passes compute (each 1-D pass reflects per
 // axis, and the second passes read the first derivatives at reflected in-image
 // points, which the +-s ring holds), in the same expression order.
-constexpr int kDTX = 64, kDTY = 16, kDMaxS = 4;
+#ifndef DP_AKZ_DTX // tile shape of the derivative and flow stages (A/B builds)
+#define DP_AKZ_DTX 64
+#endif
+#ifndef DP_AKZ_DTY
+#define DP_AKZ_DTY 16
+#endif
+constexpr int kDTX = DP_AKZ_DTX, kDTY = DP_AKZ_DTY, kDMaxS = 4;
 
 __global__ __launch_bounds__(256) void akz_deriv_kernel(AkArgs a, int level, int ls)
 {
@@ -544,7 +550,7 @@ hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_
 // kContrast (level 0, src the gray image T0, Gaussian sigma 1): no T3; the
 // gradient magnitude into T1 and its interior maximum into hmax instead (the
 // values of gauss2 + rows2 + cols2 + the magnitude/maximum pass)
-constexpr int kFTX = 64, kFTY = 16;
+constexpr int kFTX = DP_AKZ_DTX, kFTY = DP_AKZ_DTY;
 
 template <bool kContrast>
 __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, int src, AkTaps t)
