@@ -64,7 +64,7 @@ hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float ta
                           hipStream_t s);
 // k <= kAkFedPerLaunch FED steps (tau[0 .. k-1]) per launch through an LDS tile
 // (bit-identical to k launches)
-constexpr int kAkFedPerLaunch = 4;
+constexpr int kAkFedPerLaunch = 6;
 struct AkFedTaus {
     float tau[kAkFedPerLaunch];
 };

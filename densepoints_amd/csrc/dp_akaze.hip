@@ -259,7 +259,10 @@ hipError_t launch_akz_fed(const AkArgs &a, int level, int src, int dst, float ta
 // Lt and the conductance in LDS, step j over the tile + (K - j) px, the last
 // into dst.  The same expressions as akz_fed_kernel, so the result is that of
 // K launches bit for bit (zero flux where a neighbour is outside the image).
-constexpr int kFedTX = 64;
+#ifndef DP_AKZ_FED_TY // output rows of the 3- to 6-step tiles (A/B builds: 16 < 8, 24, 32 in ms)
+#define DP_AKZ_FED_TY 16
+#endif
+constexpr int kFedTX = 64, kFedTY = DP_AKZ_FED_TY;
 
 template <int K, int TY>
 __global__ __launch_bounds__(256) void akz_fedk_kernel(AkArgs a, int level, int src, int dst, AkFedTaus t)
@@ -319,20 +322,29 @@ hipError_t launch_akz_fedk(const AkArgs &a, int level, int src, int dst, const f
     AkFedTaus t{};
     for (int j = 0; j < k && j < kAkFedPerLaunch; ++j)
         t.tau[j] = tau[j];
+    const unsigned gx = (unsigned)((max_w + kFedTX - 1) / kFedTX);
     switch (k) {
     case 1:
         return launch_akz_fed(a, level, src, dst, tau[0], nv, max_w, max_h, s);
     case 2:
-        hipLaunchKernelGGL((akz_fedk_kernel<2, 16>), dim3((max_w + kFedTX - 1) / kFedTX, (max_h + 15) / 16, nv),
-                           dim3(256), 0, s, a, level, src, dst, t);
+        hipLaunchKernelGGL((akz_fedk_kernel<2, 16>), dim3(gx, (max_h + 15) / 16, nv), dim3(256), 0, s, a, level, src,
+                           dst, t);
         break;
     case 3:
-        hipLaunchKernelGGL((akz_fedk_kernel<3, 32>), dim3((max_w + kFedTX - 1) / kFedTX, (max_h + 31) / 32, nv),
-                           dim3(256), 0, s, a, level, src, dst, t);
+        hipLaunchKernelGGL((akz_fedk_kernel<3, kFedTY>), dim3(gx, (max_h + kFedTY - 1) / kFedTY, nv), dim3(256), 0, s,
+                           a, level, src, dst, t);
         break;
     case 4:
-        hipLaunchKernelGGL((akz_fedk_kernel<4, 32>), dim3((max_w + kFedTX - 1) / kFedTX, (max_h + 31) / 32, nv),
-                           dim3(256), 0, s, a, level, src, dst, t);
+        hipLaunchKernelGGL((akz_fedk_kernel<4, kFedTY>), dim3(gx, (max_h + kFedTY - 1) / kFedTY, nv), dim3(256), 0, s,
+                           a, level, src, dst, t);
+        break;
+    case 5:
+        hipLaunchKernelGGL((akz_fedk_kernel<5, kFedTY>), dim3(gx, (max_h + kFedTY - 1) / kFedTY, nv), dim3(256), 0, s,
+                           a, level, src, dst, t);
+        break;
+    case 6:
+        hipLaunchKernelGGL((akz_fedk_kernel<6, kFedTY>), dim3(gx, (max_h + kFedTY - 1) / kFedTY, nv), dim3(256), 0, s,
+                           a, level, src, dst, t);
         break;
     default:
         return hipErrorInvalidValue;

@@ -651,10 +651,10 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         DP_HIP(c, launch_akz_gauss2(a, 0, kT0, kLt, g16, nv, mw[0], mh[0], st));
         DP_HIP(c, deriv(0, kLt));
         DP_HIP(c, launch_akz_contrast(a, g10, nv, mw[0], mh[0], st));
-        // FED steps per launch: 3 (config 3, 32 views: 57.9 / 45.0 / 43.6 / 44.5 ms
-        // detect at 1 / 2 / 3 / 4); DP_AKAZE_FED_STEPS (1 .. kAkFedPerLaunch) for
-        // A/B timing -- every grouping gives the same values
-        int fed_k = 3;
+        // FED steps per launch: 4 (config 3, 32 views, 64 x 16 tiles: 44.9 / 41.9 /
+        // 40.8 / 40.7 / 41.1 ms detect at 2 / 3 / 4 / 5 / 6); DP_AKAZE_FED_STEPS
+        // (1 .. kAkFedPerLaunch) for A/B timing -- every grouping gives the same values
+        int fed_k = 4;
         if (const char *fk = std::getenv("DP_AKAZE_FED_STEPS"))
             fed_k = std::max(1, std::min(kAkFedPerLaunch, std::atoi(fk)));
         for (int i = 1; i < nlev; ++i) {

@@ -299,9 +299,9 @@ def test_akaze_chunks_and_mixed_sizes(orc, monkeypatch):
         compare_run(eng, r, kw, 3)
 
 
-@pytest.mark.parametrize("steps", [1, 2, 4])
+@pytest.mark.parametrize("steps", [1, 2, 3, 6])
 def test_akaze_fed_steps_per_launch_equal(orc, monkeypatch, steps):
-    """The FED steps of a level grouped 1, 2 or 4 per launch (the default is 3;
+    """The FED steps of a level grouped 1, 2, 3 or 6 per launch (the default is 4;
     DP_AKAZE_FED_STEPS) give the oracle's values bit for bit: the multi-step
     LDS tiles recompute their halo with the single step's expressions."""
     cfg = synth.config(n_views=2, width=640, height=480, kind=0)
