@@ -78,7 +78,7 @@ hipError_t launch_akz_cols2(const AkArgs &a, int level, int srcS, int dstS, int 
                             int max_w, int max_h, hipStream_t s);
 hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, int max_h, hipStream_t s);
 // the detector-derivative stage of a level in one LDS-tiled pass (sigma_size <= 4)
-hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_w, int max_h, hipStream_t s);
+hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int ss, int nv, int max_w, int max_h, hipStream_t s);
 // a level's Lsmooth (T3) and g2 conductance (T4) from its starting Lt (plane src) in one LDS-tiled pass
 hipError_t launch_akz_flow(const AkArgs &a, int level, int src, const AkTaps &t, int nv, int max_w, int max_h,
                            hipStream_t s);

@@ -79,8 +79,10 @@ hipError_t launch_akz_gray(const AkArgs &a, int nv, int max_w, int max_h, hipStr
 // same order as oracle/or_akaze.c's row and column passes (ak_gauss)
 constexpr int kGTX = 64, kGTY = 16, kGMaxR = 4;
 
+template <int NT> // NT: the tap count when known at compile time (0: t.n)
 __global__ __launch_bounds__(256) void akz_gauss2_kernel(AkArgs a, int level, int src, int dst, AkTaps t)
 {
+    const int n = NT ? NT : t.n;
     __shared__ float sS[kGTY + 2 * kGMaxR][kGTX + 2 * kGMaxR];
     __shared__ float sR[kGTY + 2 * kGMaxR][kGTX];
     const int z = blockIdx.z;
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(256) void akz_gauss2_kernel(AkArgs a, int level, in
     const int x0 = blockIdx.x * kGTX, y0 = blockIdx.y * kGTY;
     if (w == 0 || x0 >= w || y0 >= h) // uniform per block
         return;
-    const int r = t.n / 2;
+    const int r = n / 2;
     const int SW = kGTX + 2 * r, SH = kGTY + 2 * r;
     const float *S = ak_ptr(a, z, level, src);
     for (int q = threadIdx.x; q < SW * SH; q += blockDim.x) {
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(256) void akz_gauss2_kernel(AkArgs a, int level, in
     for (int q = threadIdx.x; q < kGTX * SH; q += blockDim.x) {
         const int ty = q / kGTX, tx = q - ty * kGTX;
         float acc = t.w[0] * sS[ty][tx];
-        for (int k = 1; k < t.n; ++k)
+        for (int k = 1; k < n; ++k)
             acc = acc + t.w[k] * sS[ty][tx + k];
         sR[ty][tx] = acc;
     }
@@ -112,7 +114,7 @@ __global__ __launch_bounds__(256) void akz_gauss2_kernel(AkArgs a, int level, in
         if (gx >= w || gy >= h)
             continue;
         float acc = t.w[0] * sR[ty][tx];
-        for (int k = 1; k < t.n; ++k)
+        for (int k = 1; k < n; ++k)
             acc = acc + t.w[k] * sR[ty + k][tx];
         D[(size_t)gy * w + gx] = acc;
     }
@@ -123,8 +125,13 @@ hipError_t launch_akz_gauss2(const AkArgs &a, int level, int src, int dst, const
 {
     if (t.n > 2 * kGMaxR + 1)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(akz_gauss2_kernel, dim3((max_w + kGTX - 1) / kGTX, (max_h + kGTY - 1) / kGTY, nv), dim3(256),
-                       0, s, a, level, src, dst, t);
+    const dim3 g((max_w + kGTX - 1) / kGTX, (max_h + kGTY - 1) / kGTY, nv);
+    if (t.n == 9) // Gaussian sigma 1.6
+        hipLaunchKernelGGL((akz_gauss2_kernel<9>), g, dim3(256), 0, s, a, level, src, dst, t);
+    else if (t.n == 5)
+        hipLaunchKernelGGL((akz_gauss2_kernel<5>), g, dim3(256), 0, s, a, level, src, dst, t);
+    else
+        hipLaunchKernelGGL((akz_gauss2_kernel<0>), g, dim3(256), 0, s, a, level, src, dst, t);
     return hipGetLastError();
 }
 
@@ -482,6 +489,7 @@ hipError_t launch_akz_cols_det(const AkArgs &a, int level, int nv, int max_w, in
 #endif
 constexpr int kDTX = DP_AKZ_DTX, kDTY = DP_AKZ_DTY, kDMaxS = 4;
 
+template <int SP> // SP: the level's sigma_size when known at compile time (0: the plane's)
 __global__ __launch_bounds__(256) void akz_deriv_kernel(AkArgs a, int level, int ls)
 {
     __shared__ float sL[kDTY + 4 * kDMaxS][kDTX + 4 * kDMaxS];
@@ -495,6 +503,8 @@ __global__ __launch_bounds__(256) void akz_deriv_kernel(AkArgs a, int level, int
     int sp;
     float k0, k1;
     akz_coef(P, 0, sp, k0, k1);
+    if (SP)
+        sp = SP; // == P.sigma_size (the host dispatches on it): constant tile arithmetic
     const int s2 = 2 * sp;
     const int LW = kDTX + 2 * s2, LH = kDTY + 2 * s2; // Lsmooth tile: origin (x0 - 2s, y0 - 2s)
     const int RW = kDTX + s2, RH = kDTY + s2;         // first-derivative ring: origin (x0 - s, y0 - s)
@@ -548,10 +558,25 @@ __global__ __launch_bounds__(256) void akz_deriv_kernel(AkArgs a, int level, int
     }
 }
 
-hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_w, int max_h, hipStream_t s)
+hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int ss, int nv, int max_w, int max_h, hipStream_t s)
 {
-    hipLaunchKernelGGL(akz_deriv_kernel, dim3((max_w + kDTX - 1) / kDTX, (max_h + kDTY - 1) / kDTY, nv), dim3(256), 0,
-                       s, a, level, ls);
+    const dim3 g((max_w + kDTX - 1) / kDTX, (max_h + kDTY - 1) / kDTY, nv);
+    switch (ss) {
+    case 1:
+        hipLaunchKernelGGL((akz_deriv_kernel<1>), g, dim3(256), 0, s, a, level, ls);
+        break;
+    case 2:
+        hipLaunchKernelGGL((akz_deriv_kernel<2>), g, dim3(256), 0, s, a, level, ls);
+        break;
+    case 3:
+        hipLaunchKernelGGL((akz_deriv_kernel<3>), g, dim3(256), 0, s, a, level, ls);
+        break;
+    case 4:
+        hipLaunchKernelGGL((akz_deriv_kernel<4>), g, dim3(256), 0, s, a, level, ls);
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -564,9 +589,10 @@ hipError_t launch_akz_deriv(const AkArgs &a, int level, int ls, int nv, int max_
 // values of gauss2 + rows2 + cols2 + the magnitude/maximum pass)
 constexpr int kFTX = DP_AKZ_DTX, kFTY = DP_AKZ_DTY;
 
-template <bool kContrast>
+template <bool kContrast, int NT> // NT: the tap count when known at compile time (0: t.n)
 __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, int src, AkTaps t)
 {
+    const int n = NT ? NT : t.n;
     __shared__ float sS[kFTY + 2 + 2 * kGMaxR][kFTX + 2 + 2 * kGMaxR];
     __shared__ float sR[kFTY + 2 + 2 * kGMaxR][kFTX + 2];
     __shared__ float sM[kFTY + 2][kFTX + 2];
@@ -576,7 +602,7 @@ __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, int 
     const int x0 = blockIdx.x * kFTX, y0 = blockIdx.y * kFTY;
     if (w == 0 || x0 >= w || y0 >= h) // uniform per block
         return;
-    const int r = t.n / 2;
+    const int r = n / 2;
     const int SW = kFTX + 2 + 2 * r, SH = kFTY + 2 + 2 * r; // origin (x0 - 1 - r, y0 - 1 - r)
     const float *L = ak_ptr(a, z, level, src);
     for (int q = threadIdx.x; q < SW * SH; q += blockDim.x) {
@@ -587,7 +613,7 @@ __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, int 
     for (int q = threadIdx.x; q < (kFTX + 2) * SH; q += blockDim.x) {
         const int ty = q / (kFTX + 2), tx = q - ty * (kFTX + 2);
         float acc = t.w[0] * sS[ty][tx];
-        for (int k = 1; k < t.n; ++k)
+        for (int k = 1; k < n; ++k)
             acc = acc + t.w[k] * sS[ty][tx + k];
         sR[ty][tx] = acc;
     }
@@ -597,7 +623,7 @@ __global__ __launch_bounds__(256) void akz_flow_kernel(AkArgs a, int level, int 
     for (int q = threadIdx.x; q < (kFTX + 2) * (kFTY + 2); q += blockDim.x) {
         const int ry = q / (kFTX + 2), rx = q - ry * (kFTX + 2);
         float acc = t.w[0] * sR[ry][rx];
-        for (int k = 1; k < t.n; ++k)
+        for (int k = 1; k < n; ++k)
             acc = acc + t.w[k] * sR[ry + k][rx];
         sM[ry][rx] = acc;
         const int gx = x0 - 1 + rx, gy = y0 - 1 + ry;
@@ -665,8 +691,11 @@ hipError_t launch_akz_flow(const AkArgs &a, int level, int src, const AkTaps &t,
 {
     if (t.n > 2 * kGMaxR + 1)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(akz_flow_kernel<false>, dim3((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv), dim3(256),
-                       0, s, a, level, src, t);
+    const dim3 g((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv);
+    if (t.n == 5) // Gaussian sigma 1: unrolled, the taps in SGPRs once
+        hipLaunchKernelGGL((akz_flow_kernel<false, 5>), g, dim3(256), 0, s, a, level, src, t);
+    else
+        hipLaunchKernelGGL((akz_flow_kernel<false, 0>), g, dim3(256), 0, s, a, level, src, t);
     return hipGetLastError();
 }
 
@@ -674,8 +703,11 @@ hipError_t launch_akz_contrast(const AkArgs &a, const AkTaps &t, int nv, int max
 {
     if (t.n > 2 * kGMaxR + 1)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(akz_flow_kernel<true>, dim3((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv), dim3(256),
-                       0, s, a, 0, kT0, t);
+    const dim3 g((max_w + kFTX - 1) / kFTX, (max_h + kFTY - 1) / kFTY, nv);
+    if (t.n == 5)
+        hipLaunchKernelGGL((akz_flow_kernel<true, 5>), g, dim3(256), 0, s, a, 0, kT0, t);
+    else
+        hipLaunchKernelGGL((akz_flow_kernel<true, 0>), g, dim3(256), 0, s, a, 0, kT0, t);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;

@@ -632,8 +632,8 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
                        s->akz_k0.p};
         // the detector's derivatives of Lsmooth (plane ls), Ldet; Lx, Ly scaled
         auto deriv = [&](int i, int ls) -> hipError_t {
-            if (full.ss[i] <= 4)
-                return launch_akz_deriv(a, i, ls, nv, mw[i], mh[i], st);
+            if (full.ss[i] >= 1 && full.ss[i] <= 4)
+                return launch_akz_deriv(a, i, ls, full.ss[i], nv, mw[i], mh[i], st);
             hipError_t e = launch_akz_rows2(a, i, ls, kT1, kT2, 0, nv, mw[i], mh[i], st);
             if (e == hipSuccess)
                 e = launch_akz_cols2(a, i, kT1, kLx, kT2, kLy, 0, nv, mw[i], mh[i], st);
