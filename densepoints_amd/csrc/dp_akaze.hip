@@ -715,13 +715,13 @@ hipError_t launch_akz_contrast(const AkArgs &a, const AkTaps &t, int nv, int max
 }
 
 // 3x3 maxima of Ldet above the threshold inside the descriptor border
-__device__ __forceinline__ bool akz_is_cand(const AkArgs &a, const AkPlane &P, int x, int y, float thr)
+// (v: the point's own Ldet value, loaded by the caller)
+__device__ __forceinline__ bool akz_is_cand(const AkArgs &a, const AkPlane &P, int x, int y, float thr, float v)
 {
     const int w = P.w, h = P.h;
     if (x < 1 || x >= w - 1 || y < 1 || y >= h - 1)
         return false;
     const float *p = a.pool + P.off + 3 * ((int64_t)w * h) + (size_t)y * w + x;
-    const float v = p[0];
     if (!(v > thr && v >= 0.00001f && v > p[-1] && v > p[1] && v > p[-w - 1] && v > p[-w] && v > p[-w + 1] &&
           v > p[w - 1] && v > p[w] && v > p[w + 1]))
         return false;
@@ -747,14 +747,29 @@ __global__ __launch_bounds__(256) void akz_count_kernel(AkArgs a, int level, flo
     if (P.w == 0 || y0 >= P.h || (int)blockIdx.x >= nbx) // uniform per block
         return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const float *det = a.pool + P.off + 3 * ((int64_t)P.w * P.h);
+    // the wave's 4 rows x 4 chunks of Ldet in flight together; the
+    // neighbourhood test only where a value passes the threshold
+    float v[kCandRows / 4][4];
+#pragma unroll
+    for (int r = 0; r < kCandRows / 4; ++r) {
+        const int y = y0 + wv * (kCandRows / 4) + r;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int x = (int)blockIdx.x * 256 + k * 64 + lane;
+            v[r][k] = (y < P.h && x < P.w) ? det[(size_t)y * P.w + x] : 0.0f;
+        }
+    }
+#pragma unroll
     for (int r = 0; r < kCandRows / 4; ++r) {
         const int y = y0 + wv * (kCandRows / 4) + r;
         if (y >= P.h)
             break;
         unsigned long long m[4];
+#pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int x = (int)blockIdx.x * 256 + k * 64 + lane;
-            m[k] = __ballot(x < P.w && akz_is_cand(a, P, x, y, thr));
+            m[k] = __ballot(x < P.w && akz_is_cand(a, P, x, y, thr, v[r][k]));
         }
         const int64_t sg = P.seg_base + (int64_t)y * nbx + blockIdx.x;
         if (lane < 4)
