@@ -85,9 +85,6 @@ def parse():
                          "value (keys n*_mv<k>, headline parents)")
     ap.add_argument("--no-fast", action="store_true", help="skip the perf_mode sub-object")
     ap.add_argument("--seed-stride", type=float, default=32.0, help="synthetic seed grid stride (px)")
-    ap.add_argument("--densify-protocol", choices=["r05", "r04"], default="r05",
-                    help="scaling_leg's generation protocol: r05 = one host wait per generation (default), r04 = the "
-                         "round-4 protocol (host-read partition and accepted counts), for A/B runs")
     ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                     help="side file for the full result (event arrays, every perf_mode run, partition probes, seed "
                          "generation); stdout carries only the compact line (compact())")
@@ -138,7 +135,7 @@ def compact(result: dict, detail_path: str | None = None) -> dict:
     sl = result.get("scaling_leg")
     if sl:
         out["scaling_leg"] = {"n_gpus": sl.get("n_gpus"), "scaling": sl.get("scaling")}
-        for m in ("parity", "fast"):
+        for m in ("parity", "fast", "fast_slots"):
             if m in sl:
                 out["scaling_leg"][m] = _pick(sl[m], ("Mpatches_per_s", "ms_per_densify", "non_refine_ms",
                                                       "ranks_store_equal", "store_crc32"))
@@ -444,21 +441,24 @@ def main():
     eng.close()
 
 
-def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast, protocol="r05"):
+def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast, exchange=False, probe_worlds=(2, 8)):
     """`steps` whole densifies with every generation partitioned over the ranks
     (dist.densify_partitioned_device), after `warmup` untimed ones, bracketed by
     barrier + synchronize; rate = candidates refined (seed stage + expansions)
-    per max-over-ranks second."""
+    per max-over-ranks second.  exchange: the multi-rank slot protocol even at
+    one rank (its per-generation cost is what every rank of an N-rank run pays)."""
+    import functools
+
     import densepoints_amd as dp
     from densepoints_amd import dist as D
 
     eng.set_fast_options(dp.FastOptions(densify=1 if fast else 0))
-    run = D.densify_partitioned_device if protocol == "r05" else D.densify_partitioned_device_r04
+    run = functools.partial(D.densify_partitioned_device, one_rank_exchange=exchange)
     probe = None
     for i in range(warmup):
         # the untimed warm-up also computes the partitions world sizes 2 and 8
         # would use on the same generations (statistics only)
-        _, wst = run(eng, seeds, dist, dev, probe_worlds=(2, 8) if i == 0 else ())
+        _, wst = run(eng, seeds, dist, dev, probe_worlds=probe_worlds if i == 0 else ())
         probe = probe or wst.get("partition_probe")
     torch.cuda.synchronize()
     if dist:
@@ -505,7 +505,7 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast, protoc
             # replicated organizer commit, host waits): the part that does not
             # shrink with the ranks
             "non_refine_ms": round(wall / steps * 1e3 - st["refine_ms"], 2),
-            "protocol": protocol,
+            "protocol": "slots" if (world > 1 or exchange) else "device-resident (dp_densify_run)",
             # host time per phase of the last densify (each phase ends in a host sync;
             # refine_compact includes this rank's refine kernels), max over ranks
             "phase_ms_max_rank": {k: round(D.max_over_ranks(v, dist, coll_dev), 2)
@@ -562,9 +562,14 @@ def scaling_leg(args, stream, dist, coll_dev, dev):
         torch.cuda.synchronize()
         eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
         seeds = synth.seeds(cfg, P)
-        out = {m: partitioned_leg(eng, seeds, dist, coll_dev, dev, args.densify_steps, 1, m == "fast",
-                                  args.densify_protocol)
+        out = {m: partitioned_leg(eng, seeds, dist, coll_dev, dev, args.densify_steps, 1, m == "fast")
                for m in ("parity", "fast")}
+        if world == 1:
+            # the multi-rank protocol's per-generation cost at one rank (partition,
+            # slot compaction, scatter, replicated commit, one wait per generation):
+            # what bounds the N-rank strong scaling beside refine_ms / N
+            out["fast_slots"] = partitioned_leg(eng, seeds, dist, coll_dev, dev, args.densify_steps, 1, True,
+                                                exchange=True, probe_worlds=())
         out["workload"] = (f"cfg4_64view_4k: {V} views {W}x{H}, one step = the whole densify (PMVS::Run minus "
                            f"matching) of {len(seeds)} seed points, every BFS generation partitioned by "
                            f"reference-view super-tile over {world} rank(s), accepted candidates all-gathered")

@@ -87,7 +87,7 @@ class DpDensifyStats(ctypes.Structure):
         ("candidates", ctypes.c_int64),
         ("evals", ctypes.c_int64),
         ("generations", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("stalls", ctypes.c_int32),
         ("refine_ms", ctypes.c_double),
         ("total_ms", ctypes.c_double),
     ]
@@ -218,22 +218,15 @@ SIGNATURES = [
     ("dp_expand_batch_device", _I, [_P, _P, _I, _P, _P, _P]),
     ("dp_densify", _I, [_P, _P, _I, _P, _P, _P]),
     ("dp_densify_begin", _I, [_P, _P, _I, _P]),
-    ("dp_densify_refine", _I, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P]),
     ("dp_densify_commit", _I, [_P, _P, _P, _P, ctypes.c_int64]),
     ("dp_densify_result", _I, [_P, _P, _P, _P]),
-    ("dp_densify_refine_device", _I, [_P, _P, ctypes.c_int64, ctypes.c_int64, _P, _P, _P]),
-    ("dp_densify_commit_device", _I, [_P, _P, _P, _P, ctypes.c_int64, _P]),
+    ("dp_densify_run", _I, [_P, _P, ctypes.c_int32]),
     ("dp_densify_owners", _I, [_P, _P, _I, _I, _P, _P]),
     ("dp_densify_partition_stats", _I, [_P, _P]),
     ("dp_densify_refine_items", _I, [_P, _P, _P, ctypes.c_int64, _P, _P]),
-    ("dp_densify_refine_items_device", _I, [_P, _P, _P, ctypes.c_int64, _P, _P, _P]),
-    ("dp_densify_commit_items_device", _I, [_P, _P, _P, _P, _P, ctypes.c_int64, _P]),
-    ("dp_densify_partition_device", _I, [_P, _P, _I, _I, _P, _P, _P]),
-    ("dp_densify_compact_accepted_device", _I, [_P, _P, _P, ctypes.c_int64, _P, _P, _P, _P, _P]),
-    ("dp_densify_commit_accepted_device", _I, [_P, _P, _P, ctypes.c_int64, _P]),
     ("dp_densify_partition_async", _I, [_P, _P, _I, _I, _P, _P, _P]),
-    ("dp_densify_compact_accepted_async", _I, [_P, _P, _P, ctypes.c_int64, _P, _P, _P, _P, _P]),
-    ("dp_densify_commit_gathered_device", _I, [_P, _P, _P, ctypes.c_int64, _P, _I, _P, _P]),
+    ("dp_densify_refine_share_async", _I, [_P, _P, _P, ctypes.c_int64, _P, ctypes.c_int64, _P]),
+    ("dp_densify_commit_gathered_device", _I, [_P, _P, _P, ctypes.c_int64, _I, _P, _P]),
     ("dp_default_filter_options", None, [_P]),
     ("dp_filter_patches", _I, [_P, _P, ctypes.c_int64, _P, _P]),
     ("dp_filter_patches_device", _I, [_P, _P, ctypes.c_int64, _P, _P, _P]),

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libdensepoints.so")
 SOURCES = ["dp_capi.hip", "dp_kernels.hip", "dp_filter.hip", "dp_seeds.hip", "dp_seeds_capi.hip", "dp_orb.hip",
-           "dp_fast.hip", "dp_akaze.hip"]
+           "dp_fast.hip", "dp_akaze.hip", "dp_bfs.hip"]
 HEADERS = ["dp_internal.h", "dp_geom.h", "dp_detmath.h", "dp_synth.h", "dp_devmath.h", "dp_ctx.h", "dp_dlt.h",
            "dp_seeds.h", "dp_orb.h", "dp_orb_pattern.h", "dp_akaze.h"]
 ARCH = os.environ.get("DP_OFFLOAD_ARCH", "gfx950")

@@ -89,20 +89,21 @@ hipError_t launch_akz_count(const AkArgs &a, int level, float thr, uint32_t *cnt
 hipError_t launch_akz_emit(const AkArgs &a, int level, const unsigned long long *mask, const uint32_t *off,
                            int64_t *cand, int nv, int max_w, int max_h, hipStream_t s);
 
-// candidate list (sorted global Ldet indices) -> keypoints (suppression +
-// subpixel refinement), keep flags
+// candidate list (sorted global Ldet indices) -> keypoints (OpenCV's
+// sequential suppression + subpixel refinement, one workgroup per view),
+// keep flags; a view with more candidates than the LDS list holds sets *err
+// (its candidate count) and keeps none
 struct AkCandArgs {
     const AkPlane *planes;
     const float *pool;
     const int64_t *cand;
     int64_t n;
-    const int32_t *plane_ids;   // existing planes sorted by det_base
-    const int64_t *plane_base;  // their det_base
-    int32_t n_planes;
+    int32_t n_views;            // views of the chunk (planes[z * kAkLevels + level])
     const int32_t *view_ids;    // chunk view -> global view
     dp_keypoint *kp;
     int32_t *kv;
     uint8_t *keep;
+    uint32_t *err;
 };
 hipError_t launch_akz_candidates(const AkCandArgs &a, hipStream_t s);
 

@@ -825,7 +825,16 @@ hipError_t launch_akz_emit(const AkArgs &a, int level, const unsigned long long 
 }
 
 // ---------------------------------------------------------------------------
-// candidates: scale-space suppression and subpixel refinement, one lane each
+// candidates: OpenCV 3.x's sequential scale-space suppression
+// (AKAZEFeatures::Find_Scale_Space_Extrema), then subpixel refinement.  One
+// 64-lane workgroup per view walks the view's candidates in (level, y, x)
+// order against the list so far (kpts_aux, in LDS): the lanes test 64 list
+// entries at a time and a ballot finds the FIRST entry of the same or the
+// previous level within the candidate's size; a weaker entry is replaced in
+// place, an equal or stronger one drops the candidate, no entry appends it.
+// Then each entry is dropped when a later entry of the next level lies
+// within its size with a larger response, and refined; keypoints leave in
+// list order (oracle/or_akaze.c ak_extrema states the same).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int64_t ak_lower(const int64_t *c, int64_t lo, int64_t hi, int64_t v)
 {
@@ -839,91 +848,130 @@ __device__ __forceinline__ int64_t ak_lower(const int64_t *c, int64_t lo, int64_
     return lo;
 }
 
-__global__ void akz_cand_kernel(AkCandArgs a)
+struct AkEntry {
+    float px, py, r;
+    uint32_t key; // level << 27 | y << 14 | x (the level's pixel)
+};
+constexpr int kAkListCap = 9216; // 147,456 B of LDS: one view's list
+
+__global__ __launch_bounds__(64) void akz_seq_kernel(AkCandArgs a)
 {
-    const int64_t ci = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (ci >= a.n)
+    __shared__ AkEntry L[kAkListCap];
+    const int z = blockIdx.x;
+    const int lane = threadIdx.x;
+    // the view's candidates: global Ldet indices of its planes (view-major)
+    int64_t vlo = -1, vhi = -1;
+    for (int i = 0; i < kAkLevels; ++i) {
+        const AkPlane &P = a.planes[z * kAkLevels + i];
+        if (P.w == 0)
+            continue;
+        if (vlo < 0)
+            vlo = P.det_base;
+        vhi = P.det_base + (int64_t)P.w * P.h;
+    }
+    if (vlo < 0)
         return;
-    const int64_t g = a.cand[ci];
-    // the plane of g: the last existing plane with det_base <= g
-    int lo = 0, hi = a.n_planes - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (a.plane_base[mid] <= g)
-            lo = mid;
-        else
-            hi = mid - 1;
+    const int64_t beg = ak_lower(a.cand, 0, a.n, vlo), end = ak_lower(a.cand, beg, a.n, vhi);
+    if (end - beg > kAkListCap) {
+        if (lane == 0)
+            atomicMax(a.err, (uint32_t)(end - beg));
+        for (int64_t ci = beg + lane; ci < end; ci += 64)
+            a.keep[ci] = 0;
+        return;
     }
-    const int pid = a.plane_ids[lo];
-    const int z = pid / kAkLevels, lev = pid % kAkLevels;
-    const AkPlane &P = a.planes[pid];
-    const int64_t li = g - P.det_base;
-    const int cy = (int)(li / P.w), cx = (int)(li - (int64_t)cy * P.w);
-    const float *det = a.pool + P.off + 3 * ((int64_t)P.w * P.h);
-    const float r = det[li];
-    const float ra = (float)(1 << P.octave);
-    const float S = P.esigma * 1.5f, S2 = S * S;
-    const float px = (float)cx * ra, py = (float)cy * ra;
-    bool drop = false;
-    for (int j = lev - 1; j <= lev + 1 && !drop; ++j) {
-        if (j < 0 || j >= kAkLevels)
-            continue;
-        const AkPlane &Q = a.planes[z * kAkLevels + j];
-        if (Q.w == 0)
-            continue;
-        const float rj = (float)(1 << Q.octave);
-        const int y0 = (int)floorf((py - S) / rj), y1 = (int)ceilf((py + S) / rj);
-        const int64_t qn = (int64_t)Q.w * Q.h;
-        const int64_t beg = ak_lower(a.cand, 0, a.n, Q.det_base), end = ak_lower(a.cand, beg, a.n, Q.det_base + qn);
-        const int64_t ylo = y0 < 0 ? 0 : (int64_t)y0 * Q.w;
-        const float *qdet = a.pool + Q.off + 3 * qn;
-        for (int64_t b = ak_lower(a.cand, beg, end, Q.det_base + ylo); b < end; ++b) {
-            const int64_t lb = a.cand[b] - Q.det_base;
-            const int by = (int)(lb / Q.w), bx = (int)(lb - (int64_t)by * Q.w);
-            if (by > y1)
-                break;
-            if (b == ci)
+    int na = 0;
+    for (int64_t ci = beg; ci < end; ++ci) {
+        const int64_t g = a.cand[ci];
+        int lev = 0;
+        for (int i = 0; i < kAkLevels; ++i) {
+            const AkPlane &P = a.planes[z * kAkLevels + i];
+            if (P.w > 0 && P.det_base <= g)
+                lev = i;
+        }
+        const AkPlane &P = a.planes[z * kAkLevels + lev];
+        const int64_t li = g - P.det_base;
+        const int cy = (int)(li / P.w), cx = (int)(li - (int64_t)cy * P.w);
+        const float r = a.pool[P.off + 3 * ((int64_t)P.w * P.h) + li];
+        const float ra = (float)(1 << P.octave);
+        const float S = P.esigma * 1.5f, S2 = S * S;
+        const float px = (float)cx * ra, py = (float)cy * ra;
+        int hit = -1;
+        for (int b0 = 0; b0 < na && hit < 0; b0 += 64) {
+            const int e = b0 + lane;
+            bool m = false;
+            if (e < na) {
+                const AkEntry q = L[e];
+                const int ql = (int)(q.key >> 27);
+                if (ql == lev - 1 || ql == lev) {
+                    const float dx = px - q.px, dy = py - q.py;
+                    m = dx * dx + dy * dy <= S2;
+                }
+            }
+            const unsigned long long bal = __ballot(m);
+            if (bal)
+                hit = b0 + __builtin_ctzll(bal);
+        }
+        const AkEntry ne{px, py, r, (uint32_t)lev << 27 | (uint32_t)cy << 14 | (uint32_t)cx};
+        if (hit < 0) {
+            if (lane == 0)
+                L[na] = ne;
+            ++na;
+        } else if (lane == 0 && r > L[hit].r) {
+            L[hit] = ne;
+        }
+        __syncthreads(); // the list update before the next candidate's reads
+    }
+    // the upper-level pass and the subpixel refinement, one lane per entry
+    for (int i = lane; i < na; i += 64) {
+        const AkEntry q = L[i];
+        const int lev = (int)(q.key >> 27), cy = (int)((q.key >> 14) & 0x1fffu), cx = (int)(q.key & 0x3fffu);
+        const AkPlane &P = a.planes[z * kAkLevels + lev];
+        const float S = P.esigma * 1.5f, S2 = S * S;
+        bool drop = false;
+        for (int j = i + 1; j < na && !drop; ++j) {
+            const AkEntry t = L[j];
+            if ((int)(t.key >> 27) != lev + 1)
                 continue;
-            const float dx = px - (float)bx * rj, dy = py - (float)by * rj;
-            const float rb = qdet[lb];
-            if (dx * dx + dy * dy <= S2 && (rb > r || (rb == r && b < ci))) {
-                drop = true;
-                break;
+            const float dx = q.px - t.px, dy = q.py - t.py;
+            drop = dx * dx + dy * dy <= S2 && q.r < t.r;
+        }
+        uint8_t keep = 0;
+        if (!drop) {
+            const float *det = a.pool + P.off + 3 * ((int64_t)P.w * P.h);
+            const int w = P.w;
+            const float *p = det + (int64_t)cy * w + cx;
+            const float Dx = 0.5f * (p[1] - p[-1]), Dy = 0.5f * (p[w] - p[-w]);
+            const float Dxx = (p[1] + p[-1]) - 2.0f * p[0], Dyy = (p[w] + p[-w]) - 2.0f * p[0];
+            const float Dxy = 0.25f * (p[w + 1] + p[-w - 1]) - 0.25f * (p[-w + 1] + p[w - 1]);
+            const float dt = Dxx * Dyy - Dxy * Dxy;
+            if (dt != 0.0f) {
+                const float ox = (Dxy * Dy - Dx * Dyy) / dt, oy = (Dxy * Dx - Dy * Dxx) / dt;
+                if (fabsf(ox) <= 1.0f && fabsf(oy) <= 1.0f) {
+                    const float ra = (float)(1 << P.octave);
+                    dp_keypoint k;
+                    k.x = ((float)cx + ox) * ra;
+                    k.y = ((float)cy + oy) * ra;
+                    k.response = q.r;
+                    k.angle = 0.0f;
+                    k.octave = P.octave;
+                    k.reserved = lev;
+                    a.kp[beg + i] = k;
+                    a.kv[beg + i] = a.view_ids[z];
+                    keep = 1;
+                }
             }
         }
+        a.keep[beg + i] = keep;
     }
-    uint8_t keep = 0;
-    if (!drop) {
-        const int w = P.w;
-        const float *p = det + li;
-        const float Dx = 0.5f * (p[1] - p[-1]), Dy = 0.5f * (p[w] - p[-w]);
-        const float Dxx = (p[1] + p[-1]) - 2.0f * p[0], Dyy = (p[w] + p[-w]) - 2.0f * p[0];
-        const float Dxy = 0.25f * (p[w + 1] + p[-w - 1]) - 0.25f * (p[-w + 1] + p[w - 1]);
-        const float dt = Dxx * Dyy - Dxy * Dxy;
-        if (dt != 0.0f) {
-            const float ox = (Dxy * Dy - Dx * Dyy) / dt, oy = (Dxy * Dx - Dy * Dxx) / dt;
-            if (fabsf(ox) <= 1.0f && fabsf(oy) <= 1.0f) {
-                dp_keypoint k;
-                k.x = ((float)cx + ox) * ra;
-                k.y = ((float)cy + oy) * ra;
-                k.response = r;
-                k.angle = 0.0f;
-                k.octave = P.octave;
-                k.reserved = lev;
-                a.kp[ci] = k;
-                a.kv[ci] = a.view_ids[z];
-                keep = 1;
-            }
-        }
-    }
-    a.keep[ci] = keep;
+    for (int64_t ci = beg + na + lane; ci < end; ci += 64)
+        a.keep[ci] = 0;
 }
 
 hipError_t launch_akz_candidates(const AkCandArgs &a, hipStream_t s)
 {
-    if (a.n <= 0)
+    if (a.n <= 0 || a.n_views <= 0)
         return hipSuccess;
-    hipLaunchKernelGGL(akz_cand_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(akz_seq_kernel, dim3((unsigned)a.n_views), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

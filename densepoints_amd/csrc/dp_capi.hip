@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <random>
@@ -174,6 +175,8 @@ extern "C" int dp_ctx_create(const dp_options *opt, int device, dp_ctx **out)
     {
         const char *e = getenv("DP_NO_LPT");
         c->lpt_off = e && e[0] == '1';
+        const char *g = getenv("DP_GEN_CAP");
+        c->gen_cap_test = g ? std::atoll(g) : 0;
     }
     if (opt)
         c->opt = *opt;
@@ -242,7 +245,14 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->oiota.release();
     c->porder.release();
     c->olo.release();
-    c->ocount.release();
+    c->gstate.release();
+    c->bsum.release();
+    c->wcand.release();
+    c->wok.release();
+    for (hipEvent_t e : c->gev)
+        if (e)
+            hipEventDestroy(e);
+    c->gev.clear();
     c->mbox.release();
     c->result.release();
     c->items.release();
@@ -260,7 +270,6 @@ extern "C" int dp_ctx_destroy(dp_ctx *c)
     c->cand.release();
     c->ok.release();
     c->acc.release();
-    c->prefix.release();
     c->scan_tmp.release();
     if (c->gray_pool)
         hipFree(c->gray_pool);
@@ -838,20 +847,15 @@ extern "C" int dp_last_kernel_ms(dp_ctx *c, double *ms)
 }
 
 // ---------------------------------------------------------------------------
-// densify: seeds -> organizer -> generation-synchronous BFS
+// densify: seeds -> organizer -> generation-synchronous BFS, device-resident.
+// Every expansion generation (refine + the dp_bfs.hip organizer) reads its
+// size from the GenDev state on the device, so dp_densify / dp_densify_run
+// queue kGenBatch generations behind ONE host wait; the state's stall flag
+// stops a batch whose next generation outgrows the candidate buffers (the
+// host grows them and resumes there).
 // ---------------------------------------------------------------------------
 
-// flags a[0 .. m-1] and a zero at index m (an exclusive scan of m + 1 of them
-// ends in the count) without a copy or a memset of the tail
-struct FlagAt {
-    const uint8_t *a;
-    int64_t m;
-    __host__ __device__ uint32_t operator()(int64_t i) const { return i < m ? (uint32_t)a[i] : 0u; }
-};
-
-struct U8ToU32 {
-    __host__ __device__ uint32_t operator()(uint8_t v) const { return v; }
-};
+static constexpr int kGenBatch = 8;
 
 // organizer grid of an empty store: capacity 1 keeps the owner seq per cell
 // (UINT32_MAX = free), capacity k > 1 the claims made (0) plus the per-round
@@ -883,75 +887,92 @@ static int64_t store_capacity(const dp_ctx *c, int64_t nseeds)
     return (by_cells < by_pops ? by_cells : by_pops) + 16;
 }
 
-// PatchOrganizer::TryInsert over n candidates in sequence order, then the
-// append of the accepted ones at store[base ..], asynchronously on s: the
-// accepted count is read with the generation's status (read_status) -- one
-// host sync per generation, not one before the append (r05).  The append
-// guards the store capacity on the device (store_capacity bounds the accepts,
-// so the guard never fires with a correct organizer).
-static int organize_async(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int32_t n, uint32_t seq0,
-                          int64_t base, int64_t parent0, int is_seed, hipStream_t s)
+// the organizer's buffers for generations of up to cap candidates (reserved
+// before anything is queued on them: a reserve that grows frees the old buffer)
+static int reserve_organizer(dp_ctx *c, int64_t cap)
 {
-    dpk::ClaimArgs ca{};
-    ca.views = c->d_views;
-    ca.cand = cand;
-    ca.ok = okf;
-    ca.n = n;
-    ca.seq0 = seq0;
-    ca.grid = c->grid.p;
-    ca.grid_scale = (double)c->opt.grid_scale;
-    DP_HIP(c, c->acc.reserve((size_t)n + 1));
-    if (c->opt.max_patches_per_cell == 1) {
-        DP_HIP(c, dpk::launch_claims(ca, s));
-        DP_HIP(c, dpk::launch_resolve(ca, c->acc.p, s));
-    } else {
-        DP_HIP(c, c->pend.reserve(2 * (size_t)n + 2));
-        DP_HIP(c, c->granted.reserve((size_t)n + 1));
-        ca.cellmin = c->cellmin.p;
-        ca.pend = c->pend.p;
-        ca.granted = c->granted.p;
-        ca.k = c->opt.max_patches_per_cell;
-        DP_HIP(c, dpk::launch_claims_k(ca, c->acc.p, s));
+    DP_HIP(c, c->gstate.reserve(2));
+    DP_HIP(c, c->bsum.reserve(dpk::kBfsBlocks));
+    DP_HIP(c, c->acc.reserve((size_t)cap + 1));
+    if (c->opt.max_patches_per_cell > 1) {
+        DP_HIP(c, c->pend.reserve(2 * (size_t)cap + 2));
+        DP_HIP(c, c->granted.reserve((size_t)cap + 1));
     }
-    DP_HIP(c, c->prefix.reserve((size_t)n + 1));
-    size_t tmp_bytes = 0;
-    // n + 1 flags, index n read as 0: prefix[n] = the accepts
-    hipcub::TransformInputIterator<uint32_t, FlagAt, hipcub::CountingInputIterator<int64_t>> it(
-        hipcub::CountingInputIterator<int64_t>(0), FlagAt{c->acc.p, (int64_t)n});
-    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, it, c->prefix.p, n + 1, s));
-    DP_HIP(c, c->scan_tmp.reserve(tmp_bytes + 16));
-    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp_bytes, it, c->prefix.p, n + 1, s));
-    DP_HIP(c, dpk::launch_append(c->d_views, c->V, cand, c->acc.p, c->prefix.p, n, c->store.p, base, parent0, is_seed,
-                                 (int64_t)c->store.cap, c->mbox.p + 7, s));
     return DP_OK;
 }
 
-// The generation's one host sync: status_kernel gathers the organizer's
-// accepts (prefix[n] of the last organize_async, n > 0), the store-overflow
-// flag, the pending partition statistics and the exchanged record total into
-// c->mbox, one copy brings them back.  st[5]: accepts, overflow, tiles, split
-// items, records exchanged.
-static int read_status(dp_ctx *c, hipStream_t s, int32_t n, const int64_t *d_counts, int world, uint64_t st[5])
+// timing events: a pair per generation of a batch, and the seed refine's pair
+static int ensure_gen_events(dp_ctx *c)
 {
-    DP_HIP(c, dpk::launch_status(n > 0 ? c->prefix.p + n : nullptr, c->part_pending ? c->ocount.p : nullptr, d_counts,
-                                 world, c->mbox.p, s));
-    unsigned long long h[5] = {0, 0, 0, 0, 0};
-    DP_HIP(c, hipMemcpyAsync(h, c->mbox.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    if (!c->gev.empty())
+        return DP_OK;
+    c->gev.assign(2 * kGenBatch + 2, nullptr);
+    for (auto &e : c->gev)
+        DP_HIP(c, hipEventCreate(&e));
+    return DP_OK;
+}
+
+static int set_state(dp_ctx *c, int slot, const dpk::GenDev &g, hipStream_t s)
+{
+    DP_HIP(c, dpk::launch_bfs_set_state(c->gstate.p + slot, g, s));
+    return DP_OK;
+}
+
+// the organizer of the generation in state slot `slot` over cand/okf (in
+// sequence order); writes the next generation's state into slot ^ 1.
+// cand_cap: the candidate buffers' capacity (the next generation stalls above it)
+static int organize_gen(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int slot, int64_t cand_cap, hipStream_t s)
+{
+    dpk::BfsArgs b{};
+    b.views = c->d_views;
+    b.V = c->V;
+    b.k = c->opt.max_patches_per_cell;
+    b.cur = c->gstate.p + slot;
+    b.nxt = c->gstate.p + (slot ^ 1);
+    b.cand = cand;
+    b.ok = okf;
+    b.acc = c->acc.p;
+    b.bsum = c->bsum.p;
+    b.grid = c->grid.p;
+    b.grid_scale = (double)c->opt.grid_scale;
+    b.cellmin = c->cellmin.p;
+    b.pend = c->pend.p;
+    b.granted = c->granted.p;
+    b.store = c->store.p;
+    b.store_cap = (int64_t)c->store.cap;
+    b.cand_cap = cand_cap;
+    b.max_pops = c->opt.max_pops;
+    b.mbox = c->mbox.p;
+    b.work = c->d_work;
+    b.lpt_scratch = c->g_lpt_scratch;
+    DP_HIP(c, dpk::launch_bfs_organize(b, s));
+    return DP_OK;
+}
+
+// The generation's status: the state in `slot` (the next generation) and the
+// status words (accepts, partition statistics, records exchanged, the
+// append's overflow flag, cleared here) -- one wait.
+static int read_state(dp_ctx *c, int slot, hipStream_t s, dpk::GenDev *g, unsigned long long mb[8])
+{
+    DP_HIP(c, hipMemcpyAsync(g, c->gstate.p + slot, sizeof(dpk::GenDev), hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipMemcpyAsync(mb, c->mbox.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     DP_HIP(c, hipStreamSynchronize(s));
-    for (int k = 0; k < 5; ++k)
-        st[k] = h[k];
+    if (mb[7]) {
+        DP_HIP(c, hipMemsetAsync(c->mbox.p + 7, 0, sizeof(unsigned long long), s));
+        return fail(c, DP_E_OOM, "patch store overflow");
+    }
+    if (g->err)
+        return fail(c, DP_E_OOM, "sequence space exhausted");
     if (c->part_pending) {
-        c->part_stats[2] = (int64_t)h[2];
-        c->part_stats[3] = (int64_t)h[3];
+        c->part_stats[2] = (int64_t)mb[2];
+        c->part_stats[3] = (int64_t)mb[3];
         c->part_pending = false;
     }
-    if (h[1])
-        return fail(c, DP_E_OOM, "patch store overflow");
     return DP_OK;
 }
 
-// the refine events of the generation (recorded by launch_timed /
-// dp_fast_launch), read after the generation's sync: no extra wait
+// the refine events of a host-driven generation (recorded by launch_timed /
+// dp_fast_launch), read after the generation's wait: no extra wait
 static int take_refine_ms(dp_ctx *c, double *acc_ms)
 {
     if (!c->g_time_pending)
@@ -974,6 +995,171 @@ static int join_streams(dp_ctx *c, hipStream_t from, hipStream_t to)
     return DP_OK;
 }
 
+// host mirror of the state: the API's generation record and the statistics
+static void take_state(dp_ctx *c, const dpk::GenDev &g, dp_generation *gen)
+{
+    c->g_np = g.np;
+    c->g_st.seed_patches = g.seed_patches;
+    c->g_st.candidates = g.cand_total;
+    c->g_st.generations = (int32_t)g.gens;
+    if (gen) {
+        gen->index = 1 + (int32_t)g.gens;
+        gen->head = g.head;
+        gen->items = g.items;
+        gen->per_item = 4;
+        gen->cell = c->opt.expand_cell_size;
+        gen->seq0 = g.seq0;
+        c->g_expected = gen->index;
+    }
+}
+
+// The refine of the generation in state slot `slot` (device-sized): Expand::
+// ExpandPatch of the queue slice [head, head + items) into c->cand / c->ok.
+static int refine_gen(dp_ctx *c, int slot, int64_t cap, hipStream_t s)
+{
+    const dpk::GenDev *g = c->gstate.p + slot;
+    if (c->fopt.densify)
+        return dp_fast_launch(c, c->cand.p, 0, c->opt.expand_cell_size, DP_MODE_FAST_REFINE, c->ok.p, c->store.p, s,
+                              0, nullptr, c->opt.max_pops, g);
+    dpk::RefineArgs a = refine_args(c, c->cand.p, (int)cap, c->opt.expand_cell_size, DP_MODE_EXPAND, c->ok.p);
+    a.parents = c->store.p;
+    a.gen = g;
+    DP_HIP(c, dpk::launch_refine(a, s));
+    return DP_OK;
+}
+
+// the device-resident loop supports the default refines (the analytic-
+// gradient performance refine is host-driven)
+static bool device_loop_ok(const dp_ctx *c) { return !(c->fopt.densify && c->fopt.gradient); }
+
+// Up to max_gens expansion generations from the state in c->g_slot, kGenBatch
+// per host wait (dp_densify, dp_densify_run).  cap0: the candidate capacity
+// to start with.  Leaves the state of the first generation not run in c->g_slot.
+static int run_generations(dp_ctx *c, int64_t max_gens, int64_t cap0, hipStream_t s, dpk::GenDev *last)
+{
+    int64_t cap = std::max<int64_t>(cap0, 1024);
+    if (c->gen_cap_test > 0)
+        cap = c->gen_cap_test; // DP_GEN_CAP (tests): small buffers, so generations stall and resume
+    int64_t done = 0;
+    dpk::GenDev g{};
+    unsigned long long mb[8];
+    int rc0 = ensure_gen_events(c);
+    if (rc0 != DP_OK)
+        return rc0;
+    for (;;) {
+        if (cap > INT32_MAX)
+            cap = INT32_MAX;
+        DP_HIP(c, c->cand.reserve((size_t)cap));
+        DP_HIP(c, c->ok.reserve((size_t)cap));
+        int rc = reserve_organizer(c, cap);
+        if (rc != DP_OK)
+            return rc;
+        c->g_lpt_scratch = nullptr;
+        if (!c->lpt_off && !c->fopt.densify) {
+            DP_HIP(c, c->lpt.reserve((size_t)cap + 2 * dpk::kLptBuckets));
+            c->g_lpt_scratch = c->lpt.p + cap;
+        }
+        // the first generation's counters (later ones are zeroed by the previous organizer)
+        DP_HIP(c, hipMemsetAsync(c->d_work, 0, dpk::kWorkCounters * sizeof(uint32_t), s));
+        if (c->g_lpt_scratch)
+            DP_HIP(c, hipMemsetAsync(c->g_lpt_scratch, 0, 2 * dpk::kLptBuckets * sizeof(uint32_t), s));
+        const int k = (int)std::min<int64_t>(kGenBatch, max_gens - done);
+        int slot = c->g_slot;
+        for (int i = 0; i < k; ++i) {
+            DP_HIP(c, hipEventRecord(c->gev[2 * i], s));
+            rc = refine_gen(c, slot, cap, s);
+            if (rc != DP_OK)
+                return rc;
+            DP_HIP(c, hipEventRecord(c->gev[2 * i + 1], s));
+            rc = organize_gen(c, c->cand.p, c->ok.p, slot, cap, s);
+            if (rc != DP_OK)
+                return rc;
+            slot ^= 1;
+        }
+        rc = read_state(c, slot, s, &g, mb);
+        if (rc != DP_OK)
+            return rc;
+        for (int i = 0; i < k; ++i) {
+            float f = 0.f;
+            DP_HIP(c, hipEventElapsedTime(&f, c->gev[2 * i], c->gev[2 * i + 1]));
+            c->g_st.refine_ms += f;
+        }
+        c->g_slot = slot;
+        done += k;
+        if (g.stall) {
+            // the next generation outgrew the buffers: grow and resume it
+            c->g_st.stalls += 1;
+            cap = std::max<int64_t>(2 * cap, 4 * g.items + (c->gen_cap_test > 0 ? 0 : 4096));
+            g.stall = 0;
+            g.ncand = 4 * g.items;
+            if (g.ncand > INT32_MAX)
+                return fail(c, DP_E_OOM, "generation too large");
+            rc = reserve_organizer(c, cap);
+            if (rc != DP_OK || (rc = set_state(c, slot, g, s)) != DP_OK)
+                return rc;
+            if (done >= max_gens)
+                break;
+            continue;
+        }
+        if (g.items == 0 || done >= max_gens)
+            break;
+    }
+    *last = g;
+    return DP_OK;
+}
+
+// the seed state: generation 0 over n seed patches (sequence numbers 0 .. n-1)
+static dpk::GenDev seed_state(int64_t n)
+{
+    dpk::GenDev g{};
+    g.items = n;
+    g.ncand = n;
+    g.nseeds = n;
+    g.per_item = 1;
+    return g;
+}
+
+static int begin_impl(dp_ctx *c, int n, hipStream_t s)
+{
+    c->g_t0 = std::chrono::steady_clock::now();
+    c->g_st = dp_densify_stats{};
+    c->g_st.seeds_in = n;
+    c->g_np = 0;
+    c->g_nseeds = n;
+    c->g_time_pending = false;
+    c->part_pending = false;
+    c->g_slot = 0;
+    c->result.clear();
+    int rc = reset_grid(c, s);
+    if (rc != DP_OK || (rc = reserve_organizer(c, std::max<int64_t>(n, 1))) != DP_OK)
+        return rc;
+    DP_HIP(c, c->store.reserve((size_t)store_capacity(c, n)));
+    DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
+    DP_HIP(c, hipMemsetAsync(c->mbox.p, 0, 8 * sizeof(unsigned long long), s));
+    return set_state(c, 0, seed_state(n), s);
+}
+
+static int result_impl(dp_ctx *c, hipStream_t s, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats)
+{
+    const int64_t np = c->g_np;
+    DP_HIP(c, c->result.resize((size_t)np));
+    if (np)
+        DP_HIP(c, hipMemcpyAsync(c->result.data(), c->store.p, sizeof(dp_patch) * np, hipMemcpyDeviceToHost, s));
+    unsigned long long ev = 0;
+    DP_HIP(c, hipMemcpyAsync(&ev, c->d_evals, sizeof(ev), hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipStreamSynchronize(s));
+    dp_densify_stats st = c->g_st;
+    st.patches = np;
+    st.pops = std::min<int64_t>(np, c->opt.max_pops);
+    st.evals = (int64_t)ev;
+    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->g_t0).count();
+    if (stats)
+        *stats = st;
+    *out = c->result.empty() ? nullptr : c->result.data();
+    *n_out = np;
+    return DP_OK;
+}
+
 extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch **out, int64_t *n_out,
                           dp_densify_stats *stats)
 {
@@ -981,35 +1167,29 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         return fail(c, DP_E_ARG, "dp_densify: bad arguments");
     if (!c->V)
         return fail(c, DP_E_STATE, "dp_densify: no views");
-    auto t_start = std::chrono::steady_clock::now();
     hipSetDevice(c->device);
     hipStream_t s = c->stream;
     const dp_options &o = c->opt;
     const bool fast = c->fopt.densify != 0;
-    dp_densify_stats st{};
-    st.seeds_in = n;
-    c->result.clear();
     *out = nullptr;
     *n_out = 0;
-
-    // organizer grid: every cell free
-    int rg = reset_grid(c, s);
-    if (rg != DP_OK)
-        return rg;
-    const int64_t store_cap = store_capacity(c, n);
-    DP_HIP(c, c->store.reserve((size_t)store_cap));
-    DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
-
-    double refine_ms = 0.0;
-    int64_t np = 0;
+    // every buffer of the first expansion generation (<= 4 per seed patch)
+    // before anything is queued on them
+    const int64_t cap = std::min<int64_t>(std::max<int64_t>(4 * (int64_t)n, 1024), INT32_MAX);
+    DP_HIP(c, c->cand.reserve((size_t)cap));
+    DP_HIP(c, c->ok.reserve((size_t)cap));
+    int rc = begin_impl(c, n, s);
+    if (rc != DP_OK || (rc = reserve_organizer(c, cap)) != DP_OK || (rc = ensure_gen_events(c)) != DP_OK)
+        return rc;
+    c->g_expected = -1;
     if (n > 0) {
-        DP_HIP(c, c->cand.reserve(n));
-        DP_HIP(c, c->ok.reserve(n));
-        int rc = seeds_device(c, seeds, n, c->cand.p, s);
+        rc = seeds_device(c, seeds, n, c->cand.p, s);
         if (rc != DP_OK)
             return rc;
         // seed.cpp:110-144: FilterPatches then OptimizePatches at the seed cell
-        // size (performance mode, dp_fast_options.densify: the fast refine)
+        // size (performance mode, dp_fast_options.densify: the fast refine),
+        // timed by its own event pair (the generations' are re-recorded)
+        DP_HIP(c, hipEventRecord(c->gev[2 * kGenBatch], s));
         if (fast) {
             rc = dp_fast_launch(c, c->cand.p, n, o.seed_cell_size, DP_MODE_FAST_REFINE, c->ok.p, nullptr, s);
         } else {
@@ -1018,91 +1198,52 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         }
         if (rc != DP_OK)
             return rc;
-        c->g_time_pending = true;
+        DP_HIP(c, hipEventRecord(c->gev[2 * kGenBatch + 1], s));
         // PatchOrganizer::SetSeeds: TryInsert in seed order (seq = seed index)
-        rc = organize_async(c, c->cand.p, c->ok.p, n, 0u, 0, 0, 1, s);
-        uint64_t gs[5];
-        if (rc != DP_OK || (rc = read_status(c, s, n, nullptr, 0, gs)) != DP_OK ||
-            (rc = take_refine_ms(c, &refine_ms)) != DP_OK)
+        c->g_lpt_scratch = nullptr;
+        rc = organize_gen(c, c->cand.p, c->ok.p, 0, cap, s);
+        if (rc != DP_OK)
             return rc;
-        np = (int64_t)gs[0];
-    }
-    st.seed_patches = np;
-    const uint32_t seq_base = (uint32_t)n;
-    int64_t head = 0;
-    int gens = 0;
-    while (head < np && head < o.max_pops) {
-        const int64_t F = np - head;
-        const int64_t nc64 = 4 * F;
-        if (nc64 > INT32_MAX)
-            return fail(c, DP_E_OOM, "generation too large");
-        const int32_t nc = (int32_t)nc64;
-        if ((uint64_t)seq_base + 4ull * (uint64_t)np > 0xFFFFFFF0ull)
-            return fail(c, DP_E_OOM, "sequence space exhausted");
-        // (the previous generation's append finished at its status read)
-        DP_HIP(c, c->cand.reserve(nc));
-        DP_HIP(c, c->ok.reserve(nc));
-        int rc;
-        if (fast) {
-            // Expand::ExpandPatch with the fast refine; parents past the pop cap stay put
-            rc = dp_fast_launch(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_FAST_REFINE, c->ok.p, c->store.p, s,
-                                head, nullptr, o.max_pops);
+        c->g_slot = 1;
+        dpk::GenDev g{};
+        if (device_loop_ok(c)) {
+            rc = run_generations(c, INT64_MAX, cap, s, &g);
         } else {
-            dpk::RefineArgs a = refine_args(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_EXPAND, c->ok.p);
-            a.parents = c->store.p;
-            a.parent0 = head;
-            rc = launch_timed(c, a, s);
+            // the analytic-gradient refine: one host wait per generation
+            unsigned long long mb[8];
+            rc = read_state(c, 1, s, &g, mb);
+            while (rc == DP_OK && g.items > 0) {
+                const int32_t nc = (int32_t)(4 * g.items);
+                DP_HIP(c, c->cand.reserve(nc));
+                DP_HIP(c, c->ok.reserve(nc));
+                if ((rc = reserve_organizer(c, nc)) != DP_OK)
+                    break;
+                rc = take_refine_ms(c, &c->g_st.refine_ms);
+                if (rc == DP_OK)
+                    rc = dp_fast_launch(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_FAST_REFINE, c->ok.p, c->store.p,
+                                        s, g.head, nullptr, o.max_pops);
+                c->g_time_pending = true;
+                if (rc == DP_OK)
+                    rc = organize_gen(c, c->cand.p, c->ok.p, c->g_slot, INT64_MAX, s);
+                if (rc == DP_OK)
+                    rc = read_state(c, c->g_slot ^ 1, s, &g, mb);
+                c->g_slot ^= 1;
+            }
         }
         if (rc != DP_OK)
             return rc;
-        c->g_time_pending = true;
-        const int64_t expandable = std::min<int64_t>(np, o.max_pops) - head;
-        st.candidates += 4 * expandable;
-        // one host sync per generation: the accepts come back with the status
-        rc = organize_async(c, c->cand.p, c->ok.p, nc, seq_base + 4u * (uint32_t)head, np, head, 0, s);
-        uint64_t gs[5];
-        if (rc != DP_OK || (rc = read_status(c, s, nc, nullptr, 0, gs)) != DP_OK ||
-            (rc = take_refine_ms(c, &refine_ms)) != DP_OK)
-            return rc;
-        head = np;
-        np += (int64_t)gs[0];
-        ++gens;
+        float f = 0.f;
+        DP_HIP(c, hipEventElapsedTime(&f, c->gev[2 * kGenBatch], c->gev[2 * kGenBatch + 1]));
+        c->g_st.refine_ms += f;
+        take_state(c, g, nullptr);
     }
-    st.pops = std::min<int64_t>(np, o.max_pops);
-    DP_HIP(c, c->result.resize((size_t)np));
-    if (np)
-        DP_HIP(c, hipMemcpyAsync(c->result.data(), c->store.p, sizeof(dp_patch) * np, hipMemcpyDeviceToHost, s));
-    unsigned long long ev = 0;
-    DP_HIP(c, hipMemcpyAsync(&ev, c->d_evals, sizeof(ev), hipMemcpyDeviceToHost, s));
-    DP_HIP(c, hipStreamSynchronize(s));
-    st.patches = np;
-    st.evals = (int64_t)ev;
-    st.generations = gens;
-    st.refine_ms = refine_ms;
-    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
-    if (stats)
-        *stats = st;
-    *out = c->result.empty() ? nullptr : c->result.data();
-    *n_out = np;
-    return DP_OK;
+    return result_impl(c, s, out, n_out, stats);
 }
 
 // ---------------------------------------------------------------------------
 // densify one generation at a time (multi-GPU sharding).  Same
 // sequence numbering, organizer and pop cap as dp_densify.
 // ---------------------------------------------------------------------------
-
-// next expansion generation after the store grew to g_np (dp_densify's loop head)
-static void next_generation(dp_ctx *c, dp_generation *g, int64_t head)
-{
-    const int64_t np = c->g_np;
-    g->index += 1;
-    g->head = head;
-    g->per_item = 4;
-    g->cell = c->opt.expand_cell_size;
-    g->items = (head < np && head < c->opt.max_pops) ? np - head : 0;
-    g->seq0 = (uint32_t)c->g_nseeds + 4u * (uint32_t)head;
-}
 
 extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_generation *gen)
 {
@@ -1112,22 +1253,12 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
         return fail(c, DP_E_STATE, "dp_densify_begin: no views");
     hipSetDevice(c->device);
     hipStream_t s = c->stream;
-    c->g_t0 = std::chrono::steady_clock::now();
-    c->g_st = dp_densify_stats{};
-    c->g_st.seeds_in = n;
-    c->g_np = 0;
-    c->g_nseeds = n;
-    c->g_time_pending = false;
-    c->part_pending = false;
-    c->result.clear();
-    int rg = reset_grid(c, s);
-    if (rg != DP_OK)
-        return rg;
-    DP_HIP(c, c->store.reserve((size_t)store_capacity(c, n)));
-    DP_HIP(c, hipMemsetAsync(c->d_evals, 0, sizeof(unsigned long long), s));
+    int rc = begin_impl(c, n, s);
+    if (rc != DP_OK)
+        return rc;
     if (n > 0) {
         DP_HIP(c, c->seedp.reserve(n));
-        int rc = seeds_device(c, seeds, n, c->seedp.p, s);
+        rc = seeds_device(c, seeds, n, c->seedp.p, s);
         if (rc != DP_OK)
             return rc;
     }
@@ -1141,176 +1272,90 @@ extern "C" int dp_densify_begin(dp_ctx *c, const double *seeds, int n, dp_genera
     return DP_OK;
 }
 
-// dp_densify_refine / _device: `dev` = the output arrays are device memory
-// (refined in place, asynchronously on `s`), else host arrays (synchronous).
-static int densify_refine_impl(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi, dp_patch *cand_out,
-                               uint8_t *accept_out, bool dev, hipStream_t s)
+static int check_gen(dp_ctx *c, const dp_generation *gen, const char *who)
 {
-    if (!c || !gen || lo < 0 || hi < lo || hi > gen->items)
-        return fail(c, DP_E_ARG, "dp_densify_refine: bad item range");
+    if (!c || !gen)
+        return fail(c, DP_E_ARG, std::string(who) + ": bad arguments");
     if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_refine: generation out of sequence");
-    const int64_t nc64 = (hi - lo) * gen->per_item;
-    if (nc64 == 0)
-        return DP_OK;
-    if (!cand_out || !accept_out)
-        return fail(c, DP_E_ARG, "dp_densify_refine: null output arrays");
-    if (nc64 > INT32_MAX)
-        return fail(c, DP_E_OOM, "dp_densify_refine: shard too large");
-    const int32_t nc = (int32_t)nc64;
-    hipSetDevice(c->device);
-    dp_patch *work = cand_out;
-    uint8_t *okp = accept_out;
-    if (!dev) {
-        DP_HIP(c, c->cand.reserve(nc));
-        DP_HIP(c, c->ok.reserve(nc));
-        work = c->cand.p;
-        okp = c->ok.p;
-    }
-    dpk::RefineArgs a{};
-    const bool fast = c->fopt.densify != 0;
-    int rc = take_refine_ms(c, &c->g_st.refine_ms); // an earlier refine's events, before they are re-recorded
-    if (rc != DP_OK)
-        return rc;
-    if (gen->index == 0) {
-        // seed.cpp:110-144 on this shard of the seed patches
-        DP_HIP(c, hipMemcpyAsync(work, c->seedp.p + lo, sizeof(dp_patch) * nc, hipMemcpyDeviceToDevice, s));
-        a = refine_args(c, work, nc, gen->cell, DP_MODE_SEED, okp);
-        rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, nullptr, s) : launch_timed(c, a, s);
-    } else {
-        // Expand::ExpandPatch of parents head+lo .. head+hi-1 (queue order)
-        a = refine_args(c, work, nc, gen->cell, DP_MODE_EXPAND, okp);
-        a.parents = c->store.p;
-        a.parent0 = gen->head + lo;
-        rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, c->store.p, s, gen->head + lo,
-                                   nullptr, c->opt.max_pops)
-                  : launch_timed(c, a, s);
-    }
-    if (rc != DP_OK)
-        return rc;
-    c->g_time_pending = true; // read at the commit's status sync
-    if (!dev) {
-        DP_HIP(c, hipMemcpyAsync(cand_out, work, sizeof(dp_patch) * nc, hipMemcpyDeviceToHost, s));
-        DP_HIP(c, hipMemcpyAsync(accept_out, okp, (size_t)nc, hipMemcpyDeviceToHost, s));
-        DP_HIP(c, hipStreamSynchronize(s));
-    }
+        return fail(c, DP_E_STATE, std::string(who) + ": generation out of sequence");
     return DP_OK;
 }
 
-extern "C" int dp_densify_refine(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi, dp_patch *cand_out,
-                                 uint8_t *accept_out)
+// The organizer step of a whole generation on stream s (cp/op: every
+// candidate in sequence order, ordered before it on s), ending in the
+// generation's one status read; advances *gen.
+static int commit_on_stream(dp_ctx *c, dp_generation *gen, const dp_patch *cp, const uint8_t *op, int64_t nc,
+                            hipStream_t s, int64_t *exchanged = nullptr)
 {
-    return densify_refine_impl(c, gen, lo, hi, cand_out, accept_out, false, c ? c->stream : nullptr);
-}
-
-extern "C" int dp_densify_refine_device(dp_ctx *c, const dp_generation *gen, int64_t lo, int64_t hi,
-                                        dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream)
-{
-    if (c && !stream) {
-        hipSetDevice(c->device);
-        int rj = join_streams(c, nullptr, c->stream);
-        if (rj != DP_OK)
-            return rj;
-    }
-    int rc = densify_refine_impl(c, gen, lo, hi, d_cand_out, d_accept_out, true,
-                                 stream ? (hipStream_t)stream : (c ? c->stream : nullptr));
-    // NULL stream: the records are read on the legacy default stream (torch's
-    // default), which does not order with the context's non-blocking stream
-    if (rc == DP_OK && !stream)
-        rc = join_streams(c, c->stream, nullptr);
-    return rc;
-}
-
-// The organizer step of a whole generation on stream s (every input already
-// ordered before it on s), ending in the generation's one status read.
-// d_counts/world: the exchanged per-rank record counts (statistics only).
-static int commit_on_stream(dp_ctx *c, dp_generation *gen, const dp_patch *cp, const uint8_t *op, int32_t nc,
-                            hipStream_t s, const int64_t *d_counts = nullptr, int world = 0, int64_t *exchanged = nullptr)
-{
-    uint64_t gs[5] = {0, 0, 0, 0, 0};
-    if (nc > 0) {
-        if ((uint64_t)gen->seq0 + (uint64_t)nc > 0xFFFFFFF0ull)
-            return fail(c, DP_E_OOM, "sequence space exhausted");
-        const int is_seed = gen->index == 0;
-        int rc = organize_async(c, cp, op, nc, gen->seq0, c->g_np, is_seed ? 0 : gen->head, is_seed, s);
-        if (rc != DP_OK)
-            return rc;
-    }
-    int rc = read_status(c, s, nc, d_counts, world, gs);
-    if (rc != DP_OK || (rc = take_refine_ms(c, &c->g_st.refine_ms)) != DP_OK)
+    int rc = reserve_organizer(c, std::max<int64_t>(nc, 1));
+    if (rc != DP_OK)
         return rc;
+    c->g_lpt_scratch = nullptr;
+    // host-driven generations size their refines on the host: no stall bound
+    rc = organize_gen(c, cp, op, c->g_slot, INT64_MAX, s);
+    dpk::GenDev g{};
+    unsigned long long mb[8];
+    if (rc != DP_OK || (rc = read_state(c, c->g_slot ^ 1, s, &g, mb)) != DP_OK ||
+        (rc = take_refine_ms(c, &c->g_st.refine_ms)) != DP_OK)
+        return rc;
+    c->g_slot ^= 1;
     if (exchanged)
-        *exchanged = (int64_t)gs[4];
-    const int64_t acc = nc > 0 ? (int64_t)gs[0] : 0;
-    int64_t head;
-    if (gen->index == 0) {
-        c->g_st.seed_patches = acc;
-        head = 0;
-    } else {
-        c->g_st.candidates += 4 * (std::min<int64_t>(c->g_np, c->opt.max_pops) - gen->head);
-        c->g_st.generations += 1;
-        head = c->g_np;
-    }
-    c->g_np += acc;
-    next_generation(c, gen, head);
-    c->g_expected = gen->index;
+        *exchanged = (int64_t)mb[4];
+    take_state(c, g, gen);
     return DP_OK;
-}
-
-static int densify_commit_impl(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
-                               int64_t n_cand, bool dev, hipStream_t user)
-{
-    if (!c || !gen || n_cand != gen->items * gen->per_item || (n_cand > 0 && (!cand || !accept)))
-        return fail(c, DP_E_ARG, "dp_densify_commit: need all candidates of the generation");
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_commit: generation out of sequence");
-    if (n_cand > INT32_MAX)
-        return fail(c, DP_E_OOM, "dp_densify_commit: generation too large");
-    hipSetDevice(c->device);
-    hipStream_t s = c->stream;
-    const int32_t nc = (int32_t)n_cand;
-    const dp_patch *cp = cand;
-    const uint8_t *op = accept;
-    if (nc > 0) {
-        if (dev) {
-            // the gathered records are produced on the caller's stream (RCCL,
-            // torch ops; NULL = the legacy default stream): the context's
-            // stream waits for it on the device
-            int rc = join_streams(c, user, s);
-            if (rc != DP_OK)
-                return rc;
-        } else {
-            DP_HIP(c, c->cand.reserve(nc));
-            DP_HIP(c, c->ok.reserve(nc));
-            DP_HIP(c, hipMemcpyAsync(c->cand.p, cand, sizeof(dp_patch) * nc, hipMemcpyHostToDevice, s));
-            DP_HIP(c, hipMemcpyAsync(c->ok.p, accept, (size_t)nc, hipMemcpyHostToDevice, s));
-            cp = c->cand.p;
-            op = c->ok.p;
-        }
-    }
-    return commit_on_stream(c, gen, cp, op, nc, s);
 }
 
 extern "C" int dp_densify_commit(dp_ctx *c, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
                                  int64_t n_cand)
 {
-    return densify_commit_impl(c, gen, cand, accept, n_cand, false, nullptr);
+    int rc = check_gen(c, gen, "dp_densify_commit");
+    if (rc != DP_OK)
+        return rc;
+    if (n_cand != gen->items * gen->per_item || (n_cand > 0 && (!cand || !accept)))
+        return fail(c, DP_E_ARG, "dp_densify_commit: need all candidates of the generation");
+    if (n_cand > INT32_MAX)
+        return fail(c, DP_E_OOM, "dp_densify_commit: generation too large");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    if (n_cand > 0) {
+        DP_HIP(c, c->cand.reserve((size_t)n_cand));
+        DP_HIP(c, c->ok.reserve((size_t)n_cand));
+        DP_HIP(c, hipMemcpyAsync(c->cand.p, cand, sizeof(dp_patch) * n_cand, hipMemcpyHostToDevice, s));
+        DP_HIP(c, hipMemcpyAsync(c->ok.p, accept, (size_t)n_cand, hipMemcpyHostToDevice, s));
+    }
+    return commit_on_stream(c, gen, c->cand.p, c->ok.p, n_cand, s);
 }
 
-extern "C" int dp_densify_commit_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_cand,
-                                        const uint8_t *d_accept, int64_t n_cand, void *stream)
+extern "C" int dp_densify_run(dp_ctx *c, dp_generation *gen, int32_t max_generations)
 {
-    return densify_commit_impl(c, gen, d_cand, d_accept, n_cand, true, (hipStream_t)stream);
+    int rc = check_gen(c, gen, "dp_densify_run");
+    if (rc != DP_OK)
+        return rc;
+    if (gen->index < 1 || max_generations < 1)
+        return fail(c, DP_E_ARG, "dp_densify_run: expansion generations only (index >= 1), max_generations >= 1");
+    if (gen->items == 0)
+        return DP_OK;
+    if (!device_loop_ok(c))
+        return fail(c, DP_E_ARG, "dp_densify_run: the analytic-gradient refine is host-driven");
+    hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    dpk::GenDev g{};
+    rc = run_generations(c, max_generations, std::max<int64_t>(4 * gen->items + 4096, (int64_t)c->cand.cap), s, &g);
+    if (rc != DP_OK)
+        return rc;
+    take_state(c, g, gen);
+    return DP_OK;
 }
 
 // ---- partitioned generations (reference-view super-tiles) -------
 
 // The partition of a generation (spec in include/densepoints.h):
 // items stable-sorted by super-tile key, the order cut into `world` contiguous
-// shares lo[r] = floor(r n / world).  Leaves the order in c->porder (complete
-// on return), the shares in counts (host) and the statistics in c->part_stats.
+// shares lo[r] = floor(r n / world).  Leaves the order in c->porder, the shares
+// in counts (host) and the statistics in the status words (mbox[2..3]; read
+// back here when sync, else with the commit's status).
 static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int tile_px, int64_t *counts,
-                          hipStream_t s = nullptr, bool sync = true)
+                          hipStream_t s, bool sync)
 {
     const int64_t n = gen->items;
     for (int r = 0; r < world; ++r)
@@ -1322,29 +1367,28 @@ static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int ti
         return DP_OK;
     if (n > INT32_MAX)
         return fail(c, DP_E_OOM, "partition: generation too large");
-    if (!s)
-        s = c->stream;
+    // s is used as given: NULL is the legacy default stream (the async entry
+    // point's caller stream), never replaced by the context's stream
     const dp_patch *items = gen->index == 0 ? c->seedp.p : c->store.p + gen->head;
     DP_HIP(c, c->tkeys.reserve((size_t)n));
     DP_HIP(c, c->okeys.reserve((size_t)n));
     DP_HIP(c, c->oiota.reserve((size_t)n));
     DP_HIP(c, c->porder.reserve((size_t)n));
-    DP_HIP(c, c->ocount.reserve(2));
-    DP_HIP(c, dpk::launch_tile_keys(c->d_views, items, n, (double)tile_px, c->tkeys.p, c->oiota.p, c->ocount.p, s));
+    unsigned long long *stats = c->mbox.p + 2;
+    DP_HIP(c, dpk::launch_tile_keys(c->d_views, items, n, (double)tile_px, c->tkeys.p, c->oiota.p, stats, s));
     size_t tmp = 0;
     DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, c->tkeys.p, c->okeys.p, c->oiota.p, c->porder.p, (int)n,
                                                  0, 64, s));
     DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
     DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->scan_tmp.p, tmp, c->tkeys.p, c->okeys.p, c->oiota.p, c->porder.p,
                                                  (int)n, 0, 64, s));
-    DP_HIP(c, dpk::launch_partition_stats(c->okeys.p, n, world, c->ocount.p, s));
+    DP_HIP(c, dpk::launch_partition_stats(c->okeys.p, n, world, stats, s));
     if (!sync) {
-        // the statistics come back with the commit's status read
         c->part_pending = true;
         return DP_OK;
     }
     unsigned long long st[2] = {0, 0};
-    DP_HIP(c, hipMemcpyAsync(st, c->ocount.p, sizeof(st), hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipMemcpyAsync(st, stats, sizeof(st), hipMemcpyDeviceToHost, s));
     // the order is read on the caller's stream (refine, compaction): complete it
     DP_HIP(c, hipStreamSynchronize(s));
     c->part_stats[2] = (int64_t)st[0];
@@ -1364,7 +1408,7 @@ extern "C" int dp_densify_owners(dp_ctx *c, const dp_generation *gen, int world,
         *fallback_out = 0;
     hipSetDevice(c->device);
     std::vector<int64_t> counts((size_t)world);
-    int rc = partition_impl(c, gen, world, tile_px, counts.data());
+    int rc = partition_impl(c, gen, world, tile_px, counts.data(), c->stream, true);
     if (rc != DP_OK || n == 0)
         return rc;
     std::vector<int64_t> order((size_t)n);
@@ -1385,6 +1429,9 @@ extern "C" int dp_densify_partition_stats(dp_ctx *c, int64_t *stats_out)
     return DP_OK;
 }
 
+// refine of the items d_items[0..n) of the generation into work / okp on s
+// (seed patches by index in generation 0; Expand::ExpandPatch of the queue
+// entries head + items[k] otherwise)
 static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const int64_t *d_items, int64_t n,
                                      dp_patch *work, uint8_t *okp, hipStream_t s)
 {
@@ -1394,7 +1441,7 @@ static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const 
     const int32_t nc = (int32_t)nc64;
     dpk::RefineArgs a{};
     const bool fast = c->fopt.densify != 0;
-    int rc = take_refine_ms(c, &c->g_st.refine_ms);
+    int rc = take_refine_ms(c, &c->g_st.refine_ms); // an earlier refine's events, before they are re-recorded
     if (rc != DP_OK)
         return rc;
     if (gen->index == 0) {
@@ -1416,21 +1463,16 @@ static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const 
     return DP_OK;
 }
 
-static int check_items(dp_ctx *c, const dp_generation *gen, int64_t n)
-{
-    if (!c || !gen || n < 0 || n > gen->items)
-        return fail(c, DP_E_ARG, "dp_densify_refine_items: bad item count");
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_refine_items: generation out of sequence");
-    return DP_OK;
-}
-
 extern "C" int dp_densify_refine_items(dp_ctx *c, const dp_generation *gen, const int64_t *items, int64_t n,
                                        dp_patch *cand_out, uint8_t *accept_out)
 {
-    int rc = check_items(c, gen, n);
-    if (rc != DP_OK || n == 0)
+    int rc = check_gen(c, gen, "dp_densify_refine_items");
+    if (rc != DP_OK)
         return rc;
+    if (n < 0 || n > gen->items)
+        return fail(c, DP_E_ARG, "dp_densify_refine_items: bad item count");
+    if (n == 0)
+        return DP_OK;
     if (!items || !cand_out || !accept_out)
         return fail(c, DP_E_ARG, "dp_densify_refine_items: null arrays");
     for (int64_t i = 0; i < n; ++i)
@@ -1440,143 +1482,22 @@ extern "C" int dp_densify_refine_items(dp_ctx *c, const dp_generation *gen, cons
     hipStream_t s = c->stream;
     const size_t nc = (size_t)n * gen->per_item;
     DP_HIP(c, c->items.reserve((size_t)n));
-    DP_HIP(c, c->cand.reserve(nc));
-    DP_HIP(c, c->ok.reserve(nc));
+    DP_HIP(c, c->wcand.reserve(nc));
+    DP_HIP(c, c->wok.reserve(nc));
     DP_HIP(c, hipMemcpyAsync(c->items.p, items, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
-    rc = densify_refine_items_impl(c, gen, c->items.p, n, c->cand.p, c->ok.p, s);
+    rc = densify_refine_items_impl(c, gen, c->items.p, n, c->wcand.p, c->wok.p, s);
     if (rc != DP_OK)
         return rc;
-    DP_HIP(c, hipMemcpyAsync(cand_out, c->cand.p, sizeof(dp_patch) * nc, hipMemcpyDeviceToHost, s));
-    DP_HIP(c, hipMemcpyAsync(accept_out, c->ok.p, nc, hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipMemcpyAsync(cand_out, c->wcand.p, sizeof(dp_patch) * nc, hipMemcpyDeviceToHost, s));
+    DP_HIP(c, hipMemcpyAsync(accept_out, c->wok.p, nc, hipMemcpyDeviceToHost, s));
     DP_HIP(c, hipStreamSynchronize(s));
     return DP_OK;
 }
 
-extern "C" int dp_densify_refine_items_device(dp_ctx *c, const dp_generation *gen, const int64_t *d_items, int64_t n,
-                                              dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream)
-{
-    int rc = check_items(c, gen, n);
-    if (rc != DP_OK || n == 0)
-        return rc;
-    if (!d_items || !d_cand_out || !d_accept_out)
-        return fail(c, DP_E_ARG, "dp_densify_refine_items_device: null arrays");
-    hipSetDevice(c->device);
-    // NULL stream: the inputs (item list) may come from the legacy default stream
-    if (!stream && (rc = join_streams(c, nullptr, c->stream)) != DP_OK)
-        return rc;
-    rc = densify_refine_items_impl(c, gen, d_items, n, d_cand_out, d_accept_out,
-                                   stream ? (hipStream_t)stream : c->stream);
-    if (rc == DP_OK && !stream)
-        rc = join_streams(c, c->stream, nullptr); // see dp_densify_refine_device
-    return rc;
-}
-
-extern "C" int dp_densify_commit_items_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_cand,
-                                              const uint8_t *d_accept, const int64_t *d_items, int64_t n_items,
-                                              void *stream)
-{
-    if (!c || !gen || n_items != gen->items || (n_items > 0 && (!d_cand || !d_accept || !d_items)))
-        return fail(c, DP_E_ARG, "dp_densify_commit_items_device: need every item of the generation");
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_commit_items_device: generation out of sequence");
-    hipSetDevice(c->device);
-    hipStream_t us = (hipStream_t)stream;
-    const size_t nc = (size_t)n_items * gen->per_item;
-    if (nc > 0) {
-        int rc = join_streams(c, us, c->stream);
-        if (rc != DP_OK)
-            return rc;
-        DP_HIP(c, c->cand.reserve(nc));
-        DP_HIP(c, c->ok.reserve(nc));
-        DP_HIP(c, dpk::launch_scatter_items(d_cand, d_accept, d_items, n_items, gen->per_item, c->cand.p, c->ok.p,
-                                            c->stream));
-    }
-    return densify_commit_impl(c, gen, c->cand.p, c->ok.p, (int64_t)nc, true, c->stream);
-}
-
-
-extern "C" int dp_densify_partition_device(dp_ctx *c, const dp_generation *gen, int world, int tile_px,
-                                           const int64_t **d_order_out, int64_t *counts_out, int32_t *fallback_out)
-{
-    if (!c || !gen || world < 1 || world > 64 || tile_px < 1 || !d_order_out || !counts_out)
-        return fail(c, DP_E_ARG, "dp_densify_partition_device: bad arguments (1 <= world <= 64)");
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_partition_device: generation out of sequence");
-    *d_order_out = nullptr;
-    if (fallback_out)
-        *fallback_out = 0;
-    hipSetDevice(c->device);
-    const int rc = partition_impl(c, gen, world, tile_px, counts_out);
-    if (rc != DP_OK)
-        return rc;
-    if (gen->items > 0)
-        *d_order_out = c->porder.p;
-    return DP_OK;
-}
-
-extern "C" int dp_densify_compact_accepted_device(dp_ctx *c, const dp_generation *gen, const int64_t *d_items,
-                                                  int64_t n, const dp_patch *d_cand, const uint8_t *d_accept,
-                                                  dp_patch *d_out, int64_t *n_out, void *stream)
-{
-    if (!c || !gen || n < 0 || !n_out || (n > 0 && (!d_items || !d_cand || !d_accept || !d_out)))
-        return fail(c, DP_E_ARG, "dp_densify_compact_accepted_device: bad arguments");
-    *n_out = 0;
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_compact_accepted_device: generation out of sequence");
-    const int64_t m = n * gen->per_item;
-    if (m == 0)
-        return DP_OK;
-    if (m > INT32_MAX)
-        return fail(c, DP_E_OOM, "dp_densify_compact_accepted_device: too many candidates");
-    hipSetDevice(c->device);
-    hipStream_t us = stream ? (hipStream_t)stream : c->stream;
-    DP_HIP(c, c->prefix.reserve((size_t)m + 1));
-    DP_HIP(c, c->acc.reserve((size_t)m + 1));
-    // flags with a zeroed tail: prefix[m] = the count
-    DP_HIP(c, hipMemcpyAsync(c->acc.p, d_accept, (size_t)m, hipMemcpyDeviceToDevice, us));
-    DP_HIP(c, hipMemsetAsync(c->acc.p + m, 0, 1, us));
-    hipcub::TransformInputIterator<uint32_t, U8ToU32, const uint8_t *> it(c->acc.p, U8ToU32());
-    size_t tmp = 0;
-    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, c->prefix.p, (int)m + 1, us));
-    DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
-    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, it, c->prefix.p, (int)m + 1, us));
-    DP_HIP(c, dpk::launch_compact_accepted(d_cand, c->acc.p, c->prefix.p, d_items, n, gen->per_item, d_out, nullptr,
-                                           us));
-    uint32_t total = 0;
-    DP_HIP(c, hipMemcpyAsync(&total, c->prefix.p + m, sizeof(uint32_t), hipMemcpyDeviceToHost, us));
-    DP_HIP(c, hipStreamSynchronize(us));
-    *n_out = total;
-    return DP_OK;
-}
-
-extern "C" int dp_densify_commit_accepted_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_recs,
-                                                 int64_t n_recs, void *stream)
-{
-    if (!c || !gen || n_recs < 0 || (n_recs > 0 && !d_recs))
-        return fail(c, DP_E_ARG, "dp_densify_commit_accepted_device: bad arguments");
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_commit_accepted_device: generation out of sequence");
-    const int64_t nc = gen->items * gen->per_item;
-    if (n_recs > nc)
-        return fail(c, DP_E_ARG, "dp_densify_commit_accepted_device: more records than candidates");
-    hipSetDevice(c->device);
-    hipStream_t us = (hipStream_t)stream;
-    if (nc > 0) {
-        int rc = join_streams(c, us, c->stream);
-        if (rc != DP_OK)
-            return rc;
-        DP_HIP(c, c->cand.reserve((size_t)nc));
-        DP_HIP(c, c->ok.reserve((size_t)nc));
-        // every other candidate of the generation failed the refine's filter
-        DP_HIP(c, hipMemsetAsync(c->ok.p, 0, (size_t)nc, c->stream));
-        DP_HIP(c, dpk::launch_scatter_accepted(d_recs, n_recs, nc, c->cand.p, c->ok.p, c->stream));
-    }
-    return densify_commit_impl(c, gen, c->cand.p, c->ok.p, nc, true, c->stream);
-}
-
-// ---- the one-sync generation step (r05) -------------------------------------
-// partition -> refine -> compact -> [exchange] -> commit, all queued on the
-// caller's stream; the only host wait is the commit's status read.
+// ---- the one-wait device protocol (r05, slots r06) ---------------------------
+// partition -> refine of the rank's share + compaction into its slot ->
+// [all-gather of the slots] -> commit, all queued on the caller's stream; the
+// only host wait is the commit's status read.
 
 extern "C" int dp_densify_partition_async(dp_ctx *c, const dp_generation *gen, int world, int tile_px, void *stream,
                                           const int64_t **d_order_out, int64_t *counts_out)
@@ -1599,57 +1520,53 @@ extern "C" int dp_densify_partition_async(dp_ctx *c, const dp_generation *gen, i
     return DP_OK;
 }
 
-extern "C" int dp_densify_compact_accepted_async(dp_ctx *c, const dp_generation *gen, const int64_t *d_items,
-                                                 int64_t n, const dp_patch *d_cand, const uint8_t *d_accept,
-                                                 dp_patch *d_out, int64_t *d_count, void *stream)
+extern "C" int dp_densify_refine_share_async(dp_ctx *c, const dp_generation *gen, const int64_t *d_items, int64_t n,
+                                             dp_patch *d_slot, int64_t stride, void *stream)
 {
-    if (!c || !gen || n < 0 || !d_count || (n > 0 && (!d_items || !d_cand || !d_accept || !d_out)))
-        return fail(c, DP_E_ARG, "dp_densify_compact_accepted_async: bad arguments");
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_compact_accepted_async: generation out of sequence");
-    const int64_t m = n * gen->per_item;
-    if (m > INT32_MAX)
-        return fail(c, DP_E_OOM, "dp_densify_compact_accepted_async: too many candidates");
+    int rc = check_gen(c, gen, "dp_densify_refine_share_async");
+    if (rc != DP_OK)
+        return rc;
+    if (n < 0 || n > gen->items || !d_slot || stride < n * gen->per_item || (n > 0 && !d_items))
+        return fail(c, DP_E_ARG, "dp_densify_refine_share_async: bad arguments (stride >= n * per_item)");
     hipSetDevice(c->device);
-    hipStream_t us = (hipStream_t)stream; // the caller's stream (NULL: the legacy default stream)
-    if (m == 0) {
-        DP_HIP(c, hipMemsetAsync(d_count, 0, sizeof(int64_t), us));
-        return DP_OK;
+    hipStream_t s = (hipStream_t)stream; // the caller's stream (NULL: the legacy default stream)
+    const size_t nc = (size_t)n * gen->per_item;
+    if (nc > 0) {
+        DP_HIP(c, c->wcand.reserve(nc));
+        DP_HIP(c, c->wok.reserve(nc));
+        rc = densify_refine_items_impl(c, gen, d_items, n, c->wcand.p, c->wok.p, s);
+        if (rc != DP_OK)
+            return rc;
     }
-    DP_HIP(c, c->prefix.reserve((size_t)m + 1));
-    // the flags read in place, index m as 0 (no copy of the flags)
-    hipcub::TransformInputIterator<uint32_t, FlagAt, hipcub::CountingInputIterator<int64_t>> it(
-        hipcub::CountingInputIterator<int64_t>(0), FlagAt{d_accept, m});
-    size_t tmp = 0;
-    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, c->prefix.p, (int)m + 1, us));
-    DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
-    DP_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, it, c->prefix.p, (int)m + 1, us));
-    DP_HIP(c, dpk::launch_compact_accepted(d_cand, d_accept, c->prefix.p, d_items, n, gen->per_item, d_out, d_count,
-                                           us));
+    DP_HIP(c, dpk::launch_compact_slot(c->wcand.p, c->wok.p, d_items, n, gen->per_item, d_slot, s));
     return DP_OK;
 }
 
 extern "C" int dp_densify_commit_gathered_device(dp_ctx *c, dp_generation *gen, const dp_patch *d_recs, int64_t stride,
-                                                 const int64_t *d_counts, int world, void *stream,
-                                                 int64_t *exchanged_out)
+                                                 int world, void *stream, int64_t *exchanged_out)
 {
-    if (!c || !gen || world < 1 || world > 64 || stride < 0 || !d_counts || (stride > 0 && !d_recs))
+    int rc = check_gen(c, gen, "dp_densify_commit_gathered_device");
+    if (rc != DP_OK)
+        return rc;
+    if (world < 1 || world > 64 || stride < 0 || !d_recs)
         return fail(c, DP_E_ARG, "dp_densify_commit_gathered_device: bad arguments");
-    if (gen->index != c->g_expected)
-        return fail(c, DP_E_STATE, "dp_densify_commit_gathered_device: generation out of sequence");
     const int64_t nc = gen->items * gen->per_item;
     if (nc > INT32_MAX)
         return fail(c, DP_E_OOM, "dp_densify_commit_gathered_device: generation too large");
     hipSetDevice(c->device);
     hipStream_t s = (hipStream_t)stream; // the caller's stream (NULL: the legacy default stream)
+    DP_HIP(c, c->cand.reserve((size_t)std::max<int64_t>(nc, 1)));
+    DP_HIP(c, c->ok.reserve((size_t)std::max<int64_t>(nc, 1)));
     if (nc > 0) {
-        DP_HIP(c, c->cand.reserve((size_t)nc));
-        DP_HIP(c, c->ok.reserve((size_t)nc));
         // every other candidate of the generation failed the refine's filter
         DP_HIP(c, hipMemsetAsync(c->ok.p, 0, (size_t)nc, s));
-        DP_HIP(c, dpk::launch_scatter_gathered(d_recs, stride, d_counts, world, nc, c->cand.p, c->ok.p, s));
     }
-    return commit_on_stream(c, gen, c->cand.p, c->ok.p, (int32_t)nc, s, d_counts, world, exchanged_out);
+    DP_HIP(c, dpk::launch_scatter_slots(d_recs, stride, world, nc, c->cand.p, c->ok.p, c->mbox.p + 4, s));
+    int64_t ex = 0;
+    rc = commit_on_stream(c, gen, c->cand.p, c->ok.p, nc, s, &ex);
+    if (rc == DP_OK && exchanged_out)
+        *exchanged_out = ex;
+    return rc;
 }
 
 extern "C" int dp_densify_result(dp_ctx *c, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats)
@@ -1659,24 +1576,7 @@ extern "C" int dp_densify_result(dp_ctx *c, const dp_patch **out, int64_t *n_out
     if (c->g_expected < 0)
         return fail(c, DP_E_STATE, "dp_densify_result: no generation run");
     hipSetDevice(c->device);
-    hipStream_t s = c->stream;
-    const int64_t np = c->g_np;
-    DP_HIP(c, c->result.resize((size_t)np));
-    if (np)
-        DP_HIP(c, hipMemcpyAsync(c->result.data(), c->store.p, sizeof(dp_patch) * np, hipMemcpyDeviceToHost, s));
-    unsigned long long ev = 0;
-    DP_HIP(c, hipMemcpyAsync(&ev, c->d_evals, sizeof(ev), hipMemcpyDeviceToHost, s));
-    DP_HIP(c, hipStreamSynchronize(s));
-    dp_densify_stats st = c->g_st;
-    st.patches = np;
-    st.pops = std::min<int64_t>(np, c->opt.max_pops);
-    st.evals = (int64_t)ev;
-    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->g_t0).count();
-    if (stats)
-        *stats = st;
-    *out = c->result.empty() ? nullptr : c->result.data();
-    *n_out = np;
-    return DP_OK;
+    return result_impl(c, c->stream, out, n_out, stats);
 }
 
 // ---------------------------------------------------------------------------

@@ -125,9 +125,9 @@ struct dp_ctx {
     DevBuf<uint8_t> granted;
     DevBuf<uint32_t> lpt;    // refine dequeue order + its counters
     bool lpt_off = false;    // DP_NO_LPT=1 at dp_ctx_create: index-order dequeue
+    int64_t gen_cap_test = 0; // DP_GEN_CAP at dp_ctx_create: the device BFS's first candidate capacity (tests)
     DevBuf<dp_patch> pat, store, cand;
     DevBuf<uint8_t> ok, acc;
-    DevBuf<uint32_t> prefix;
     DevBuf<unsigned char> scan_tmp;
     // patch filter scratch
     DevBuf<unsigned long long> front;
@@ -144,14 +144,23 @@ struct dp_ctx {
     // (the rank-major order), the cut positions, partition statistics
     DevBuf<uint64_t> tkeys, okeys;
     DevBuf<int64_t> oiota, porder, olo;
-    DevBuf<unsigned long long> ocount;
     int64_t part_stats[4] = {0, 0, 0, 0}; // items, world, tiles, items in split tiles
-    bool part_pending = false;            // a partition's tiles/split counts wait in ocount
-    // one-sync generation step (r05): device status words gathered by one small
-    // kernel and read back with ONE copy per generation -- [0] organizer accepts,
-    // [1] store overflow, [2] tiles, [3] items in split tiles, [4] records
-    // exchanged; [7] the append's overflow flag (cleared when read)
+    bool part_pending = false;            // a partition's tiles/split counts wait in mbox[2..3]
+    // status words read back with the generation's state (one wait per
+    // generation or batch): [0] organizer accepts, [2] tiles, [3] items in
+    // split tiles (the partition), [4] records exchanged (the slot scatter),
+    // [7] the append's overflow flag (cleared when read)
     DevBuf<unsigned long long> mbox;
+    // device-resident BFS (dp_bfs.hip): the GenDev pair, chunk counts, the slot
+    // holding the next generation's state, the LPT counters the organizer
+    // zeroes, the timing events of a batch
+    DevBuf<dpk::GenDev> gstate;
+    DevBuf<uint32_t> bsum;
+    int g_slot = 0;
+    uint32_t *g_lpt_scratch = nullptr;
+    std::vector<hipEvent_t> gev;
+    DevBuf<dp_patch> wcand; // a rank's refined share (partitioned generations)
+    DevBuf<uint8_t> wok;
     hipEvent_t ej = nullptr;   // stream joins (no host wait)
     bool g_time_pending = false; // a densify refine's events (e0, e1) not yet read
     int64_t g_np = 0;        // patches in the replicated store
@@ -175,9 +184,10 @@ struct dp_ctx {
 // memory, or the 4 (n / 4) expansion children of parents
 // d_parents[parent0 + (items ? items[k] : k)], k < n / 4, of which only those
 // with a parent index below max_pops expand (dp_densify's pop cap)
+// gen: a device-resident BFS generation (n and parent0 read on the device)
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
                    hipStream_t s, int64_t parent0 = 0, const int64_t *items = nullptr,
-                   int64_t max_pops = INT64_MAX);
+                   int64_t max_pops = INT64_MAX, const dpk::GenDev *gen = nullptr);
 
 static inline int fail(dp_ctx *c, int code, const std::string &msg)
 {

@@ -74,6 +74,8 @@ struct FastArgs {
     unsigned long long *stats; // dp_fast_stats: patches, evals, view_evals, staged_bytes
     uint32_t chunk;          // candidates per dequeue: 4 (siblings share one parent read), or 1
                              // when the launch has fewer than 4 candidates per resident wave
+    uint32_t resident;       // resident waves of the launch (the kGen instances pick chunk on the device)
+    const GenDev *gen;       // device-resident BFS generation: n and parent0 read here (kGen)
 };
 
 // per evaluation, per staged view: A.xyz 2^23+umax | B1.xyz 2^23+vmax | B2.xyz
@@ -1415,9 +1417,12 @@ template <int kArena> struct FastOcc {
 // register allocation
 constexpr int kFastRefineGrad = 100;
 
-template <int G, int NS, bool kTail, bool kMask, int kArena, int kMode>
+template <int G, int NS, bool kTail, bool kMask, int kArena, int kMode, bool kGen = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kArena>::value))) void fast_kernel(FastArgs a)
 {
+    // kGen: a generation of the device-resident BFS (dp_bfs.hip), sized here
+    const int n = kGen ? (int)a.gen->ncand : a.n;
+    const int64_t parent0 = kGen ? a.gen->head : a.parent0;
     __shared__ FastLds<kArena> L;
     const int lane = lane_id();
     const Slots sl = make_slots<G, NS, kMask>(L, a.cell);
@@ -1429,7 +1434,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
     // candidates per resident wave (the BFS's tail generations) dequeues them
     // one at a time (cs = 1), so siblings run on different waves instead of one
     // after another on one: its latency is one candidate's, not four.
-    const uint32_t cs = a.chunk == 1u ? 1u : 4u;
+    const uint32_t cs = kGen ? ((int64_t)n < 4 * (int64_t)a.resident ? 1u : 4u) : (a.chunk == 1u ? 1u : 4u);
+    // the full-chip grid of a device-sized launch keeps the workgroups a
+    // host-sized one would have (min(chunks, resident)): a small generation's
+    // waves spread over the CUs instead of crowding the first ones to dequeue
+    if (kGen && (int64_t)blockIdx.x * cs >= (int64_t)n)
+        return;
     uint32_t chunk_idx = 0xffffffffu, q4 = cs;
     bool par_live = true;
 #ifdef DP_FAST_TIMING
@@ -1445,11 +1455,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
                 c = atomicAdd(a.work, 1u);
             chunk_idx = (uint32_t)uni((int)c);
             q4 = 0;
-            if ((uint64_t)chunk_idx * cs >= (uint64_t)a.n)
+            if ((uint64_t)chunk_idx * cs >= (uint64_t)n)
                 break;
             if (a.parents) {
                 const uint32_t pk = cs == 4u ? chunk_idx : chunk_idx >> 2; // the parent's item
-                const int64_t q = a.parent0 + (a.items ? a.items[pk] : (int64_t)pk);
+                const int64_t q = parent0 + (a.items ? a.items[pk] : (int64_t)pk);
                 par_live = q < a.max_pops;
                 const uint32_t *src = (const uint32_t *)(a.parents + q);
                 if (lane < (int)(sizeof(dp_patch) / 4))
@@ -1464,7 +1474,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
         }
         TMARK(L, 0);
         const uint32_t idx = chunk_idx * cs + q4++;
-        if (idx >= (uint32_t)a.n) {
+        if (idx >= (uint32_t)n) {
             q4 = cs;
             continue;
         }
@@ -1731,8 +1741,17 @@ static hipError_t launch_fast_m(const FastArgs &a, hipStream_t s)
     const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1); // resident waves (1-wave workgroups)
     FastArgs b = a;
     b.chunk = (int64_t)a.n < 4 * cap ? 1u : 4u;
+    b.resident = (uint32_t)cap;
     const int64_t want = ((int64_t)a.n + b.chunk - 1) / b.chunk;
-    const int grid = (int)(want < cap ? want : cap);
+    const int grid = a.gen ? (int)cap : (int)(want < cap ? want : cap);
+    if (a.gen) {
+        // device-resident BFS generation: the forward-difference refine only
+        if (a.mode != DP_MODE_FAST_REFINE || a.fo.gradient || !a.parents)
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_REFINE, true>), dim3(grid), dim3(64),
+                           0, s, b);
+        return hipGetLastError();
+    }
     if (a.mode == DP_MODE_FAST_EVAL)
         hipLaunchKernelGGL((fast_kernel<G, NS, kTail, kMask, kBudget, DP_MODE_FAST_EVAL>), dim3(grid), dim3(64), 0, s, b);
     else if (a.fo.gradient)
@@ -1895,7 +1914,7 @@ template <int B> static hipError_t fast_dispatch(int N, const dpk::FastArgs &a, 
 }
 
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
-                   hipStream_t s, int64_t parent0, const int64_t *items, int64_t max_pops)
+                   hipStream_t s, int64_t parent0, const int64_t *items, int64_t max_pops, const dpk::GenDev *gen)
 {
     int rc = ensure_gray(c);
     if (rc != DP_OK)
@@ -1918,6 +1937,7 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.parent0 = parent0;
     a.items = items;
     a.max_pops = max_pops;
+    a.gen = gen;
     // the InitRelatedImages thresholds as cosines, by the host libm (the
     // spec's), rounded to fp32, and their fp32 squares
     a.cvis = (float)std::cos(c->opt.visible_angle);

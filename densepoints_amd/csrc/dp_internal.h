@@ -15,6 +15,8 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kWorkStride = 16;
 constexpr int kWorkCounters = 8 * kWorkStride;
 
+struct GenDev;
+
 // Arguments of the fused refine kernel (one wavefront per patch).
 struct RefineArgs {
     const dpg::ViewDev *views;
@@ -45,24 +47,76 @@ struct RefineArgs {
     // optional item list of a partitioned generation: child c
     // expands queue entry parent0 + items[c / 4] instead of parent0 + c / 4
     const int64_t *items;
+    // device-resident BFS generation (dp_bfs.hip): n = gen->ncand and parent0 =
+    // gen->head are read on the device (the refine_kernel<.., kGen = true>
+    // instances), so a generation is queued before its size is known
+    const GenDev *gen;
 };
 constexpr int kLptBuckets = 129; // visible-view counts 0..128
 
-// organizer / BFS kernels
-struct ClaimArgs {
-    const dpg::ViewDev *views;
-    const dp_patch *cand;    // candidates of this generation, in seq order
-    const uint8_t *ok;       // filter passed
-    int32_t n;
-    uint32_t seq0;           // seq of cand[0]; seq grows by one per candidate
-    uint32_t *grid;          // cell owner = min seq (capacity 1) / claims made (capacity k > 1)
-    double grid_scale;
-    // capacity k > 1 (PatchGrid::TryInsert's size() < max_patches_per_cell)
-    uint32_t *cellmin;       // per cell, the round's smallest pending seq (UINT32_MAX between rounds)
-    uint64_t *pend;          // per candidate, its visible views whose claim is undecided (2 words)
-    uint8_t *granted;        // per candidate, claims granted so far
-    int32_t k;
+// The device-resident BFS state of one generation (dp_bfs.hip).  Generation g
+// reads state[g & 1] and its organizer writes generation g + 1's into
+// state[(g + 1) & 1], so the host queues K generations behind one wait; every
+// kernel of a generation sizes itself from here (ncand = 0: nothing runs).
+struct GenDev {
+    int64_t np;         // patches in the store before this generation's append
+    int64_t head;       // queue index of the first parent (0 for the seed generation)
+    int64_t items;      // parents (or seed patches) of this generation; 0 = finished
+    int64_t ncand;      // candidates refined/organized: items * per_item, 0 when stalled
+    int64_t cand_total; // running statistic: 4 x the expandable parents so far
+    int64_t gens;       // expansion generations organized so far
+    int64_t accepted;   // the previous generation's organizer accepts
+    int64_t nseeds;     // seed points of the densify (sequence base of generation 1)
+    int64_t seed_patches; // the seed generation's accepts (statistic)
+    uint32_t seq0;      // sequence number of candidate 0
+    int32_t per_item;   // 1 (seed generation) or 4 (expansion)
+    int32_t stall;      // 1: ncand exceeded the candidate buffers; the host regrows them
+    int32_t err;        // 1: the 32-bit sequence space is exhausted
 };
+static_assert(sizeof(GenDev) % 8 == 0, "GenDev is copied as 64-bit words");
+
+// organizer of one generation on the device (dp_bfs.hip)
+struct BfsArgs {
+    const dpg::ViewDev *views;
+    int32_t V;
+    int32_t k;                 // max_patches_per_cell (1: claims/resolve; > 1: k rounds)
+    const GenDev *cur;
+    GenDev *nxt;
+    const dp_patch *cand;      // the generation's candidates in sequence order
+    const uint8_t *ok;         // the refine's filter flags
+    uint8_t *acc;              // organizer accepts
+    uint32_t *bsum;            // kBfsBlocks per-chunk accept counts -> offsets
+    uint32_t *grid;
+    double grid_scale;
+    uint32_t *cellmin;         // k > 1 scratch (ClaimArgs)
+    uint64_t *pend;
+    uint8_t *granted;
+    dp_patch *store;
+    int64_t store_cap;
+    int64_t cand_cap;          // candidate buffer capacity (stall above it)
+    int64_t max_pops;
+    unsigned long long *mbox;  // status words (see dp_ctx::mbox); [7] append overflow
+    uint32_t *work;            // the refine's dequeue counters, zeroed for the next generation
+    uint32_t *lpt_scratch;     // the LPT order's counters, zeroed for the next generation
+};
+constexpr int kBfsBlocks = 1024; // chunks of the generation's scan (one block each)
+
+// device-resident organizer (dp_bfs.hip): claims, resolve + chunk counts, the
+// chunk scan that also writes the next generation's state, and the append
+// (ComputeColor) in sequence order -- four launches, every size read from
+// a.cur, no host wait
+hipError_t launch_bfs_organize(const BfsArgs &a, hipStream_t s);
+// *dst = v on stream s (a state written by the host without a staging copy)
+hipError_t launch_bfs_set_state(GenDev *dst, const GenDev &v, hipStream_t s);
+// per-rank accepted records of one refined share, compacted (any order) into
+// a rank slot: slot[0].seq..: count header (int64 in the first 8 B of record
+// 0), records from slot + 1, each with seq = its generation position
+hipError_t launch_compact_slot(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n, int per,
+                               dp_patch *slot, hipStream_t s);
+// the gathered rank slots (world of them, stride records + header each) to
+// their generation positions; ok must be zeroed first
+hipError_t launch_scatter_slots(const dp_patch *recs, int64_t stride, int world, int64_t nc, dp_patch *cand,
+                                uint8_t *ok, unsigned long long *exchanged, hipStream_t s);
 
 // one image plane of a pyramid level (BGRA8, B in the low byte)
 struct PyrPlane {
@@ -90,23 +144,11 @@ hipError_t launch_filter_visibility(const FilterArgs &a, uint8_t *keep, hipStrea
 hipError_t launch_filter_neighbors(const FilterArgs &a, uint8_t *keep, hipStream_t s);
 
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s);
-// the organizer step with cell capacity a.k > 1 (k rounds of claims in
-// sequence order); accepted[i] = more than one claim granted
-hipError_t launch_claims_k(const ClaimArgs &a, uint8_t *accepted, hipStream_t s);
 hipError_t launch_pyr_down(const PyrPlane *d_src, const PyrPlane *d_dst, int V, int max_dw, int max_dh,
                            hipStream_t s);
 int read_stamps(unsigned long long *out);
 hipError_t launch_probe_texel(const unsigned long long *ta, const unsigned long long *tb, const uint32_t *fxy, int n,
                               int32_t *gray);
-hipError_t launch_claims(const ClaimArgs &a, hipStream_t s);
-hipError_t launch_resolve(const ClaimArgs &a, uint8_t *accepted, hipStream_t s);
-hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand, const uint8_t *accepted,
-                         const uint32_t *prefix, int32_t n, dp_patch *store, int64_t base,
-                         int64_t parent0, int is_seed, int64_t cap, unsigned long long *overflow, hipStream_t s);
-hipError_t launch_status(const uint32_t *prefix_end, const unsigned long long *ocount, const int64_t *counts,
-                         int world, unsigned long long *mbox, hipStream_t s);
-hipError_t launch_scatter_gathered(const dp_patch *recs, int64_t stride, const int64_t *counts, int world, int64_t nc,
-                                   dp_patch *cand, uint8_t *ok, hipStream_t s);
 hipError_t launch_render(const dp_synth_config &cfg, const double *P, uint32_t *out, int v,
                          hipStream_t s);
 // Seed::CreatePatchesFromPoints: seed patches of n points (xyz device, 3n f64)
@@ -119,16 +161,4 @@ hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, in
                             uint64_t *key, int64_t *iota, unsigned long long *stats, hipStream_t s);
 hipError_t launch_partition_stats(const uint64_t *key, int64_t n, int world, unsigned long long *stats, hipStream_t s);
 hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s);
-hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s);
-// accepted candidates of items[0..n) (per_item each), out[prefix[j]] = cand[j]
-// with seq = items[j / per] * per + j % per (the generation position)
-hipError_t launch_compact_accepted(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
-                                   const int64_t *items, int64_t n, int per, dp_patch *out, int64_t *count,
-                                   hipStream_t s);
-// cand[r.seq] = r, ok[r.seq] = 1 for each gathered accepted record r (seq < nc)
-hipError_t launch_scatter_accepted(const dp_patch *recs, int64_t n, int64_t nc, dp_patch *cand, uint8_t *ok,
-                                   hipStream_t s);
-hipError_t launch_scatter_items(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n, int per,
-                                dp_patch *cand_out, uint8_t *acc_out, hipStream_t s);
-
 } // namespace dpk

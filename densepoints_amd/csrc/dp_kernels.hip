@@ -1353,9 +1353,18 @@ __device__ __forceinline__ uint32_t range_lo(int n, int x)
     return (uint32_t)(((uint64_t)n * (uint64_t)x) / (uint64_t)kXcds);
 }
 
-template <int kMode, int G>
+template <int kMode, int G, bool kGen = false>
 __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
 {
+    // kGen: a generation of the device-resident BFS (dp_bfs.hip) -- its size and
+    // first parent are read here, not passed (the launch was queued before the
+    // previous generation's organizer had run)
+    const int n = kGen ? (int)a.gen->ncand : a.n;
+    const int64_t parent0 = kGen ? a.gen->head : a.parent0;
+    // the full-chip grid of a device-sized launch keeps the blocks a
+    // host-sized one would have (launch_refine: ceil(n / 4), capped)
+    if (kGen && (int64_t)blockIdx.x * kWavesPerBlock >= (int64_t)n)
+        return;
     __shared__ WaveLds lds[kWavesPerBlock];
     WaveLds &L = lds[uni((int)(threadIdx.x / kWave))];
     const int lane = lane_id();
@@ -1372,7 +1381,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
     int cur = (int)(xcc_id() & (kXcds - 1));
     int left = kXcds;
     const uint32_t gs = a.parents ? 4u : 1u;                     // LPT group size
-    const int npos = a.order ? (int)(((uint32_t)a.n + gs - 1) / gs * gs) : a.n; // dequeue positions
+    const int npos = a.order ? (int)(((uint32_t)n + gs - 1) / gs * gs) : n; // dequeue positions
     // positions per dequeue: DP_SIBLING_DEQUEUE = 4 takes a parent's 4 children
     // at once (one wave refines them back to back: their windows overlap)
     const uint32_t step = (a.order && gs == 4u) ? (uint32_t)DP_SIBLING_DEQUEUE : 1u;
@@ -1380,12 +1389,16 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
     for (;;) {
         uint32_t idx = (uint32_t)npos;
         if (run_left == 0) {
+            uint32_t cnt = 0;
             if (lane == 0) {
                 while (left > 0) {
                     const uint32_t lo = range_lo(npos, cur), hi = range_lo(npos, cur + 1);
                     const uint32_t t = lo + atomicAdd(a.work + kWorkStride * cur, step);
                     if (t < hi) {
                         idx = t;
+                        // a run never crosses into the next XCD range (whose own
+                        // waves dequeue those positions)
+                        cnt = hi - t < step ? hi - t : step;
                         break;
                     }
                     cur = (cur + 1) & (kXcds - 1);
@@ -1396,7 +1409,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
             if (idx >= (uint32_t)npos)
                 break;
             run_pos = idx;
-            run_left = step;
+            run_left = (uint32_t)uni((int)cnt);
         }
         idx = run_pos++;
         --run_left;
@@ -1404,7 +1417,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
             continue;
         if (a.order) {
             idx = (uint32_t)uni((int)(a.order[idx / gs] * gs + idx % gs));
-            if (idx >= (uint32_t)a.n) // the last group's missing children
+            if (idx >= (uint32_t)n) // the last group's missing children
                 continue;
         }
         dp_patch *out = a.patches + idx;
@@ -1418,7 +1431,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
             float cpos[3] = {0.f, 0.f, 0.f};
             int64_t qi = 0;
             if (a.parents) {
-                qi = a.parent0 + (a.items ? a.items[idx >> 2] : (int64_t)(idx >> 2));
+                qi = parent0 + (a.items ? a.items[idx >> 2] : (int64_t)(idx >> 2));
                 src = a.parents + qi;
                 const int pm = __popcll(src->vis[0]) + __popcll(src->vis[1]);
                 live = qi < a.max_pops && pm >= a.opt.min_expand_visible && src->ref < (uint32_t)a.V;
@@ -1535,223 +1548,7 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
 #endif
 }
 
-// ---- organizer --------------------------------------------------------------
-
-__device__ __forceinline__ bool cell_of(const dpg::ViewDev &v, const float *pos, double gs, int64_t &cell)
-{
-    double u, w;
-    dpg::project(v.P, pos[0], pos[1], pos[2], u, w);
-    const int64_t row = dpg::grid_coord(w, gs), col = dpg::grid_coord(u, gs);
-    if (col < 0 || col >= v.gw || row < 0 || row >= v.gh)
-        return false;
-    cell = v.grid_off + row * (int64_t)v.gw + col;
-    return true;
-}
-
-// PatchOrganizer::TryInsert claims (patch_organizer.cpp:47-55): every visible
-// view's cell is claimed unconditionally; the first attempt in sequence order
-// owns it for good (rejected patches keep their claims).
-__global__ void claim_kernel(ClaimArgs a)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n || !a.ok[i])
-        return;
-    const dp_patch &p = a.cand[i];
-    const uint32_t seq = a.seq0 + (uint32_t)i;
-    for (int w = 0; w < 2; ++w) {
-        uint64_t bits = p.vis[w];
-        while (bits) {
-            const int b = __builtin_ctzll(bits);
-            bits &= bits - 1;
-            int64_t cell;
-            if (cell_of(a.views[w * 64 + b], p.pos, a.grid_scale, cell))
-                atomicMin(&a.grid[cell], seq);
-        }
-    }
-}
-
-// accept iff more than one cell was claimed (patch_organizer.cpp:58)
-__global__ void resolve_kernel(ClaimArgs a, uint8_t *accepted)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n)
-        return;
-    int claims = 0;
-    if (a.ok[i]) {
-        const dp_patch &p = a.cand[i];
-        const uint32_t seq = a.seq0 + (uint32_t)i;
-        for (int w = 0; w < 2; ++w) {
-            uint64_t bits = p.vis[w];
-            while (bits) {
-                const int b = __builtin_ctzll(bits);
-                bits &= bits - 1;
-                int64_t cell;
-                if (cell_of(a.views[w * 64 + b], p.pos, a.grid_scale, cell) && a.grid[cell] == seq)
-                    ++claims;
-            }
-        }
-    }
-    accepted[i] = claims > 1 ? 1 : 0;
-}
-
-// ---- organizer with cell capacity k > 1 --------------------------------------
-// PatchGrid::TryInsert (patch_organizer.cpp:15-30) admits a claim while the
-// cell holds fewer than max_patches_per_cell patches, and claims persist
-// (rejected patches keep theirs), so a cell's claims are its first k attempts
-// in sequence order.  Every earlier generation's attempt has a lower seq than
-// this generation's, so grid[cell] (claims so far) plus k rounds over this
-// generation -- each round every cell with room grants its smallest pending
-// seq -- reproduces the sequential order exactly.
-
-__global__ void claimk_init_kernel(ClaimArgs a)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n)
-        return;
-    uint64_t pend[2] = {0, 0};
-    if (a.ok[i]) {
-        const dp_patch &p = a.cand[i];
-        for (int w = 0; w < 2; ++w) {
-            uint64_t bits = p.vis[w];
-            while (bits) {
-                const int b = __builtin_ctzll(bits);
-                bits &= bits - 1;
-                int64_t cell;
-                if (cell_of(a.views[w * 64 + b], p.pos, a.grid_scale, cell))
-                    pend[w] |= 1ull << b;
-            }
-        }
-    }
-    a.pend[2 * i] = pend[0];
-    a.pend[2 * i + 1] = pend[1];
-    a.granted[i] = 0;
-}
-
-__global__ void claimk_round_kernel(ClaimArgs a)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n)
-        return;
-    const dp_patch &p = a.cand[i];
-    const uint32_t seq = a.seq0 + (uint32_t)i;
-    for (int w = 0; w < 2; ++w) {
-        uint64_t bits = a.pend[2 * i + w];
-        while (bits) {
-            const int b = __builtin_ctzll(bits);
-            bits &= bits - 1;
-            int64_t cell;
-            if (cell_of(a.views[w * 64 + b], p.pos, a.grid_scale, cell) && a.grid[cell] < (uint32_t)a.k)
-                atomicMin(&a.cellmin[cell], seq);
-        }
-    }
-}
-
-__global__ void claimk_grant_kernel(ClaimArgs a)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n)
-        return;
-    const dp_patch &p = a.cand[i];
-    const uint32_t seq = a.seq0 + (uint32_t)i;
-    int granted = a.granted[i];
-    for (int w = 0; w < 2; ++w) {
-        uint64_t bits = a.pend[2 * i + w], left = bits;
-        while (bits) {
-            const int b = __builtin_ctzll(bits);
-            bits &= bits - 1;
-            int64_t cell;
-            cell_of(a.views[w * 64 + b], p.pos, a.grid_scale, cell);
-            if (a.cellmin[cell] == seq) {
-                // the round's winner: one per cell, so plain updates
-                a.grid[cell] += 1u;
-                a.cellmin[cell] = 0xffffffffu;
-                ++granted;
-                left &= ~(1ull << b);
-            } else if (a.grid[cell] >= (uint32_t)a.k) {
-                left &= ~(1ull << b); // full: denied for good
-            }
-        }
-        a.pend[2 * i + w] = left;
-    }
-    a.granted[i] = (uint8_t)(granted < 255 ? granted : 255);
-}
-
-__global__ void claimk_resolve_kernel(ClaimArgs a, uint8_t *accepted)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < a.n)
-        accepted[i] = a.granted[i] > 1 ? 1 : 0;
-}
-
-// append accepted candidates in sequence order + Patch::ComputeColor
-// (patch.cpp:51-73)
-// The organizer's append (PatchOrganizer::TryInsert's push_back + ComputeColor), one
-// WAVE per candidate (4 per block): lane v projects
-// the centre into views v and v + 64 (Patch::ComputeColor, patch.cpp:51-73),
-// the BGR sums are exact integers in any order, so the wave reduction gives
-// the reference's fp64 sums; lanes 0..19 copy the 80-byte record
-__global__ __launch_bounds__(256) void append_wave_kernel(const dpg::ViewDev *views, int V, const dp_patch *cand,
-                                                          const uint8_t *accepted, const uint32_t *prefix, int32_t n,
-                                                          dp_patch *store, int64_t base, int64_t parent0, int is_seed,
-                                                          int64_t cap, unsigned long long *overflow)
-{
-    const int i = (int)(blockIdx.x * 4u + (threadIdx.x >> 6));
-    const int lane = (int)(threadIdx.x & 63u);
-    if (i >= n || !accepted[i])
-        return;
-    const int64_t pos = base + (int64_t)prefix[i];
-    if (pos >= cap) {
-        // cannot happen with a correct organizer (store_capacity bounds the
-        // accepts); reported at the generation's status read, nothing written
-        if (lane == 0)
-            overflow[0] = 1ull;
-        return;
-    }
-    const float p0 = cand[i].pos[0], p1 = cand[i].pos[1], p2 = cand[i].pos[2];
-    uint32_t s0 = 0, s1 = 0, s2 = 0, cnt = 0;
-    for (int v = lane; v < V; v += 64) {
-        const dpg::ViewDev &vw = views[v];
-        double u, w;
-        dpg::project(vw.P, p0, p1, p2, u, w);
-        if (dpg::inside(u, w, vw.W, vw.H)) {
-            const uint32_t px = vw.img[(size_t)(int)w * (size_t)vw.pitch + (size_t)(int)u];
-            s0 += px & 255u;
-            s1 += (px >> 8) & 255u;
-            s2 += (px >> 16) & 255u;
-            ++cnt;
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        s0 += __shfl_xor(s0, o);
-        s1 += __shfl_xor(s1, o);
-        s2 += __shfl_xor(s2, o);
-        cnt += __shfl_xor(cnt, o);
-    }
-    uint8_t c0 = 0, c1 = 0, c2 = 0;
-    if (cnt) {
-        c0 = (uint8_t)((double)s2 / (double)cnt);
-        c1 = (uint8_t)((double)s1 / (double)cnt);
-        c2 = (uint8_t)((double)s0 / (double)cnt);
-    }
-    // the record, one 32-bit word per lane, with seq, parent, rgb and the
-    // accepted flag patched into their words (one store per word)
-    constexpr int kWords = (int)(sizeof(dp_patch) / 4);
-    constexpr int kSeq = (int)(offsetof(dp_patch, seq) / 4), kPar = (int)(offsetof(dp_patch, parent) / 4);
-    constexpr int kRgb = (int)(offsetof(dp_patch, rgb) / 4);
-    static_assert(sizeof(dp_patch) % 4 == 0 && kWords <= 64, "record copy by lanes");
-    static_assert(offsetof(dp_patch, rgb) % 4 == 0 && offsetof(dp_patch, flags) == offsetof(dp_patch, rgb) + 3,
-                  "rgb[3] and flags share one word");
-    if (lane < kWords) {
-        uint32_t w = ((const uint32_t *)(cand + i))[lane];
-        if (lane == kSeq)
-            w = (uint32_t)pos;
-        else if (lane == kPar)
-            w = is_seed ? 0xFFFFFFFFu : (uint32_t)(parent0 + (i >> 2));
-        else if (lane == kRgb)
-            w = (uint32_t)c0 | (uint32_t)c1 << 8 | (uint32_t)c2 << 16 | ((w >> 24) | DP_PATCH_ACCEPTED) << 24;
-        ((uint32_t *)(store + pos))[lane] = w;
-    }
-}
+// (the organizer kernels -- claims, resolve, scan, append -- are in dp_bfs.hip)
 
 // probe: the texel loop's bilinear + BGR2GRAY on explicit taps (fxy = fx |
 // fy << 5, fx already 0 where the right tap replicates)
@@ -1864,24 +1661,31 @@ int read_stamps(unsigned long long *out)
 
 // LPT order: a counting sort of the groups by 128 - |V| (the parent's visible
 // views for expansion children, the patch's own otherwise)
-__device__ __forceinline__ int lpt_key(const RefineArgs &a, int64_t g)
+__device__ __forceinline__ int lpt_key(const RefineArgs &a, int64_t parent0, int64_t g)
 {
-    const dp_patch &p = a.parents ? a.parents[a.parent0 + (a.items ? a.items[g] : g)] : a.patches[g];
+    const dp_patch &p = a.parents ? a.parents[parent0 + (a.items ? a.items[g] : g)] : a.patches[g];
     return kLptBuckets - 1 - (__popcll(p.vis[0]) + __popcll(p.vis[1]));
+}
+
+// groups of the launch: host-given, or (device-resident BFS) from the generation state
+__device__ __forceinline__ int lpt_groups(const RefineArgs &a, int ng)
+{
+    return a.gen ? (int)((a.gen->ncand + 3) / 4) : ng;
 }
 
 // Per-block LDS histogram, flushed with one global atomic per non-empty
 // bucket (only a dozen of the 129 buckets are hot in practice, so per-thread
-// global atomics serialised on them).
-__global__ void lpt_hist_kernel(RefineArgs a, int ng)
+// global atomics serialised on them).  Grid-stride over 256-group tiles.
+__global__ void lpt_hist_kernel(RefineArgs a, int ng_host)
 {
     __shared__ uint32_t h[kLptBuckets];
+    const int ng = lpt_groups(a, ng_host);
+    const int64_t parent0 = a.gen ? a.gen->head : a.parent0;
     for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
         h[b] = 0;
     __syncthreads();
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < ng)
-        atomicAdd(&h[lpt_key(a, g)], 1u);
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += gridDim.x * blockDim.x)
+        atomicAdd(&h[lpt_key(a, parent0, g)], 1u);
     __syncthreads();
     for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
         if (h[b])
@@ -1904,53 +1708,79 @@ __global__ void lpt_scan_kernel(RefineArgs a)
 // per non-empty bucket from the global cursor, then writes.  Positions inside
 // a bucket depend on block timing; only the bucket order matters (the order
 // schedules the dequeue and never changes a candidate's output).
-__global__ void lpt_scatter_kernel(RefineArgs a, int ng)
+__global__ void lpt_scatter_kernel(RefineArgs a, int ng_host)
 {
     __shared__ uint32_t h[kLptBuckets];
-    for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
-        h[b] = 0;
-    __syncthreads();
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    int key = 0;
-    uint32_t rank = 0;
-    if (g < ng) {
-        key = lpt_key(a, g);
-        rank = atomicAdd(&h[key], 1u);
+    const int ng = lpt_groups(a, ng_host);
+    const int64_t parent0 = a.gen ? a.gen->head : a.parent0;
+    for (int t0 = blockIdx.x * blockDim.x; t0 < ng; t0 += gridDim.x * blockDim.x) {
+        for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
+            h[b] = 0;
+        __syncthreads();
+        const int g = t0 + threadIdx.x;
+        int key = 0;
+        uint32_t rank = 0;
+        if (g < ng) {
+            key = lpt_key(a, parent0, g);
+            rank = atomicAdd(&h[key], 1u);
+        }
+        __syncthreads();
+        for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
+            if (h[b])
+                h[b] = atomicAdd(a.order_scratch + kLptBuckets + b, h[b]);
+        __syncthreads();
+        if (g < ng)
+            a.order[h[key] + rank] = (uint32_t)g;
+        __syncthreads();
     }
-    __syncthreads();
-    for (int b = threadIdx.x; b < kLptBuckets; b += blockDim.x)
-        if (h[b])
-            h[b] = atomicAdd(a.order_scratch + kLptBuckets + b, h[b]);
-    __syncthreads();
-    if (g < ng)
-        a.order[h[key] + rank] = (uint32_t)g;
 }
 
 hipError_t launch_refine(const RefineArgs &a, hipStream_t s)
 {
-    if (a.n <= 0)
+    // a.gen: a device-resident BFS generation (expansion mode): sized on the
+    // device, full-chip grids, counters zeroed by the previous organizer
+    const bool gen = a.gen != nullptr;
+    if (!gen && a.n <= 0)
         return hipSuccess;
+    if (gen && (a.mode != DP_MODE_EXPAND || !a.parents))
+        return hipErrorInvalidValue;
     int dev = 0;
     hipGetDevice(&dev);
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t want = ((int64_t)a.n + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t cap = (int64_t)cus * 8;
-    const int grid = (int)(want < cap ? want : cap);
-    hipError_t e = hipMemsetAsync(a.work, 0, kWorkCounters * sizeof(uint32_t), s);
-    if (e != hipSuccess)
+    const int grid = gen ? (int)cap : (int)(want < cap ? want : cap);
+    hipError_t e = hipSuccess;
+    if (!gen && (e = hipMemsetAsync(a.work, 0, kWorkCounters * sizeof(uint32_t), s)) != hipSuccess)
         return e;
     const int g = pass_width(a.cell);
     if (g <= 0)
         return hipErrorInvalidValue;
     if (a.order) {
         const int ng = a.parents ? (a.n + 3) / 4 : a.n;
-        e = hipMemsetAsync(a.order_scratch, 0, 2 * kLptBuckets * sizeof(uint32_t), s);
-        if (e != hipSuccess)
+        if (!gen && (e = hipMemsetAsync(a.order_scratch, 0, 2 * kLptBuckets * sizeof(uint32_t), s)) != hipSuccess)
             return e;
-        hipLaunchKernelGGL(lpt_hist_kernel, dim3((ng + 255) / 256), dim3(256), 0, s, a, ng);
+        const int gb = gen ? cus : (ng + 255) / 256;
+        hipLaunchKernelGGL(lpt_hist_kernel, dim3(gb), dim3(256), 0, s, a, ng);
         hipLaunchKernelGGL(lpt_scan_kernel, dim3(1), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(lpt_scatter_kernel, dim3((ng + 255) / 256), dim3(256), 0, s, a, ng);
+        hipLaunchKernelGGL(lpt_scatter_kernel, dim3(gb), dim3(256), 0, s, a, ng);
+    }
+    if (gen) {
+        switch (g) {
+#define DP_LAUNCH_REFINE_GEN(GG)                                                                               \
+    case GG:                                                                                                   \
+        hipLaunchKernelGGL((refine_kernel<DP_MODE_EXPAND, GG, true>), dim3(grid), dim3(kBlock), 0, s, a);      \
+        break;
+            DP_LAUNCH_REFINE_GEN(8)
+            DP_LAUNCH_REFINE_GEN(4)
+            DP_LAUNCH_REFINE_GEN(2)
+            DP_LAUNCH_REFINE_GEN(1)
+#undef DP_LAUNCH_REFINE_GEN
+        default:
+            return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
     }
     switch (a.mode * 16 + g) {
 #define DP_LAUNCH_REFINE(M, GG)                                                                               \
@@ -2111,79 +1941,6 @@ __global__ void gather_patches_kernel(const dp_patch *src, const int64_t *idx, i
         dst[i] = src[idx[i]];
 }
 
-__global__ void scatter_items_kernel(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n,
-                                     int per, dp_patch *cand_out, uint8_t *acc_out)
-{
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n * per)
-        return;
-    const int64_t dst = items[j / per] * per + j % per;
-    cand_out[dst] = cand[j];
-    acc_out[dst] = acc[j];
-}
-
-__global__ void iota_kernel(int64_t *v, int64_t n)
-{
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n)
-        v[i] = i;
-}
-
-__global__ void compact_accepted_kernel(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
-                                        const int64_t *items, int64_t m, int per, dp_patch *out, int64_t *count)
-{
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j == 0 && count)
-        count[0] = (int64_t)prefix[m]; // the compacted count (exclusive scan of m + 1 flags)
-    if (j >= m || !acc[j])
-        return;
-    dp_patch r = cand[j];
-    r.seq = (uint32_t)(items[j / per] * per + j % per);
-    out[prefix[j]] = r;
-}
-
-__global__ void scatter_accepted_kernel(const dp_patch *recs, int64_t n, int64_t nc, dp_patch *cand, uint8_t *ok)
-{
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const uint32_t pos = recs[i].seq;
-    if ((int64_t)pos < nc) {
-        cand[pos] = recs[i];
-        ok[pos] = 1;
-    }
-}
-
-hipError_t launch_iota(int64_t *v, int64_t n, hipStream_t s)
-{
-    if (n <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(iota_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, v, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_compact_accepted(const dp_patch *cand, const uint8_t *acc, const uint32_t *prefix,
-                                   const int64_t *items, int64_t n, int per, dp_patch *out, int64_t *count,
-                                   hipStream_t s)
-{
-    const int64_t m = n * per;
-    if (m <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(compact_accepted_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, cand, acc, prefix,
-                       items, m, per, out, count);
-    return hipGetLastError();
-}
-
-hipError_t launch_scatter_accepted(const dp_patch *recs, int64_t n, int64_t nc, dp_patch *cand, uint8_t *ok,
-                                   hipStream_t s)
-{
-    if (n <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(scatter_accepted_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, recs, n, nc, cand,
-                       ok);
-    return hipGetLastError();
-}
-
 hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s)
 {
     if (n <= 0)
@@ -2191,115 +1948,5 @@ hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_
     hipLaunchKernelGGL(gather_patches_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, idx, n, dst);
     return hipGetLastError();
 }
-
-hipError_t launch_scatter_items(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n, int per,
-                                dp_patch *cand_out, uint8_t *acc_out, hipStream_t s)
-{
-    if (n <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(scatter_items_kernel, dim3((unsigned)((n * per + 255) / 256)), dim3(256), 0, s, cand, acc,
-                       items, n, per, cand_out, acc_out);
-    return hipGetLastError();
-}
-
-hipError_t launch_claims(const ClaimArgs &a, hipStream_t s)
-{
-    if (a.n <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(claim_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_resolve(const ClaimArgs &a, uint8_t *accepted, hipStream_t s)
-{
-    if (a.n <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(resolve_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a, accepted);
-    return hipGetLastError();
-}
-
-hipError_t launch_claims_k(const ClaimArgs &a, uint8_t *accepted, hipStream_t s)
-{
-    if (a.n <= 0)
-        return hipSuccess;
-    const dim3 g((a.n + 255) / 256), b(256);
-    hipLaunchKernelGGL(claimk_init_kernel, g, b, 0, s, a);
-    for (int r = 0; r < a.k; ++r) {
-        hipLaunchKernelGGL(claimk_round_kernel, g, b, 0, s, a);
-        hipLaunchKernelGGL(claimk_grant_kernel, g, b, 0, s, a);
-    }
-    hipLaunchKernelGGL(claimk_resolve_kernel, g, b, 0, s, a, accepted);
-    return hipGetLastError();
-}
-
-hipError_t launch_append(const dpg::ViewDev *views, int V, const dp_patch *cand, const uint8_t *accepted,
-                         const uint32_t *prefix, int32_t n, dp_patch *store, int64_t base,
-                         int64_t parent0, int is_seed, int64_t cap, unsigned long long *overflow, hipStream_t s)
-{
-    if (n <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(append_wave_kernel, dim3((n + 3) / 4), dim3(256), 0, s, views, V, cand, accepted, prefix, n,
-                       store, base, parent0, is_seed, cap, overflow);
-    return hipGetLastError();
-}
-
-// The generation's status in one place (one small copy per generation):
-// mbox[0] = the organizer's accepts (prefix[n], 0 without candidates), [1] =
-// the append's overflow flag (mbox[7], cleared), [2..3] = the partition's
-// tiles and split items (ocount, when given), [4] = records exchanged (the sum
-// of counts[world], when given).  One thread.
-__global__ void status_kernel(const uint32_t *prefix_end, const unsigned long long *ocount, const int64_t *counts,
-                              int world, unsigned long long *mbox)
-{
-    if (threadIdx.x != 0)
-        return;
-    mbox[0] = prefix_end ? (unsigned long long)prefix_end[0] : 0ull;
-    mbox[1] = mbox[7];
-    mbox[7] = 0ull;
-    mbox[2] = ocount ? ocount[0] : 0ull;
-    mbox[3] = ocount ? ocount[1] : 0ull;
-    unsigned long long t = 0;
-    for (int r = 0; counts && r < world; ++r)
-        t += (unsigned long long)counts[r];
-    mbox[4] = t;
-}
-
-hipError_t launch_status(const uint32_t *prefix_end, const unsigned long long *ocount, const int64_t *counts,
-                         int world, unsigned long long *mbox, hipStream_t s)
-{
-    hipLaunchKernelGGL(status_kernel, dim3(1), dim3(64), 0, s, prefix_end, ocount, counts, world, mbox);
-    return hipGetLastError();
-}
-
-// scatter of the gathered accepted records of `world` ranks (rank r's
-// counts[r] records at recs + r * stride, any order within a rank) to their
-// generation positions; ok must be zeroed first (every other candidate was
-// rejected by the refine's filter)
-__global__ void scatter_gathered_kernel(const dp_patch *recs, int64_t stride, const int64_t *counts, int world,
-                                        int64_t nc, dp_patch *cand, uint8_t *ok)
-{
-    const int r = blockIdx.y;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= world || i >= counts[r] || i >= stride)
-        return;
-    const dp_patch &p = recs[(int64_t)r * stride + i];
-    const uint32_t pos = p.seq;
-    if ((int64_t)pos < nc) {
-        cand[pos] = p;
-        ok[pos] = 1;
-    }
-}
-
-hipError_t launch_scatter_gathered(const dp_patch *recs, int64_t stride, const int64_t *counts, int world, int64_t nc,
-                                   dp_patch *cand, uint8_t *ok, hipStream_t s)
-{
-    if (stride <= 0 || world <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(scatter_gathered_kernel, dim3((unsigned)((stride + 255) / 256), (unsigned)world), dim3(256), 0, s,
-                       recs, stride, counts, world, nc, cand, ok);
-    return hipGetLastError();
-}
-
-
 
 } // namespace dpk

@@ -56,8 +56,9 @@ struct dp_seedgen {
     DevBuf<dpk::AkView> akz_views;
     DevBuf<uint32_t> akz_hmax, akz_hist, akz_bits;
     DevBuf<uint32_t> akz_seg;
-    DevBuf<int64_t> akz_cand, akz_pbase;
-    DevBuf<int32_t> akz_pids, akz_vids;
+    DevBuf<int64_t> akz_cand;
+    DevBuf<int32_t> akz_vids;
+    DevBuf<uint32_t> akz_err; // a view's candidates overflowed the suppression list
     int desc_words = 8; // 8 (ORB) or 16 (AKAZE) dwords per descriptor
     std::vector<dpk::SeedPair> h_pairs;
     std::vector<dpk::KnnJob> h_jobs;
@@ -121,9 +122,8 @@ void dp_seedgen_free(dp_seedgen *s)
         b->release();
     s->akz_seg.release();
     s->akz_cand.release();
-    s->akz_pbase.release();
-    s->akz_pids.release();
     s->akz_vids.release();
+    s->akz_err.release();
     delete s;
 }
 
@@ -697,21 +697,12 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         DP_HIP(c, s->akz_cand.reserve(n_cand + 1));
         for (int i = 0; i < nlev; ++i)
             DP_HIP(c, launch_akz_emit(a, i, seg_mask, seg_off, s->akz_cand.p, nv, mw[i], mh[i], st));
-        std::vector<int32_t> pids, vids(nv);
-        std::vector<int64_t> pbase;
-        for (int z = 0; z < nv; ++z) {
+        std::vector<int32_t> vids(nv);
+        for (int z = 0; z < nv; ++z)
             vids[z] = v0 + z;
-            for (int i = 0; i < kAkLevels; ++i)
-                if (planes[(size_t)z * kAkLevels + i].w > 0) {
-                    pids.push_back(z * kAkLevels + i);
-                    pbase.push_back(planes[(size_t)z * kAkLevels + i].det_base);
-                }
-        }
-        DP_HIP(c, s->akz_pids.reserve(pids.size() + nv));
-        DP_HIP(c, s->akz_pbase.reserve(pbase.size()));
         DP_HIP(c, s->akz_vids.reserve(nv));
-        DP_HIP(c, hipMemcpyAsync(s->akz_pids.p, pids.data(), pids.size() * 4, hipMemcpyHostToDevice, st));
-        DP_HIP(c, hipMemcpyAsync(s->akz_pbase.p, pbase.data(), pbase.size() * 8, hipMemcpyHostToDevice, st));
+        DP_HIP(c, s->akz_err.reserve(1));
+        DP_HIP(c, hipMemsetAsync(s->akz_err.p, 0, sizeof(uint32_t), st));
         DP_HIP(c, hipMemcpyAsync(s->akz_vids.p, vids.data(), nv * 4, hipMemcpyHostToDevice, st));
         DP_HIP(c, s->kp_a.reserve(n_cand + 1));
         DP_HIP(c, s->kv_a.reserve(n_cand + 1));
@@ -719,8 +710,8 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
         DP_HIP(c, s->kv_b.reserve(n_cand + 1));
         DP_HIP(c, s->flag.reserve(n_cand + 1));
         DP_HIP(c, s->idx_a.reserve(n_cand + 1));
-        AkCandArgs ca{s->akz_planes.p, s->akz_pool.p, s->akz_cand.p, n_cand, s->akz_pids.p, s->akz_pbase.p,
-                      (int32_t)pids.size(), s->akz_vids.p, s->kp_b.p, s->kv_b.p, s->flag.p};
+        AkCandArgs ca{s->akz_planes.p, s->akz_pool.p, s->akz_cand.p, n_cand, nv, s->akz_vids.p, s->kp_b.p,
+                      s->kv_b.p, s->flag.p, s->akz_err.p};
         DP_HIP(c, launch_akz_candidates(ca, st));
         {
             hipcub::CountingInputIterator<int32_t> iota(0);
@@ -728,8 +719,13 @@ static int akaze_stage(dp_ctx *c, dp_seedgen *s, const dp_matcher_options &mo, c
                                                         (int)n_cand, st));
         }
         int64_t n_det = 0;
+        uint32_t akz_err = 0;
         DP_HIP(c, hipMemcpyAsync(&n_det, s->n_sel.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        DP_HIP(c, hipMemcpyAsync(&akz_err, s->akz_err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         DP_HIP(c, hipStreamSynchronize(st));
+        if (akz_err)
+            return fail(c, DP_E_OOM, "AKAZE: a view has " + std::to_string(akz_err) +
+                                         " extrema candidates, more than the suppression list holds (9216)");
         DP_HIP(c, dpk::launch_gather_kp(s->kp_b.p, s->kv_b.p, s->idx_a.p, n_det, s->kp_a.p, s->kv_a.p, st));
         n_det_total += n_det;
         int64_t n_f = 0;

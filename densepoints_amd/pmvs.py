@@ -361,24 +361,16 @@ class Engine:
         res = empty_patches(n.value)
         if n.value:
             ctypes.memmove(res.ctypes.data, out.value, n.value * PATCH_DTYPE.itemsize)
-        stats = {name: getattr(st, name) for name, _ in N.DpDensifyStats._fields_ if name != "reserved"}
+        stats = {name: getattr(st, name) for name, _ in N.DpDensifyStats._fields_}
         return res, stats
 
 
-    # ---- one generation at a time (multi-GPU sharding; dist.densify_sharded) ----
+    # ---- one generation at a time (multi-GPU partitioning; dist.py) ----
     def densify_begin(self, seeds_xyz: np.ndarray) -> N.DpGeneration:
         seeds = np.ascontiguousarray(seeds_xyz, dtype=np.float64).reshape(-1, 3)
         g = N.DpGeneration()
         self._check(lib.dp_densify_begin(self._ctx, ptr(seeds), len(seeds), ctypes.byref(g)))
         return g
-
-    def densify_refine(self, gen: N.DpGeneration, lo: int, hi: int):
-        """Refine items [lo, hi) of the generation: (candidates, accept) host arrays."""
-        n = (hi - lo) * gen.per_item
-        cand = empty_patches(n)
-        acc = np.zeros(n, dtype=np.uint8)
-        self._check(lib.dp_densify_refine(self._ctx, ctypes.byref(gen), lo, hi, ptr(cand), ptr(acc)))
-        return cand, acc
 
     def densify_commit(self, gen: N.DpGeneration, cand: np.ndarray, acc: np.ndarray) -> N.DpGeneration:
         cand = np.ascontiguousarray(cand, dtype=PATCH_DTYPE)
@@ -386,18 +378,10 @@ class Engine:
         self._check(lib.dp_densify_commit(self._ctx, ctypes.byref(gen), ptr(cand), ptr(acc), len(cand)))
         return gen
 
-    def densify_refine_device(self, gen: N.DpGeneration, lo: int, hi: int, d_cand: int, d_accept: int,
-                              stream: int | None = None):
-        """Refine items [lo, hi) into device arrays ((hi-lo)*per_item records / flags)."""
-        self._check(lib.dp_densify_refine_device(self._ctx, ctypes.byref(gen), lo, hi, ctypes.c_void_p(d_cand),
-                                                 ctypes.c_void_p(d_accept),
-                                                 ctypes.c_void_p(stream) if stream else None))
-
-    def densify_commit_device(self, gen: N.DpGeneration, d_cand: int, d_accept: int, n: int,
-                              stream: int | None = None) -> N.DpGeneration:
-        self._check(lib.dp_densify_commit_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_cand),
-                                                 ctypes.c_void_p(d_accept), n,
-                                                 ctypes.c_void_p(stream) if stream else None))
+    def densify_run(self, gen: N.DpGeneration, max_generations: int = 1 << 30) -> N.DpGeneration:
+        """Up to max_generations expansion generations device-resident on this
+        context (dp_densify_run: 8 per host wait)."""
+        self._check(lib.dp_densify_run(self._ctx, ctypes.byref(gen), int(min(max_generations, 2**31 - 1))))
         return gen
 
     # ---- partitioned generations (reference-view super-tiles, SURVEY 8e) ----
@@ -426,47 +410,7 @@ class Engine:
                                                 ptr(acc)))
         return cand, acc
 
-    def densify_refine_items_device(self, gen: N.DpGeneration, d_items: int, n: int, d_cand: int, d_accept: int,
-                                    stream: int | None = None):
-        self._check(lib.dp_densify_refine_items_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_items), n,
-                                                       ctypes.c_void_p(d_cand), ctypes.c_void_p(d_accept),
-                                                       ctypes.c_void_p(stream) if stream else None))
-
-    def densify_commit_items_device(self, gen: N.DpGeneration, d_cand: int, d_accept: int, d_items: int, n: int,
-                                    stream: int | None = None) -> N.DpGeneration:
-        self._check(lib.dp_densify_commit_items_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_cand),
-                                                       ctypes.c_void_p(d_accept), ctypes.c_void_p(d_items), n,
-                                                       ctypes.c_void_p(stream) if stream else None))
-        return gen
-
-    def densify_partition_device(self, gen: N.DpGeneration, world: int, tile_px: int = 64):
-        """(device address of the rank-major item order, items per rank (np.int64
-        array), fallback flag -- always False): dp_densify_partition_device."""
-        d_order = ctypes.c_void_p()
-        counts = np.zeros(world, dtype=np.int64)
-        fb = ctypes.c_int32()
-        self._check(lib.dp_densify_partition_device(self._ctx, ctypes.byref(gen), world, tile_px,
-                                                    ctypes.byref(d_order), ptr(counts), ctypes.byref(fb)))
-        return int(d_order.value or 0), counts, bool(fb.value)
-
-    def densify_compact_accepted_device(self, gen: N.DpGeneration, d_items: int, n: int, d_cand: int, d_accept: int,
-                                        d_out: int, stream: int | None = None) -> int:
-        """Accepted candidates of a rank's items into d_out (generation position in
-        seq); returns their count."""
-        cnt = ctypes.c_int64()
-        self._check(lib.dp_densify_compact_accepted_device(
-            self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_items), n, ctypes.c_void_p(d_cand),
-            ctypes.c_void_p(d_accept), ctypes.c_void_p(d_out), ctypes.byref(cnt),
-            ctypes.c_void_p(stream) if stream else None))
-        return int(cnt.value)
-
-    def densify_commit_accepted_device(self, gen: N.DpGeneration, d_recs: int, n: int,
-                                       stream: int | None = None) -> N.DpGeneration:
-        self._check(lib.dp_densify_commit_accepted_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_recs), n,
-                                                          ctypes.c_void_p(stream) if stream else None))
-        return gen
-
-    # ---- the one-sync generation step (r05): everything on the caller's stream ----
+    # ---- the one-wait device protocol: everything on the caller's stream ----
     def densify_partition_async(self, gen: N.DpGeneration, world: int, tile_px: int = 64,
                                 stream: int | None = None):
         """(device address of the rank-major item order, items per rank):
@@ -480,24 +424,22 @@ class Engine:
                                                    ctypes.byref(d_order), ptr(counts)))
         return int(d_order.value or 0), counts
 
-    def densify_compact_accepted_async(self, gen: N.DpGeneration, d_items: int, n: int, d_cand: int, d_accept: int,
-                                       d_out: int, d_count: int, stream: int | None = None) -> None:
-        """Accepted candidates of a rank's items into d_out, their count (int64)
-        into device memory d_count: no host wait."""
-        self._check(lib.dp_densify_compact_accepted_async(
-            self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_items), n, ctypes.c_void_p(d_cand),
-            ctypes.c_void_p(d_accept), ctypes.c_void_p(d_out), ctypes.c_void_p(d_count),
-            ctypes.c_void_p(stream) if stream else None))
+    def densify_refine_share_async(self, gen: N.DpGeneration, d_items: int, n: int, d_slot: int, stride: int,
+                                   stream: int | None = None) -> None:
+        """Refine this rank's n items (device list d_items) and compact the
+        accepted candidates into its exchange slot (header + stride records)."""
+        self._check(lib.dp_densify_refine_share_async(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_items), n,
+                                                      ctypes.c_void_p(d_slot), stride,
+                                                      ctypes.c_void_p(stream) if stream else None))
 
-    def densify_commit_gathered_device(self, gen: N.DpGeneration, d_recs: int, stride: int, d_counts: int, world: int,
+    def densify_commit_gathered_device(self, gen: N.DpGeneration, d_recs: int, stride: int, world: int,
                                        stream: int | None = None) -> int:
-        """Commit from the gathered fixed-capacity rank slots (rank r's
-        d_counts[r] records at d_recs + r * stride records); the generation's
-        one host wait.  Returns the records exchanged."""
+        """Commit from the `world` gathered rank slots at d_recs (stride + 1
+        records each); the generation's one host wait.  Returns the records
+        exchanged."""
         ex = ctypes.c_int64()
         self._check(lib.dp_densify_commit_gathered_device(self._ctx, ctypes.byref(gen), ctypes.c_void_p(d_recs), stride,
-                                                          ctypes.c_void_p(d_counts), world,
-                                                          ctypes.c_void_p(stream) if stream else None,
+                                                          world, ctypes.c_void_p(stream) if stream else None,
                                                           ctypes.byref(ex)))
         return int(ex.value)
 
@@ -509,7 +451,7 @@ class Engine:
         res = empty_patches(n.value)
         if n.value:
             ctypes.memmove(res.ctypes.data, out.value, n.value * PATCH_DTYPE.itemsize)
-        stats = {name: getattr(st, name) for name, _ in N.DpDensifyStats._fields_ if name != "reserved"}
+        stats = {name: getattr(st, name) for name, _ in N.DpDensifyStats._fields_}
         return res, stats
 
 

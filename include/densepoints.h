@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DP_ABI_VERSION 1
+#define DP_ABI_VERSION 2
 
 /* ---- status codes (replace LOG(FATAL) / cv::Exception) ------- */
 #define DP_OK 0
@@ -109,7 +109,8 @@ typedef struct dp_densify_stats {
     int64_t candidates;        /* expansion candidates refined (4 per expanded pop)*/
     int64_t evals;             /* objective evaluations in all refine kernels      */
     int32_t generations;       /* BFS generations                                  */
-    int32_t reserved;
+    int32_t stalls;            /* device-resident generations that outgrew the
+                                  candidate buffers and were resumed (dp_densify_run) */
     double refine_ms;          /* device time in the fused refine kernels          */
     double total_ms;           /* wall time of dp_densify                          */
 } dp_densify_stats;
@@ -199,20 +200,23 @@ int dp_densify(dp_ctx *ctx, const double *seeds_xyz, int n, const dp_patch **out
 
 /* ---- the same BFS one generation at a time, for sharding it across GPUs ----
  * (SURVEY 8e).  Every rank (one context per GPU) keeps a replicated organizer
- * grid and patch store.  Per generation each rank refines its own contiguous
- * range of the generation's work items; the caller all-gathers the candidate
- * records and accept flags in item order (a rank-order concatenation of
- * contiguous shards); every rank then commits the full generation.  Claims
- * are deterministic (owner = lowest sequence number), so every rank's store
- * equals dp_densify's bit for bit.
+ * grid and patch store.  Per generation each rank refines its own items; the
+ * candidates of the whole generation reach every rank (an all-gather); every
+ * rank then commits the full generation.  Claims are deterministic (owner =
+ * lowest sequence number), so every rank's store equals dp_densify's bit for
+ * bit.  Host-array form (any binding, no device memory):
  *   dp_densify_begin(ctx, seeds, n, &g)
  *   while (g.items > 0) {
- *     dp_densify_refine(ctx, &g, lo, hi, my_cands, my_accept);   (hi-lo)*g.per_item
- *     <all-gather>
- *     dp_densify_commit(ctx, &g, all_cands, all_accept, g.items*g.per_item);
+ *     dp_densify_owners(ctx, &g, world, 64, owner, NULL);   the rank of each item
+ *     dp_densify_refine_items(ctx, &g, mine, n_mine, my_cands, my_accept);
+ *     <all-gather; put every candidate at its generation position
+ *      item * per_item + direction>
+ *     dp_densify_commit(ctx, &g, all_cands, all_accept, g.items * g.per_item);
  *   }
  *   dp_densify_result(ctx, &out, &n_out, &stats);   evals/refine_ms: this rank's share
- */
+ * On one GPU dp_densify_run(ctx, &g, K) runs up to K expansion generations
+ * device-resident with one host wait (what dp_densify does after the seed
+ * generation). */
 typedef struct dp_generation {
     int64_t items;    /* work items: seed points (generation 0) or parents; 0 = finished */
     int64_t head;     /* queue index of the first parent (expansion generations)          */
@@ -223,25 +227,17 @@ typedef struct dp_generation {
 } dp_generation;
 
 int dp_densify_begin(dp_ctx *ctx, const double *seeds_xyz, int n, dp_generation *gen);
-/* Refine items [item_lo, item_hi) of the generation (host output arrays of
- * (item_hi - item_lo) * per_item entries; the seed generation runs
- * DP_MODE_SEED, expansion generations Expand::ExpandPatch as dp_expand_batch). */
-int dp_densify_refine(dp_ctx *ctx, const dp_generation *gen, int64_t item_lo, int64_t item_hi,
-                      dp_patch *cand_out, uint8_t *accept_out);
 /* Organizer step over ALL candidates of the generation (host arrays in item
  * order, n_cand = items * per_item); advances *gen to the next generation. */
 int dp_densify_commit(dp_ctx *ctx, dp_generation *gen, const dp_patch *cand, const uint8_t *accept,
                       int64_t n_cand);
 int dp_densify_result(dp_ctx *ctx, const dp_patch **out, int64_t *n_out, dp_densify_stats *stats);
-/* Device-resident variants (the records never leave HBM; the all-gather runs
- * over RCCL on device buffers): refine writes (item_hi - item_lo) * per_item
- * records/flags into device arrays asynchronously on `stream` (NULL = the
- * context's stream); commit reads the gathered device arrays after waiting
- * for `stream` (NULL = the default stream). */
-int dp_densify_refine_device(dp_ctx *ctx, const dp_generation *gen, int64_t item_lo, int64_t item_hi,
-                             dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream);
-int dp_densify_commit_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_cand,
-                             const uint8_t *d_accept, int64_t n_cand, void *stream);
+/* Up to max_generations expansion generations (gen->index >= 1) on this
+ * context alone, device-resident: each generation's refine and organizer read
+ * its size from device memory, so they are queued 8 at a time behind ONE host
+ * wait; advances *gen (items == 0: finished).  Not with the analytic-gradient
+ * performance refine (dp_fast_options.gradient), which is host-driven. */
+int dp_densify_run(dp_ctx *ctx, dp_generation *gen, int32_t max_generations);
 /* Partitioned generations (north star: "reference-view grid cells shard across
  * the 8 GPUs").  owner_out[i] (host, gen->items) = the rank that
  * refines item i.  Partition spec (round 4; round 3 hashed the tiles and fell
@@ -258,12 +254,7 @@ int dp_densify_commit_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_
  *    at most one item above the mean; only the <= world - 1 tiles a cut falls
  *    in are shared by two ranks.
  * Every rank computes the same owners from its replicated store.
- * *fallback_out is always 0 (kept for ABI compatibility).  Each rank then
- * refines its own items with dp_densify_refine_items[_device] -- candidates in
- * list order -- the caller all-gathers them in rank order, and
- * dp_densify_commit_items_device scatters the gathered candidates back to item
- * order (d_items = the concatenated item lists, a permutation of the
- * generation) and commits: the store equals dp_densify's bit for bit.
+ * *fallback_out is always 0 (kept for ABI compatibility).
  * dp_densify_partition_stats: the last partition's {items, world, distinct
  * super-tiles, items in tiles split between two ranks}. */
 int dp_densify_owners(dp_ctx *ctx, const dp_generation *gen, int world, int tile_px, int32_t *owner_out,
@@ -271,61 +262,36 @@ int dp_densify_owners(dp_ctx *ctx, const dp_generation *gen, int world, int tile
 int dp_densify_partition_stats(dp_ctx *ctx, int64_t *stats_out);
 int dp_densify_refine_items(dp_ctx *ctx, const dp_generation *gen, const int64_t *items, int64_t n,
                             dp_patch *cand_out, uint8_t *accept_out);
-int dp_densify_refine_items_device(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
-                                   dp_patch *d_cand_out, uint8_t *d_accept_out, void *stream);
-int dp_densify_commit_items_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_cand, const uint8_t *d_accept,
-                                   const int64_t *d_items, int64_t n_items, void *stream);
-/* The same protocol with the partition on the device and only the accepted
- * candidates exchanged (the records that can claim cells):
- *  - dp_densify_partition_device: the partition of dp_densify_owners, the
- *    generation's items in rank-major order = the key-sorted order
- *    (*d_order_out: context-owned device array, valid
- *    until the next generation, complete on return so any stream may read
- *    it), items per rank in counts_out[world] (host); world <= 64;
- *  - each rank refines its slice d_order + offset with
- *    dp_densify_refine_items_device, then dp_densify_compact_accepted_device
- *    writes the candidates whose filter passed into d_out (capacity n *
- *    per_item), each carrying its generation position (item * per_item +
- *    direction) in `seq`, and the count in *n_out (host);
- *  - after an all-gather of those records (any order),
- *    dp_densify_commit_accepted_device commits the generation: every other
- *    candidate counts as rejected by the filter (it claims nothing), so the
- *    store equals dp_densify's bit for bit. */
-int dp_densify_partition_device(dp_ctx *ctx, const dp_generation *gen, int world, int tile_px,
-                                const int64_t **d_order_out, int64_t *counts_out, int32_t *fallback_out);
-int dp_densify_compact_accepted_device(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
-                                       const dp_patch *d_cand, const uint8_t *d_accept, dp_patch *d_out,
-                                       int64_t *n_out, void *stream);
-int dp_densify_commit_accepted_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_recs, int64_t n_recs,
-                                      void *stream);
-/* The same protocol with ONE host wait per generation (round 5).  Everything is
- * queued on `stream` (NULL = the legacy default stream), in this order:
- *  - dp_densify_partition_async: the partition of dp_densify_partition_device
- *    (same order, same shares counts_out[r] = floor((r+1) n / world) -
- *    floor(r n / world), host, no device read); its statistics arrive with the
- *    commit (dp_densify_partition_stats after it);
- *  - dp_densify_refine_items_device on the rank's slice of *d_order_out;
- *  - dp_densify_compact_accepted_async: as _compact_accepted_device, the
- *    count (int64) written to device memory *d_count instead of the host;
- *  - the exchange: all-gather of the counts (world int64) and of FIXED-CAPACITY
- *    rank slots of `stride` records (stride >= max_r counts_out[r] *
- *    per_item, host-known: no count has to reach the host first);
- *  - dp_densify_commit_gathered_device: scatters rank r's d_counts[r]
- *    records at d_recs + r * stride to their generation positions, commits the
- *    organizer step and reads the generation's status (accepts, store overflow,
- *    partition statistics, *exchanged_out = the records exchanged) with one
- *    small copy -- the only host wait.  With one rank, pass the compacted
- *    buffer and its count directly (world 1).
+/* The device-resident form with ONE host wait per generation.  Everything is
+ * queued on `stream` (NULL = the legacy default stream itself; the context's
+ * own stream is joined in), in this order:
+ *  - dp_densify_partition_async: the partition of dp_densify_owners as a
+ *    rank-major item order on the device (*d_order_out, context-owned, valid
+ *    until the next generation) and the shares counts_out[r] = floor((r+1) n /
+ *    world) - floor(r n / world) (host, no device read); its statistics
+ *    arrive with the commit (dp_densify_partition_stats after it);
+ *  - dp_densify_refine_share_async: refines the rank's n items d_items[0..n)
+ *    (its slice of *d_order_out) and compacts the candidates whose filter
+ *    passed into the rank's exchange SLOT d_slot: record 0 is a header whose
+ *    first 8 bytes hold the count (int64), records 1..count the candidates (any
+ *    order), each with its generation position (item * per_item + direction)
+ *    in `seq`; the slot holds stride + 1 records, stride >= n * per_item;
+ *  - the exchange: ONE all-gather of every rank's slot (stride + 1 records
+ *    each, stride the same on every rank -- e.g. max_r counts_out[r] *
+ *    per_item, host-known);
+ *  - dp_densify_commit_gathered_device: scatters the `world` gathered slots at
+ *    d_recs (rank r's at d_recs + r * (stride + 1)) to their generation
+ *    positions (every other candidate counts as rejected: it claims nothing),
+ *    commits the organizer step and reads the generation's status with one
+ *    small copy -- the only host wait; *exchanged_out = the records exchanged.
+ *    With one rank, pass the rank's own slot (world 1).
  * Every rank's store equals dp_densify's bit for bit. */
-/* (here NULL `stream` = the legacy default stream itself, so a caller on it
- * needs no other ordering; the context's own stream is joined in.) */
 int dp_densify_partition_async(dp_ctx *ctx, const dp_generation *gen, int world, int tile_px, void *stream,
                                const int64_t **d_order_out, int64_t *counts_out);
-int dp_densify_compact_accepted_async(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
-                                      const dp_patch *d_cand, const uint8_t *d_accept, dp_patch *d_out,
-                                      int64_t *d_count, void *stream);
+int dp_densify_refine_share_async(dp_ctx *ctx, const dp_generation *gen, const int64_t *d_items, int64_t n,
+                                  dp_patch *d_slot, int64_t stride, void *stream);
 int dp_densify_commit_gathered_device(dp_ctx *ctx, dp_generation *gen, const dp_patch *d_recs, int64_t stride,
-                                      const int64_t *d_counts, int world, void *stream, int64_t *exchanged_out);
+                                      int world, void *stream, int64_t *exchanged_out);
 
 /* ---- patch filter ----------------------------------------
  * PMVS::FilterPatches is declared (methods/pmvs/pmvs.h:27) but never defined

@@ -36,11 +36,12 @@
  *     Lsmooth, Lxx, Lxy of Lx, Lyy of Ly; Lx, Ly x s, second derivatives
  *     x s^2; Ldet = Lxx Lyy - Lxy^2.
  *  6. extrema: Ldet > threshold, > its 8 neighbours, inside the descriptor
- *     border (10 sqrt2 s + 1 px); a candidate is dropped when a candidate of
- *     the same or an adjacent level lies within its size (esigma 1.5, level-0
- *     px) with a larger response (equal: the earlier in (level, y, x)) -- the
- *     order-independent form of OpenCV's sequential scan; then the 2x2
- *     subpixel fit of Ldet, kept iff both offsets are within 1.
+ *     border (10 sqrt2 s + 1 px); then OpenCV 3.x's sequential duplicate
+ *     scan in (level, y, x) order (ak_extrema: the first list entry of the
+ *     same or the previous level within the candidate's size -- esigma 1.5,
+ *     level-0 px -- is replaced by a stronger candidate or drops it), the
+ *     upper-level pass over the list, and the 2x2 subpixel fit of Ldet,
+ *     kept iff both offsets are within 1.  Keypoints leave in list order.
  *  7. FilterKeypoints (matcher.cpp:89-153): or_cell_filter.
  *  8. orientation: Gaussian(2.5)-weighted scaled Lx, Ly at the 109 points of
  *     radius 6 s, the pi/3 window slid in 0.15 rad steps, the longest sum's
@@ -423,26 +424,11 @@ static int ak_inside(const AkLevel *L, int x, int y)
     return lx >= 0 && rx < L->w && uy >= 0 && dy < L->h;
 }
 
-/* first index in c[lo, hi) (sorted by (y, x)) with y >= yy */
-static int ak_lower_y(const AkCand *c, int lo, int hi, int yy)
-{
-    while (lo < hi) {
-        const int m = (lo + hi) / 2;
-        if (c[m].y < yy)
-            lo = m + 1;
-        else
-            hi = m;
-    }
-    return lo;
-}
-
 static int ak_extrema(const AkLevel *lv, int n, float thr, or_keypoint **out)
 {
     int cap = 4096, m = 0;
     AkCand *c = (AkCand *)malloc(sizeof(AkCand) * (size_t)cap);
-    int off[AK_MAX_LEVELS + 1];
     for (int i = 0; i < n; ++i) {
-        off[i] = m;
         const AkLevel *L = &lv[i];
         const int w = L->w;
         for (int y = 1; y < L->h - 1; ++y)
@@ -463,31 +449,60 @@ static int ak_extrema(const AkLevel *lv, int n, float thr, or_keypoint **out)
                 }
             }
     }
-    off[n] = m;
-    or_keypoint *kp = (or_keypoint *)malloc(sizeof(or_keypoint) * (size_t)(m + 1));
-    int nk = 0;
+    /* OpenCV 3.x AKAZEFeatures::Find_Scale_Space_Extrema, its sequential scan:
+     * the candidates in (level, y, x) order against the list built so far
+     * (kpts_aux): the FIRST entry in list order of the same or the previous
+     * level within the candidate's size (esigma 1.5, level-0 px) decides -- a
+     * weaker entry is replaced in place by the candidate, an equal or
+     * stronger one drops it; no such entry appends the candidate.  (A
+     * candidate outside the descriptor border changes nothing there, so the
+     * border test above is equivalent.) */
+    AkCand *A = (AkCand *)malloc(sizeof(AkCand) * (size_t)(m + 1));
+    float *Ax = (float *)malloc(sizeof(float) * (size_t)(m + 1)), *Ay = (float *)malloc(sizeof(float) * (size_t)(m + 1));
+    int na = 0;
     for (int a = 0; a < m; ++a) {
         const AkCand *ca = &c[a];
         const AkLevel *La = &lv[ca->level];
         const float ra = (float)(1 << La->octave);
         const float S = La->esigma * 1.5f, S2 = S * S;
         const float px = (float)ca->x * ra, py = (float)ca->y * ra;
-        int drop = 0;
-        for (int j = ca->level - 1; j <= ca->level + 1 && !drop; ++j) {
-            if (j < 0 || j >= n)
+        int hit = -1;
+        for (int k = 0; k < na; ++k) {
+            if (A[k].level != ca->level - 1 && A[k].level != ca->level)
                 continue;
-            const float rj = (float)(1 << lv[j].octave);
-            /* rows of level j whose level-0 y lies within S of py */
-            const int y0 = (int)floorf((py - S) / rj), y1 = (int)ceilf((py + S) / rj);
-            for (int b = ak_lower_y(c, off[j], off[j + 1], y0); b < off[j + 1] && c[b].y <= y1; ++b) {
-                if (b == a)
-                    continue;
-                const float dx = px - (float)c[b].x * rj, dy = py - (float)c[b].y * rj;
-                if (dx * dx + dy * dy <= S2 && (c[b].r > ca->r || (c[b].r == ca->r && b < a))) {
-                    drop = 1;
-                    break;
-                }
+            const float dx = px - Ax[k], dy = py - Ay[k];
+            if (dx * dx + dy * dy <= S2) {
+                hit = k;
+                break;
             }
+        }
+        if (hit < 0) {
+            A[na] = *ca;
+            Ax[na] = px;
+            Ay[na] = py;
+            ++na;
+        } else if (ca->r > A[hit].r) {
+            A[hit] = *ca;
+            Ax[hit] = px;
+            Ay[hit] = py;
+        }
+    }
+    or_keypoint *kp = (or_keypoint *)malloc(sizeof(or_keypoint) * (size_t)(na + 1));
+    int nk = 0;
+    for (int a = 0; a < na; ++a) {
+        const AkCand *ca = &A[a];
+        const AkLevel *La = &lv[ca->level];
+        const float ra = (float)(1 << La->octave);
+        const float S = La->esigma * 1.5f, S2 = S * S;
+        /* the upper-scale pass: removed when a LATER entry of the next level
+         * lies within this entry's size with a larger response */
+        int drop = 0;
+        for (int j = a + 1; j < na && !drop; ++j) {
+            if (A[j].level != ca->level + 1)
+                continue;
+            const float dx = Ax[a] - Ax[j], dy = Ay[a] - Ay[j];
+            if (dx * dx + dy * dy <= S2 && ca->r < A[j].r)
+                drop = 1;
         }
         if (drop)
             continue;
@@ -512,6 +527,9 @@ static int ak_extrema(const AkLevel *lv, int n, float thr, or_keypoint **out)
         ++nk;
     }
     free(c);
+    free(A);
+    free(Ax);
+    free(Ay);
     *out = kp;
     return nk;
 }

@@ -17,6 +17,9 @@
 
 #include "../../include/densepoints.h"
 
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -39,7 +42,10 @@ void usage()
                  "               [--matcher knn|flann]  (MatcherType, matcher.h:12)\n"
                  "               [--detector orb|akaze] [--akaze-threshold T]  (DetectorType, matcher.h:11)\n"
                  "               [--gpus N]   (one context per GPU, generations partitioned by\n"
-                 "                             reference-view super-tile; output identical to 1 GPU)\n"
+                 "                             reference-view super-tile, accepted candidates\n"
+                 "                             all-gathered device to device; output identical to 1 GPU)\n"
+                 "               [--exchange auto|rccl|copy]  (auto: RCCL when every context has its\n"
+                 "                             own GPU, else peer copies; --multi: that protocol at 1 GPU)\n"
                  "               [--mode parity|fast] [--fast-iters N] [--fast-gradient 0|1]\n"
                  "                            (fast: the performance-mode refine -- LDS-staged gray\n"
                  "                             tiles, fused CG -- for the seed stage and every expansion;\n"
@@ -134,83 +140,231 @@ int write_synthetic(const std::string &spec, const std::string &dir)
     return 0;
 }
 
-// dp_densify over `ctxs.size()` contexts (one per GPU): every generation's
-// items are partitioned by reference-view super-tile (dp_densify_owners), each
-// context refines its own items in its own host thread, the candidates are
-// gathered in host memory (one process: shared memory is the all-gather) and
-// put back in item order, and every context commits the whole generation to
-// its replicated organizer -- the store equals dp_densify's bit for bit.
-// Returns the stats of context 0 (evals / refine_ms summed / maxed).
-int densify_multi(std::vector<dp_ctx *> &ctxs, const std::vector<double> &seeds, std::vector<dp_patch> &out,
-                  dp_densify_stats &st, std::string &err)
+// The exchange of the device protocol between the contexts of this process:
+// RCCL (ncclAllGather of the rank slots in one ncclGroup, over xGMI) when
+// every context has its own device, else device-to-device peer copies (the
+// contexts share a GPU, as on a one-GPU box).
+struct Exchange {
+    int G = 0;
+    bool rccl = false;
+    std::vector<int> dev;
+    std::vector<hipStream_t> stream;
+    std::vector<hipEvent_t> ready; // each context's slot is complete
+    std::vector<ncclComm_t> comm;
+    std::vector<dp_patch *> slot, recv;
+    std::vector<size_t> slot_cap, recv_cap; // records
+    std::string err;
+
+    bool hip(hipError_t e, const char *what)
+    {
+        if (e == hipSuccess)
+            return true;
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return false;
+    }
+    bool init(const std::vector<int> &devices, const char *mode)
+    {
+        G = (int)devices.size();
+        dev = devices;
+        std::vector<int> sorted(devices);
+        std::sort(sorted.begin(), sorted.end());
+        const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+        rccl = std::strcmp(mode, "rccl") == 0 || (std::strcmp(mode, "auto") == 0 && distinct);
+        if (rccl && !distinct) {
+            err = "--exchange rccl needs one device per context";
+            return false;
+        }
+        stream.assign(G, nullptr);
+        ready.assign(G, nullptr);
+        slot.assign(G, nullptr);
+        recv.assign(G, nullptr);
+        slot_cap.assign(G, 0);
+        recv_cap.assign(G, 0);
+        for (int g = 0; g < G; ++g) {
+            if (!hip(hipSetDevice(dev[g]), "hipSetDevice") ||
+                !hip(hipStreamCreateWithFlags(&stream[g], hipStreamNonBlocking), "hipStreamCreate") ||
+                !hip(hipEventCreateWithFlags(&ready[g], hipEventDisableTiming), "hipEventCreate"))
+                return false;
+        }
+        if (rccl) {
+            comm.assign(G, nullptr);
+            const ncclResult_t r = ncclCommInitAll(comm.data(), G, dev.data());
+            if (r != ncclSuccess) {
+                err = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+                return false;
+            }
+        }
+        return true;
+    }
+    // slot: stride + 1 records; recv: G slots
+    bool reserve(int64_t stride)
+    {
+        const size_t need = (size_t)stride + 1;
+        for (int g = 0; g < G; ++g) {
+            if (!hip(hipSetDevice(dev[g]), "hipSetDevice"))
+                return false;
+            if (slot_cap[g] < need) {
+                if (slot[g] && !hip(hipFree(slot[g]), "hipFree"))
+                    return false;
+                slot_cap[g] = need + need / 4;
+                if (!hip(hipMalloc(&slot[g], slot_cap[g] * sizeof(dp_patch)), "hipMalloc"))
+                    return false;
+            }
+            if (recv_cap[g] < need * G) {
+                if (recv[g] && !hip(hipFree(recv[g]), "hipFree"))
+                    return false;
+                recv_cap[g] = (need + need / 4) * G;
+                if (!hip(hipMalloc(&recv[g], recv_cap[g] * sizeof(dp_patch)), "hipMalloc"))
+                    return false;
+            }
+        }
+        return true;
+    }
+    // every context's slot into every context's recv, rank order (queued on
+    // the contexts' streams after their compaction: no host wait)
+    bool all_gather(int64_t stride)
+    {
+        const size_t bytes = ((size_t)stride + 1) * sizeof(dp_patch);
+        if (rccl) {
+            ncclGroupStart();
+            for (int g = 0; g < G; ++g) {
+                const ncclResult_t r = ncclAllGather(slot[g], recv[g], bytes, ncclUint8, comm[g], stream[g]);
+                if (r != ncclSuccess) {
+                    ncclGroupEnd();
+                    err = std::string("ncclAllGather: ") + ncclGetErrorString(r);
+                    return false;
+                }
+            }
+            const ncclResult_t r = ncclGroupEnd();
+            if (r != ncclSuccess) {
+                err = std::string("ncclGroupEnd: ") + ncclGetErrorString(r);
+                return false;
+            }
+            return true;
+        }
+        for (int g = 0; g < G; ++g)
+            if (!hip(hipSetDevice(dev[g]), "hipSetDevice") || !hip(hipEventRecord(ready[g], stream[g]), "hipEventRecord"))
+                return false;
+        for (int g = 0; g < G; ++g) {
+            if (!hip(hipSetDevice(dev[g]), "hipSetDevice"))
+                return false;
+            for (int q = 0; q < G; ++q) {
+                if (!hip(hipStreamWaitEvent(stream[g], ready[q], 0), "hipStreamWaitEvent") ||
+                    !hip(hipMemcpyPeerAsync((char *)recv[g] + (size_t)q * bytes, dev[g], slot[q], dev[q], bytes,
+                                            stream[g]),
+                         "hipMemcpyPeerAsync"))
+                    return false;
+            }
+        }
+        return true;
+    }
+    ~Exchange()
+    {
+        // teardown: errors here have nowhere to go
+        for (int g = 0; g < G; ++g) {
+            (void)hipSetDevice(dev[g]);
+            if (stream[g])
+                (void)hipStreamSynchronize(stream[g]);
+            if (rccl && g < (int)comm.size() && comm[g])
+                ncclCommDestroy(comm[g]);
+            if (slot[g])
+                (void)hipFree(slot[g]);
+            if (recv[g])
+                (void)hipFree(recv[g]);
+            if (ready[g])
+                (void)hipEventDestroy(ready[g]);
+            if (stream[g])
+                (void)hipStreamDestroy(stream[g]);
+        }
+    }
+};
+
+// dp_densify over `ctxs.size()` contexts (one per GPU), the device-resident
+// protocol of include/densepoints.h with ONE host wait per generation per
+// context: every generation's items are partitioned by reference-view
+// super-tile on the device (dp_densify_partition_async; the shares are
+// host-known floor cuts), each context refines its share and compacts the
+// accepted candidates into its slot (dp_densify_refine_share_async), the slots
+// are all-gathered device to device (Exchange: RCCL or peer copies), and every
+// context commits the whole generation to its replicated organizer
+// (dp_densify_commit_gathered_device, in its own host thread so the waits
+// overlap) -- no candidate touches host memory, and the store equals
+// dp_densify's bit for bit.  Returns the stats of context 0 (evals /
+// refine_ms summed / maxed).
+int densify_multi(std::vector<dp_ctx *> &ctxs, const std::vector<int> &devices, const char *exchange_mode,
+                  const std::vector<double> &seeds, std::vector<dp_patch> &out, dp_densify_stats &st,
+                  std::string &err, int64_t &exchanged)
 {
     const int G = (int)ctxs.size();
     const int n = (int)(seeds.size() / 3);
+    Exchange ex;
+    if (!ex.init(devices, exchange_mode)) {
+        err = ex.err;
+        return DP_E_HIP;
+    }
     std::vector<dp_generation> gen((size_t)G);
     std::vector<int> rcs((size_t)G, DP_OK);
-    auto all = [&](auto f) {
+    auto fail_of = [&](int g, int rc) {
+        err = dp_last_error(ctxs[(size_t)g]);
+        return rc;
+    };
+    for (int g = 0; g < G; ++g) {
+        const int rc = dp_densify_begin(ctxs[(size_t)g], seeds.data(), n, &gen[(size_t)g]);
+        if (rc != DP_OK)
+            return fail_of(g, rc);
+    }
+    exchanged = 0;
+    std::vector<int64_t> counts((size_t)G), ex_g((size_t)G, 0);
+    while (gen[0].items > 0) {
+        const int per = gen[0].per_item;
+        // the partition and each context's share, queued (no host wait)
+        int64_t stride = 1;
+        for (int g = 0; g < G; ++g) {
+            const int64_t *d_order = nullptr;
+            int rc = dp_densify_partition_async(ctxs[(size_t)g], &gen[(size_t)g], G, 64, ex.stream[(size_t)g], &d_order,
+                                                counts.data());
+            if (rc != DP_OK)
+                return fail_of(g, rc);
+            if (g == 0) {
+                stride = std::max<int64_t>(*std::max_element(counts.begin(), counts.end()) * per, 1);
+                if (!ex.reserve(stride)) {
+                    err = ex.err;
+                    return DP_E_HIP;
+                }
+            }
+            int64_t off = 0;
+            for (int q = 0; q < g; ++q)
+                off += counts[(size_t)q];
+            rc = dp_densify_refine_share_async(ctxs[(size_t)g], &gen[(size_t)g], counts[(size_t)g] ? d_order + off : nullptr,
+                                               counts[(size_t)g], ex.slot[(size_t)g], stride, ex.stream[(size_t)g]);
+            if (rc != DP_OK)
+                return fail_of(g, rc);
+        }
+        if (!ex.all_gather(stride)) {
+            err = ex.err;
+            return DP_E_HIP;
+        }
         std::vector<std::thread> th;
         for (int g = 0; g < G; ++g)
-            th.emplace_back([&, g]() { rcs[(size_t)g] = f(g); });
+            th.emplace_back([&, g]() {
+                rcs[(size_t)g] = dp_densify_commit_gathered_device(ctxs[(size_t)g], &gen[(size_t)g], ex.recv[(size_t)g],
+                                                                   stride, G, ex.stream[(size_t)g], &ex_g[(size_t)g]);
+            });
         for (auto &t : th)
             t.join();
         for (int g = 0; g < G; ++g)
-            if (rcs[(size_t)g] != DP_OK) {
-                err = dp_last_error(ctxs[(size_t)g]);
-                return rcs[(size_t)g];
-            }
-        return DP_OK;
-    };
-    int rc = all([&](int g) { return dp_densify_begin(ctxs[(size_t)g], seeds.data(), n, &gen[(size_t)g]); });
-    if (rc != DP_OK)
-        return rc;
-    while (gen[0].items > 0) {
-        const int64_t items = gen[0].items;
-        const int per = gen[0].per_item;
-        std::vector<int32_t> owner((size_t)items);
-        int32_t fallback = 0;
-        if ((rc = dp_densify_owners(ctxs[0], &gen[0], G, 64, owner.data(), &fallback)) != DP_OK) {
-            err = dp_last_error(ctxs[0]);
-            return rc;
-        }
-        std::vector<std::vector<int64_t>> mine((size_t)G);
-        for (int64_t i = 0; i < items; ++i)
-            mine[(size_t)owner[(size_t)i]].push_back(i);
-        std::vector<std::vector<dp_patch>> cand((size_t)G);
-        std::vector<std::vector<uint8_t>> acc((size_t)G);
-        rc = all([&](int g) {
-            const size_t k = mine[(size_t)g].size() * (size_t)per;
-            cand[(size_t)g].resize(k);
-            acc[(size_t)g].resize(k);
-            return dp_densify_refine_items(ctxs[(size_t)g], &gen[(size_t)g], mine[(size_t)g].data(),
-                                           (int64_t)mine[(size_t)g].size(), cand[(size_t)g].data(),
-                                           acc[(size_t)g].data());
-        });
-        if (rc != DP_OK)
-            return rc;
-        std::vector<dp_patch> all_c((size_t)(items * per));
-        std::vector<uint8_t> all_a((size_t)(items * per));
-        for (int g = 0; g < G; ++g)
-            for (size_t j = 0; j < mine[(size_t)g].size(); ++j)
-                for (int d = 0; d < per; ++d) {
-                    const size_t dst = (size_t)mine[(size_t)g][j] * per + d;
-                    all_c[dst] = cand[(size_t)g][j * per + d];
-                    all_a[dst] = acc[(size_t)g][j * per + d];
-                }
-        rc = all([&](int g) {
-            return dp_densify_commit(ctxs[(size_t)g], &gen[(size_t)g], all_c.data(), all_a.data(), items * per);
-        });
-        if (rc != DP_OK)
-            return rc;
+            if (rcs[(size_t)g] != DP_OK)
+                return fail_of(g, rcs[(size_t)g]);
+        exchanged += ex_g[0];
     }
     std::vector<dp_densify_stats> sts((size_t)G);
     const dp_patch *res = nullptr;
     int64_t np = 0;
-    for (int g = G - 1; g >= 0; --g)
-        if ((rc = dp_densify_result(ctxs[(size_t)g], &res, &np, &sts[(size_t)g])) != DP_OK) {
-            err = dp_last_error(ctxs[(size_t)g]);
-            return rc;
-        }
+    for (int g = G - 1; g >= 0; --g) {
+        const int rc = dp_densify_result(ctxs[(size_t)g], &res, &np, &sts[(size_t)g]);
+        if (rc != DP_OK)
+            return fail_of(g, rc);
+    }
     out.assign(res, res + np);
     st = sts[0];
     for (int g = 1; g < G; ++g) {
@@ -226,6 +380,8 @@ int main(int argc, char **argv)
 {
     std::string input, settings, output = "points.ply", seeds_path, synth, scene_dir;
     int device = 0, gpus = 1;
+    bool force_multi = false;
+    std::string exchange_mode = "auto";
     long long max_pops = -1;
     int level = 0;
     bool check_only = false, do_filter = false, fast = false;
@@ -247,6 +403,14 @@ int main(int argc, char **argv)
         else if (a == "--seeds") seeds_path = next();
         else if (a == "--device") device = std::atoi(next().c_str());
         else if (a == "--gpus") gpus = std::atoi(next().c_str());
+        else if (a == "--multi") force_multi = true;
+        else if (a == "--exchange") {
+            exchange_mode = next();
+            if (exchange_mode != "auto" && exchange_mode != "rccl" && exchange_mode != "copy") {
+                std::fprintf(stderr, "densify: --exchange expects auto, rccl or copy\n");
+                return 2;
+            }
+        }
         else if (a == "--max-pops") max_pops = std::atoll(next().c_str());
         else if (a == "--level") level = std::atoi(next().c_str());
         else if (a == "--filter") do_filter = true;
@@ -382,10 +546,12 @@ int main(int argc, char **argv)
         dp_densify_stats st;
         std::memset(&st, 0, sizeof st);
         std::vector<dp_patch> multi_out;
-        if (gpus > 1) {
+        int64_t exchanged = -1;
+        if (gpus > 1 || force_multi) {
             // contexts 1..N-1 on the next devices (wrapping: several ranks may share a GPU)
             const int ndev = dp_device_count();
             std::vector<dp_ctx *> ctxs{ctx};
+            std::vector<int> devices{device};
             // a failure on a secondary context reports THAT context's error and
             // releases every context created so far before exiting
             auto check_g = [&](int rc, dp_ctx *cg, const char *what) {
@@ -401,8 +567,10 @@ int main(int argc, char **argv)
             };
             for (int g = 1; g < gpus; ++g) {
                 dp_ctx *cg = nullptr;
-                check_g(dp_ctx_create(&opt, (device + g) % (ndev > 0 ? ndev : 1), &cg), cg, "dp_ctx_create");
+                const int dg = (device + g) % (ndev > 0 ? ndev : 1);
+                check_g(dp_ctx_create(&opt, dg, &cg), cg, "dp_ctx_create");
                 ctxs.push_back(cg);
+                devices.push_back(dg);
                 check_g(dp_set_views(cg, (int)imgs.size(), P.data(), dimg.data()), cg, "dp_set_views");
                 check_g(dp_set_fast_options(cg, &fo), cg, "dp_set_fast_options");
                 if (level > 0) {
@@ -411,7 +579,7 @@ int main(int argc, char **argv)
                 }
             }
             std::string err;
-            const int mrc = densify_multi(ctxs, use, multi_out, st, err);
+            const int mrc = densify_multi(ctxs, devices, exchange_mode.c_str(), use, multi_out, st, err, exchanged);
             for (int g = 1; g < gpus; ++g)
                 dp_ctx_destroy(ctxs[(size_t)g]);
             if (mrc != DP_OK) {
@@ -451,12 +619,12 @@ int main(int argc, char **argv)
         std::printf("{\"output\": \"%s\", \"patches\": %lld, \"written\": %zu, \"seeds\": %zu, \"generated_seeds\": %s, "
                     "\"keypoints\": %lld, \"matches\": %lld, \"seed_ms\": %.3f, \"seed_patches\": %lld, "
                     "\"pops\": %lld, \"candidates\": %lld, \"evals\": %lld, \"generations\": %d, \"refine_ms\": %.3f, "
-                    "\"densify_ms\": %.3f, \"wall_ms\": %.3f, \"gpus\": %d, \"mode\": \"%s\"}\n",
+                    "\"densify_ms\": %.3f, \"wall_ms\": %.3f, \"gpus\": %d, \"mode\": \"%s\", \"exchanged\": %lld}\n",
                     output.c_str(), (long long)st.patches, cloud.size(), use.size() / 3,
                     seeds_path.empty() ? "true" : "false", (long long)sst.keypoints, (long long)sst.matches,
                     sst.total_ms, (long long)st.seed_patches, (long long)st.pops, (long long)st.candidates,
                     (long long)st.evals, st.generations, st.refine_ms, st.total_ms, wall, gpus,
-                    fast ? "fast" : "parity");
+                    fast ? "fast" : "parity", (long long)exchanged);
         return 0;
     } catch (const std::exception &e) {
         std::fprintf(stderr, "densify: %s\n", e.what());

@@ -56,9 +56,16 @@ def generate(options=OPTIONS, inputs=None):
 
 
 if __name__ == "__main__":
-    out = generate()
-    np.savez_compressed(os.path.join(HERE, "seeds_small.npz"), **out)
-    print({k: v.shape for k, v in out.items()}, out["counts"])
+    import sys
+
+    if "--akaze-only" in sys.argv:
+        # regenerate the AKAZE fixture alone, on the committed seeds_small.npz inputs
+        g = np.load(os.path.join(HERE, "seeds_small.npz"))
+        out = {"P": g["P"], "images": g["images"]}
+    else:
+        out = generate()
+        np.savez_compressed(os.path.join(HERE, "seeds_small.npz"), **out)
+        print({k: v.shape for k, v in out.items()}, out["counts"])
     ak = generate(AKAZE_OPTIONS, (out["P"], list(out["images"])))
     del ak["P"], ak["images"]  # the inputs are seeds_small.npz's
     np.savez_compressed(os.path.join(HERE, "seeds_akaze_small.npz"), **ak)

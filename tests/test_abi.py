@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_layouts():
-    assert N.lib.dp_abi_version() == 1
+    assert N.lib.dp_abi_version() == 2
     assert N.PATCH_DTYPE.itemsize == 80
     assert ctypes.sizeof(N.DpOptions) == 104
     o = N.default_options()

@@ -233,17 +233,26 @@ def test_cli_baseline_cfg1_vga(tmp_path_factory, tmp_path, orc, views):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpus", [2, 3])
-def test_cli_gpus_partitioned_equals_one_gpu(scene_dir, tmp_path, gpus):
+@pytest.mark.parametrize("gpus,extra", [(2, ()), (3, ()), (1, ("--multi", "--exchange", "rccl")),
+                                        (2, ("--mode", "fast"))])
+def test_cli_gpus_partitioned_equals_one_gpu(scene_dir, tmp_path, gpus, extra):
     """densify --gpus N: N contexts (wrapping onto the available devices),
-    every generation partitioned by reference-view super-tile; the PLY is
-    byte-identical to the 1-GPU run."""
+    every generation partitioned by reference-view super-tile on the device,
+    each context's accepted candidates compacted into its slot and the slots
+    all-gathered device to device (peer copies when contexts share a GPU; the
+    RCCL path -- ncclCommInitAll + ncclAllGather in one group -- forced at one
+    context with --multi --exchange rccl); the PLY is byte-identical to the
+    1-GPU run."""
     one, many = tmp_path / "one.ply", tmp_path / "many.ply"
     args = ["-i", os.path.join(scene_dir, "scene.json"), "--seeds", os.path.join(scene_dir, "seeds.xyz")]
-    r1 = json.loads(run(*args, "-o", str(one)).stdout)
-    rn = json.loads(run(*args, "-o", str(many), "--gpus", str(gpus)).stdout)
+    mode = list(extra[extra.index("--mode"):extra.index("--mode") + 2]) if "--mode" in extra else []
+    r1 = json.loads(run(*args, *mode, "-o", str(one)).stdout)
+    # (RCCL prints its version banner on stdout: the report is the last line)
+    rn = json.loads(run(*args, "-o", str(many), "--gpus", str(gpus), *extra).stdout.strip().splitlines()[-1])
     assert rn["gpus"] == gpus and rn["patches"] == r1["patches"] > 0
     assert rn["evals"] == r1["evals"]
+    # only accepted candidates crossed: at least every stored patch, at most every candidate
+    assert r1["patches"] <= rn["exchanged"] <= r1["candidates"] + len(open(os.path.join(scene_dir, "seeds.xyz")).readlines())
     assert many.read_bytes() == one.read_bytes()
 
 

@@ -1,9 +1,10 @@
-"""Multi-process path on CPU (gloo, world_size 2): candidates are sharded by
-contiguous rank ranges, each rank refines its shard, and the all-gathered
-shards equal the single-process result bit for bit (the
-candidate loop shards with no data-path collective).  The per-rank refine
-here is the oracle (CPU test infrastructure); the GPU runs the same sharding
-in bench.py."""
+"""Multi-process path on CPU (gloo, world_size 2 and 3): candidates are
+sharded by contiguous rank ranges (the bench's weak-scaled batch), or a
+densify's generations are partitioned by reference-view super-tile
+(dist.densify_partitioned, the host-array form of the device protocol); the
+all-gathered results equal the single-process result bit for bit.
+The per-rank refine here is the oracle (CPU test infrastructure); the GPU runs
+the same protocols in bench.py and tests/test_gpu_dist.py."""
 import os
 import socket
 
@@ -96,43 +97,6 @@ def test_gloo_world2_sharded_expand_equals_single_process(tmp_path, orc):
 def _hf6():
     # 6-view tilted-facet scene, 320x240 (the GPU suite's "hf6")
     return synth.scene_host(synth.config(6, 320, 240, 1))
-
-
-def _dens_worker(rank, world, port, out_path, max_pops):
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import densepoints_amd as dp
-    from oracle import pyoracle
-
-    dist = D.init("gloo")
-    P, imgs, seeds = _hf6()
-    S = pyoracle.Scene(P, imgs, dp.Options(max_pops=max_pops) if max_pops else None)
-    patches, st = D.densify_sharded(pyoracle.GenerationEngine(S), seeds, dist)
-    if rank == 0:
-        np.save(out_path, patches.view(np.uint8), allow_pickle=False)
-    else:  # every rank holds the same replicated store
-        np.save(out_path + f".r{rank}.npy", patches.view(np.uint8), allow_pickle=False)
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("max_pops", [0, 23])
-def test_gloo_world2_sharded_densify_equals_single_process(tmp_path, orc, max_pops):
-    """every generation sharded over 2 ranks, candidates all-gathered,
-    replicated deterministic claims -> the 1-process densify, bit for bit."""
-    import densepoints_amd as dp
-    from densepoints_amd._native import PATCH_DTYPE
-
-    out = str(tmp_path / "dense.npy")
-    mp.spawn(_dens_worker, args=(2, _free_port(), out, max_pops), nprocs=2, join=True)
-    got = np.frombuffer(np.load(out, allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
-    got1 = np.frombuffer(np.load(out + ".r1.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
-    P, imgs, seeds = _hf6()
-    S = orc.Scene(P, imgs, dp.Options(max_pops=max_pops) if max_pops else None)
-    ref, st = S.densify(seeds)
-    assert len(ref) > 50
-    assert got.tobytes() == ref.tobytes()
-    assert got1.tobytes() == ref.tobytes()
 
 
 def test_partition_is_rank_major_and_stable():

@@ -1,8 +1,9 @@
-"""Generation-at-a-time densify on the GPU (dp_densify_begin/refine/commit/
-result) and its multi-rank driver (densepoints_amd.dist.densify_sharded):
-one rank equals dp_densify; two ranks (two processes sharing cuda:0, gloo
-all-gathers of host records) equal it too -- the replicated-claims design of
-SURVEY 8e, bit for bit."""
+"""Generation-at-a-time densify on the GPU (dp_densify_begin / refine_items /
+commit / run / result) and its multi-rank drivers (densepoints_amd.dist):
+one rank equals dp_densify, also when the device-resident generations run a
+few at a time or stall on small buffers; two and three ranks (processes
+sharing cuda:0, gloo all-gathers) equal it too -- the replicated-claims design
+of SURVEY 8e, bit for bit."""
 import json
 import os
 import socket
@@ -33,15 +34,55 @@ def _scene(name):
 
 @pytest.mark.parametrize("name,max_pops", [("hf6", 0), ("hf6", 37), ("wide70", 0)])
 def test_generation_api_equals_dp_densify(name, max_pops):
+    """The host-array generation API (dist.densify_partitioned at one rank:
+    owners, refine_items, commit) and the device-resident dp_densify_run in
+    batches of 1 and 3 generations equal dp_densify, statistics included."""
     P, imgs, seeds = _scene(name)
     opts = dp.Options(max_pops=max_pops) if max_pops else dp.Options()
     with dp.Engine(opts, device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
         ref, rst = eng.densify(seeds)
-        got, gst = D.densify_sharded(eng, seeds, None)
+        got, gst = D.densify_partitioned(eng, seeds, None)
+        runs = []
+        for k in (1, 3):
+            g = eng.densify_begin(seeds)
+            cand, acc = eng.densify_refine_items(g, np.arange(g.items))
+            g = eng.densify_commit(g, cand, acc)
+            calls = 0
+            while g.items > 0:
+                g = eng.densify_run(g, k)
+                calls += 1
+            runs.append((k, calls, eng.densify_result()))
     assert len(ref) > 20
     assert got.tobytes() == ref.tobytes()
     for k in ("patches", "seed_patches", "pops", "candidates", "generations", "evals"):
+        assert gst[k] == rst[k], k
+    for k, calls, (rp, rs) in runs:
+        assert rp.tobytes() == ref.tobytes(), f"batch {k}"
+        for key in ("patches", "seed_patches", "pops", "candidates", "generations", "evals"):
+            assert rs[key] == rst[key], (k, key)
+        assert calls >= rst["generations"] // k
+
+
+def test_device_loop_stall_resumes():
+    """DP_GEN_CAP caps the device-resident loop's candidate buffers, so its
+    generations outgrow them: each stalls on the device (nothing runs), the
+    host grows the buffers and resumes it -- the store equals the uncapped
+    dp_densify's."""
+    P, imgs, seeds = _scene("hf6")
+    with dp.Engine(device=0) as eng:
+        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+        ref, rst = eng.densify(seeds)
+    os.environ["DP_GEN_CAP"] = "64"
+    try:
+        with dp.Engine(device=0) as eng:
+            eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+            got, gst = eng.densify(seeds)
+            assert gst["stalls"] > 0
+    finally:
+        del os.environ["DP_GEN_CAP"]
+    assert got.tobytes() == ref.tobytes()
+    for k in ("patches", "seed_patches", "candidates", "generations", "evals"):
         assert gst[k] == rst[k], k
 
 
@@ -58,7 +99,7 @@ def _worker(rank, world, port, out_path):
     P, imgs, seeds = _scene("hf6")
     with dp.Engine(device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
-        got, st = D.densify_sharded(eng, seeds, dist)
+        got, st = D.densify_partitioned(eng, seeds, dist)
     np.save(out_path + f".r{rank}.npy", got.view(np.uint8), allow_pickle=False)
     with open(out_path + f".r{rank}.evals", "w") as f:
         f.write(str(st["evals"]))
@@ -66,7 +107,7 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_two_ranks_sharded_densify_equals_dp_densify(tmp_path):
+def test_two_ranks_host_partitioned_densify_equals_dp_densify(tmp_path):
     out = str(tmp_path / "dense")
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     P, imgs, seeds = _scene("hf6")
@@ -76,84 +117,87 @@ def test_two_ranks_sharded_densify_equals_dp_densify(tmp_path):
     for r in range(2):
         got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
         assert got.tobytes() == ref.tobytes(), f"rank {r}"
-        # each rank refined half of every generation; the summed evaluation count is the 1-GPU one
+        # each rank refined its share of every generation; the summed evaluation count is the 1-GPU one
         assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
 
 
-def _worker_dev(rank, world, port, out_path, backend, partitioned=False, cap=1):
+def _worker_dev(rank, world, port, out_path, backend, exchange=False, cap=1, scene="hf6"):
     import torch
     import torch.distributed as tdist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     # torch's HIP runtime initialises the device before libdensepoints' (the
-    # wheel bundles its own libamdhip64; bench.py uses the same order)
+    # wheel bundles its own libamdhip64; bench.py uses the same order); the
+    # torch default stream is the legacy NULL stream (the ABI's stream = NULL case)
     torch.cuda.set_device(0)
     group = None
     if backend:
         kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
         tdist.init_process_group(backend, rank=rank, world_size=world, **kw)
         group = tdist
-    P, imgs, seeds = _scene("hf6")
+    P, imgs, seeds = _scene(scene)
     with dp.Engine(dp.Options(max_patches_per_cell=cap), device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
-        if partitioned == "all":
-            got, st = D.densify_partitioned_device_all(eng, seeds, group, torch.device("cuda", 0))
-        elif partitioned == "r04":
-            got, st = D.densify_partitioned_device_r04(eng, seeds, group, torch.device("cuda", 0))
-        elif partitioned:
-            got, st = D.densify_partitioned_device(eng, seeds, group, torch.device("cuda", 0))
-        else:
-            got, st = D.densify_sharded_device(eng, seeds, group, torch.device("cuda", 0))
+        got, st = D.densify_partitioned_device(eng, seeds, group, torch.device("cuda", 0), one_rank_exchange=exchange)
+        # the same densify in the host-array form: the partitions (and their
+        # statistics, read back by the async path with the commit) must agree
+        _, hst = D.densify_partitioned(eng, seeds, group, torch.device("cuda", 0) if backend == "nccl" else None)
     np.save(out_path + f".r{rank}.npy", got.view(np.uint8), allow_pickle=False)
-    with open(out_path + f".r{rank}.evals", "w") as f:
-        f.write(str(st["evals"]))
+    with open(out_path + f".r{rank}.json", "w") as f:
+        f.write(json.dumps({"evals": st["evals"], "partition": st["partition"], "host_partition": hst["partition"]}))
     if group:
         tdist.barrier()
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("backend,world", [(None, 1), ("nccl", 1), ("gloo", 2)])
-def test_device_resident_sharded_densify(tmp_path, backend, world):
-    """dp_densify_refine_device / dp_densify_commit_device with the candidate
-    shards all-gathered on the device (no group; world 1 over RCCL
-    all_gather_into_tensor; two ranks sharing cuda:0 over gloo) equal
-    dp_densify bit for bit."""
+@pytest.mark.parametrize("backend,world,exchange,cap", [(None, 1, False, 1), (None, 1, True, 1), ("nccl", 1, True, 1),
+                                                       ("gloo", 2, False, 1), ("gloo", 3, False, 1),
+                                                       ("gloo", 2, False, 2)])
+def test_partitioned_densify_device(tmp_path, backend, world, exchange, cap):
+    """Reference-view super-tile partition of every generation: the device
+    partition, refine of the rank's share with its accepted candidates
+    compacted into the rank's slot, ONE all-gather of the slots and the
+    scatter + commit (dist.densify_partitioned_device: one host wait per
+    generation; at one rank the device-resident generations, or with
+    `exchange` the slot protocol itself): every rank's store equals dp_densify
+    -- also with organizer cell capacity 2 (max_patches_per_cell,
+    patch_organizer.h:42-46).  The ranks run on the legacy NULL stream, and
+    the partition statistics the async path reads back with the commit equal
+    the synchronous host-array path's, generation by generation."""
     out = str(tmp_path / "dense")
-    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend), nprocs=world, join=True)
+    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, exchange, cap), nprocs=world, join=True)
     P, imgs, seeds = _scene("hf6")
+    with dp.Engine(dp.Options(max_patches_per_cell=cap), device=0) as eng:
+        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+        ref, rst = eng.densify(seeds)
+    for r in range(world):
+        got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
+        assert got.tobytes() == ref.tobytes(), f"rank {r}"
+        st = json.loads(open(out + f".r{r}.json").read())
+        assert st["evals"] == rst["evals"]
+        if world > 1 or exchange:
+            assert st["partition"] == st["host_partition"], f"rank {r}"
+
+
+def test_partitioned_densify_more_ranks_than_items(tmp_path):
+    """three ranks on the legacy NULL stream over a scene whose
+    late generations have fewer items than ranks (a rank with no share
+    refines nothing and still commits): the stores equal dp_densify and the
+    partition statistics read back with the commit equal the synchronous
+    path's."""
+    world = 3
+    out = str(tmp_path / "dense")
+    mp.spawn(_worker_dev, args=(world, _free_port(), out, "gloo", False, 1, "wide70"), nprocs=world, join=True)
+    P, imgs, seeds = _scene("wide70")
     with dp.Engine(device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
         ref, rst = eng.densify(seeds)
     for r in range(world):
         got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
         assert got.tobytes() == ref.tobytes(), f"rank {r}"
-        assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
-
-
-@pytest.mark.parametrize("backend,world,variant,cap", [(None, 1, "accepted", 1), ("nccl", 1, "accepted", 1),
-                                                      ("gloo", 2, "accepted", 1), ("gloo", 3, "accepted", 1),
-                                                      ("gloo", 2, "all", 1), ("gloo", 2, "accepted", 2),
-                                                      ("nccl", 1, "r04", 1), ("gloo", 2, "r04", 1)])
-def test_partitioned_densify_device(tmp_path, backend, world, variant, cap):
-    """Reference-view super-tile partition of every generation: the device
-    partition, refine of the rank's items, all-gather of the ACCEPTED
-    candidates only and dp_densify_commit_accepted_device (variant
-    "accepted", dist.densify_partitioned_device: one host wait per generation,
-    fixed-capacity rank slots; "r04": the round-4 protocol with host-read
-    counts), or of every candidate slot with dp_densify_commit_items_device
-    ("all"): every rank's store equals
-    dp_densify -- also with organizer cell capacity 2
-    (max_patches_per_cell, patch_organizer.h:42-46)."""
-    out = str(tmp_path / "dense")
-    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, variant, cap), nprocs=world, join=True)
-    P, imgs, seeds = _scene("hf6")
-    with dp.Engine(dp.Options(max_patches_per_cell=cap), device=0) as eng:
-        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
-        ref, rst = eng.densify(seeds)
-    for r in range(world):
-        got = np.frombuffer(np.load(out + f".r{r}.npy", allow_pickle=False).tobytes(), dtype=PATCH_DTYPE)
-        assert got.tobytes() == ref.tobytes(), f"rank {r}"
-        assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
+        st = json.loads(open(out + f".r{r}.json").read())
+        assert st["partition"] == st["host_partition"]
+        assert any(items < world for items, _, _, _ in st["partition"]), st["partition"]
 
 
 @pytest.mark.parametrize("world", [2, 8])
@@ -175,9 +219,9 @@ def test_owners_equal_oracle_and_host_path(orc, world):
             oown, ofb = G.densify_owners(og, world)
             assert fb == ofb and np.array_equal(own, oown), f"generation {gens}"
             assert eng.densify_partition_stats() == G.densify_partition_stats(), f"generation {gens}"
-            cand, acc = eng.densify_refine(g, 0, g.items)
+            cand, acc = eng.densify_refine_items(g, np.arange(g.items))
             g = eng.densify_commit(g, cand, acc)
-            oc, oa = G.densify_refine(og, 0, og.items)
+            oc, oa = G.densify_refine_items(og, np.arange(og.items))
             og = G.densify_commit(og, oc, oa)
             gens += 1
         assert gens > 3

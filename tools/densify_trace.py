@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""The config-4 partitioned densify of bench.py's scaling_leg at one rank
-(dist.densify_partitioned_device, or the r04 protocol), for a rocprofv3
-kernel trace: where the non-refine time of a densify goes (kernel time of the
-partition / compaction / organizer kernels vs GPU idle between launches).
-Prints one JSON line per repetition: wall ms, refine ms (events), generations.
+"""The config-4 densify of bench.py's scaling_leg at one rank, for a
+rocprofv3 kernel trace: where the non-refine time of a densify goes (kernel
+time of the partition / compaction / organizer kernels vs GPU idle between
+launches).  --protocol device: the device-resident generations (dp_densify
+/ dp_densify_run); slots: the multi-rank slot protocol at one rank
+(dist.densify_partitioned_device one_rank_exchange).  Prints one JSON line
+per repetition: wall ms, refine ms (events), generations.
 
     rocprofv3 --kernel-trace --stats -d OUT -- python3 tools/densify_trace.py --mode fast
 """
@@ -29,7 +31,7 @@ def main():
     ap.add_argument("--config", default="cfg4_64view_4k")
     ap.add_argument("--mode", default="fast")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--protocol", default="r05")
+    ap.add_argument("--protocol", choices=["device", "slots"], default="device")
     a = ap.parse_args()
     cfg = synth.named(a.config)
     V, W, H = cfg.n_views, cfg.width, cfg.height
@@ -47,7 +49,9 @@ def main():
     eng.set_views_device(P, [W] * V, [H] * V, [W] * V, [p.data_ptr() for p in planes])
     seeds = synth.seeds(cfg, P)
     eng.set_fast_options(dp.FastOptions(densify=1 if a.mode == "fast" else 0))
-    run = D.densify_partitioned_device if a.protocol == "r05" else D.densify_partitioned_device_r04
+    def run(eng, seeds, dist, dev):
+        return D.densify_partitioned_device(eng, seeds, dist, dev, one_rank_exchange=a.protocol == "slots")
+
     for rep in range(a.reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
