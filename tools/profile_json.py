@@ -63,6 +63,16 @@ def one(d):
                 lib_sha = j.get("lib_sha256", lib_sha)
                 ev_ms = j.get("kernel_ms_per_launch", ev_ms)
                 ev_list = j.get("kernel_ms_events", ev_list)
+    # bench.py's full result (the stdout line is a compact summary since r06)
+    det = os.path.join(d, "detail.json")
+    if os.path.exists(det):
+        try:
+            j = json.load(open(det))
+            lib_sha = j.get("lib_sha256", lib_sha)
+            ev_ms = j.get("kernel_ms_per_launch", ev_ms)
+            ev_list = j.get("kernel_ms_events", ev_list)
+        except ValueError:
+            pass
     for k in set(durs) | set(ctr):
         if not any(s in k for s in KEEP):
             continue
