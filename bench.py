@@ -427,7 +427,7 @@ def main():
     lib_sha = lib_stamp(N.LIB_PATH)
     result["lib_sha256"] = lib_sha
     prof = profiled("parity" if not fast else "fast%d" % args.cell,
-                    "refine_kernel<4, 2>" if not fast else fast_kernel_tag(args.cell), B, lib_sha)
+                    "refine_kernel<4, 2," if not fast else fast_kernel_tag(args.cell), B, lib_sha)
     if prof:
         attach_profile(result["roofline"], prof, B, launch_ms)
 
@@ -795,8 +795,9 @@ def fast_kernel_tag(cell, gradient=0):
     """the performance kernel instance bench runs at this window (dp_fast.hip fast_dispatch;
     kMode 100 = the analytic-gradient refine, 6 = forward differences)"""
     mode = 100 if gradient else 6
-    return {7: f"fast_kernel<4, 3, true, false, 6656, {mode}>",
-            11: f"fast_kernel<2, 4, false, true, 6656, {mode}>"}.get(cell, "?")
+    # a prefix of the instance name: later template parameters (build knobs) may follow
+    return {7: f"fast_kernel<4, 3, true, false, 6656, {mode},",
+            11: f"fast_kernel<2, 4, false, true, 6656, {mode},"}.get(cell, "?")
 
 
 def profiled(workload, kernel, B, lib_sha):
