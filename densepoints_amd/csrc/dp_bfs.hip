@@ -24,17 +24,6 @@ namespace dpk {
 
 namespace {
 
-__device__ __forceinline__ bool bfs_cell(const dpg::ViewDev &v, const float *pos, double gs, int64_t &cell)
-{
-    double u, w;
-    dpg::project(v.P, pos[0], pos[1], pos[2], u, w);
-    const int64_t row = dpg::grid_coord(w, gs), col = dpg::grid_coord(u, gs);
-    if (col < 0 || col >= v.gw || row < 0 || row >= v.gh)
-        return false;
-    cell = v.grid_off + row * (int64_t)v.gw + col;
-    return true;
-}
-
 __device__ __forceinline__ int64_t bfs_chunk(int64_t n)
 {
     const int64_t per = (n + kBfsBlocks - 1) / kBfsBlocks;
@@ -64,7 +53,7 @@ __global__ __launch_bounds__(256) void bfs_claims_kernel(BfsArgs a)
                 const int b = __builtin_ctzll(bits);
                 bits &= bits - 1;
                 int64_t cell;
-                if (bfs_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell))
+                if (org_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell))
                     atomicMin(&a.grid[cell], seq);
             }
         }
@@ -87,7 +76,7 @@ __global__ __launch_bounds__(256) void bfs_claimk_init_kernel(BfsArgs a)
                     const int b = __builtin_ctzll(bits);
                     bits &= bits - 1;
                     int64_t cell;
-                    if (bfs_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell))
+                    if (org_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell))
                         pend[w] |= 1ull << b;
                 }
             }
@@ -111,7 +100,7 @@ __global__ __launch_bounds__(256) void bfs_claimk_round_kernel(BfsArgs a)
                 const int b = __builtin_ctzll(bits);
                 bits &= bits - 1;
                 int64_t cell;
-                if (bfs_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell) && a.grid[cell] < (uint32_t)a.k)
+                if (org_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell) && a.grid[cell] < (uint32_t)a.k)
                     atomicMin(&a.cellmin[cell], seq);
             }
         }
@@ -132,7 +121,7 @@ __global__ __launch_bounds__(256) void bfs_claimk_grant_kernel(BfsArgs a)
                 const int b = __builtin_ctzll(bits);
                 bits &= bits - 1;
                 int64_t cell = 0;
-                bfs_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell);
+                org_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell);
                 if (a.cellmin[cell] == seq) {
                     // the round's winner: one per cell, so plain updates
                     a.grid[cell] += 1u;
@@ -176,7 +165,7 @@ __global__ __launch_bounds__(256) void bfs_resolve_kernel(BfsArgs a)
                         const int b = __builtin_ctzll(bits);
                         bits &= bits - 1;
                         int64_t cell;
-                        if (bfs_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell) && a.grid[cell] == seq)
+                        if (org_cell(a.views[w * 64 + b], p.pos, a.grid_scale, cell) && a.grid[cell] == seq)
                             ++claims;
                     }
                 }
@@ -269,8 +258,7 @@ __global__ __launch_bounds__(kBfsBlocks) void bfs_scan_kernel(BfsArgs a)
 
 // -- append in sequence order + Patch::ComputeColor (patch.cpp:51-73): the
 // chunk's accepted candidates re-ranked by ballots, then one wave per record
-// (lane v projects into views v, v + 64; the BGR sums are exact integers in
-// any order, so the wave sum is the reference's fp64 sum)
+// (wave_color, unless the refine's epilogue coloured the candidates)
 __global__ __launch_bounds__(256) void bfs_append_kernel(BfsArgs a)
 {
     __shared__ uint32_t wc[4];
@@ -312,32 +300,10 @@ __global__ __launch_bounds__(256) void bfs_append_kernel(BfsArgs a)
                 continue;
             }
             const dp_patch *cp = a.cand + ci;
-            const float p0 = cp->pos[0], p1 = cp->pos[1], p2 = cp->pos[2];
-            uint32_t s0 = 0, s1 = 0, s2 = 0, nin = 0;
-            for (int v = lane; v < a.V; v += 64) {
-                const dpg::ViewDev &vw = a.views[v];
-                double u, w;
-                dpg::project(vw.P, p0, p1, p2, u, w);
-                if (dpg::inside(u, w, vw.W, vw.H)) {
-                    const uint32_t px = vw.img[(size_t)(int)w * (size_t)vw.pitch + (size_t)(int)u];
-                    s0 += px & 255u;
-                    s1 += (px >> 8) & 255u;
-                    s2 += (px >> 16) & 255u;
-                    ++nin;
-                }
-            }
-            for (int o = 32; o > 0; o >>= 1) {
-                s0 += __shfl_xor(s0, o);
-                s1 += __shfl_xor(s1, o);
-                s2 += __shfl_xor(s2, o);
-                nin += __shfl_xor(nin, o);
-            }
-            uint8_t c0 = 0, c1 = 0, c2 = 0;
-            if (nin) {
-                c0 = (uint8_t)((double)s2 / (double)nin);
-                c1 = (uint8_t)((double)s1 / (double)nin);
-                c2 = (uint8_t)((double)s0 / (double)nin);
-            }
+            // the refine's epilogue coloured the candidate already (kEpiColor),
+            // or Patch::ComputeColor here
+            const uint32_t rgb = (a.fused & kEpiColor) ? (cp->rgb[0] | (uint32_t)cp->rgb[1] << 8 | (uint32_t)cp->rgb[2] << 16)
+                                                       : wave_color(a.views, a.V, cp->pos, lane);
             constexpr int kWords = (int)(sizeof(dp_patch) / 4);
             constexpr int kSeq = (int)(offsetof(dp_patch, seq) / 4), kPar = (int)(offsetof(dp_patch, parent) / 4);
             constexpr int kRgb = (int)(offsetof(dp_patch, rgb) / 4);
@@ -349,7 +315,7 @@ __global__ __launch_bounds__(256) void bfs_append_kernel(BfsArgs a)
                 else if (lane == kPar)
                     wd = is_seed ? 0xFFFFFFFFu : (uint32_t)(parent0 + (ci >> 2));
                 else if (lane == kRgb)
-                    wd = (uint32_t)c0 | (uint32_t)c1 << 8 | (uint32_t)c2 << 16 | ((wd >> 24) | DP_PATCH_ACCEPTED) << 24;
+                    wd = rgb | ((wd >> 24) | DP_PATCH_ACCEPTED) << 24;
                 ((uint32_t *)(a.store + pos))[lane] = wd;
             }
         }
@@ -429,7 +395,9 @@ hipError_t launch_bfs_organize(const BfsArgs &a, hipStream_t s)
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const dim3 g((unsigned)(cus * 4)), b(256);
     if (a.k <= 1) {
-        hipLaunchKernelGGL(bfs_claims_kernel, g, b, 0, s, a);
+        // capacity 1: the claims pass, unless the refine's epilogue claimed
+        if (!(a.fused & kEpiClaims))
+            hipLaunchKernelGGL(bfs_claims_kernel, g, b, 0, s, a);
     } else {
         hipLaunchKernelGGL(bfs_claimk_init_kernel, g, b, 0, s, a);
         for (int r = 0; r < a.k; ++r) {

@@ -702,6 +702,22 @@ static dpk::RefineArgs refine_args(dp_ctx *c, dp_patch *d, int n, int cell, int 
     return a;
 }
 
+// the densify epilogue of a refine launch (dpk::kEpi* bits; claims at seq0 + index)
+static void set_epi(dp_ctx *c, dpk::RefineArgs &a, int epi, uint32_t seq0)
+{
+    a.epi = epi;
+    a.seq0 = seq0;
+    a.claim_grid = c->grid.p;
+    a.grid_scale = (double)c->opt.grid_scale;
+}
+
+// the epilogue a densify generation's refine runs: the colours always, the
+// claims when the organizer's capacity is 1 (k > 1 claims in rounds)
+static int densify_epi(const dp_ctx *c)
+{
+    return dpk::kEpiColor | (c->opt.max_patches_per_cell == 1 ? dpk::kEpiClaims : 0);
+}
+
 static int launch_timed(dp_ctx *c, const dpk::RefineArgs &a, hipStream_t s)
 {
     DP_HIP(c, hipEventRecord(c->e0, s));
@@ -921,7 +937,8 @@ static int set_state(dp_ctx *c, int slot, const dpk::GenDev &g, hipStream_t s)
 // the organizer of the generation in state slot `slot` over cand/okf (in
 // sequence order); writes the next generation's state into slot ^ 1.
 // cand_cap: the candidate buffers' capacity (the next generation stalls above it)
-static int organize_gen(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int slot, int64_t cand_cap, hipStream_t s)
+static int organize_gen(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int slot, int64_t cand_cap, hipStream_t s,
+                        int fused)
 {
     dpk::BfsArgs b{};
     b.views = c->d_views;
@@ -945,6 +962,7 @@ static int organize_gen(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int
     b.mbox = c->mbox.p;
     b.work = c->d_work;
     b.lpt_scratch = c->g_lpt_scratch;
+    b.fused = fused;
     DP_HIP(c, dpk::launch_bfs_organize(b, s));
     return DP_OK;
 }
@@ -1020,10 +1038,11 @@ static int refine_gen(dp_ctx *c, int slot, int64_t cap, hipStream_t s)
     const dpk::GenDev *g = c->gstate.p + slot;
     if (c->fopt.densify)
         return dp_fast_launch(c, c->cand.p, 0, c->opt.expand_cell_size, DP_MODE_FAST_REFINE, c->ok.p, c->store.p, s,
-                              0, nullptr, c->opt.max_pops, g);
+                              0, nullptr, c->opt.max_pops, g, densify_epi(c));
     dpk::RefineArgs a = refine_args(c, c->cand.p, (int)cap, c->opt.expand_cell_size, DP_MODE_EXPAND, c->ok.p);
     a.parents = c->store.p;
     a.gen = g;
+    set_epi(c, a, densify_epi(c), 0); // seq0 from the state
     DP_HIP(c, dpk::launch_refine(a, s));
     return DP_OK;
 }
@@ -1071,7 +1090,7 @@ static int run_generations(dp_ctx *c, int64_t max_gens, int64_t cap0, hipStream_
             if (rc != DP_OK)
                 return rc;
             DP_HIP(c, hipEventRecord(c->gev[2 * i + 1], s));
-            rc = organize_gen(c, c->cand.p, c->ok.p, slot, cap, s);
+            rc = organize_gen(c, c->cand.p, c->ok.p, slot, cap, s, densify_epi(c));
             if (rc != DP_OK)
                 return rc;
             slot ^= 1;
@@ -1191,9 +1210,11 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         // timed by its own event pair (the generations' are re-recorded)
         DP_HIP(c, hipEventRecord(c->gev[2 * kGenBatch], s));
         if (fast) {
-            rc = dp_fast_launch(c, c->cand.p, n, o.seed_cell_size, DP_MODE_FAST_REFINE, c->ok.p, nullptr, s);
+            rc = dp_fast_launch(c, c->cand.p, n, o.seed_cell_size, DP_MODE_FAST_REFINE, c->ok.p, nullptr, s, 0, nullptr,
+                                INT64_MAX, nullptr, densify_epi(c), 0);
         } else {
             dpk::RefineArgs a = refine_args(c, c->cand.p, n, o.seed_cell_size, DP_MODE_SEED, c->ok.p);
+            set_epi(c, a, densify_epi(c), 0);
             rc = launch_timed(c, a, s);
         }
         if (rc != DP_OK)
@@ -1201,7 +1222,7 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
         DP_HIP(c, hipEventRecord(c->gev[2 * kGenBatch + 1], s));
         // PatchOrganizer::SetSeeds: TryInsert in seed order (seq = seed index)
         c->g_lpt_scratch = nullptr;
-        rc = organize_gen(c, c->cand.p, c->ok.p, 0, cap, s);
+        rc = organize_gen(c, c->cand.p, c->ok.p, 0, cap, s, densify_epi(c));
         if (rc != DP_OK)
             return rc;
         c->g_slot = 1;
@@ -1221,10 +1242,10 @@ extern "C" int dp_densify(dp_ctx *c, const double *seeds, int n, const dp_patch 
                 rc = take_refine_ms(c, &c->g_st.refine_ms);
                 if (rc == DP_OK)
                     rc = dp_fast_launch(c, c->cand.p, nc, o.expand_cell_size, DP_MODE_FAST_REFINE, c->ok.p, c->store.p,
-                                        s, g.head, nullptr, o.max_pops);
+                                        s, g.head, nullptr, o.max_pops, nullptr, densify_epi(c), g.seq0);
                 c->g_time_pending = true;
                 if (rc == DP_OK)
-                    rc = organize_gen(c, c->cand.p, c->ok.p, c->g_slot, INT64_MAX, s);
+                    rc = organize_gen(c, c->cand.p, c->ok.p, c->g_slot, INT64_MAX, s, densify_epi(c));
                 if (rc == DP_OK)
                     rc = read_state(c, c->g_slot ^ 1, s, &g, mb);
                 c->g_slot ^= 1;
@@ -1285,14 +1306,14 @@ static int check_gen(dp_ctx *c, const dp_generation *gen, const char *who)
 // candidate in sequence order, ordered before it on s), ending in the
 // generation's one status read; advances *gen.
 static int commit_on_stream(dp_ctx *c, dp_generation *gen, const dp_patch *cp, const uint8_t *op, int64_t nc,
-                            hipStream_t s, int64_t *exchanged = nullptr)
+                            hipStream_t s, int64_t *exchanged = nullptr, int fused = 0)
 {
     int rc = reserve_organizer(c, std::max<int64_t>(nc, 1));
     if (rc != DP_OK)
         return rc;
     c->g_lpt_scratch = nullptr;
     // host-driven generations size their refines on the host: no stall bound
-    rc = organize_gen(c, cp, op, c->g_slot, INT64_MAX, s);
+    rc = organize_gen(c, cp, op, c->g_slot, INT64_MAX, s, fused);
     dpk::GenDev g{};
     unsigned long long mb[8];
     if (rc != DP_OK || (rc = read_state(c, c->g_slot ^ 1, s, &g, mb)) != DP_OK ||
@@ -1433,7 +1454,7 @@ extern "C" int dp_densify_partition_stats(dp_ctx *c, int64_t *stats_out)
 // (seed patches by index in generation 0; Expand::ExpandPatch of the queue
 // entries head + items[k] otherwise)
 static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const int64_t *d_items, int64_t n,
-                                     dp_patch *work, uint8_t *okp, hipStream_t s)
+                                     dp_patch *work, uint8_t *okp, hipStream_t s, int epi = 0)
 {
     const int64_t nc64 = n * gen->per_item;
     if (nc64 > INT32_MAX)
@@ -1447,14 +1468,18 @@ static int densify_refine_items_impl(dp_ctx *c, const dp_generation *gen, const 
     if (gen->index == 0) {
         DP_HIP(c, dpk::launch_gather_patches(c->seedp.p, d_items, n, work, s));
         a = refine_args(c, work, nc, gen->cell, DP_MODE_SEED, okp);
-        rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, nullptr, s) : launch_timed(c, a, s);
+        set_epi(c, a, epi, 0);
+        rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, nullptr, s, 0, nullptr, INT64_MAX,
+                                   nullptr, epi, 0)
+                  : launch_timed(c, a, s);
     } else {
         a = refine_args(c, work, nc, gen->cell, DP_MODE_EXPAND, okp);
         a.parents = c->store.p;
         a.parent0 = gen->head;
         a.items = d_items;
+        set_epi(c, a, epi, 0);
         rc = fast ? dp_fast_launch(c, work, nc, gen->cell, DP_MODE_FAST_REFINE, okp, c->store.p, s, gen->head, d_items,
-                                   c->opt.max_pops)
+                                   c->opt.max_pops, nullptr, epi, 0)
                   : launch_timed(c, a, s);
     }
     if (rc != DP_OK)
@@ -1534,7 +1559,9 @@ extern "C" int dp_densify_refine_share_async(dp_ctx *c, const dp_generation *gen
     if (nc > 0) {
         DP_HIP(c, c->wcand.reserve(nc));
         DP_HIP(c, c->wok.reserve(nc));
-        rc = densify_refine_items_impl(c, gen, d_items, n, c->wcand.p, c->wok.p, s);
+        // the owner colours its accepted candidates (Patch::ComputeColor off the
+        // replicated commit); claims stay with the commit, which sees every rank's
+        rc = densify_refine_items_impl(c, gen, d_items, n, c->wcand.p, c->wok.p, s, dpk::kEpiColor);
         if (rc != DP_OK)
             return rc;
     }
@@ -1563,7 +1590,8 @@ extern "C" int dp_densify_commit_gathered_device(dp_ctx *c, dp_generation *gen, 
     }
     DP_HIP(c, dpk::launch_scatter_slots(d_recs, stride, world, nc, c->cand.p, c->ok.p, c->mbox.p + 4, s));
     int64_t ex = 0;
-    rc = commit_on_stream(c, gen, c->cand.p, c->ok.p, nc, s, &ex);
+    // the slots' records were coloured by their owners' refines (dp_densify_refine_share_async)
+    rc = commit_on_stream(c, gen, c->cand.p, c->ok.p, nc, s, &ex, dpk::kEpiColor);
     if (rc == DP_OK && exchanged_out)
         *exchanged_out = ex;
     return rc;

@@ -185,9 +185,10 @@ struct dp_ctx {
 // d_parents[parent0 + (items ? items[k] : k)], k < n / 4, of which only those
 // with a parent index below max_pops expand (dp_densify's pop cap)
 // gen: a device-resident BFS generation (n and parent0 read on the device)
+// epi: the densify epilogue (dpk::kEpi* bits; claims at seq0 + index into c->grid)
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
                    hipStream_t s, int64_t parent0 = 0, const int64_t *items = nullptr,
-                   int64_t max_pops = INT64_MAX, const dpk::GenDev *gen = nullptr);
+                   int64_t max_pops = INT64_MAX, const dpk::GenDev *gen = nullptr, int epi = 0, uint32_t seq0 = 0);
 
 static inline int fail(dp_ctx *c, int code, const std::string &msg)
 {

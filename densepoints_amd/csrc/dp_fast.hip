@@ -76,6 +76,12 @@ struct FastArgs {
                              // when the launch has fewer than 4 candidates per resident wave
     uint32_t resident;       // resident waves of the launch (the kGen instances pick chunk on the device)
     const GenDev *gen;       // device-resident BFS generation: n and parent0 read here (kGen)
+    // densify epilogue (kEpi* bits, dp_internal.h): colour / claims of the
+    // candidates that pass the filter, a claim's seq = (gen ? gen->seq0 : seq0) + index
+    int32_t epi;
+    uint32_t seq0;
+    uint32_t *claim_grid;
+    double grid_scale;
 };
 
 // per evaluation, per staged view: A.xyz 2^23+umax | B1.xyz 2^23+vmax | B2.xyz
@@ -1619,6 +1625,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FastOcc<kAre
                 p.flags &= (uint8_t)~DP_PATCH_ACCEPTED;
         }
         wave_sync();
+        // densify epilogue: colour / claims of a candidate that passed the filter
+        // (the arguments read at their use: DP_FKARG)
+        if (ok && DP_FKARG(int32_t, epi) != 0) {
+            typedef uint32_t *u32_ptr; // DP_FKARG's type is one token
+            const int epi = DP_FKARG(int32_t, epi);
+            const uint32_t rgb = refine_epilogue(a.views, a.V, p.pos[0], p.pos[1], p.pos[2], p.vis[0], p.vis[1], epi,
+                                                 DP_FKARG(double, grid_scale), DP_FKARG(u32_ptr, claim_grid),
+                                                 (kGen ? a.gen->seq0 : DP_FKARG(uint32_t, seq0)) + idx, lane);
+            wave_sync();
+            if ((epi & kEpiColor) && lane == 0) {
+                p.rgb[0] = (uint8_t)rgb;
+                p.rgb[1] = (uint8_t)(rgb >> 8);
+                p.rgb[2] = (uint8_t)(rgb >> 16);
+            }
+            wave_sync();
+        }
         wave_evals += p.evals;
         wave_patches += 1;
         if (lane == 0) {
@@ -1914,7 +1936,8 @@ template <int B> static hipError_t fast_dispatch(int N, const dpk::FastArgs &a, 
 }
 
 int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *acc, const dp_patch *d_parents,
-                   hipStream_t s, int64_t parent0, const int64_t *items, int64_t max_pops, const dpk::GenDev *gen)
+                   hipStream_t s, int64_t parent0, const int64_t *items, int64_t max_pops, const dpk::GenDev *gen,
+                   int epi, uint32_t seq0)
 {
     int rc = ensure_gray(c);
     if (rc != DP_OK)
@@ -1938,6 +1961,10 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     a.items = items;
     a.max_pops = max_pops;
     a.gen = gen;
+    a.epi = epi;
+    a.seq0 = seq0;
+    a.claim_grid = c->grid.p;
+    a.grid_scale = (double)c->opt.grid_scale;
     // the InitRelatedImages thresholds as cosines, by the host libm (the
     // spec's), rounded to fp32, and their fp32 squares
     a.cvis = (float)std::cos(c->opt.visible_angle);

@@ -17,6 +17,88 @@ constexpr int kWorkCounters = 8 * kWorkStride;
 
 struct GenDev;
 
+// ---- the organizer's per-record work, shared by the organizer kernels
+// (dp_bfs.hip) and the refine kernels' densify epilogue ------------------------
+
+// PatchGrid cell of a record centre in one view (patch_organizer.cpp:42-65):
+// false when it projects outside the view's grid
+__device__ __forceinline__ bool org_cell(const dpg::ViewDev &v, const float *pos, double gs, int64_t &cell)
+{
+    double u, w;
+    dpg::project(v.P, pos[0], pos[1], pos[2], u, w);
+    const int64_t row = dpg::grid_coord(w, gs), col = dpg::grid_coord(u, gs);
+    if (col < 0 || col >= v.gw || row < 0 || row >= v.gh)
+        return false;
+    cell = v.grid_off + row * (int64_t)v.gw + col;
+    return true;
+}
+
+// Patch::ComputeColor (patch.cpp:51-73) by one wave: lane l projects the centre
+// into views l, l + 64; the BGR sums are exact integers in any order, so the
+// wave sum is the reference's fp64 sum.  Returns R | G << 8 | B << 16 (the
+// record's rgb bytes) in every lane.
+__device__ __forceinline__ uint32_t wave_color(const dpg::ViewDev *views, int V, const float *pos, int lane)
+{
+    const float p0 = pos[0], p1 = pos[1], p2 = pos[2];
+    uint32_t s0 = 0, s1 = 0, s2 = 0, nin = 0;
+    for (int v = lane; v < V; v += 64) {
+        const dpg::ViewDev &vw = views[v];
+        double u, w;
+        dpg::project(vw.P, p0, p1, p2, u, w);
+        if (dpg::inside(u, w, vw.W, vw.H)) {
+            const uint32_t px = vw.img[(size_t)(int)w * (size_t)vw.pitch + (size_t)(int)u];
+            s0 += px & 255u;
+            s1 += (px >> 8) & 255u;
+            s2 += (px >> 16) & 255u;
+            ++nin;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_xor(s0, o);
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+        nin += __shfl_xor(nin, o);
+    }
+    if (!nin)
+        return 0u;
+    const uint32_t c0 = (uint8_t)((double)s2 / (double)nin), c1 = (uint8_t)((double)s1 / (double)nin),
+                   c2 = (uint8_t)((double)s0 / (double)nin);
+    return c0 | c1 << 8 | c2 << 16;
+}
+
+// capacity-1 claims of one record by one wave (PatchGrid::TryInsert's first
+// come, first served as atomicMin(seq)): lane l claims its cell in views l and
+// 64 + l when they are visible
+__device__ __forceinline__ void wave_claims(const dpg::ViewDev *views, const float *pos, uint64_t vis0, uint64_t vis1,
+                                            double gs, uint32_t *grid, uint32_t seq, int lane)
+{
+    int64_t cell;
+    if (((vis0 >> lane) & 1ull) && org_cell(views[lane], pos, gs, cell))
+        atomicMin(&grid[cell], seq);
+    if (((vis1 >> lane) & 1ull) && org_cell(views[64 + lane], pos, gs, cell))
+        atomicMin(&grid[cell], seq);
+}
+
+// densify epilogue of a refine launch (RefineArgs::epi, FastArgs::epi): the
+// organizer work a refined candidate that passed the filter can do at once,
+// by the wave that refined it
+constexpr int kEpiColor = 1;  // Patch::ComputeColor into the record's rgb
+constexpr int kEpiClaims = 2; // capacity-1 claims at seq0 + index (the organizer skips its claims pass)
+
+// The epilogue as a call, not inlined: its fp64 projections would otherwise
+// join the refine kernels' register allocation (the parity kernel's spills
+// grew 4 -> 20 VGPRs inlined); as a call only the values live across it are
+// saved, once per candidate.  Returns the colour (wave_color) or 0.
+static __device__ __noinline__ uint32_t refine_epilogue(const dpg::ViewDev *views, int V, float p0, float p1,
+                                                        float p2, uint64_t vis0, uint64_t vis1, int epi, double gs,
+                                                        uint32_t *grid, uint32_t seq, int lane)
+{
+    const float pf[3] = {p0, p1, p2};
+    if (epi & kEpiClaims)
+        wave_claims(views, pf, vis0, vis1, gs, grid, seq, lane);
+    return (epi & kEpiColor) ? wave_color(views, V, pf, lane) : 0u;
+}
+
 // Arguments of the fused refine kernel (one wavefront per patch).
 struct RefineArgs {
     const dpg::ViewDev *views;
@@ -51,6 +133,12 @@ struct RefineArgs {
     // gen->head are read on the device (the refine_kernel<.., kGen = true>
     // instances), so a generation is queued before its size is known
     const GenDev *gen;
+    // densify epilogue (kEpi* bits): colour and/or claims of the candidates that
+    // pass the filter; a claim's seq is (gen ? gen->seq0 : seq0) + index
+    int32_t epi;
+    uint32_t seq0;
+    uint32_t *claim_grid;
+    double grid_scale;
 };
 constexpr int kLptBuckets = 129; // visible-view counts 0..128
 
@@ -98,6 +186,7 @@ struct BfsArgs {
     unsigned long long *mbox;  // status words (see dp_ctx::mbox); [7] append overflow
     uint32_t *work;            // the refine's dequeue counters, zeroed for the next generation
     uint32_t *lpt_scratch;     // the LPT order's counters, zeroed for the next generation
+    int32_t fused;             // kEpi* bits the generation's refine already did (claims: k = 1 only)
 };
 constexpr int kBfsBlocks = 1024; // chunks of the generation's scan (one block each)
 

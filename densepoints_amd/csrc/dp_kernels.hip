@@ -1519,7 +1519,18 @@ __global__ DP_REFINE_BOUNDS void refine_kernel(RefineArgs a)
         L.stamp[7] += __builtin_amdgcn_s_memtime() - _t_patch;
         L.stamp[6] += 1;
 #endif
+        // densify epilogue: colour / claims of a candidate that passed the filter
+        uint32_t rgb = 0;
+        const bool epi = ok && live && a.epi != 0;
+        if (epi)
+            rgb = refine_epilogue(a.views, a.V, (float)L.X[0], (float)L.X[1], (float)L.X[2], L.vis[0], L.vis[1], a.epi,
+                                  a.grid_scale, a.claim_grid, (kGen ? a.gen->seq0 : a.seq0) + idx, lane);
         if (lane == 0) {
+            if (epi && (a.epi & kEpiColor)) {
+                out->rgb[0] = (uint8_t)rgb;
+                out->rgb[1] = (uint8_t)(rgb >> 8);
+                out->rgb[2] = (uint8_t)(rgb >> 16);
+            }
             if (live) {
                 for (int i = 0; i < 3; ++i) {
                     out->pos[i] = (float)L.X[i];

@@ -183,7 +183,7 @@ class _DeviceBuffers:
 
 
 def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64,
-                               probe_worlds: tuple = (), one_rank_exchange: bool = False):
+                               probe_worlds: tuple = (), one_rank_exchange: bool = False, copy_result: bool = True):
     """dp_densify with every generation partitioned by reference-view super-tile,
     the records in HBM, only the ACCEPTED candidates exchanged and ONE host
     wait per generation.  Per generation, all queued on the torch current
@@ -200,11 +200,14 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
       4. dp_densify_commit_gathered_device scatters the slots to sequence
          order, commits the replicated organizer step and reads the next
          generation's state: the one host wait.
-    With one rank there is nothing to partition or exchange: after the seed
-    generation the expansion generations run device-resident, eight per host
-    wait (dp_densify_run), unless one_rank_exchange keeps the multi-rank
-    protocol (slots, scatter) at world 1 for measurement.  Every rank's store
-    equals dp_densify bit for bit.  stats gains "partition" (items, largest
+    With one rank there is nothing to partition or exchange: the whole densify
+    is dp_densify (seed generation, then the expansion generations
+    device-resident, eight per host wait), unless one_rank_exchange keeps the
+    multi-rank protocol (slots, scatter) at world 1 for measurement, or
+    probe_worlds asks for the partitions of every generation.  Every rank's
+    store equals dp_densify bit for bit.  copy_result=False returns the store
+    as a view of the library's pinned result buffer (valid until the engine's
+    next densify) instead of a copy.  stats gains "partition" (items, largest
     share, items in split tiles, tiles per generation), "accepted" (records
     exchanged), "gathered_bytes", "phase_ms" (host time: begin; launch = the
     queued partition, refine and exchange calls; commit = up to the status
@@ -213,6 +216,14 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
     records} of the partitions those world sizes would use (statistics only)."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
+    if world == 1 and not one_rank_exchange and not probe_worlds:
+        t = time.perf_counter()
+        patches, stats = eng.densify(seeds_xyz, copy=copy_result)
+        stats["phase_ms"] = {"densify": round((time.perf_counter() - t) * 1e3, 2)}
+        stats["partition"] = []
+        stats["gathered_bytes"] = [0]
+        stats["accepted"] = []
+        return patches, stats
     rccl = dist is not None and dist.get_backend() == "nccl"
     rec = PATCH_DTYPE.itemsize
     stream = torch.cuda.current_stream(device)
@@ -260,7 +271,7 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
         parts.append(_part_record(eng, counts))
         gathered.append(world * (stride + 1) * rec if dist is not None else 0)
         accepted.append(n_ex)
-    patches, stats = eng.densify_result()
+    patches, stats = eng.densify_result(copy=copy_result)
     stats = _reduce_stats(stats, dist, device)
     stats["phase_ms"] = {k: round(v * 1e3, 2) for k, v in ph.items()}
     stats["partition"] = parts

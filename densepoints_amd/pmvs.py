@@ -144,6 +144,17 @@ def empty_patches(n: int) -> np.ndarray:
     return np.zeros(n, dtype=PATCH_DTYPE)
 
 
+def result_array(addr, n: int, copy: bool = True) -> np.ndarray:
+    """n dp_patch records at a library-owned address (a densify's pinned result
+    buffer) as a numpy array: a copy, or (copy=False) a view that stays valid
+    until the library reuses the buffer"""
+    if not n:
+        return empty_patches(0)
+    buf = (ctypes.c_char * (n * PATCH_DTYPE.itemsize)).from_address(addr)
+    view = np.frombuffer(buf, dtype=PATCH_DTYPE, count=n)
+    return view.copy() if copy else view
+
+
 def visible_list(mask) -> list[int]:
     """Bitmask (u64[2]) -> ascending view list (Patch::GetTrullyVisibleImages)."""
     out = []
@@ -351,18 +362,19 @@ class Engine:
         """Optimization::FilterByErrorMeasurement over a batch."""
         return self.refine(patches, cell, N.MODE_FILTER)
 
-    def densify(self, seeds_xyz: np.ndarray):
+    def densify(self, seeds_xyz: np.ndarray, copy: bool = True):
+        """dp_densify: (patches, stats).  copy=False returns a view of the
+        library's pinned result buffer instead of a copy -- valid until the next
+        densify on this engine, the C ABI's own contract for *out
+        (include/densepoints.h dp_densify)."""
         seeds = np.ascontiguousarray(seeds_xyz, dtype=np.float64).reshape(-1, 3)
         out = ctypes.c_void_p()
         n = ctypes.c_int64()
         st = N.DpDensifyStats()
         self._check(lib.dp_densify(self._ctx, ptr(seeds), len(seeds), ctypes.byref(out), ctypes.byref(n),
                                    ctypes.byref(st)))
-        res = empty_patches(n.value)
-        if n.value:
-            ctypes.memmove(res.ctypes.data, out.value, n.value * PATCH_DTYPE.itemsize)
         stats = {name: getattr(st, name) for name, _ in N.DpDensifyStats._fields_}
-        return res, stats
+        return result_array(out.value, n.value, copy), stats
 
 
     # ---- one generation at a time (multi-GPU partitioning; dist.py) ----
@@ -443,16 +455,14 @@ class Engine:
                                                           ctypes.byref(ex)))
         return int(ex.value)
 
-    def densify_result(self):
+    def densify_result(self, copy: bool = True):
+        """dp_densify_result: (patches, stats); copy=False as in densify()."""
         out = ctypes.c_void_p()
         n = ctypes.c_int64()
         st = N.DpDensifyStats()
         self._check(lib.dp_densify_result(self._ctx, ctypes.byref(out), ctypes.byref(n), ctypes.byref(st)))
-        res = empty_patches(n.value)
-        if n.value:
-            ctypes.memmove(res.ctypes.data, out.value, n.value * PATCH_DTYPE.itemsize)
         stats = {name: getattr(st, name) for name, _ in N.DpDensifyStats._fields_}
-        return res, stats
+        return result_array(out.value, n.value, copy), stats
 
 
 class PMVS:
