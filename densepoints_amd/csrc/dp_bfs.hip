@@ -350,9 +350,11 @@ __global__ __launch_bounds__(256) void compact_slot_kernel(const dp_patch *cand,
 }
 
 // -- the gathered slots to their generation positions; block (x, r) covers
-// rank r's records, block (0, 0) also totals the exchanged records
-__global__ __launch_bounds__(256) void scatter_slots_kernel(const dp_patch *recs, int64_t stride, int world, int64_t nc,
-                                                            dp_patch *cand, uint8_t *ok, unsigned long long *exchanged)
+// rank r's records, block (0, 0) also totals the exchanged records.  With a
+// grid (capacity 1) each record also claims its cells at seq0 + position (the
+// organizer then skips its claims pass: one read of the gathered records).
+__global__ void scatter_slots_kernel(const dp_patch *recs, int64_t stride, int world, int64_t nc, dp_patch *cand,
+                                     uint8_t *ok, unsigned long long *exchanged, ScatterClaims sc)
 {
     const int r = blockIdx.y;
     const dp_patch *slot = recs + (int64_t)r * (stride + 1);
@@ -363,6 +365,7 @@ __global__ __launch_bounds__(256) void scatter_slots_kernel(const dp_patch *recs
             t += (unsigned long long)*(const int64_t *)(recs + (int64_t)q * (stride + 1));
         *exchanged = t;
     }
+    const uint32_t seq0 = sc.grid ? sc.gen->seq0 : 0u;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt && i < stride;
          i += (int64_t)gridDim.x * blockDim.x) {
         const dp_patch &p = slot[1 + i];
@@ -370,6 +373,18 @@ __global__ __launch_bounds__(256) void scatter_slots_kernel(const dp_patch *recs
         if ((int64_t)pos < nc) {
             cand[pos] = p;
             ok[pos] = 1;
+            if (sc.grid) {
+                for (int w = 0; w < 2; ++w) {
+                    uint64_t bits = p.vis[w];
+                    while (bits) {
+                        const int b = __builtin_ctzll(bits);
+                        bits &= bits - 1;
+                        int64_t cell;
+                        if (org_cell(sc.views[w * 64 + b], p.pos, sc.grid_scale, cell))
+                            atomicMin(&sc.grid[cell], seq0 + pos);
+                    }
+                }
+            }
         }
     }
 }
@@ -426,14 +441,14 @@ hipError_t launch_compact_slot(const dp_patch *cand, const uint8_t *acc, const i
 }
 
 hipError_t launch_scatter_slots(const dp_patch *recs, int64_t stride, int world, int64_t nc, dp_patch *cand,
-                                uint8_t *ok, unsigned long long *exchanged, hipStream_t s)
+                                uint8_t *ok, unsigned long long *exchanged, const ScatterClaims &sc, hipStream_t s)
 {
     if (world <= 0)
         return hipSuccess;
     int64_t bx = (stride + 255) / 256;
     bx = bx < 1 ? 1 : bx > 1024 ? 1024 : bx;
     hipLaunchKernelGGL(scatter_slots_kernel, dim3((unsigned)bx, (unsigned)world), dim3(256), 0, s, recs, stride, world,
-                       nc, cand, ok, exchanged);
+                       nc, cand, ok, exchanged, sc);
     return hipGetLastError();
 }
 

@@ -1396,13 +1396,26 @@ static int partition_impl(dp_ctx *c, const dp_generation *gen, int world, int ti
     DP_HIP(c, c->oiota.reserve((size_t)n));
     DP_HIP(c, c->porder.reserve((size_t)n));
     unsigned long long *stats = c->mbox.p + 2;
-    DP_HIP(c, dpk::launch_tile_keys(c->d_views, items, n, (double)tile_px, c->tkeys.p, c->oiota.p, stats, s));
+    // the dense key's range: tile rows / columns of the largest view, clamped
+    // to [-1, TY] x [-1, TX]; the sort covers only the bits that range needs
+    int64_t wmax = 1, hmax = 1;
+    for (const auto &v : c->hv) {
+        wmax = std::max<int64_t>(wmax, v.W);
+        hmax = std::max<int64_t>(hmax, v.H);
+    }
+    const int64_t tx_max = (wmax + tile_px - 1) / tile_px, ty_max = (hmax + tile_px - 1) / tile_px;
+    const unsigned __int128 kmax = (unsigned __int128)c->V * (unsigned __int128)(ty_max + 2) * (unsigned __int128)(tx_max + 2);
+    int bits = 1;
+    while (bits < 64 && ((unsigned __int128)1 << bits) < kmax)
+        ++bits;
+    DP_HIP(c, dpk::launch_tile_keys(c->d_views, items, n, (double)tile_px, tx_max, ty_max, c->tkeys.p, c->oiota.p, stats,
+                                    s));
     size_t tmp = 0;
     DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, c->tkeys.p, c->okeys.p, c->oiota.p, c->porder.p, (int)n,
-                                                 0, 64, s));
+                                                 0, bits, s));
     DP_HIP(c, c->scan_tmp.reserve(tmp + 16));
     DP_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->scan_tmp.p, tmp, c->tkeys.p, c->okeys.p, c->oiota.p, c->porder.p,
-                                                 (int)n, 0, 64, s));
+                                                 (int)n, 0, bits, s));
     DP_HIP(c, dpk::launch_partition_stats(c->okeys.p, n, world, stats, s));
     if (!sync) {
         c->part_pending = true;
@@ -1588,10 +1601,16 @@ extern "C" int dp_densify_commit_gathered_device(dp_ctx *c, dp_generation *gen, 
         // every other candidate of the generation failed the refine's filter
         DP_HIP(c, hipMemsetAsync(c->ok.p, 0, (size_t)nc, s));
     }
-    DP_HIP(c, dpk::launch_scatter_slots(d_recs, stride, world, nc, c->cand.p, c->ok.p, c->mbox.p + 4, s));
+    // capacity 1: the scatter claims the records' cells as it places them
+    const bool claims = c->opt.max_patches_per_cell == 1;
+    DP_HIP(c, c->gstate.reserve(2));
+    const dpk::ScatterClaims sc{c->d_views, claims ? c->grid.p : nullptr, (double)c->opt.grid_scale,
+                                c->gstate.p + c->g_slot};
+    DP_HIP(c, dpk::launch_scatter_slots(d_recs, stride, world, nc, c->cand.p, c->ok.p, c->mbox.p + 4, sc, s));
     int64_t ex = 0;
     // the slots' records were coloured by their owners' refines (dp_densify_refine_share_async)
-    rc = commit_on_stream(c, gen, c->cand.p, c->ok.p, nc, s, &ex, dpk::kEpiColor);
+    rc = commit_on_stream(c, gen, c->cand.p, c->ok.p, nc, s, &ex,
+                          dpk::kEpiColor | (claims ? dpk::kEpiClaims : 0));
     if (rc == DP_OK && exchanged_out)
         *exchanged_out = ex;
     return rc;

@@ -203,9 +203,16 @@ hipError_t launch_bfs_set_state(GenDev *dst, const GenDev &v, hipStream_t s);
 hipError_t launch_compact_slot(const dp_patch *cand, const uint8_t *acc, const int64_t *items, int64_t n, int per,
                                dp_patch *slot, hipStream_t s);
 // the gathered rank slots (world of them, stride records + header each) to
-// their generation positions; ok must be zeroed first
+// their generation positions; ok must be zeroed first.  grid != null: each
+// record also claims its cells (capacity 1) at gen->seq0 + its position
+struct ScatterClaims {
+    const dpg::ViewDev *views;
+    uint32_t *grid;
+    double grid_scale;
+    const GenDev *gen;
+};
 hipError_t launch_scatter_slots(const dp_patch *recs, int64_t stride, int world, int64_t nc, dp_patch *cand,
-                                uint8_t *ok, unsigned long long *exchanged, hipStream_t s);
+                                uint8_t *ok, unsigned long long *exchanged, const ScatterClaims &sc, hipStream_t s);
 
 // one image plane of a pyramid level (BGRA8, B in the low byte)
 struct PyrPlane {
@@ -246,8 +253,8 @@ hipError_t launch_seed_patches(const dpg::ViewDev *views, int V, const double *x
 // multi-GPU partition of a generation's items: super-tile keys
 // (ref, tile row, tile column) of the items' centres, and the statistics of a
 // cut of the key-sorted order at lo[1..world-1] (stats[2], zeroed here)
-hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
-                            uint64_t *key, int64_t *iota, unsigned long long *stats, hipStream_t s);
+hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile, int64_t tx_max,
+                            int64_t ty_max, uint64_t *key, int64_t *iota, unsigned long long *stats, hipStream_t s);
 hipError_t launch_partition_stats(const uint64_t *key, int64_t n, int world, unsigned long long *stats, hipStream_t s);
 hipError_t launch_gather_patches(const dp_patch *src, const int64_t *idx, int64_t n, dp_patch *dst, hipStream_t s);
 } // namespace dpk

@@ -1866,23 +1866,24 @@ hipError_t launch_seed_patches(const dpg::ViewDev *views, int V, const double *x
     return hipGetLastError();
 }
 
-// Super-tile key of each item: the centre projected into its
-// reference view, key = ref << 56 | ty' << 28 | tx' with ty = floor(v / tile),
-// tx = floor(u / tile) clamped to [-2^27, 2^27) and biased by 2^27 (NaN and
-// out-of-range coordinates count as 0).  Sorting by key orders the items by
-// (reference view, tile row, tile column); the partition cuts that order into
-// `world` contiguous equal shares.
-__device__ __forceinline__ uint64_t tile_coord(double q)
+// Super-tile key of each item (spec in include/densepoints.h): the
+// centre projected into its reference view, ty = floor(v / tile) and tx =
+// floor(u / tile) clamped to [-1, TY] / [-1, TX] (NaN and |q| >= 2e9 count as
+// 0), key = (ref (TY + 2) + ty + 1) (TX + 2) + tx + 1: dense, so the sort
+// covers only the key's ceil(log2(V (TY + 2) (TX + 2))) low bits.  Sorting by
+// key orders the items by (reference view, tile row, tile column); the
+// partition cuts that order into `world` contiguous equal shares.
+__device__ __forceinline__ uint64_t tile_coord(double q, int64_t tmax)
 {
     int64_t t = 0;
     if (q > -2.0e9 && q < 2.0e9)
         t = (int64_t)floor(q);
-    t = t < -(1ll << 27) ? -(1ll << 27) : t > (1ll << 27) - 1 ? (1ll << 27) - 1 : t;
-    return (uint64_t)(t + (1ll << 27));
+    t = t < -1 ? -1 : t > tmax ? tmax : t;
+    return (uint64_t)(t + 1);
 }
 
-__global__ void tile_keys_kernel(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
-                                 uint64_t *key, int64_t *iota, unsigned long long *stats)
+__global__ void tile_keys_kernel(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile, int64_t tx_max,
+                                 int64_t ty_max, uint64_t *key, int64_t *iota, unsigned long long *stats)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) // the partition statistics' counters (partition_stats_kernel adds to them)
@@ -1894,7 +1895,8 @@ __global__ void tile_keys_kernel(const dpg::ViewDev *views, const dp_patch *item
     const dpg::ViewDev &v = views[p.ref];
     double u, w;
     dpg::project(v.P, (double)p.pos[0], (double)p.pos[1], (double)p.pos[2], u, w);
-    key[i] = (uint64_t)(p.ref & 0xffu) << 56 | tile_coord(w / tile) << 28 | tile_coord(u / tile);
+    key[i] = ((uint64_t)p.ref * (uint64_t)(ty_max + 2) + tile_coord(w / tile, ty_max)) * (uint64_t)(tx_max + 2) +
+             tile_coord(u / tile, tx_max);
 }
 
 // partition statistics over the key-sorted items: stats[0] = distinct tiles,
@@ -1925,13 +1927,13 @@ __global__ void partition_stats_kernel(const uint64_t *key, int64_t n, int world
     }
 }
 
-hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile,
-                            uint64_t *key, int64_t *iota, unsigned long long *stats, hipStream_t s)
+hipError_t launch_tile_keys(const dpg::ViewDev *views, const dp_patch *items, int64_t n, double tile, int64_t tx_max,
+                            int64_t ty_max, uint64_t *key, int64_t *iota, unsigned long long *stats, hipStream_t s)
 {
     if (n <= 0)
         return hipSuccess;
     hipLaunchKernelGGL(tile_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, views, items, n, tile,
-                       key, iota, stats);
+                       tx_max, ty_max, key, iota, stats);
     return hipGetLastError();
 }
 

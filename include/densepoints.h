@@ -242,11 +242,13 @@ int dp_densify_run(dp_ctx *ctx, dp_generation *gen, int32_t max_generations);
  * the 8 GPUs").  owner_out[i] (host, gen->items) = the rank that
  * refines item i.  Partition spec (round 4; round 3 hashed the tiles and fell
  * back to round robin above 1.1x the mean share):
- *  - key(i) = ref << 56 | ty' << 28 | tx', the item's centre (seed patch or
- *    parent) projected into its reference view (fp64, ((p0 x + p1 y) + p2 z) +
- *    p3, one division per coordinate), ty = floor(v / tile_px), tx =
- *    floor(u / tile_px) (NaN or |q| >= 2e9 -> 0), clamped to [-2^27, 2^27) and
- *    biased by 2^27 (ty', tx' < 2^28; ref < 256);
+ *  - key(i) = (ref (TY + 2) + ty + 1) (TX + 2) + tx + 1 (round 6; dense, so
+ *    the device sort covers ceil(log2(V (TY + 2) (TX + 2))) bits), from the
+ *    item's centre (seed patch or parent) projected into its reference view
+ *    (fp64, ((p0 x + p1 y) + p2 z) + p3, one division per coordinate):
+ *    ty = floor(v / tile_px), tx = floor(u / tile_px) (NaN or |q| >= 2e9 -> 0),
+ *    clamped to [-1, TY] and [-1, TX], TX = ceil(Wmax / tile_px), TY =
+ *    ceil(Hmax / tile_px) over the largest view sizes;
  *  - the items stable-sorted by key (ties: ascending item index) -- reference
  *    view, then super-tile row, then column -- and that order cut into `world`
  *    contiguous shares: rank r refines sorted positions [lo_r, lo_{r+1}),

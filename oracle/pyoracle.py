@@ -371,10 +371,11 @@ class GenerationEngine:
     def densify_owners(self, g, world, tile_px=64):
         """Owner rank per item (include/densepoints.h, partition spec): the
         centre projected into the reference view (fp64, ((p0 x + p1 y) + p2 z)
-        + p3 then one division), key = ref << 56 | ty' << 28 | tx' (tile
-        coordinates floored, clamped to [-2^27, 2^27), biased), items stable-
-        sorted by key and cut into `world` contiguous shares lo_r = floor(r n /
-        world).  Returns (owners, False); densify_partition_stats() gives the
+        + p3 then one division), tile coordinates floored and clamped to
+        [-1, TY] / [-1, TX] (TX, TY: tiles of the largest view), the dense key
+        (ref (TY + 2) + ty + 1) (TX + 2) + tx + 1, items stable-sorted by key
+        and cut into `world` contiguous shares lo_r = floor(r n / world).
+        Returns (owners, False); densify_partition_stats() gives the
         partition's statistics."""
         items = self.sp if g.index == 0 else np.array(self.store[g.head: g.head + g.items], dtype=PATCH_DTYPE)
         n = len(items)
@@ -384,15 +385,17 @@ class GenerationEngine:
              for k in range(3)]
         with np.errstate(divide="ignore", invalid="ignore"):
             u, w = h[0] / h[2], h[1] / h[2]
+        Wmax, Hmax = int(max(self.S._keep[1].max(), 1)), int(max(self.S._keep[2].max(), 1))
+        TX, TY = -(-Wmax // tile_px), -(-Hmax // tile_px)
 
-        def tc(q):
+        def tc(q, tmax):
             with np.errstate(invalid="ignore"):
                 q = q / float(tile_px)
                 ok = (q > -2.0e9) & (q < 2.0e9)
             t = np.where(ok, np.floor(np.where(ok, q, 0.0)), 0.0).astype(np.int64)
-            return (np.clip(t, -(1 << 27), (1 << 27) - 1) + (1 << 27)).astype(np.uint64)
+            return (np.clip(t, -1, tmax) + 1).astype(np.uint64)
 
-        key = ((items["ref"].astype(np.uint64) & np.uint64(0xFF)) << np.uint64(56)) | (tc(w) << np.uint64(28)) | tc(u)
+        key = ((items["ref"].astype(np.uint64) * np.uint64(TY + 2) + tc(w, TY)) * np.uint64(TX + 2) + tc(u, TX))
         order = np.argsort(key, kind="stable")
         lo = np.array([(r * n) // world for r in range(world + 1)], dtype=np.int64)
         own = np.empty(n, dtype=np.int32)
