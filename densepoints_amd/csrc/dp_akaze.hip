@@ -199,7 +199,39 @@ hipError_t launch_akz_kcontrast(const AkArgs &a, int nv, int max_w, int max_h, h
     return hipGetLastError();
 }
 
-// halfsample: the 2x2 box average of the previous level's Lt into plane dst
+// one axis of cv::resize INTER_AREA's general path (computeResizeAreaTab):
+// destination d's source cells and float weights from double cell bounds, in
+// the table's order (<= 4 cells at scales below 3)
+__device__ int akz_area_tab(int ssize, int dsize, int d, int *si, float *alpha)
+{
+    const double scale = 1.0 / ((double)dsize / (double)ssize);
+    const double fs1 = (double)d * scale, fs2 = fs1 + scale;
+    const double cw = (ssize - fs1) < scale ? (ssize - fs1) : scale;
+    int s1 = (int)ceil(fs1), s2 = (int)floor(fs2);
+    if (s2 > ssize - 1)
+        s2 = ssize - 1;
+    if (s1 > s2)
+        s1 = s2;
+    int k = 0;
+    if (s1 - fs1 > 1e-3) {
+        si[k] = s1 - 1;
+        alpha[k++] = (float)((s1 - fs1) / cw);
+    }
+    for (int q = s1; q < s2 && k < 4; ++q) {
+        si[k] = q;
+        alpha[k++] = (float)(1.0 / cw);
+    }
+    if (fs2 - s2 > 1e-3 && k < 4) {
+        const double f = fs2 - s2 < 1.0 ? fs2 - s2 : 1.0;
+        si[k] = s2;
+        alpha[k++] = (float)((f < cw ? f : cw) / cw);
+    }
+    return k;
+}
+
+// halfsample (OpenCV 3.4 AKAZE's halfsample_image = cv::resize INTER_AREA) of
+// the previous level's Lt into plane dst: the 2x2 box when both sides halve
+// exactly, else the general area path (an odd source side, scale src / dst)
 __global__ void akz_half_kernel(AkArgs a, int level, int dst)
 {
     const int z = blockIdx.z, y = blockIdx.y, x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -207,8 +239,25 @@ __global__ void akz_half_kernel(AkArgs a, int level, int dst)
     if (L.w == 0 || x >= L.w || y >= L.h)
         return;
     const AkPlane &P = a.planes[z * kAkLevels + level - 1];
-    const float *r0 = a.pool + P.off + (size_t)(2 * y) * P.w + 2 * x, *r1 = r0 + P.w;
-    ak_ptr(a, z, level, dst)[(size_t)y * L.w + x] = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
+    const float *src = a.pool + P.off;
+    float v;
+    if (P.w == 2 * L.w && P.h == 2 * L.h) {
+        const float *r0 = src + (size_t)(2 * y) * P.w + 2 * x, *r1 = r0 + P.w;
+        v = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
+    } else {
+        int sy[4], sx[4];
+        float by[4], ax[4];
+        const int ny = akz_area_tab(P.h, L.h, y, sy, by), nx = akz_area_tab(P.w, L.w, x, sx, ax);
+        v = 0.0f;
+        for (int i = 0; i < ny; ++i) {
+            const float *row = src + (size_t)sy[i] * P.w;
+            float buf = 0.0f;
+            for (int j = 0; j < nx; ++j)
+                buf = buf + row[sx[j]] * ax[j];
+            v = v + by[i] * buf;
+        }
+    }
+    ak_ptr(a, z, level, dst)[(size_t)y * L.w + x] = v;
 }
 
 hipError_t launch_akz_half(const AkArgs &a, int level, int dst, int nv, int max_w, int max_h, hipStream_t s)

@@ -22,8 +22,10 @@
  *     getGaussianKernel weights, separable, BORDER_REPLICATE; fp32, taps
  *     accumulated in order).  kcontrast: the 70th percentile (300 bins) of
  *     |Scharr(Gaussian(img, 1.0))| over the interior, 0.03 if undefined.
- *  4. level i > 0: Lt = the previous Lt, or its 2x2 box average (halfsample,
- *     INTER_AREA for even sizes; odd remainders dropped) with kcontrast x 0.75
+ *  4. level i > 0: Lt = the previous Lt, or (octave change) its halfsample
+ *     -- cv::resize INTER_AREA: the 2x2 box for even sides, the general
+ *     area path with fractional cell weights when a side is odd -- with
+ *     kcontrast x 0.75
  *     at an octave change; Lsmooth = Gaussian(Lt, 1.0); Lflow = g2 =
  *     1 / (1 + |Scharr(Lsmooth)|^2 / k^2); FED: fed_tau_by_process_time(
  *     etime_i - etime_{i-1}, 1, 0.25, reordering) explicit steps Lt += tau/2
@@ -204,6 +206,71 @@ static void ak_scharr(const float *src, float *lx, float *ly, float *tmp, int w,
 }
 
 /* compute_k_percentile(img, 0.7, 1.0, 300): the gradient histogram's 70th percentile */
+/* cv::resize(src, dst, dst.size(), 0, 0, INTER_AREA) of an fp32 plane, the
+ * halfsample_image of OpenCV 3.4's AKAZE (imgproc resize.cpp): with both
+ * scales exactly 2 the fast path, ((s00 + s01) + (s10 + s11)) * 0.25; else
+ * (an odd source side: dst = floor(src / 2), scale = src / dst) the general
+ * area path on both axes -- computeResizeAreaTab's cells and float weights
+ * from double cell bounds, each destination the weighted sum over its source
+ * rows of the weighted row sums, fp32, in the table's order. */
+static int ak_area_tab(int ssize, int dsize, int d, int *si, float *alpha)
+{
+    const double scale = 1.0 / ((double)dsize / (double)ssize);
+    const double fs1 = (double)d * scale, fs2 = fs1 + scale;
+    const double cw = (ssize - fs1) < scale ? (ssize - fs1) : scale;
+    int s1 = (int)ceil(fs1), s2 = (int)floor(fs2);
+    if (s2 > ssize - 1)
+        s2 = ssize - 1;
+    if (s1 > s2)
+        s1 = s2;
+    int k = 0;
+    if (s1 - fs1 > 1e-3) {
+        si[k] = s1 - 1;
+        alpha[k++] = (float)((s1 - fs1) / cw);
+    }
+    for (int q = s1; q < s2 && k < 4; ++q) {
+        si[k] = q;
+        alpha[k++] = (float)(1.0 / cw);
+    }
+    if (fs2 - s2 > 1e-3 && k < 4) {
+        const double f = fs2 - s2 < 1.0 ? fs2 - s2 : 1.0;
+        si[k] = s2;
+        alpha[k++] = (float)((f < cw ? f : cw) / cw);
+    }
+    return k;
+}
+
+static void ak_halfsample(const float *src, int sw, int sh, float *dst, int w, int h)
+{
+    if (sw == 2 * w && sh == 2 * h) {
+        for (int y = 0; y < h; ++y)
+            for (int x = 0; x < w; ++x) {
+                const float *r0 = src + (size_t)(2 * y) * sw + 2 * x, *r1 = r0 + sw;
+                dst[(size_t)y * w + x] = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
+            }
+        return;
+    }
+    for (int y = 0; y < h; ++y) {
+        int sy[4];
+        float by[4];
+        const int ny = ak_area_tab(sh, h, y, sy, by);
+        for (int x = 0; x < w; ++x) {
+            int sx[4];
+            float ax[4];
+            const int nx = ak_area_tab(sw, w, x, sx, ax);
+            float sum = 0.0f;
+            for (int i = 0; i < ny; ++i) {
+                const float *row = src + (size_t)sy[i] * sw;
+                float buf = 0.0f;
+                for (int j = 0; j < nx; ++j)
+                    buf = buf + row[sx[j]] * ax[j];
+                sum = sum + by[i] * buf;
+            }
+            dst[(size_t)y * w + x] = sum;
+        }
+    }
+}
+
 static float ak_kcontrast(const float *img, int w, int h)
 {
     const size_t N = (size_t)w * h;
@@ -365,11 +432,7 @@ static int ak_scale_space(const uint8_t *bgr, int W, int H, AkLevel *lv, float *
         const int w = L->w, h = L->h;
         const size_t N = (size_t)w * h;
         if (L->octave > P->octave) {
-            for (int y = 0; y < h; ++y)
-                for (int x = 0; x < w; ++x) {
-                    const float *r0 = P->Lt + (size_t)(2 * y) * P->w + 2 * x, *r1 = r0 + P->w;
-                    L->Lt[(size_t)y * w + x] = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
-                }
+            ak_halfsample(P->Lt, P->w, P->h, L->Lt, w, h);
             k = k * 0.75f;
         } else {
             memcpy(L->Lt, P->Lt, sizeof(float) * N);
@@ -720,5 +783,14 @@ int or_akaze_plane(const uint8_t *bgr, int W, int H, int level, int which, float
     const float *src = which == 0 ? lv[level].Lt : which == 1 ? lv[level].Lx : which == 2 ? lv[level].Ly : lv[level].Ldet;
     memcpy(out, src, sizeof(float) * (size_t)lv[level].w * lv[level].h);
     ak_free(lv, n);
+    return 0;
+}
+
+/* test access: the halfsample (cv::resize INTER_AREA) of one fp32 plane */
+int or_akaze_halfsample(const float *src, int sw, int sh, float *dst, int w, int h)
+{
+    if (!src || !dst || w < 1 || h < 1 || sw < 2 * w || sh < 2 * h || sw > 2 * w + 1 || sh > 2 * h + 1)
+        return -1;
+    ak_halfsample(src, sw, sh, dst, w, h);
     return 0;
 }

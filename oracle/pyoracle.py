@@ -130,6 +130,7 @@ def _load():
         # AKAZE (or_akaze.c)
         "or_akaze_levels": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P, P]),
         "or_akaze_plane": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]),
+        "or_akaze_halfsample": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int]),
     }
     for k, (r, a) in sig.items():
         f = getattr(L, k)
@@ -557,6 +558,17 @@ def akaze_levels(W: int, H: int):
     es = np.zeros(16, dtype=np.float32)
     n = lib.or_akaze_levels(W, H, _p(info), _p(es))
     return info[:n], es[:n]
+
+
+def akaze_halfsample(src: np.ndarray) -> np.ndarray:
+    """AKAZE's halfsample_image (cv::resize INTER_AREA to floor(side / 2)) of
+    an fp32 plane, as the oracle's scale space computes it"""
+    src = np.ascontiguousarray(src, dtype=np.float32)
+    sh, sw = src.shape
+    out = np.zeros((sh // 2, sw // 2), dtype=np.float32)
+    if lib.or_akaze_halfsample(_p(src), sw, sh, _p(out), sw // 2, sh // 2) != 0:
+        raise ValueError("or_akaze_halfsample failed")
+    return out
 
 
 def akaze_plane(img_bgr: np.ndarray, level: int, which: int):

@@ -283,6 +283,21 @@ def test_generate_seeds_akaze_matches_oracle(orc, kind, thr):
         assert m.keypoints(0)[1].shape[1] == 64
 
 
+@pytest.mark.parametrize("size", [(500, 375), (333, 250)])
+def test_akaze_odd_octave_sides(orc, size):
+    """Views whose octaves halve an odd side (375 -> 187 -> 93, 333 -> 166 ->
+    83): the device halfsample takes cv::resize INTER_AREA's general
+    fractional-weight path like the oracle, keypoints,
+    descriptors and seeds bit-exact."""
+    cfg = synth.config(n_views=3, width=size[0], height=size[1], kind=0)
+    P, imgs, _ = synth.scene_host(cfg)
+    kw = dict(detector_type=M.DETECTOR_AKAZE, akaze_threshold=0.0002)
+    r = orc.seeds_run(P, imgs, orc.matcher_options(**kw))
+    assert r["counts"]["keypoints"] > 20
+    with engine_with(P, imgs) as eng:
+        compare_run(eng, r, kw, 3)
+
+
 def test_akaze_chunks_and_mixed_sizes(orc, monkeypatch):
     """Views of different sizes (different level counts: 400 x 150 has two
     octaves) and a chunk budget that puts every view in its own chunk give

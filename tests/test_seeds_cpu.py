@@ -293,6 +293,72 @@ def test_akaze_scale_space_is_diffusion(orc):
     assert kc[0] > 0 and np.allclose(kc[4], kc[0] * np.float32(0.75))
 
 
+def _inter_area_numpy(src):
+    """cv::resize(src, floor(size / 2), INTER_AREA) on an fp32 plane, stated
+    independently of the oracle (OpenCV 3.4 imgproc/src/resize.cpp): the fast
+    2x2 path when both sides halve exactly, else computeResizeAreaTab's cells
+    per axis and the row-by-row weighted sums in fp32 (AKAZE's
+    halfsample_image on odd sides)"""
+    sh, sw = src.shape
+    h, w = sh // 2, sw // 2
+    f32 = np.float32
+    if sw == 2 * w and sh == 2 * h:
+        return ((src[0::2, 0::2] + src[0::2, 1::2]) + (src[1::2, 0::2] + src[1::2, 1::2])) * f32(0.25)
+
+    def tab(ssize, dsize):
+        scale = 1.0 / (dsize / ssize)
+        out = []
+        for d in range(dsize):
+            fs1 = d * scale
+            fs2 = fs1 + scale
+            cw = min(scale, ssize - fs1)
+            s2 = min(int(np.floor(fs2)), ssize - 1)
+            s1 = min(int(np.ceil(fs1)), s2)
+            cells = []
+            if s1 - fs1 > 1e-3:
+                cells.append((s1 - 1, f32((s1 - fs1) / cw)))
+            cells += [(q, f32(1.0 / cw)) for q in range(s1, s2)]
+            if fs2 - s2 > 1e-3:
+                cells.append((s2, f32(min(min(fs2 - s2, 1.0), cw) / cw)))
+            out.append(cells)
+        return out
+
+    ty, tx = tab(sh, h), tab(sw, w)
+    dst = np.zeros((h, w), dtype=f32)
+    for y in range(h):
+        for x in range(w):
+            acc = f32(0)
+            for sy, b in ty[y]:
+                buf = f32(0)
+                for sx, a in tx[x]:
+                    buf = f32(buf + f32(src[sy, sx] * a))
+                acc = f32(acc + f32(b * buf))
+            dst[y, x] = acc
+    return dst
+
+
+@pytest.mark.parametrize("shape", [(40, 30), (41, 30), (40, 31), (37, 23), (75, 150), (187, 125)])
+def test_akaze_halfsample_is_inter_area(orc, shape):
+    """AKAZE's octave halfsample is cv::resize INTER_AREA to floor(side / 2):
+    the oracle equals an independent numpy statement of OpenCV's two paths bit
+    for bit -- the 2x2 box for even sides, fractional cell weights (every
+    source row and column used) when a side is odd; a constant plane stays
+    within one fp32 rounding per weight of the constant."""
+    rng = np.random.default_rng(sum(shape))
+    src = rng.random(shape, dtype=np.float32)
+    got = orc.akaze_halfsample(src)
+    ref = _inter_area_numpy(src)
+    assert got.shape == (shape[0] // 2, shape[1] // 2)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    c = orc.akaze_halfsample(np.full(shape, 0.5, dtype=np.float32))
+    assert np.abs(c - 0.5).max() < 1e-6
+    if shape[0] % 2 or shape[1] % 2:
+        # the odd side's last source row / column reaches the output
+        bumped = src.copy()
+        bumped[-1, -1] += 1.0
+        assert not np.array_equal(orc.akaze_halfsample(bumped), got)
+
+
 def test_akaze_oracle_keypoints_and_descriptors(orc):
     """AKAZE through GenerateSeeds: 486-bit descriptors in 64-byte rows (the
     padding bits zero), at most max_keypoints_per_cell per cell, keypoints
