@@ -135,7 +135,7 @@ def compact(result: dict, detail_path: str | None = None) -> dict:
     sl = result.get("scaling_leg")
     if sl:
         out["scaling_leg"] = {"n_gpus": sl.get("n_gpus"), "scaling": sl.get("scaling")}
-        for m in ("parity", "fast", "fast_slots"):
+        for m in ("parity", "fast", "fast_slots", "fast_hybrid8"):
             if m in sl:
                 out["scaling_leg"][m] = _pick(sl[m], ("Mpatches_per_s", "ms_per_densify", "non_refine_ms",
                                                       "ranks_store_equal", "store_crc32"))
@@ -444,7 +444,8 @@ def main():
     eng.close()
 
 
-def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast, exchange=False, probe_worlds=(2, 8)):
+def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast, exchange=False, probe_worlds=(2, 8),
+                    replicate_below=None):
     """`steps` whole densifies with every generation partitioned over the ranks
     (dist.densify_partitioned_device), after `warmup` untimed ones, bracketed by
     barrier + synchronize; rate = candidates refined (seed stage + expansions)
@@ -458,7 +459,8 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast, exchan
     eng.set_fast_options(dp.FastOptions(densify=1 if fast else 0))
     # the store comes back as a view of the library's pinned result buffer (the
     # C ABI's *out contract), consumed before the next densify
-    run = functools.partial(D.densify_partitioned_device, one_rank_exchange=exchange, copy_result=False)
+    run = functools.partial(D.densify_partitioned_device, one_rank_exchange=exchange, copy_result=False,
+                            replicate_below=replicate_below)
     probe = None
     for i in range(warmup):
         # the untimed warm-up also computes the partitions world sizes 2 and 8
@@ -511,6 +513,7 @@ def partitioned_leg(eng, seeds, dist, coll_dev, dev, steps, warmup, fast, exchan
             # shrink with the ranks
             "non_refine_ms": round(wall / steps * 1e3 - st["refine_ms"], 2),
             "protocol": "slots" if (world > 1 or exchange) else "dp_densify (device-resident generations)",
+            "replicate_below": st.get("replicate_below"), "replicated_calls": st.get("replicated_calls"),
             # host time per phase of the last densify (each phase ends in a host sync;
             # refine_compact includes this rank's refine kernels), max over ranks
             "phase_ms_max_rank": {k: round(D.max_over_ranks(v, dist, coll_dev), 2)
@@ -546,13 +549,16 @@ def partition_summary(parts, world):
 
 def scaling_leg(args, stream, dist, coll_dev, dev):
     """The strong-scaling series, under this key at every N (N = 1 included):
-    BASELINE config 4 (64 views 4K), the whole densify with every generation
-    partitioned by reference-view super-tile over the ranks and the accepted
-    candidates all-gathered (RCCL over xGMI), both refine modes."""
+    BASELINE config 4 (64 views 4K), the whole densify with every large
+    generation partitioned by reference-view super-tile over the ranks and the
+    accepted candidates all-gathered (RCCL over xGMI), the small ones
+    replicated device-resident (dist.replicate_below_default), both refine
+    modes."""
     import ctypes
 
     import densepoints_amd as dp
     from densepoints_amd import _native as N
+    from densepoints_amd import dist as D
     from densepoints_amd import synth
 
     cfg = synth.named("cfg4_64view_4k")
@@ -574,7 +580,13 @@ def scaling_leg(args, stream, dist, coll_dev, dev):
             # slot compaction, scatter, replicated commit, one wait per generation):
             # what bounds the N-rank strong scaling beside refine_ms / N
             out["fast_slots"] = partitioned_leg(eng, seeds, dist, coll_dev, dev, args.densify_steps, 1, True,
-                                                exchange=True, probe_worlds=())
+                                                exchange=True, probe_worlds=(), replicate_below=0)
+            # the hybrid an 8-rank run uses (generations below 8,192 items on every
+            # rank, device-resident): the per-rank protocol cost at N = 8 beside
+            # refine_ms / 8 of the partitioned generations
+            out["fast_hybrid8"] = partitioned_leg(eng, seeds, dist, coll_dev, dev, args.densify_steps, 1, True,
+                                                  exchange=True, probe_worlds=(),
+                                                  replicate_below=D.replicate_below_default(8))
         out["workload"] = (f"cfg4_64view_4k: {V} views {W}x{H}, one step = the whole densify (PMVS::Run minus "
                            f"matching) of {len(seeds)} seed points, every BFS generation partitioned by "
                            f"reference-view super-tile over {world} rank(s), accepted candidates all-gathered")

@@ -221,6 +221,7 @@ SIGNATURES = [
     ("dp_densify_commit", _I, [_P, _P, _P, _P, ctypes.c_int64]),
     ("dp_densify_result", _I, [_P, _P, _P, _P]),
     ("dp_densify_run", _I, [_P, _P, ctypes.c_int32]),
+    ("dp_densify_run_until", _I, [_P, _P, ctypes.c_int32, ctypes.c_int64, _P]),
     ("dp_densify_owners", _I, [_P, _P, _I, _I, _P, _P]),
     ("dp_densify_partition_stats", _I, [_P, _P]),
     ("dp_densify_refine_items", _I, [_P, _P, _P, ctypes.c_int64, _P, _P]),

@@ -247,6 +247,9 @@ __global__ __launch_bounds__(kBfsBlocks) void bfs_scan_kernel(BfsArgs a)
         if (x2.items > 0 && (uint64_t)c.nseeds + 4ull * (uint64_t)np > 0xFFFFFFF0ull) {
             x2.err = 1; // dp_densify: "sequence space exhausted"
             x2.ncand = 0;
+        } else if (a.yield_items > 0 && x2.items >= a.yield_items) {
+            x2.stall = 2; // dp_densify_run_until: the generation goes back to the caller unrun
+            x2.ncand = 0;
         } else if (x2.ncand > a.cand_cap || x2.ncand > 0x7fffffffll) {
             x2.stall = 1; // the host grows the candidate buffers and resumes here
             x2.ncand = 0;

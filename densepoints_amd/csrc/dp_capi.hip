@@ -938,7 +938,7 @@ static int set_state(dp_ctx *c, int slot, const dpk::GenDev &g, hipStream_t s)
 // sequence order); writes the next generation's state into slot ^ 1.
 // cand_cap: the candidate buffers' capacity (the next generation stalls above it)
 static int organize_gen(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int slot, int64_t cand_cap, hipStream_t s,
-                        int fused)
+                        int fused, int64_t yield_items = 0)
 {
     dpk::BfsArgs b{};
     b.views = c->d_views;
@@ -963,6 +963,7 @@ static int organize_gen(dp_ctx *c, const dp_patch *cand, const uint8_t *okf, int
     b.work = c->d_work;
     b.lpt_scratch = c->g_lpt_scratch;
     b.fused = fused;
+    b.yield_items = yield_items;
     DP_HIP(c, dpk::launch_bfs_organize(b, s));
     return DP_OK;
 }
@@ -1054,7 +1055,8 @@ static bool device_loop_ok(const dp_ctx *c) { return !(c->fopt.densify && c->fop
 // Up to max_gens expansion generations from the state in c->g_slot, kGenBatch
 // per host wait (dp_densify, dp_densify_run).  cap0: the candidate capacity
 // to start with.  Leaves the state of the first generation not run in c->g_slot.
-static int run_generations(dp_ctx *c, int64_t max_gens, int64_t cap0, hipStream_t s, dpk::GenDev *last)
+static int run_generations(dp_ctx *c, int64_t max_gens, int64_t cap0, hipStream_t s, dpk::GenDev *last,
+                           int64_t yield_items = 0)
 {
     int64_t cap = std::max<int64_t>(cap0, 1024);
     if (c->gen_cap_test > 0)
@@ -1090,7 +1092,7 @@ static int run_generations(dp_ctx *c, int64_t max_gens, int64_t cap0, hipStream_
             if (rc != DP_OK)
                 return rc;
             DP_HIP(c, hipEventRecord(c->gev[2 * i + 1], s));
-            rc = organize_gen(c, c->cand.p, c->ok.p, slot, cap, s, densify_epi(c));
+            rc = organize_gen(c, c->cand.p, c->ok.p, slot, cap, s, densify_epi(c), yield_items);
             if (rc != DP_OK)
                 return rc;
             slot ^= 1;
@@ -1105,6 +1107,15 @@ static int run_generations(dp_ctx *c, int64_t max_gens, int64_t cap0, hipStream_
         }
         c->g_slot = slot;
         done += k;
+        if (g.stall == 2) {
+            // the next generation reached the yield bound: hand it back unrun
+            g.stall = 0;
+            g.ncand = 4 * g.items;
+            rc = set_state(c, slot, g, s);
+            if (rc != DP_OK)
+                return rc;
+            break;
+        }
         if (g.stall) {
             // the next generation outgrew the buffers: grow and resume it
             c->g_st.stalls += 1;
@@ -1347,25 +1358,44 @@ extern "C" int dp_densify_commit(dp_ctx *c, dp_generation *gen, const dp_patch *
     return commit_on_stream(c, gen, c->cand.p, c->ok.p, n_cand, s);
 }
 
-extern "C" int dp_densify_run(dp_ctx *c, dp_generation *gen, int32_t max_generations)
+extern "C" int dp_densify_run_until(dp_ctx *c, dp_generation *gen, int32_t max_generations, int64_t yield_items,
+                                    int64_t *evals_out)
 {
     int rc = check_gen(c, gen, "dp_densify_run");
     if (rc != DP_OK)
         return rc;
-    if (gen->index < 1 || max_generations < 1)
-        return fail(c, DP_E_ARG, "dp_densify_run: expansion generations only (index >= 1), max_generations >= 1");
+    if (gen->index < 1 || max_generations < 1 || yield_items < 0)
+        return fail(c, DP_E_ARG,
+                    "dp_densify_run: expansion generations only (index >= 1), max_generations >= 1, yield_items >= 0");
+    if (evals_out)
+        *evals_out = 0;
     if (gen->items == 0)
         return DP_OK;
     if (!device_loop_ok(c))
         return fail(c, DP_E_ARG, "dp_densify_run: the analytic-gradient refine is host-driven");
     hipSetDevice(c->device);
     hipStream_t s = c->stream;
+    // the evaluation counter before this call's refines (read after its waits)
+    unsigned long long ev[2] = {0, 0};
+    if (evals_out)
+        DP_HIP(c, hipMemcpyAsync(&ev[0], c->d_evals, sizeof(ev[0]), hipMemcpyDeviceToHost, s));
     dpk::GenDev g{};
-    rc = run_generations(c, max_generations, std::max<int64_t>(4 * gen->items + 4096, (int64_t)c->cand.cap), s, &g);
+    rc = run_generations(c, max_generations, std::max<int64_t>(4 * gen->items + 4096, (int64_t)c->cand.cap), s, &g,
+                         yield_items);
     if (rc != DP_OK)
         return rc;
     take_state(c, g, gen);
+    if (evals_out) {
+        DP_HIP(c, hipMemcpyAsync(&ev[1], c->d_evals, sizeof(ev[1]), hipMemcpyDeviceToHost, s));
+        DP_HIP(c, hipStreamSynchronize(s));
+        *evals_out = (int64_t)(ev[1] - ev[0]);
+    }
     return DP_OK;
+}
+
+extern "C" int dp_densify_run(dp_ctx *c, dp_generation *gen, int32_t max_generations)
+{
+    return dp_densify_run_until(c, gen, max_generations, 0, nullptr);
 }
 
 // ---- partitioned generations (reference-view super-tiles) -------

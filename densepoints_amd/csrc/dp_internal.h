@@ -158,7 +158,8 @@ struct GenDev {
     int64_t seed_patches; // the seed generation's accepts (statistic)
     uint32_t seq0;      // sequence number of candidate 0
     int32_t per_item;   // 1 (seed generation) or 4 (expansion)
-    int32_t stall;      // 1: ncand exceeded the candidate buffers; the host regrows them
+    int32_t stall;      // 1: ncand exceeded the candidate buffers, the host regrows them;
+                        // 2: items >= the run's yield bound, the host hands the generation back
     int32_t err;        // 1: the 32-bit sequence space is exhausted
 };
 static_assert(sizeof(GenDev) % 8 == 0, "GenDev is copied as 64-bit words");
@@ -187,6 +188,7 @@ struct BfsArgs {
     uint32_t *work;            // the refine's dequeue counters, zeroed for the next generation
     uint32_t *lpt_scratch;     // the LPT order's counters, zeroed for the next generation
     int32_t fused;             // kEpi* bits the generation's refine already did (claims: k = 1 only)
+    int64_t yield_items;       // > 0: a next generation of this many items or more is not run (stall 2)
 };
 constexpr int kBfsBlocks = 1024; // chunks of the generation's scan (one block each)
 

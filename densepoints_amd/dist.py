@@ -182,8 +182,17 @@ class _DeviceBuffers:
         return t
 
 
+def replicate_below_default(world: int) -> int:
+    """Items below which a generation runs replicated on every rank: a share of
+    fewer than ~1024 parents (4,096 candidates, one resident wave per SIMD of
+    the chip) leaves the refine latency-bound, so partitioning it buys nothing
+    while the exchange costs a host turnaround per generation."""
+    return 1024 * max(int(world), 1)
+
+
 def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_px: int = 64,
-                               probe_worlds: tuple = (), one_rank_exchange: bool = False, copy_result: bool = True):
+                               probe_worlds: tuple = (), one_rank_exchange: bool = False, copy_result: bool = True,
+                               replicate_below: int | None = None):
     """dp_densify with every generation partitioned by reference-view super-tile,
     the records in HBM, only the ACCEPTED candidates exchanged and ONE host
     wait per generation.  Per generation, all queued on the torch current
@@ -207,7 +216,14 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
     probe_worlds asks for the partitions of every generation.  Every rank's
     store equals dp_densify bit for bit.  copy_result=False returns the store
     as a view of the library's pinned result buffer (valid until the engine's
-    next densify) instead of a copy.  stats gains "partition" (items, largest
+    next densify) instead of a copy.
+    Hybrid (r06): an expansion generation of fewer than `replicate_below`
+    items (default replicate_below_default(world); 0 = partition every
+    generation) runs on every rank at once, device-resident with no partition
+    and no exchange (dp_densify_run_until, eight generations per host wait,
+    handing back the first generation that reaches the bound), its
+    evaluations counted on rank 0 only.  Those are the BFS's long tail: their
+    refine is one candidate's latency, whatever the share.  stats gains "partition" (items, largest
     share, items in split tiles, tiles per generation), "accepted" (records
     exchanged), "gathered_bytes", "phase_ms" (host time: begin; launch = the
     queued partition, refine and exchange calls; commit = up to the status
@@ -225,15 +241,19 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
         stats["accepted"] = []
         return patches, stats
     rccl = dist is not None and dist.get_backend() == "nccl"
+    if replicate_below is None:
+        replicate_below = replicate_below_default(world)
+    repl_evals = 0
     rec = PATCH_DTYPE.itemsize
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
     pool = _DeviceBuffers(device)
-    ph = {"begin": 0.0, "launch": 0.0, "commit": 0.0, "run": 0.0}
+    ph = {"begin": 0.0, "launch": 0.0, "commit": 0.0, "run": 0.0, "replicated": 0.0}
     t = time.perf_counter()
     gen = eng.densify_begin(seeds_xyz)
     ph["begin"] += time.perf_counter() - t
     parts, gathered, accepted = [], [], []
+    replicated_calls = 0
     probe = {int(w): [] for w in probe_worlds}
     while gen.items > 0:
         per = gen.per_item
@@ -245,6 +265,15 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
             torch.cuda.current_stream(device).synchronize()
             gen = eng.densify_run(gen)
             ph["run"] += time.perf_counter() - t
+            continue
+        if gen.index >= 1 and gen.items < replicate_below and not probe:
+            # the small generations, on every rank, until one reaches the bound
+            t = time.perf_counter()
+            torch.cuda.current_stream(device).synchronize()
+            gen, ev = eng.densify_run_until(gen, replicate_below)
+            repl_evals += ev
+            replicated_calls += 1
+            ph["replicated"] += time.perf_counter() - t
             continue
         t = time.perf_counter()
         d_order, counts = eng.densify_partition_async(gen, world, tile_px, sp)
@@ -272,7 +301,12 @@ def densify_partitioned_device(eng, seeds_xyz, dist, device: torch.device, tile_
         gathered.append(world * (stride + 1) * rec if dist is not None else 0)
         accepted.append(n_ex)
     patches, stats = eng.densify_result(copy=copy_result)
+    if rank != 0:
+        # every rank ran the replicated generations: rank 0 counts them
+        stats["evals"] -= repl_evals
     stats = _reduce_stats(stats, dist, device)
+    stats["replicated_calls"] = replicated_calls
+    stats["replicate_below"] = int(replicate_below)
     stats["phase_ms"] = {k: round(v * 1e3, 2) for k, v in ph.items()}
     stats["partition"] = parts
     stats["gathered_bytes"] = gathered or [0]

@@ -396,6 +396,15 @@ class Engine:
         self._check(lib.dp_densify_run(self._ctx, ctypes.byref(gen), int(min(max_generations, 2**31 - 1))))
         return gen
 
+    def densify_run_until(self, gen: N.DpGeneration, yield_items: int, max_generations: int = 1 << 30):
+        """dp_densify_run_until: device-resident generations until the densify
+        ends or the next generation has >= yield_items items (returned unrun);
+        (gen, objective evaluations this call spent)."""
+        ev = ctypes.c_int64()
+        self._check(lib.dp_densify_run_until(self._ctx, ctypes.byref(gen), int(min(max_generations, 2**31 - 1)),
+                                             int(yield_items), ctypes.byref(ev)))
+        return gen, int(ev.value)
+
     # ---- partitioned generations (reference-view super-tiles, SURVEY 8e) ----
     def densify_owners(self, gen: N.DpGeneration, world: int, tile_px: int = 64):
         """(owner rank per item, fallback flag -- always False since the round-4

@@ -238,6 +238,14 @@ int dp_densify_result(dp_ctx *ctx, const dp_patch **out, int64_t *n_out, dp_dens
  * wait; advances *gen (items == 0: finished).  Not with the analytic-gradient
  * performance refine (dp_fast_options.gradient), which is host-driven. */
 int dp_densify_run(dp_ctx *ctx, dp_generation *gen, int32_t max_generations);
+/* dp_densify_run that also stops BEFORE a generation of yield_items or more
+ * items (returned unrun in *gen; 0 = no such stop), and reports in *evals_out
+ * (optional) the objective evaluations its refines spent.  The multi-rank
+ * densify runs its small generations this way on every rank -- their refine is
+ * latency-bound, so partitioning them gains nothing while the exchange costs a
+ * host turnaround -- and counts their evaluations on one rank only. */
+int dp_densify_run_until(dp_ctx *ctx, dp_generation *gen, int32_t max_generations, int64_t yield_items,
+                         int64_t *evals_out);
 /* Partitioned generations (north star: "reference-view grid cells shard across
  * the 8 GPUs").  owner_out[i] (host, gen->items) = the rank that
  * refines item i.  Partition spec (round 4; round 3 hashed the tiles and fell

@@ -21,6 +21,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -46,6 +47,8 @@ void usage()
                  "                             all-gathered device to device; output identical to 1 GPU)\n"
                  "               [--exchange auto|rccl|copy]  (auto: RCCL when every context has its\n"
                  "                             own GPU, else peer copies; --multi: that protocol at 1 GPU)\n"
+                 "               [--replicate-below N]  (generations of fewer items run on every\n"
+                 "                             context, device-resident, no exchange; default 1024 x gpus)\n"
                  "               [--mode parity|fast] [--fast-iters N] [--fast-gradient 0|1]\n"
                  "                            (fast: the performance-mode refine -- LDS-staged gray\n"
                  "                             tiles, fused CG -- for the seed stage and every expansion;\n"
@@ -289,11 +292,13 @@ struct Exchange {
 // context commits the whole generation to its replicated organizer
 // (dp_densify_commit_gathered_device, in its own host thread so the waits
 // overlap) -- no candidate touches host memory, and the store equals
-// dp_densify's bit for bit.  Returns the stats of context 0 (evals /
-// refine_ms summed / maxed).
+// dp_densify's bit for bit.  Expansion generations of fewer than
+// replicate_below items run on every context device-resident instead
+// (dp_densify_run_until: no partition, no exchange, eight per host wait).
+// Returns the stats of context 0 (evals / refine_ms summed / maxed).
 int densify_multi(std::vector<dp_ctx *> &ctxs, const std::vector<int> &devices, const char *exchange_mode,
                   const std::vector<double> &seeds, std::vector<dp_patch> &out, dp_densify_stats &st,
-                  std::string &err, int64_t &exchanged)
+                  std::string &err, int64_t &exchanged, int64_t replicate_below)
 {
     const int G = (int)ctxs.size();
     const int n = (int)(seeds.size() / 3);
@@ -314,9 +319,27 @@ int densify_multi(std::vector<dp_ctx *> &ctxs, const std::vector<int> &devices, 
             return fail_of(g, rc);
     }
     exchanged = 0;
-    std::vector<int64_t> counts((size_t)G), ex_g((size_t)G, 0);
+    std::vector<int64_t> counts((size_t)G), ex_g((size_t)G, 0), repl_evals((size_t)G, 0);
     while (gen[0].items > 0) {
         const int per = gen[0].per_item;
+        if (gen[0].index >= 1 && gen[0].items < replicate_below) {
+            // the BFS's small generations (latency-bound refines) on every
+            // context at once, device-resident, no exchange, until one reaches
+            // the bound; their evaluations count once (context 0)
+            std::vector<std::thread> th;
+            for (int g = 0; g < G; ++g)
+                th.emplace_back([&, g]() {
+                    int64_t ev = 0;
+                    rcs[(size_t)g] = dp_densify_run_until(ctxs[(size_t)g], &gen[(size_t)g], INT32_MAX, replicate_below, &ev);
+                    repl_evals[(size_t)g] += ev;
+                });
+            for (auto &t : th)
+                t.join();
+            for (int g = 0; g < G; ++g)
+                if (rcs[(size_t)g] != DP_OK)
+                    return fail_of(g, rcs[(size_t)g]);
+            continue;
+        }
         // the partition and each context's share, queued (no host wait)
         int64_t stride = 1;
         for (int g = 0; g < G; ++g) {
@@ -368,7 +391,7 @@ int densify_multi(std::vector<dp_ctx *> &ctxs, const std::vector<int> &devices, 
     out.assign(res, res + np);
     st = sts[0];
     for (int g = 1; g < G; ++g) {
-        st.evals += sts[(size_t)g].evals;
+        st.evals += sts[(size_t)g].evals - repl_evals[(size_t)g];
         st.refine_ms = std::max(st.refine_ms, sts[(size_t)g].refine_ms);
     }
     return DP_OK;
@@ -382,6 +405,7 @@ int main(int argc, char **argv)
     int device = 0, gpus = 1;
     bool force_multi = false;
     std::string exchange_mode = "auto";
+    long long replicate_below = -1; // default 1024 x contexts
     long long max_pops = -1;
     int level = 0;
     bool check_only = false, do_filter = false, fast = false;
@@ -404,6 +428,7 @@ int main(int argc, char **argv)
         else if (a == "--device") device = std::atoi(next().c_str());
         else if (a == "--gpus") gpus = std::atoi(next().c_str());
         else if (a == "--multi") force_multi = true;
+        else if (a == "--replicate-below") replicate_below = std::atoll(next().c_str());
         else if (a == "--exchange") {
             exchange_mode = next();
             if (exchange_mode != "auto" && exchange_mode != "rccl" && exchange_mode != "copy") {
@@ -579,7 +604,9 @@ int main(int argc, char **argv)
                 }
             }
             std::string err;
-            const int mrc = densify_multi(ctxs, devices, exchange_mode.c_str(), use, multi_out, st, err, exchanged);
+            const int64_t rb = replicate_below >= 0 ? (int64_t)replicate_below : 1024 * (int64_t)gpus;
+            const int mrc =
+                densify_multi(ctxs, devices, exchange_mode.c_str(), use, multi_out, st, err, exchanged, rb);
             for (int g = 1; g < gpus; ++g)
                 dp_ctx_destroy(ctxs[(size_t)g]);
             if (mrc != DP_OK) {

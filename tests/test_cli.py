@@ -233,16 +233,21 @@ def test_cli_baseline_cfg1_vga(tmp_path_factory, tmp_path, orc, views):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpus,extra", [(2, ()), (3, ()), (1, ("--multi", "--exchange", "rccl")),
-                                        (2, ("--mode", "fast"))])
+@pytest.mark.parametrize("gpus,extra", [(2, ("--replicate-below", "0")), (3, ("--replicate-below", "0")),
+                                        (1, ("--multi", "--exchange", "rccl", "--replicate-below", "0")),
+                                        (2, ("--mode", "fast", "--replicate-below", "0")),
+                                        (2, ("--replicate-below", "5")), (3, ("--mode", "fast",))])
 def test_cli_gpus_partitioned_equals_one_gpu(scene_dir, tmp_path, gpus, extra):
     """densify --gpus N: N contexts (wrapping onto the available devices),
     every generation partitioned by reference-view super-tile on the device,
     each context's accepted candidates compacted into its slot and the slots
     all-gathered device to device (peer copies when contexts share a GPU; the
     RCCL path -- ncclCommInitAll + ncclAllGather in one group -- forced at one
-    context with --multi --exchange rccl); the PLY is byte-identical to the
-    1-GPU run."""
+    context with --multi --exchange rccl); with --replicate-below the small
+    generations run on every context device-resident instead (hybrid; the
+    default bound, 1024 x contexts, replicates every expansion generation of
+    this small scene).  The PLY is byte-identical to the 1-GPU run and the
+    evaluations are counted once."""
     one, many = tmp_path / "one.ply", tmp_path / "many.ply"
     args = ["-i", os.path.join(scene_dir, "scene.json"), "--seeds", os.path.join(scene_dir, "seeds.xyz")]
     mode = list(extra[extra.index("--mode"):extra.index("--mode") + 2]) if "--mode" in extra else []
@@ -251,8 +256,14 @@ def test_cli_gpus_partitioned_equals_one_gpu(scene_dir, tmp_path, gpus, extra):
     rn = json.loads(run(*args, "-o", str(many), "--gpus", str(gpus), *extra).stdout.strip().splitlines()[-1])
     assert rn["gpus"] == gpus and rn["patches"] == r1["patches"] > 0
     assert rn["evals"] == r1["evals"]
-    # only accepted candidates crossed: at least every stored patch, at most every candidate
-    assert r1["patches"] <= rn["exchanged"] <= r1["candidates"] + len(open(os.path.join(scene_dir, "seeds.xyz")).readlines())
+    # only accepted candidates crossed: at least every stored patch (every
+    # generation exchanged), at most every candidate
+    nseeds = len(open(os.path.join(scene_dir, "seeds.xyz")).readlines())
+    assert rn["exchanged"] <= r1["candidates"] + nseeds
+    if "--replicate-below" in extra and extra[extra.index("--replicate-below") + 1] == "0":
+        assert r1["patches"] <= rn["exchanged"]
+    else:
+        assert 0 < rn["exchanged"] < r1["patches"]
     assert many.read_bytes() == one.read_bytes()
 
 

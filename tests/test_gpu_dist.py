@@ -121,7 +121,7 @@ def test_two_ranks_host_partitioned_densify_equals_dp_densify(tmp_path):
         assert int(open(out + f".r{r}.evals").read()) == rst["evals"]
 
 
-def _worker_dev(rank, world, port, out_path, backend, exchange=False, cap=1, scene="hf6"):
+def _worker_dev(rank, world, port, out_path, backend, exchange=False, cap=1, scene="hf6", rb=0):
     import torch
     import torch.distributed as tdist
 
@@ -138,22 +138,31 @@ def _worker_dev(rank, world, port, out_path, backend, exchange=False, cap=1, sce
     P, imgs, seeds = _scene(scene)
     with dp.Engine(dp.Options(max_patches_per_cell=cap), device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
-        got, st = D.densify_partitioned_device(eng, seeds, group, torch.device("cuda", 0), one_rank_exchange=exchange)
         # the same densify in the host-array form: the partitions (and their
         # statistics, read back by the async path with the commit) must agree
         _, hst = D.densify_partitioned(eng, seeds, group, torch.device("cuda", 0) if backend == "nccl" else None)
+        if rb == "hybrid":
+            # a bound between the expansion generations' sizes: some partitioned, some replicated
+            sizes = sorted(p[0] for p in hst["partition"][1:])
+            rb = max(2, sizes[len(sizes) // 2])
+        got, st = D.densify_partitioned_device(eng, seeds, group, torch.device("cuda", 0), one_rank_exchange=exchange,
+                                               replicate_below=rb)
     np.save(out_path + f".r{rank}.npy", got.view(np.uint8), allow_pickle=False)
     with open(out_path + f".r{rank}.json", "w") as f:
-        f.write(json.dumps({"evals": st["evals"], "partition": st["partition"], "host_partition": hst["partition"]}))
+        f.write(json.dumps({"evals": st["evals"], "partition": st["partition"], "host_partition": hst["partition"],
+                            "replicated_calls": st.get("replicated_calls", 0)}))
     if group:
         tdist.barrier()
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("backend,world,exchange,cap", [(None, 1, False, 1), (None, 1, True, 1), ("nccl", 1, True, 1),
-                                                       ("gloo", 2, False, 1), ("gloo", 3, False, 1),
-                                                       ("gloo", 2, False, 2)])
-def test_partitioned_densify_device(tmp_path, backend, world, exchange, cap):
+@pytest.mark.parametrize("backend,world,exchange,cap,rb", [(None, 1, False, 1, 0), (None, 1, True, 1, 0),
+                                                          ("nccl", 1, True, 1, 0), ("gloo", 2, False, 1, 0),
+                                                          ("gloo", 3, False, 1, 0), ("gloo", 2, False, 2, 0),
+                                                          ("gloo", 2, False, 1, "hybrid"),
+                                                          ("gloo", 3, False, 2, "hybrid"),
+                                                          ("nccl", 1, True, 1, "hybrid")])
+def test_partitioned_densify_device(tmp_path, backend, world, exchange, cap, rb):
     """Reference-view super-tile partition of every generation: the device
     partition, refine of the rank's share with its accepted candidates
     compacted into the rank's slot, ONE all-gather of the slots and the
@@ -163,9 +172,13 @@ def test_partitioned_densify_device(tmp_path, backend, world, exchange, cap):
     -- also with organizer cell capacity 2 (max_patches_per_cell,
     patch_organizer.h:42-46).  The ranks run on the legacy NULL stream, and
     the partition statistics the async path reads back with the commit equal
-    the synchronous host-array path's, generation by generation."""
+    the synchronous host-array path's, generation by generation.  rb "hybrid":
+    the generations below a median size run on every rank device-resident
+    (dp_densify_run_until) and hand back the first larger one -- same store,
+    evaluations counted once, the partitioned generations' statistics a
+    subsequence of the host path's."""
     out = str(tmp_path / "dense")
-    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, exchange, cap), nprocs=world, join=True)
+    mp.spawn(_worker_dev, args=(world, _free_port(), out, backend, exchange, cap, "hf6", rb), nprocs=world, join=True)
     P, imgs, seeds = _scene("hf6")
     with dp.Engine(dp.Options(max_patches_per_cell=cap), device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
@@ -175,7 +188,11 @@ def test_partitioned_densify_device(tmp_path, backend, world, exchange, cap):
         assert got.tobytes() == ref.tobytes(), f"rank {r}"
         st = json.loads(open(out + f".r{r}.json").read())
         assert st["evals"] == rst["evals"]
-        if world > 1 or exchange:
+        if rb == "hybrid":
+            assert st["replicated_calls"] > 0 and 1 < len(st["partition"]) < len(st["host_partition"]), st
+            it = iter(st["host_partition"])
+            assert all(any(p == q for q in it) for p in st["partition"]), f"rank {r}"
+        elif world > 1 or exchange:
             assert st["partition"] == st["host_partition"], f"rank {r}"
 
 
@@ -187,7 +204,7 @@ def test_partitioned_densify_more_ranks_than_items(tmp_path):
     path's."""
     world = 3
     out = str(tmp_path / "dense")
-    mp.spawn(_worker_dev, args=(world, _free_port(), out, "gloo", False, 1, "wide70"), nprocs=world, join=True)
+    mp.spawn(_worker_dev, args=(world, _free_port(), out, "gloo", False, 1, "wide70", 0), nprocs=world, join=True)
     P, imgs, seeds = _scene("wide70")
     with dp.Engine(device=0) as eng:
         eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
@@ -245,9 +262,12 @@ def _worker_cfg4(rank, world, port, out_path, max_pops, nseeds):
     with dp.Engine(dp.Options(max_pops=max_pops), device=0) as eng:
         sc = DeviceScene("cfg4_64view_4k", eng, host_views=[])
         seeds = spread(sc.seeds, nseeds)
-        for mode in ("parity", "fast"):
-            eng.set_fast_options(dp.FastOptions(densify=1 if mode == "fast" else 0))
-            got, st = D.densify_partitioned_device(eng, seeds, tdist, torch.device("cuda", 0))
+        for mode in ("parity", "fast", "hybrid"):
+            eng.set_fast_options(dp.FastOptions(densify=0 if mode == "parity" else 1))
+            # parity / fast: every generation partitioned; hybrid: the default
+            # bound (the small generations on every rank, device-resident)
+            got, st = D.densify_partitioned_device(eng, seeds, tdist, torch.device("cuda", 0),
+                                                   replicate_below=None if mode == "hybrid" else 0)
             np.save(out_path + f".{mode}.r{rank}.npy", got.view(np.uint8), allow_pickle=False)
             with open(out_path + f".{mode}.r{rank}.json", "w") as f:
                 f.write(json.dumps({"evals": st["evals"], "partition": st["partition"],
@@ -281,8 +301,8 @@ def test_partitioned_densify_cfg4_two_ranks(tmp_path):
     with dp.Engine(dp.Options(max_pops=max_pops), device=0) as eng:
         sc = DeviceScene("cfg4_64view_4k", eng, host_views=[])
         seeds = spread(sc.seeds, nseeds)
-        for mode in ("parity", "fast"):
-            eng.set_fast_options(dp.FastOptions(densify=1 if mode == "fast" else 0))
+        for mode in ("parity", "fast", "hybrid"):
+            eng.set_fast_options(dp.FastOptions(densify=0 if mode == "parity" else 1))
             ref, rst = eng.densify(seeds)
             assert rst["patches"] > 1000 and 0 < rst["pops"] <= max_pops
             for r in range(2):
@@ -292,7 +312,8 @@ def test_partitioned_densify_cfg4_two_ranks(tmp_path):
             st = json.loads(open(out + f".{mode}.r0.json").read())
             assert st["evals"] == rst["evals"]
             _check_partition(st["partition"], 2)
-            assert sum(st["accepted"]) >= rst["patches"]
+            if mode != "hybrid":
+                assert sum(st["accepted"]) >= rst["patches"]
         eng.set_fast_options(dp.FastOptions())
         _, pst = D.densify_partitioned_device(eng, seeds, None, torch.device("cuda", 0), probe_worlds=(8,))
         _check_partition(pst["partition_probe"][8], 8)
