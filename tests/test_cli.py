@@ -263,7 +263,8 @@ def test_cli_gpus_partitioned_equals_one_gpu(scene_dir, tmp_path, gpus, extra):
     if "--replicate-below" in extra and extra[extra.index("--replicate-below") + 1] == "0":
         assert r1["patches"] <= rn["exchanged"]
     else:
-        assert 0 < rn["exchanged"] < r1["patches"]
+        # hybrid: only the partitioned generations' accepted records crossed
+        assert 0 < rn["exchanged"] <= r1["patches"]
     assert many.read_bytes() == one.read_bytes()
 
 
