@@ -4,7 +4,8 @@ rocprofv3 kernel trace: where the non-refine time of a densify goes (kernel
 time of the partition / compaction / organizer kernels vs GPU idle between
 launches).  --protocol device: the device-resident generations (dp_densify
 / dp_densify_run); slots: the multi-rank slot protocol at one rank
-(dist.densify_partitioned_device one_rank_exchange).  Prints one JSON line
+(dist.densify_partitioned_device one_rank_exchange); hybrid8: that protocol
+on the generations an 8-rank run partitions, the rest replicated.  Prints one JSON line
 per repetition: wall ms, refine ms (events), generations.
 
     rocprofv3 --kernel-trace --stats -d OUT -- python3 tools/densify_trace.py --mode fast
@@ -31,7 +32,7 @@ def main():
     ap.add_argument("--config", default="cfg4_64view_4k")
     ap.add_argument("--mode", default="fast")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--protocol", choices=["device", "slots"], default="device")
+    ap.add_argument("--protocol", choices=["device", "slots", "hybrid8"], default="device")
     a = ap.parse_args()
     cfg = synth.named(a.config)
     V, W, H = cfg.n_views, cfg.width, cfg.height
@@ -50,7 +51,10 @@ def main():
     seeds = synth.seeds(cfg, P)
     eng.set_fast_options(dp.FastOptions(densify=1 if a.mode == "fast" else 0))
     def run(eng, seeds, dist, dev):
-        return D.densify_partitioned_device(eng, seeds, dist, dev, one_rank_exchange=a.protocol == "slots")
+        # hybrid8: the slot protocol on the generations an 8-rank run partitions, the rest replicated
+        return D.densify_partitioned_device(eng, seeds, dist, dev, one_rank_exchange=a.protocol != "device",
+                                            replicate_below={"slots": 0, "hybrid8": D.replicate_below_default(8)}
+                                            .get(a.protocol))
 
     for rep in range(a.reps):
         torch.cuda.synchronize()
