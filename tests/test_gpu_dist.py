@@ -64,6 +64,47 @@ def test_generation_api_equals_dp_densify(name, max_pops):
         assert calls >= rst["generations"] // k
 
 
+@pytest.mark.parametrize("bound", [3, 30, 200])
+def test_run_until_yields_at_the_bound(bound):
+    """dp_densify_run_until hands back the first generation of >= bound items
+    unrun (its items and index as the host-array path reaches them), the
+    evaluations it reports add up to dp_densify's, and alternating it with
+    host-driven generations (the hybrid multi-rank loop at one rank) gives
+    dp_densify's store."""
+    P, imgs, seeds = _scene("hf6")
+    with dp.Engine(device=0) as eng:
+        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+        ref, rst = eng.densify(seeds)
+        _, hst = D.densify_partitioned(eng, seeds, None)
+        sizes = [p[0] for p in hst["partition"]]  # items of generation 0, 1, ...
+        g = eng.densify_begin(seeds)
+        cand, acc = eng.densify_refine_items(g, np.arange(g.items))
+        g = eng.densify_commit(g, cand, acc)
+        evals_run, yields = 0, 0
+        while g.items > 0:
+            assert g.items == sizes[g.index], (g.index, g.items)
+            if g.items < bound:
+                idx = g.index
+                g, ev = eng.densify_run_until(g, bound)
+                evals_run += ev
+                if g.items > 0:
+                    # stopped at the bound: the returned generation is the first
+                    # large one after idx, unrun
+                    assert g.items >= bound and g.index > idx
+                    assert all(s < bound for s in sizes[idx:g.index])
+                    yields += 1
+            else:
+                cand, acc = eng.densify_refine_items(g, np.arange(g.items))
+                g = eng.densify_commit(g, cand, acc)
+        got, st = eng.densify_result()
+    assert got.tobytes() == ref.tobytes()
+    for k in ("patches", "seed_patches", "candidates", "generations", "evals"):
+        assert st[k] == rst[k], k
+    assert evals_run <= rst["evals"] and (evals_run > 0) == any(s < bound for s in sizes[1:])
+    # hf6's generation sizes end 8, 3, 2, 2, 3, 3: at bound 3 the run stops before the second 3
+    assert yields == (1 if bound == 3 else 0)
+
+
 def test_device_loop_stall_resumes():
     """DP_GEN_CAP caps the device-resident loop's candidate buffers, so its
     generations outgrow them: each stalls on the device (nothing runs), the
