@@ -618,7 +618,8 @@ __device__ __forceinline__ uint32_t lane_select(uint64_t mask, uint32_t x)
 // One view's sample in 1/16 gray levels (or_fast.c fast_sample), in three
 // phases so that a pass issues every lane's LDS reads before it consumes any:
 // tap_addr (affine map, clamp, 1/32-px split), tap_load (the two aligned
-// words around each row's tap pair), tap_blend (funnel shift, bilinear).
+// words around each row's tap pair), the funnel shift and tap_blend_rows
+// (bilinear).
 struct Tap {
     uint32_t a0, a1;   // aligned LDS byte addresses of rows y0, y0 + 1
     uint32_t sh;       // 16 if the pair starts at an odd pixel
@@ -688,13 +689,6 @@ __device__ __forceinline__ uint32_t tap_blend_rows(const Tap &t, uint32_t r0, ui
     const uint32_t b = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, c), __builtin_bit_cast(us2, t.wx),
                                               32u - 0x8000u * 32u, false);
     return b >> 6;
-}
-
-__device__ __forceinline__ uint32_t tap_blend(const Tap &t, const TapWords &w)
-{
-    const uint32_t r0 = __builtin_amdgcn_alignbit(w.d[1], w.d[0], t.sh);
-    const uint32_t r1 = __builtin_amdgcn_alignbit(w.d[3], w.d[2], t.sh);
-    return tap_blend_rows(t, r0, r1);
 }
 
 // Spec v4's per-sample derivatives (or_fast.c fast_sample_q), from the same tap

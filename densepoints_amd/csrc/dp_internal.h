@@ -89,9 +89,10 @@ constexpr int kEpiClaims = 2; // capacity-1 claims at seq0 + index (the organize
 // join the refine kernels' register allocation (the parity kernel's spills
 // grew 4 -> 20 VGPRs inlined); as a call only the values live across it are
 // saved, once per candidate.  Returns the colour (wave_color) or 0.
-static __device__ __noinline__ uint32_t refine_epilogue(const dpg::ViewDev *views, int V, float p0, float p1,
-                                                        float p2, uint64_t vis0, uint64_t vis1, int epi, double gs,
-                                                        uint32_t *grid, uint32_t seq, int lane)
+[[maybe_unused]] static __device__ __noinline__ uint32_t refine_epilogue(const dpg::ViewDev *views, int V, float p0,
+                                                                        float p1, float p2, uint64_t vis0,
+                                                                        uint64_t vis1, int epi, double gs,
+                                                                        uint32_t *grid, uint32_t seq, int lane)
 {
     const float pf[3] = {p0, p1, p2};
     if (epi & kEpiClaims)

@@ -143,19 +143,6 @@ __device__ __forceinline__ void decode_vis(WaveLds &L, uint64_t v0, uint64_t v1)
 typedef const __attribute__((address_space(1))) uint32_t *gpix_t;
 typedef const __attribute__((address_space(1))) unsigned long long *gpair_t;
 
-// Full-wavefront integer sum (DPP row_shr / row_bcast), result in every lane
-// via readlane 63 (uniform).
-__device__ __forceinline__ int wave_total(int v)
-{
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false); // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false); // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xe, false); // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xc, false); // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); // row_bcast:15
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31
-    return __builtin_amdgcn_readlane(v, 63);
-}
-
 // Window coordinate of texel (px, py) of the view in table slot j, whose
 // row/column terms are in L.rowt[j] / L.colt[j] (same roundings as
 // dpg::window_tap: X0 = m1*y + m2, W0 = m7*y + m8, W = W0 + m6*x,
