@@ -1082,6 +1082,12 @@ static int run_generations(dp_ctx *c, int64_t max_gens, int64_t cap0, hipStream_
         }
         // the first generation's counters (later ones are zeroed by the previous organizer)
         DP_HIP(c, hipMemsetAsync(c->d_work, 0, dpk::kWorkCounters * sizeof(uint32_t), s));
+        if (c->fopt.densify) {
+            // dp_fast_last_stats: the batch's generations count as one launch
+            if (!c->d_fstats)
+                DP_HIP(c, hipMalloc(&c->d_fstats, 8 * sizeof(unsigned long long)));
+            DP_HIP(c, hipMemsetAsync(c->d_fstats, 0, 8 * sizeof(unsigned long long), s));
+        }
         if (c->g_lpt_scratch)
             DP_HIP(c, hipMemsetAsync(c->g_lpt_scratch, 0, 2 * dpk::kLptBuckets * sizeof(uint32_t), s));
         const int k = (int)std::min<int64_t>(kGenBatch, max_gens - done);

@@ -1974,8 +1974,12 @@ int dp_fast_launch(dp_ctx *c, dp_patch *d, int n, int cell, int mode, uint8_t *a
     if (!c->d_fstats)
         DP_HIP(c, hipMalloc(&c->d_fstats, 8 * sizeof(unsigned long long)));
     a.stats = c->d_fstats;
-    DP_HIP(c, hipMemsetAsync(c->d_fstats, 0, 8 * sizeof(unsigned long long), s));
-    DP_HIP(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), s));
+    if (!gen) {
+        // a device-resident generation's counters are zeroed by the previous
+        // organizer (dp_bfs.hip) and its statistics by its batch (run_generations)
+        DP_HIP(c, hipMemsetAsync(c->d_fstats, 0, 8 * sizeof(unsigned long long), s));
+        DP_HIP(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), s));
+    }
     DP_HIP(c, hipEventRecord(c->e0, s));
     const int N = cell * cell;
     const int tb = c->fopt.tile_budget;

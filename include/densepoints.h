@@ -538,7 +538,8 @@ int dp_read_gray(dp_ctx *ctx, int view, uint16_t *fp16_out);
  * mode: DP_MODE_FAST_REFINE on the parent's visible set, cell =
  * expand_cell_size. */
 int dp_fast_expand_batch(dp_ctx *ctx, const dp_patch *parents, int n, dp_patch *children, uint8_t *accept_out);
-/* Work counters of the most recent performance-mode launch (device-counted):
+/* Work counters of the most recent performance-mode launch (device-counted; a
+ * batch of device-resident densify generations counts as one launch):
  * view_evals = sum over patches and evaluations of the staged views sampled,
  * i.e. algorithmic bytes = view_evals * (n+1)^2 * 2 (fp16 texels);
  * staged_bytes = bytes the tiles copy from the gray planes (the compulsory
