@@ -28,6 +28,12 @@
 namespace dpk {
 namespace {
 
+// A/B build knob (DP_EXTRA_FLAGS=-DDP_FAST_TAP_MAD=0): the tap address as the
+// compiler selects it
+#ifndef DP_FAST_TAP_MAD
+#define DP_FAST_TAP_MAD 1
+#endif
+
 constexpr int kFastMaxV = 32;     // staged views per patch (per-view records)
 constexpr int kFastMaxBbox = 48;  // window bounding-box side cap (grazing views)
 constexpr int kFastMaxMargin = 7; // keeps a tile row <= 64 entries (one lane each)
@@ -647,8 +653,18 @@ __device__ __forceinline__ Tap tap_addr(const float4 &qa, const float4 &qb, cons
     // aligned word of the pair: byte (x0 >> 1) * 4 of the row = bits 6..21 of
     // bu shifted left by 2 (one v_bfe + one v_lshl_add, the row term by one
     // v_mad_u32_u24); x0 odd -> the pair straddles two words, shifted by 16 bits
+#if DP_FAST_TAP_MAD
+    // row term by v_mad_u32_u24 and the word offset by v_bfe + v_lshl_add: four
+    // VALU where the compiler's own selection (shift, multiply, shift, mask,
+    // three-way add) takes five
+    uint32_t row, a0;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(row) : "v"(bv >> 5), "v"(rowb), "v"(off));
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a0) : "v"(__builtin_amdgcn_ubfe(bu, 6u, 16u)), "v"(row));
+    t.a0 = a0;
+#else
     const uint32_t row = __umul24(bv >> 5, rowb) + off;
     t.a0 = (__builtin_amdgcn_ubfe(bu, 6u, 16u) << 2) + row;
+#endif
     t.a1 = t.a0 + rowb;
     t.sh = (bu >> 1) & 16u;
     const uint32_t fx = bu & 31u;
