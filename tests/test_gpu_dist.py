@@ -105,6 +105,22 @@ def test_run_until_yields_at_the_bound(bound):
     assert yields == (1 if bound == 3 else 0)
 
 
+def test_densify_result_view_equals_copy():
+    """Engine.densify(copy=False) / densify_result(copy=False): a view of the
+    context's pinned result buffer (not owning its memory) with the same
+    records as the copy, valid until the next densify on the engine; also
+    through the partitioned driver at one rank (copy_result=False)."""
+    P, imgs, seeds = _scene("hf6")
+    with dp.Engine(device=0) as eng:
+        eng.set_views([dp.View(P[v], imgs[v]) for v in range(len(P))])
+        ref, rst = eng.densify(seeds)
+        view, vst = eng.densify(seeds, copy=False)
+        assert view.tobytes() == ref.tobytes() and vst["patches"] == rst["patches"]
+        assert not view.flags.owndata
+        got, _ = D.densify_partitioned_device(eng, seeds, None, torch.device("cuda", 0), copy_result=False)
+        assert got.tobytes() == ref.tobytes()
+
+
 def test_device_loop_stall_resumes():
     """DP_GEN_CAP caps the device-resident loop's candidate buffers, so its
     generations outgrow them: each stalls on the device (nothing runs), the
